@@ -1,0 +1,269 @@
+/*
+ * slatedb_amd.h — C ABI of the MI355X-native SST block codec + bloom-filter builder.
+ *
+ * This is the drop-in boundary for slatedb's SST encode/decode hot path.  Every entry point is
+ * plain C (no HIP/torch types): pointers, sizes, an opaque stream handle and a status code.
+ * Citations are `path:line` relative to the slatedb reference (workspace 0.15.0).
+ *
+ * What each group replaces (the reference side is Rust; the binding a maintainer would add is in
+ * INTEGRATION.md):
+ *   - sdb_encode_sst*          -> EncodedSsTableBuilder::{add, finish_block, build}
+ *                                 (slatedb/src/sst_builder.rs:224-254, 284-326, 370-417) with
+ *                                 BlockBuilderV2 / BlockBuilderV1 (format/block_v2.rs:118-240,
+ *                                 format/block.rs:76-218), SstRowCodecV2 / SstRowCodecV0
+ *                                 (format/row_codec_v2.rs:127-169, format/row.rs:159-198), the
+ *                                 per-block CRC32 of compress_and_transform (format/sst.rs:525-554)
+ *                                 and BloomFilterBuilder (filter.rs:40-90).
+ *   - sdb_bloom_build*         -> FilterBuilder::build for BloomFilterPolicy "_bf"
+ *                                 (filter_policy.rs:170-283, filter.rs:71-90, 196-239).
+ *   - sdb_bloom_might_contain  -> BloomFilter::might_contain (filter.rs:124-136).
+ *   - sdb_decode_blocks*       -> SsTableFormat::read_blocks/decode_block + validate_checksum
+ *                                 (format/sst.rs:938-999, 1029-1038) followed by draining
+ *                                 DataBlockIterator ascending (block_iterator.rs:54-101,
+ *                                 block_iterator_v2.rs:235-267) — the contract of the public
+ *                                 SstFile::read_block (sst_reader.rs:287-309).
+ *   - sdb_sst_builder_*        -> host-side mirror of EncodedSsTableBuilder's add()/build()/
+ *                                 next_block() call order (sst_builder.rs:224-276), batching
+ *                                 entries into a columnar pinned buffer and encoding on the GPU.
+ *
+ * Conventions
+ *   - "device" entry points take device pointers and enqueue on `stream` (a hipStream_t passed as
+ *     void*; NULL = the legacy default stream).  They never allocate, never synchronise, and are
+ *     safe to capture into a HIP graph.  Results that the host needs (lengths, status) are written
+ *     to a device-resident summary struct the caller copies back.
+ *   - "host" entry points take host pointers, manage a per-handle device arena + pinned staging and
+ *     return synchronously.
+ *   - Keys/values are Arrow-style columnar: entry i's key is key_bytes[key_off[i] .. key_off[i+1]).
+ *     Offsets are monotone (n+1 entries, key_off[0] may be non-zero).
+ *   - The library fails loudly: if no HIP device is present every compute entry point returns
+ *     SDB_DEVICE_ERROR.  There is no CPU fallback.
+ */
+#ifndef SLATEDB_AMD_H
+#define SLATEDB_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDB_ABI_VERSION 1u
+
+/* Status codes.  Mirrors the hot-path variants of SlateDBError (slatedb/src/error.rs:23-38,
+ * 142-152, 197); the reference *panics* where SDB_LIMIT_EXCEEDED is returned. */
+typedef enum sdb_status {
+    SDB_OK = 0,
+    SDB_EMPTY_KEY = 1,              /* SlateDBError::EmptyKey (block_v2.rs:168-170) / assert in
+                                       compute_lower_bound (utils.rs:210) */
+    SDB_EMPTY_BLOCK = 2,            /* SlateDBError::EmptyBlock */
+    SDB_CHECKSUM_MISMATCH = 3,      /* SlateDBError::ChecksumMismatch (format/sst.rs:1029-1038) */
+    SDB_INVALID_ROW_FLAGS = 4,      /* SlateDBError::InvalidRowFlags (row_codec_v2.rs:234-249) */
+    SDB_INVALID_VERSION = 5,        /* SlateDBError::InvalidVersion (block_iterator.rs:60-77) */
+    SDB_LIMIT_EXCEEDED = 6,         /* reference panics: u16 asserts row.rs:73-85, block_v2.rs:195 */
+    SDB_UNSUPPORTED = 7,            /* compression / block transformer (not on this path) */
+    SDB_INVALID_ARGUMENT = 8,       /* bad kind byte, capacity too small, NULL pointer, ... */
+    SDB_CORRUPT_BLOCK = 9,          /* block bytes that the reference would panic on while parsing */
+    SDB_DEVICE_ERROR = 100          /* no HIP device / launch failure */
+} sdb_status;
+
+/* Entry kinds: ValueDeletable::{Value, Merge, Tombstone} (types.rs:166-173). */
+enum { SDB_KIND_VALUE = 0, SDB_KIND_MERGE = 1, SDB_KIND_TOMBSTONE = 2 };
+/* Row flags, RowFlags (format/row.rs:8-16). */
+enum { SDB_FLAG_TOMBSTONE = 1, SDB_FLAG_HAS_EXPIRE_TS = 2, SDB_FLAG_HAS_CREATE_TS = 4,
+       SDB_FLAG_MERGE_OPERAND = 8 };
+/* ts_mask bits. */
+enum { SDB_TS_CREATE = 1, SDB_TS_EXPIRE = 2 };
+
+/* A sorted run of RowEntry (types.rs:17-29), key asc / seq desc (mem_table.rs:38-44), columnar. */
+typedef struct sdb_kv_batch {
+    uint64_t n;
+    const uint8_t *key_bytes;
+    const uint64_t *key_off;    /* n+1 */
+    const uint8_t *val_bytes;   /* tombstones: value bytes are ignored (treated as empty) */
+    const uint64_t *val_off;    /* n+1 */
+    const uint8_t *kind;        /* n; NULL = all SDB_KIND_VALUE */
+    const uint64_t *seq;        /* n; NULL = all 0 */
+    const int64_t *create_ts;   /* n; read only where ts_mask & SDB_TS_CREATE */
+    const int64_t *expire_ts;   /* n; read only where ts_mask & SDB_TS_EXPIRE */
+    const uint8_t *ts_mask;     /* n; NULL = no timestamps */
+} sdb_kv_batch;
+
+/* SsTableFormat knobs on this path (format/sst.rs:620-643, db/builder.rs:439-531). */
+typedef struct sdb_sst_params {
+    uint32_t block_size;         /* SstBlockSize, default 4096 (config.rs:231-267) */
+    uint16_t sst_version;        /* 1 = BlockBuilderV1 + SstRowCodecV0, 2 = BlockBuilderV2 + V2 */
+    uint16_t restart_interval;   /* V2 only; reference constant 16 (block_v2.rs:8) */
+    uint32_t bloom_bits_per_key; /* BloomFilterPolicy::new(bpk) (filter_policy.rs:201); 0 = none */
+    uint32_t min_filter_keys;    /* filter built iff num_rows >= min_filter_keys (sst_builder.rs:390) */
+} sdb_sst_params;
+
+/* Scalar results of one SST encode, written by the device. */
+typedef struct sdb_sst_summary {
+    uint64_t data_len;           /* bytes of data section (all blocks incl. CRC) */
+    uint64_t num_blocks;
+    uint64_t num_entries;
+    uint64_t raw_key_size;       /* SstStats::raw_key_size (sst_builder.rs:225) */
+    uint64_t raw_val_size;       /* SstStats::raw_val_size (sst_builder.rs:226) */
+    uint64_t num_puts, num_deletes, num_merges;
+    uint64_t bloom_len;          /* bitmap bytes (0 if no filter) */
+    uint32_t num_probes;         /* optimal_num_probes(bpk) (filter.rs:235-239) */
+    uint32_t filter_built;       /* 1 iff a filter was built */
+    int32_t status;              /* sdb_status of the device-side checks */
+    uint32_t max_block_entries;  /* diagnostics: longest block in entries */
+    uint64_t first_error_entry;  /* entry index that raised `status` (UINT64_MAX if none) */
+} sdb_sst_summary;
+
+/* Caller-owned outputs.  For sdb_encode_sst (device) every pointer is device memory. */
+typedef struct sdb_sst_out {
+    uint8_t *data;               /* data section: blocks (Block::encode ++ crc32 BE), contiguous */
+    uint64_t data_cap;
+    uint64_t *block_off;         /* num_blocks+1 byte offsets into data (BlockMeta.offset) */
+    uint32_t *block_first_entry; /* num_blocks+1 entry indices (last = n) */
+    uint32_t *index_key_len;     /* per block: BlockMeta.first_key = key(first entry)[..len]
+                                    (compute_index_key, utils.rs:198-226); block 0 -> 0 */
+    uint16_t *block_stats;       /* 3 per block: num_puts, num_deletes, num_merges (sst_stats.rs:9-16) */
+    uint64_t block_cap;          /* capacity (in blocks) of the four arrays above */
+    uint8_t *bloom;              /* bloom bitmap (BloomFilter.buffer; the u16 BE num_probes header of
+                                    Filter::encode is NOT included) */
+    uint64_t bloom_cap;
+    sdb_sst_summary *summary;    /* device-writable */
+} sdb_sst_out;
+
+/* ---------------------------------------------------------------------------------------------
+ * Sizing (pure host arithmetic, no device needed)
+ * ------------------------------------------------------------------------------------------- */
+uint32_t sdb_abi_version(void);
+/* Upper bounds on the output arrays for a batch of n entries holding the given key/value bytes. */
+sdb_status sdb_encode_bounds(uint64_t n, uint64_t total_key_bytes, uint64_t total_val_bytes,
+                             const sdb_sst_params *params, uint64_t *data_cap,
+                             uint64_t *block_cap, uint64_t *bloom_cap);
+/* Device scratch needed by sdb_encode_sst for n entries. */
+uint64_t sdb_encode_workspace_bytes(uint64_t n, const sdb_sst_params *params);
+/* BloomFilterBuilder::filter_size_bytes (filter.rs:65-69): ceil(u32(n*bpk)/8). */
+uint64_t sdb_bloom_filter_bytes(uint64_t num_keys, uint32_t bits_per_key);
+/* optimal_num_probes (filter.rs:235-239). */
+uint32_t sdb_bloom_num_probes(uint32_t bits_per_key);
+
+/* ---------------------------------------------------------------------------------------------
+ * Device entry points (device pointers, async on `stream`)
+ * ------------------------------------------------------------------------------------------- */
+/* Encode one SST's data section + bloom bitmap from a device-resident sorted batch.  Host-side
+ * argument errors are returned directly; data-dependent errors (empty key, V1 u16 overflow, bad
+ * kind) are reported in out->summary->status after the stream completes. */
+sdb_status sdb_encode_sst(const sdb_kv_batch *batch, const sdb_sst_params *params,
+                          const sdb_sst_out *out, void *workspace, uint64_t workspace_bytes,
+                          void *stream);
+
+/* Bloom bitmap over n keys (BloomFilterBuilder with whole-key filtering, filter.rs:40-90).
+ * bitmap must hold sdb_bloom_filter_bytes(n, bpk) bytes; it is zeroed and filled on `stream`. */
+sdb_status sdb_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
+                           uint32_t bits_per_key, uint8_t *bitmap, uint64_t bitmap_bytes,
+                           void *stream);
+
+/* Batched BloomFilter::might_contain(filter_hash(key)) (filter.rs:124-136, 150-175): result[i]=1
+ * iff every probe bit is set.  An empty bitmap answers 0. */
+sdb_status sdb_bloom_might_contain(const uint8_t *bitmap, uint64_t bitmap_bytes,
+                                   uint32_t num_probes, const uint8_t *key_bytes,
+                                   const uint64_t *key_off, uint64_t n, uint8_t *result,
+                                   void *stream);
+
+/* Decoded entries, columnar, ascending order within and across blocks. */
+typedef struct sdb_decode_summary {
+    uint64_t num_entries;
+    uint64_t key_bytes;
+    uint64_t num_bad_blocks;
+    int32_t status;              /* error of the lowest-index failing block (try_join_all order) */
+    uint32_t pad;
+} sdb_decode_summary;
+
+typedef struct sdb_decoded_out {
+    uint64_t *block_entry_start; /* nblocks+1 */
+    uint8_t *key_arena;          /* full keys restored (restore_full_key, row_codec_v2.rs:83-89) */
+    uint64_t key_arena_cap;
+    uint64_t *key_off;           /* cap_entries+1 */
+    uint64_t *val_off;           /* byte offset of the value inside `blocks` (zero-copy, like
+                                    Bytes::slice); tombstones -> 0 */
+    uint32_t *val_len;
+    uint64_t *seq;
+    uint8_t *flags;              /* RowFlags of the row; kind = tombstone/merge/value from it */
+    int64_t *create_ts;          /* valid iff flags & HAS_CREATE_TS */
+    int64_t *expire_ts;          /* valid iff flags & HAS_EXPIRE_TS (V0 tombstones: never) */
+    uint64_t cap_entries;
+    uint32_t *bad_block;         /* indices of blocks that failed (CRC / flags / parse) */
+    uint64_t bad_cap;
+    sdb_decode_summary *summary; /* device-writable */
+} sdb_decoded_out;
+
+uint64_t sdb_decode_workspace_bytes(uint64_t nblocks);
+/* Decode nblocks encoded blocks (each = Block::encode ++ crc32 BE) located at
+ * blocks[block_off[k] .. block_off[k+1]).  sst_version 1 or 2 selects the row codec. */
+sdb_status sdb_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                             uint16_t sst_version, const sdb_decoded_out *out, void *workspace,
+                             uint64_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Host entry points: device arena + pinned staging per handle (E2E path: H2D -> kernels -> D2H)
+ * ------------------------------------------------------------------------------------------- */
+typedef struct sdb_encoder sdb_encoder;
+
+/* Host-memory view of one encoded SST (arrays owned by the encoder, valid until the next call). */
+typedef struct sdb_sst_host_result {
+    sdb_sst_summary summary;
+    const uint8_t *data;
+    const uint64_t *block_off;
+    const uint32_t *block_first_entry;
+    const uint32_t *index_key_len;
+    const uint16_t *block_stats;
+    const uint8_t *bloom;
+    double h2d_ms, kernel_ms, d2h_ms;   /* hipEvent timings of the last call */
+} sdb_sst_host_result;
+
+sdb_encoder *sdb_encoder_create(int device, const sdb_sst_params *params);
+void sdb_encoder_destroy(sdb_encoder *enc);
+/* Encode a host batch; returns the first error (host-side or device-side). */
+sdb_status sdb_encoder_encode_host(sdb_encoder *enc, const sdb_kv_batch *host_batch,
+                                   sdb_sst_host_result *result);
+
+/* Mirror of EncodedSsTableBuilder's per-entry surface (sst_builder.rs:224-276,370-417). */
+typedef struct sdb_sst_builder sdb_sst_builder;
+sdb_sst_builder *sdb_sst_builder_new(int device, const sdb_sst_params *params);
+void sdb_sst_builder_free(sdb_sst_builder *b);
+/* add(entry): kind per SDB_KIND_*, timestamps present iff the has_* flags are non-zero. */
+sdb_status sdb_sst_builder_add(sdb_sst_builder *b, const uint8_t *key, uint64_t key_len,
+                               uint8_t kind, const uint8_t *val, uint64_t val_len, uint64_t seq,
+                               int32_t has_create_ts, int64_t create_ts, int32_t has_expire_ts,
+                               int64_t expire_ts);
+/* build(): encode everything added so far on the GPU. */
+sdb_status sdb_sst_builder_build(sdb_sst_builder *b, sdb_sst_host_result *result);
+
+/* Host decode of encoded blocks (H2D, decode kernels, D2H).  Arrays owned by the handle. */
+typedef struct sdb_decoder sdb_decoder;
+typedef struct sdb_decode_host_result {
+    sdb_decode_summary summary;
+    const uint64_t *block_entry_start;
+    const uint8_t *key_arena;
+    const uint64_t *key_off;
+    const uint64_t *val_off;
+    const uint32_t *val_len;
+    const uint64_t *seq;
+    const uint8_t *flags;
+    const int64_t *create_ts;
+    const int64_t *expire_ts;
+    const uint32_t *bad_block;
+} sdb_decode_host_result;
+sdb_decoder *sdb_decoder_create(int device);
+void sdb_decoder_destroy(sdb_decoder *dec);
+sdb_status sdb_decoder_decode_host(sdb_decoder *dec, const uint8_t *blocks,
+                                   const uint64_t *block_off, uint64_t nblocks,
+                                   uint16_t sst_version, sdb_decode_host_result *result);
+
+/* Device query: number of visible HIP devices (0 on a machine without a GPU). */
+int sdb_device_count(void);
+/* Human-readable name of a status code. */
+const char *sdb_status_name(int status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SLATEDB_AMD_H */

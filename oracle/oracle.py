@@ -1,0 +1,261 @@
+"""ctypes front-end of oracle/liboracle.so — the CPU restatement used as the parity checker.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg; never by slatedb_amd/.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from slatedb_amd import _abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def _load():
+    if not os.path.exists(LIB):
+        build()
+    lib = C.CDLL(LIB)
+    V, P = C.c_void_p, C.POINTER
+    sig = {
+        "orc_varint_len": (C.c_uint32, [C.c_uint32]),
+        "orc_encode_varint": (C.c_size_t, [V, C.c_uint32]),
+        "orc_crc32": (C.c_uint32, [V, C.c_size_t]),
+        "orc_siphash": (C.c_uint64, [V, C.c_size_t, C.c_uint64, C.c_uint64, C.c_int, C.c_int]),
+        "orc_filter_hash": (C.c_uint64, [V, C.c_size_t]),
+        "orc_probes_for_key": (None, [C.c_uint64, C.c_uint16, C.c_uint32, V]),
+        "orc_optimal_num_probes": (C.c_uint16, [C.c_uint32]),
+        "orc_filter_size_bytes": (C.c_uint64, [C.c_uint64, C.c_uint32]),
+        "orc_compute_prefix": (C.c_size_t, [V, C.c_size_t, V, C.c_size_t]),
+        "orc_index_key_len": (C.c_int64, [V, C.c_size_t, C.c_int, V, C.c_size_t]),
+        "orc_encode_row": (C.c_size_t, [C.c_uint16, C.c_uint32, V, C.c_size_t, C.c_uint8, V,
+                                        C.c_size_t, C.c_uint64, C.c_int, C.c_int64, C.c_int,
+                                        C.c_int64, V, C.c_size_t]),
+        "orc_build_block": (C.c_int, [P(_abi.KvBatch), C.c_uint16, C.c_uint32, C.c_uint16, V,
+                                      C.c_uint64, P(C.c_uint64), V]),
+        "orc_encode_sst": (C.c_int, [P(_abi.KvBatch), P(_abi.SstParams), P(_abi.SstOut)]),
+        "orc_bloom_build": (C.c_int, [V, V, C.c_uint64, C.c_uint32, V, C.c_uint64]),
+        "orc_bloom_might_contain": (C.c_int, [V, C.c_uint64, C.c_uint32, V, C.c_size_t]),
+        "orc_decode_blocks": (C.c_int, [V, V, C.c_uint64, C.c_uint16, P(_abi.DecodedOut)]),
+    }
+    for k, (r, a) in sig.items():
+        f = getattr(lib, k)
+        f.restype, f.argtypes = r, a
+    return lib
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = _load()
+    return _lib
+
+
+def _buf(b):
+    b = bytes(b)
+    return C.create_string_buffer(b, max(len(b), 1)), len(b)
+
+
+def varint_len(v):
+    return lib().orc_varint_len(v)
+
+
+def encode_varint(v):
+    out = C.create_string_buffer(8)
+    n = lib().orc_encode_varint(out, v)
+    return out.raw[:n]
+
+
+def crc32(data):
+    b, n = _buf(data)
+    return lib().orc_crc32(b, n)
+
+
+def siphash(data, k0=0, k1=0, c=1, d=3):
+    b, n = _buf(data)
+    return lib().orc_siphash(b, n, k0, k1, c, d)
+
+
+def filter_hash(key):
+    b, n = _buf(key)
+    return lib().orc_filter_hash(b, n)
+
+
+def probes_for_key(h, k, m):
+    out = (C.c_uint32 * k)()
+    lib().orc_probes_for_key(h, k, m, out)
+    return list(out)
+
+
+def optimal_num_probes(bpk):
+    return lib().orc_optimal_num_probes(bpk)
+
+
+def filter_size_bytes(n, bpk):
+    return lib().orc_filter_size_bytes(n, bpk)
+
+
+def compute_prefix(a, b):
+    ba, na = _buf(a)
+    bb, nb = _buf(b)
+    return lib().orc_compute_prefix(ba, na, bb, nb)
+
+
+def index_key(prev, first):
+    """compute_index_key; returns bytes, or None where the reference panics."""
+    bf, nf = _buf(first)
+    if prev is None:
+        r = lib().orc_index_key_len(None, 0, 0, bf, nf)
+    else:
+        bp, npv = _buf(prev)
+        r = lib().orc_index_key_len(bp, npv, 1, bf, nf)
+    return None if r < 0 else bytes(first)[:r]
+
+
+def encode_row(version, shared, suffix, kind, value, seq, create_ts=None, expire_ts=None):
+    bs, ns = _buf(suffix)
+    bv, nv = _buf(value or b"")
+    cap = ns + nv + 64
+    out = C.create_string_buffer(cap)
+    n = lib().orc_encode_row(version, shared, bs, ns, kind, bv, nv, seq, create_ts is not None,
+                             create_ts or 0, expire_ts is not None, expire_ts or 0, out, cap)
+    return out.raw[:n]
+
+
+def build_block(batch, version=2, block_size=4096, restart_interval=16):
+    cap = int(batch.key_off[-1] + batch.val_off[-1]) + 64 * (batch.n + 1)
+    out = (C.c_uint8 * cap)()
+    ln = C.c_uint64(0)
+    acc = np.zeros(max(batch.n, 1), np.uint8)
+    kb = batch.to_ctypes()
+    st = lib().orc_build_block(C.byref(kb), version, block_size, restart_interval, out, cap,
+                               C.byref(ln), acc.ctypes.data)
+    return st, bytes(out)[:ln.value] if st == 0 else b"", acc[:batch.n]
+
+
+class SstResult:
+    def __init__(self, status, summary, data, block_off, block_first_entry, index_key_len,
+                 block_stats, bloom):
+        self.status = status
+        self.summary = summary
+        self.data = data
+        self.block_off = block_off
+        self.block_first_entry = block_first_entry
+        self.index_key_len = index_key_len
+        self.block_stats = block_stats
+        self.bloom = bloom
+
+
+def bounds(batch, params):
+    """Same upper bounds as sdb_encode_bounds (restated so the oracle needs no GPU library)."""
+    n = batch.n
+    kb = int(batch.key_off[-1] - batch.key_off[0])
+    vb = int(batch.val_off[-1] - batch.val_off[0])
+    data_cap = kb + vb + n * 64 + 64
+    block_cap = n + 1
+    bloom_cap = filter_size_bytes(n, params.bloom_bits_per_key) + 16 if params.bloom_bits_per_key else 16
+    return data_cap, block_cap, bloom_cap
+
+
+def params(block_size=4096, sst_version=2, restart_interval=16, bloom_bits_per_key=10,
+           min_filter_keys=0):
+    return _abi.SstParams(block_size, sst_version, restart_interval, bloom_bits_per_key,
+                          min_filter_keys)
+
+
+def encode_sst(batch, prm):
+    data_cap, block_cap, bloom_cap = bounds(batch, prm)
+    data = np.zeros(data_cap, np.uint8)
+    block_off = np.zeros(block_cap + 1, np.uint64)
+    bfe = np.zeros(block_cap + 1, np.uint32)
+    ikl = np.zeros(block_cap, np.uint32)
+    bst = np.zeros(3 * block_cap, np.uint16)
+    bloom = np.zeros(bloom_cap, np.uint8)
+    sm = _abi.SstSummary()
+    out = _abi.SstOut(data.ctypes.data, data_cap, block_off.ctypes.data, bfe.ctypes.data,
+                      ikl.ctypes.data, bst.ctypes.data, block_cap, bloom.ctypes.data, bloom_cap,
+                      C.addressof(sm))
+    kb = batch.to_ctypes()
+    st = lib().orc_encode_sst(C.byref(kb), C.byref(prm), C.byref(out))
+    nb = sm.num_blocks
+    return SstResult(st, sm, data[:sm.data_len].copy(), block_off[:nb + 1].copy(),
+                     bfe[:nb + 1].copy(), ikl[:nb].copy(), bst[:3 * nb].reshape(-1, 3).copy(),
+                     bloom[:sm.bloom_len].copy())
+
+
+def bloom_build(key_bytes, key_off, bpk):
+    n = len(key_off) - 1
+    fb = filter_size_bytes(n, bpk)
+    bm = np.zeros(max(fb, 1), np.uint8)
+    st = lib().orc_bloom_build(key_bytes.ctypes.data, key_off.ctypes.data, n, bpk, bm.ctypes.data, fb)
+    assert st == 0
+    return bm[:fb]
+
+
+def might_contain(bitmap, num_probes, key):
+    bk, nk = _buf(key)
+    bm = np.ascontiguousarray(bitmap, np.uint8)
+    return bool(lib().orc_bloom_might_contain(bm.ctypes.data if bm.size else None, bm.size,
+                                              num_probes, bk, nk))
+
+
+class DecodeResult:
+    pass
+
+
+def decode_blocks(blocks, block_off, version=2, cap_entries=None, key_cap=None):
+    blocks = np.ascontiguousarray(blocks, np.uint8)
+    total = int(np.asarray(block_off)[-1] - np.asarray(block_off)[0]) if len(block_off) > 1 else 0
+    key_cap = key_cap or (total * 4 + 4096)
+    while True:
+        r = _decode_blocks(blocks, block_off, version, cap_entries, key_cap)
+        if r.status != _abi.SDB_INVALID_ARGUMENT or key_cap > (total + 1) * 1024:
+            return r
+        key_cap *= 8
+
+
+def _decode_blocks(blocks, block_off, version, cap_entries, key_cap):
+    block_off = np.ascontiguousarray(block_off, np.uint64)
+    nb = len(block_off) - 1
+    total = int(block_off[-1] - block_off[0]) if nb else 0
+    cap_entries = cap_entries or (total // 12 + 16)
+    key_cap = key_cap or (total * 64 + 64)
+    r = DecodeResult()
+    r.block_entry_start = np.zeros(nb + 1, np.uint64)
+    r.key_arena = np.zeros(key_cap, np.uint8)
+    r.key_off = np.zeros(cap_entries + 1, np.uint64)
+    r.val_off = np.zeros(cap_entries, np.uint64)
+    r.val_len = np.zeros(cap_entries, np.uint32)
+    r.seq = np.zeros(cap_entries, np.uint64)
+    r.flags = np.zeros(cap_entries, np.uint8)
+    r.create_ts = np.zeros(cap_entries, np.int64)
+    r.expire_ts = np.zeros(cap_entries, np.int64)
+    r.bad_block = np.zeros(max(nb, 1), np.uint32)
+    sm = _abi.DecodeSummary()
+    out = _abi.DecodedOut(r.block_entry_start.ctypes.data, r.key_arena.ctypes.data, key_cap,
+                          r.key_off.ctypes.data, r.val_off.ctypes.data, r.val_len.ctypes.data,
+                          r.seq.ctypes.data, r.flags.ctypes.data, r.create_ts.ctypes.data,
+                          r.expire_ts.ctypes.data, cap_entries, r.bad_block.ctypes.data,
+                          max(nb, 1), C.addressof(sm))
+    st = lib().orc_decode_blocks(blocks.ctypes.data if blocks.size else None, block_off.ctypes.data,
+                                 nb, version, C.byref(out))
+    r.status = st
+    r.summary = sm
+    n = sm.num_entries
+    r.n = n
+    r.key_off = r.key_off[:n + 1]
+    r.key_arena = r.key_arena[:sm.key_bytes]
+    for f in ("val_off", "val_len", "seq", "flags", "create_ts", "expire_ts"):
+        setattr(r, f, getattr(r, f)[:n])
+    r.bad_block = r.bad_block[:min(sm.num_bad_blocks, max(nb, 1))]
+    return r

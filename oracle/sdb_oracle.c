@@ -1,0 +1,741 @@
+/*
+ * sdb_oracle.c — CPU restatement of slatedb's SST block codec, SST data-section builder, per-block
+ * CRC32, bloom-filter builder and block decoder.
+ *
+ * TEST INFRASTRUCTURE ONLY (see sdb_oracle.h).  It is the parity checker for the HIP path and the
+ * timed "port" CPU baseline of bench.py; the product library never links it.
+ *
+ * Parity pins (tests/test_oracle_kats.py): the V1 block insta snapshots (format/block.rs:250-343,
+ * testdata/snapshots/..block..snap), the V0 row snapshots (format/row.rs:288-465), varint KATs
+ * (utils.rs:1615-1735), index-key KATs (utils.rs:846-887), the probes KAT (filter.rs:313-329), the
+ * bit KATs (filter.rs:250-311), the 15-scenario V1/V2 size table (format/block_v2.rs:636-657), the
+ * V2 builder structure tests (block_v2.rs:282-630) and the derived 500-entry SST data section.
+ * SipHash-1-3 outputs are not pinned by any reference fixture: the (c,d)-parametrised SipHash below
+ * is pinned at (2,4) against the published vectors and CPython's zero-key siphash24, and the bloom
+ * false-positive KAT of filter.rs:331-367 is reproduced — see DESIGN.md "Parity".
+ */
+#include "sdb_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------------------------- */
+/* Byte helpers: bytes::BufMut big-endian put_* (bytes 1.11)                                    */
+/* ------------------------------------------------------------------------------------------- */
+typedef struct {
+    uint8_t *p;
+    size_t len, cap;
+} vbuf;
+
+static int vb_reserve(vbuf *b, size_t extra) {
+    if (b->len + extra <= b->cap) return 1;
+    size_t nc = b->cap ? b->cap * 2 : 256;
+    while (nc < b->len + extra) nc *= 2;
+    uint8_t *np = (uint8_t *)realloc(b->p, nc);
+    if (!np) return 0;
+    b->p = np;
+    b->cap = nc;
+    return 1;
+}
+static void vb_put(vbuf *b, const void *src, size_t n) {
+    if (!n) return;
+    vb_reserve(b, n);
+    memcpy(b->p + b->len, src, n);
+    b->len += n;
+}
+static void vb_u8(vbuf *b, uint8_t v) { vb_put(b, &v, 1); }
+static void vb_be(vbuf *b, uint64_t v, int nbytes) {
+    uint8_t t[8];
+    for (int i = 0; i < nbytes; i++) t[i] = (uint8_t)(v >> (8 * (nbytes - 1 - i)));
+    vb_put(b, t, (size_t)nbytes);
+}
+static uint64_t rd_be(const uint8_t *p, int nbytes) {
+    uint64_t v = 0;
+    for (int i = 0; i < nbytes; i++) v = (v << 8) | p[i];
+    return v;
+}
+
+/* ------------------------------------------------------------------------------------------- */
+/* Varint (LEB128 u32): utils.rs:609-645                                                        */
+/* ------------------------------------------------------------------------------------------- */
+uint32_t orc_varint_len(uint32_t v) {
+    uint32_t len = 1;
+    while (v >= 0x80) {
+        v >>= 7;
+        len++;
+    }
+    return len;
+}
+size_t orc_encode_varint(uint8_t *out, uint32_t v) {
+    size_t i = 0;
+    while (v >= 0x80) {
+        out[i++] = (uint8_t)(v | 0x80);
+        v >>= 7;
+    }
+    out[i++] = (uint8_t)v;
+    return i;
+}
+static void vb_varint(vbuf *b, uint32_t v) {
+    uint8_t t[5];
+    vb_put(b, t, orc_encode_varint(t, v));
+}
+/* decode_varint (utils.rs:622-634); returns 0 where Buf::get_u8 would panic (out of bytes).  The
+ * reference's `shift` keeps growing past 28 and `<<` by >=32 panics in debug / wraps in release; we
+ * accept at most 5 bytes like a well-formed u32 and flag longer runs as corrupt. */
+static int rd_varint(const uint8_t *p, size_t avail, size_t *pos, uint32_t *v) {
+    uint32_t r = 0;
+    int shift = 0;
+    for (;;) {
+        if (*pos >= avail || shift > 28) return 0;
+        uint8_t byte = p[(*pos)++];
+        r |= (uint32_t)(byte & 0x7F) << shift;
+        if (!(byte & 0x80)) break;
+        shift += 7;
+    }
+    *v = r;
+    return 1;
+}
+
+/* ------------------------------------------------------------------------------------------- */
+/* CRC32 (crc32fast 1.5 = CRC-32/ISO-HDLC, reflected poly 0xEDB88320), format/sst.rs:541        */
+/* ------------------------------------------------------------------------------------------- */
+static uint32_t crc_tab[8][256];
+static int crc_ready = 0;
+static void crc_init(void) {
+    if (crc_ready) return;
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : (c >> 1);
+        crc_tab[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; i++)
+        for (int t = 1; t < 8; t++) crc_tab[t][i] = (crc_tab[t - 1][i] >> 8) ^ crc_tab[0][crc_tab[t - 1][i] & 0xFF];
+    crc_ready = 1;
+}
+uint32_t orc_crc32(const uint8_t *p, size_t n) {
+    crc_init();
+    uint32_t c = 0xFFFFFFFFu;
+    while (n >= 8) {
+        uint32_t lo = c ^ ((uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24);
+        uint32_t hi = (uint32_t)p[4] | (uint32_t)p[5] << 8 | (uint32_t)p[6] << 16 | (uint32_t)p[7] << 24;
+        c = crc_tab[7][lo & 0xFF] ^ crc_tab[6][(lo >> 8) & 0xFF] ^ crc_tab[5][(lo >> 16) & 0xFF] ^
+            crc_tab[4][lo >> 24] ^ crc_tab[3][hi & 0xFF] ^ crc_tab[2][(hi >> 8) & 0xFF] ^
+            crc_tab[1][(hi >> 16) & 0xFF] ^ crc_tab[0][hi >> 24];
+        p += 8;
+        n -= 8;
+    }
+    while (n--) c = crc_tab[0][(c ^ *p++) & 0xFF] ^ (c >> 8);
+    return c ^ 0xFFFFFFFFu;
+}
+
+/* ------------------------------------------------------------------------------------------- */
+/* SipHash-c-d, 64-bit output (siphasher 1.0.3 SipHasher13::hash = write(bytes) + finish)       */
+/* ------------------------------------------------------------------------------------------- */
+#define ROTL64(x, b) (uint64_t)(((x) << (b)) | ((x) >> (64 - (b))))
+#define SIPROUND                                                                                   \
+    do {                                                                                           \
+        v0 += v1; v1 = ROTL64(v1, 13); v1 ^= v0; v0 = ROTL64(v0, 32);                              \
+        v2 += v3; v3 = ROTL64(v3, 16); v3 ^= v2;                                                   \
+        v0 += v3; v3 = ROTL64(v3, 21); v3 ^= v0;                                                   \
+        v2 += v1; v1 = ROTL64(v1, 17); v1 ^= v2; v2 = ROTL64(v2, 32);                              \
+    } while (0)
+
+uint64_t orc_siphash(const uint8_t *p, size_t n, uint64_t k0, uint64_t k1, int c, int d) {
+    uint64_t v0 = k0 ^ 0x736f6d6570736575ULL, v1 = k1 ^ 0x646f72616e646f6dULL;
+    uint64_t v2 = k0 ^ 0x6c7967656e657261ULL, v3 = k1 ^ 0x7465646279746573ULL;
+    size_t full = n & ~(size_t)7;
+    for (size_t i = 0; i < full; i += 8) {
+        uint64_t m = 0;
+        for (int j = 7; j >= 0; j--) m = (m << 8) | p[i + (size_t)j];
+        v3 ^= m;
+        for (int r = 0; r < c; r++) SIPROUND;
+        v0 ^= m;
+    }
+    uint64_t b = ((uint64_t)n & 0xFF) << 56;
+    for (size_t j = 0; j < (n & 7); j++) b |= (uint64_t)p[full + j] << (8 * j);
+    v3 ^= b;
+    for (int r = 0; r < c; r++) SIPROUND;
+    v0 ^= b;
+    v2 ^= 0xFF;
+    for (int r = 0; r < d; r++) SIPROUND;
+    return v0 ^ v1 ^ v2 ^ v3;
+}
+uint64_t orc_filter_hash(const uint8_t *p, size_t n) { return orc_siphash(p, n, 0, 0, 1, 3); }
+
+/* probes_for_key: enhanced double hashing (filter.rs:206-221), all arithmetic in u64. */
+void orc_probes_for_key(uint64_t h64, uint16_t k, uint32_t m32, uint32_t *out) {
+    uint64_t m = m32;
+    uint64_t h = ((h64 << 32) >> 32) % m;
+    uint64_t delta = (h64 >> 32) % m;
+    for (uint16_t i = 0; i < k; i++) {
+        delta = (delta + i) % m;
+        out[i] = (uint32_t)h;
+        h = (h + delta) % m;
+    }
+}
+uint16_t orc_optimal_num_probes(uint32_t bpk) { return (uint16_t)((float)bpk * 0.69f); }
+uint64_t orc_filter_size_bytes(uint64_t num_keys, uint32_t bpk) {
+    uint32_t bits = (uint32_t)num_keys * bpk; /* u32 multiply (filter.rs:66), wraps in release */
+    return (uint64_t)(bits / 8u + (bits % 8u != 0)); /* u32::div_ceil(8) */
+}
+
+sdb_status orc_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
+                           uint32_t bpk, uint8_t *bitmap, uint64_t bitmap_bytes) {
+    uint64_t fb = orc_filter_size_bytes(n, bpk);
+    if (bitmap_bytes < fb) return SDB_INVALID_ARGUMENT;
+    memset(bitmap, 0, fb);
+    if (fb == 0) return SDB_OK;
+    uint16_t k = orc_optimal_num_probes(bpk);
+    uint32_t m = (uint32_t)(fb * 8);
+    uint32_t pr[64];
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t h = orc_filter_hash(key_bytes + key_off[i], (size_t)(key_off[i + 1] - key_off[i]));
+        if (k <= 64) {
+            orc_probes_for_key(h, k, m, pr);
+            for (uint16_t j = 0; j < k; j++) bitmap[pr[j] / 8] |= (uint8_t)(1u << (pr[j] % 8)); /* set_bit */
+        } else {
+            uint32_t *big = (uint32_t *)malloc(sizeof(uint32_t) * k);
+            orc_probes_for_key(h, k, m, big);
+            for (uint16_t j = 0; j < k; j++) bitmap[big[j] / 8] |= (uint8_t)(1u << (big[j] % 8));
+            free(big);
+        }
+    }
+    return SDB_OK;
+}
+
+int orc_bloom_might_contain(const uint8_t *bitmap, uint64_t bitmap_bytes, uint32_t num_probes,
+                            const uint8_t *key, size_t klen) {
+    if (bitmap_bytes == 0) return 0; /* filter.rs:124-129 */
+    uint32_t m = (uint32_t)(bitmap_bytes * 8);
+    uint64_t hash = orc_filter_hash(key, klen);
+    uint64_t mm = m, h = ((hash << 32) >> 32) % mm, delta = (hash >> 32) % mm;
+    for (uint32_t i = 0; i < num_probes; i++) {
+        delta = (delta + i) % mm;
+        if (!(bitmap[h / 8] & (1u << (h % 8)))) return 0; /* check_bit (filter.rs:223-227) */
+        h = (h + delta) % mm;
+    }
+    return 1;
+}
+
+/* ------------------------------------------------------------------------------------------- */
+/* compute_prefix (block_v2.rs:52-75 / block.rs:84-96): 128-byte chunks then bytewise == LCP     */
+/* ------------------------------------------------------------------------------------------- */
+size_t orc_compute_prefix(const uint8_t *a, size_t na, const uint8_t *b, size_t nb) {
+    size_t n = na < nb ? na : nb, off = 0;
+    while (off + 128 <= n && memcmp(a + off, b + off, 128) == 0) off += 128;
+    while (off < n && a[off] == b[off]) off++;
+    return off;
+}
+
+/* compute_index_key / compute_lower_bound (utils.rs:198-226). */
+int64_t orc_index_key_len(const uint8_t *prev, size_t nprev, int has_prev, const uint8_t *first,
+                          size_t nfirst) {
+    if (!has_prev) return 0;                    /* first block: EMPTY_KEY */
+    if (nprev == 0 || nfirst == 0) return -1;   /* assert!(!prev.is_empty() && !first.is_empty()) */
+    for (size_t i = 0; i < nprev; i++) {
+        if (i >= nfirst) return -1;             /* this_block_first_key[i] out of bounds: panic */
+        if (prev[i] != first[i]) return (int64_t)i + 1;
+    }
+    if (nprev == nfirst) return (int64_t)nfirst;
+    return (int64_t)nprev + 1;
+}
+
+/* ------------------------------------------------------------------------------------------- */
+/* Entry view over a columnar batch (RowEntry, types.rs:17-29)                                  */
+/* ------------------------------------------------------------------------------------------- */
+typedef struct {
+    const uint8_t *key;
+    size_t klen;
+    const uint8_t *val;
+    size_t vlen;      /* 0 for tombstones (ValueDeletable::len) */
+    uint8_t kind;
+    uint64_t seq;
+    int has_create, has_expire;
+    int64_t create_ts, expire_ts;
+} entry_t;
+
+static int get_entry(const sdb_kv_batch *b, uint64_t i, entry_t *e) {
+    e->key = b->key_bytes + b->key_off[i];
+    e->klen = (size_t)(b->key_off[i + 1] - b->key_off[i]);
+    e->kind = b->kind ? b->kind[i] : SDB_KIND_VALUE;
+    if (e->kind > SDB_KIND_TOMBSTONE) return 0;
+    e->val = b->val_bytes ? b->val_bytes + b->val_off[i] : NULL;
+    e->vlen = (e->kind == SDB_KIND_TOMBSTONE) ? 0 : (size_t)(b->val_off[i + 1] - b->val_off[i]);
+    e->seq = b->seq ? b->seq[i] : 0;
+    uint8_t m = b->ts_mask ? b->ts_mask[i] : 0;
+    e->has_create = (m & SDB_TS_CREATE) != 0;
+    e->has_expire = (m & SDB_TS_EXPIRE) != 0;
+    e->create_ts = e->has_create ? b->create_ts[i] : 0;
+    e->expire_ts = e->has_expire ? b->expire_ts[i] : 0;
+    return 1;
+}
+
+static uint8_t row_flags(const entry_t *e) { /* SstRowEntryV2::flags (row_codec_v2.rs:67-80) */
+    uint8_t f = e->kind == SDB_KIND_MERGE ? SDB_FLAG_MERGE_OPERAND
+              : e->kind == SDB_KIND_TOMBSTONE ? SDB_FLAG_TOMBSTONE : 0;
+    if (e->has_expire) f |= SDB_FLAG_HAS_EXPIRE_TS;
+    if (e->has_create) f |= SDB_FLAG_HAS_CREATE_TS;
+    return f;
+}
+
+/* ------------------------------------------------------------------------------------------- */
+/* Block builders                                                                               */
+/* ------------------------------------------------------------------------------------------- */
+typedef struct {
+    uint16_t version;
+    size_t block_size;
+    size_t restart_interval;
+    vbuf data;
+    uint16_t *offs; /* V2: restarts; V1: per-entry offsets */
+    size_t noffs, capoffs;
+    size_t counter;
+    const uint8_t *last_key; size_t last_klen;   /* V2: previous key (block_v2.rs:88) */
+    const uint8_t *first_key; size_t first_klen; /* V1: block's first key (block.rs:79) */
+    int has_first;
+    uint16_t puts, deletes, merges;               /* BlockBuilderWithStats (format/sst.rs:108-141) */
+} blk_t;
+
+static void blk_reset(blk_t *b) {
+    b->data.len = 0;
+    b->noffs = 0;
+    b->counter = 0;
+    b->last_key = NULL; b->last_klen = 0;
+    b->first_key = NULL; b->first_klen = 0; b->has_first = 0;
+    b->puts = b->deletes = b->merges = 0;
+}
+static void blk_push_off(blk_t *b, uint16_t v) {
+    if (b->noffs == b->capoffs) {
+        b->capoffs = b->capoffs ? b->capoffs * 2 : 64;
+        b->offs = (uint16_t *)realloc(b->offs, b->capoffs * sizeof(uint16_t));
+    }
+    b->offs[b->noffs++] = v;
+}
+static int blk_empty(const blk_t *b) { return b->version == 2 ? b->counter == 0 : b->noffs == 0; }
+static size_t blk_size(const blk_t *b) { return b->data.len + b->noffs * 2 + 2; } /* Block::size */
+
+/* SstRowEntryV2::encoded_size (row_codec_v2.rs:92-116) */
+static size_t v2_row_size(const entry_t *e, size_t shared) {
+    size_t suf = e->klen - shared;
+    return orc_varint_len((uint32_t)shared) + orc_varint_len((uint32_t)suf) +
+           orc_varint_len((uint32_t)e->vlen) + suf + e->vlen + 8 + 1 + (e->has_expire ? 8 : 0) +
+           (e->has_create ? 8 : 0);
+}
+/* RowEntry::encoded_size (V0 layout, types.rs:64-83) */
+static size_t v0_row_size(const entry_t *e, size_t prefix) {
+    size_t s = 2 + 2 + (e->klen - prefix) + 8 + 1 + (e->has_expire ? 8 : 0) + (e->has_create ? 8 : 0);
+    if (e->kind != SDB_KIND_TOMBSTONE) s += 4 + e->vlen;
+    return s;
+}
+
+static int blk_would_fit(const blk_t *b, const entry_t *e) {
+    if (blk_empty(b)) return 1; /* empty blocks accept anything (block_v2.rs:151-154, block.rs:117-120) */
+    if (b->version == 2) {      /* block_v2.rs:151-164 */
+        int restart = (b->counter % b->restart_interval) == 0;
+        size_t shared = restart ? 0 : orc_compute_prefix(b->last_key, b->last_klen, e->key, e->klen);
+        size_t sz = v2_row_size(e, shared);
+        return blk_size(b) + sz + (restart ? 2 : 0) <= b->block_size;
+    } else {                    /* block.rs:117-123: the new entry's 2-byte offset is not counted */
+        size_t prefix = orc_compute_prefix(b->first_key, b->first_klen, e->key, e->klen);
+        return blk_size(b) + v0_row_size(e, prefix) <= b->block_size;
+    }
+}
+
+/* SstRowCodecV2::encode (row_codec_v2.rs:127-169) */
+static void v2_encode_row(vbuf *o, const entry_t *e, size_t shared) {
+    vb_varint(o, (uint32_t)shared);
+    vb_varint(o, (uint32_t)(e->klen - shared));
+    vb_varint(o, (uint32_t)e->vlen);
+    vb_put(o, e->key + shared, e->klen - shared);
+    if (e->kind != SDB_KIND_TOMBSTONE) vb_put(o, e->val, e->vlen);
+    uint8_t f = row_flags(e);
+    vb_be(o, e->seq, 8);
+    vb_u8(o, f);
+    if (f & SDB_FLAG_HAS_EXPIRE_TS) vb_be(o, (uint64_t)e->expire_ts, 8);
+    if (f & SDB_FLAG_HAS_CREATE_TS) vb_be(o, (uint64_t)e->create_ts, 8);
+}
+/* SstRowCodecV0::encode (row.rs:159-198) */
+static void v0_encode_row(vbuf *o, const entry_t *e, size_t prefix) {
+    vb_be(o, prefix, 2);
+    vb_be(o, e->klen - prefix, 2);
+    vb_put(o, e->key + prefix, e->klen - prefix);
+    uint8_t f = row_flags(e);
+    vb_be(o, e->seq, 8);
+    vb_u8(o, f);
+    if (f & SDB_FLAG_HAS_EXPIRE_TS) vb_be(o, (uint64_t)e->expire_ts, 8);
+    if (f & SDB_FLAG_HAS_CREATE_TS) vb_be(o, (uint64_t)e->create_ts, 8);
+    if (e->kind != SDB_KIND_TOMBSTONE) {
+        vb_be(o, (uint64_t)e->vlen, 4);
+        vb_put(o, e->val, e->vlen);
+    }
+}
+
+/* Direct row encode for the row-codec KATs: SstRowCodecV2::encode (row_codec_v2.rs:127-169) with
+ * version 2 (`shared` = shared_bytes) or SstRowCodecV0::encode (row.rs:159-198) with version 1
+ * (`shared` = key_prefix_len).  Returns the encoded length (out must hold it), 0 on bad args. */
+size_t orc_encode_row(uint16_t version, uint32_t shared, const uint8_t *suffix, size_t suffix_len,
+                      uint8_t kind, const uint8_t *val, size_t vlen, uint64_t seq, int has_create,
+                      int64_t create_ts, int has_expire, int64_t expire_ts, uint8_t *out, size_t cap) {
+    if (kind > SDB_KIND_TOMBSTONE) return 0;
+    uint8_t *key = (uint8_t *)calloc((size_t)shared + suffix_len + 1, 1);
+    if (suffix_len) memcpy(key + shared, suffix, suffix_len);
+    entry_t e = {key, (size_t)shared + suffix_len, val, kind == SDB_KIND_TOMBSTONE ? 0 : vlen, kind, seq,
+                 has_create, has_expire, create_ts, expire_ts};
+    vbuf o = {0};
+    if (version == 2) v2_encode_row(&o, &e, shared);
+    else v0_encode_row(&o, &e, shared);
+    size_t n = o.len;
+    if (n <= cap) memcpy(out, o.p, n);
+    else n = 0;
+    free(o.p);
+    free(key);
+    return n;
+}
+
+/* BlockBuilder{V1,V2}::add. Returns 1 added, 0 not fitting, <0 status. */
+static int blk_add(blk_t *b, const entry_t *e) {
+    if (e->klen == 0) return -SDB_EMPTY_KEY; /* block_v2.rs:168-170, block.rs:126-128 */
+    if (!blk_would_fit(b, e)) return 0;
+    if (b->version == 2) { /* block_v2.rs:167-224 */
+        size_t shared;
+        if (b->counter % b->restart_interval == 0) {
+            if (b->data.len > 0xFFFF) return -SDB_LIMIT_EXCEEDED; /* assert at block_v2.rs:195-199 */
+            blk_push_off(b, (uint16_t)b->data.len);
+            shared = 0;
+        } else {
+            shared = orc_compute_prefix(b->last_key, b->last_klen, e->key, e->klen);
+        }
+        if ((uint64_t)e->klen > 0xFFFFFFFFull || (uint64_t)e->vlen > 0xFFFFFFFFull) return -SDB_LIMIT_EXCEEDED;
+        v2_encode_row(&b->data, e, shared);
+        b->last_key = e->key;
+        b->last_klen = e->klen;
+        b->counter++;
+    } else { /* block.rs:125-172 */
+        size_t prefix = b->has_first ? orc_compute_prefix(b->first_key, b->first_klen, e->key, e->klen) : 0;
+        size_t suf = e->klen - prefix;
+        /* SstRowEntry::new asserts (row.rs:73-85) */
+        if (prefix > 0xFFFF || suf > 0xFFFF || prefix + suf > 0xFFFF || (uint64_t)e->vlen > 0xFFFFFFFFull)
+            return -SDB_LIMIT_EXCEEDED;
+        blk_push_off(b, (uint16_t)b->data.len); /* `as u16`: truncating cast (block.rs:163) */
+        v0_encode_row(&b->data, e, prefix);
+        if (!b->has_first) {
+            b->first_key = e->key;
+            b->first_klen = e->klen;
+            b->has_first = 1;
+        }
+    }
+    if (e->kind == SDB_KIND_VALUE) b->puts++;
+    else if (e->kind == SDB_KIND_MERGE) b->merges++;
+    else b->deletes++;
+    return 1;
+}
+
+/* Block::encode (format/block.rs:17-26): data ++ u16BE offsets ++ u16BE count. */
+static void blk_encode(const blk_t *b, vbuf *o) {
+    vb_put(o, b->data.p, b->data.len);
+    for (size_t i = 0; i < b->noffs; i++) vb_be(o, b->offs[i], 2);
+    vb_be(o, (uint64_t)(uint16_t)b->noffs, 2);
+}
+
+static void blk_free(blk_t *b) {
+    free(b->data.p);
+    free(b->offs);
+}
+
+sdb_status orc_build_block(const sdb_kv_batch *batch, uint16_t version, uint32_t block_size,
+                           uint16_t restart_interval, uint8_t *out, uint64_t cap, uint64_t *len,
+                           uint8_t *accepted) {
+    if ((version != 1 && version != 2) || (version == 2 && restart_interval == 0)) return SDB_INVALID_ARGUMENT;
+    blk_t b;
+    memset(&b, 0, sizeof b);
+    b.version = version;
+    b.block_size = block_size;
+    b.restart_interval = restart_interval;
+    sdb_status st = SDB_OK;
+    for (uint64_t i = 0; i < batch->n; i++) {
+        entry_t e;
+        if (!get_entry(batch, i, &e)) { st = SDB_INVALID_ARGUMENT; break; }
+        int r = blk_add(&b, &e);
+        if (r < 0) { st = (sdb_status)(-r); break; }
+        if (accepted) accepted[i] = (uint8_t)r;
+    }
+    if (st == SDB_OK) {
+        if (blk_empty(&b)) st = SDB_EMPTY_BLOCK; /* build() on an empty builder */
+        else {
+            vbuf o = {0};
+            blk_encode(&b, &o);
+            *len = o.len;
+            if (o.len > cap) st = SDB_INVALID_ARGUMENT;
+            else memcpy(out, o.p, o.len);
+            free(o.p);
+        }
+    }
+    blk_free(&b);
+    return st;
+}
+
+/* ------------------------------------------------------------------------------------------- */
+/* EncodedSsTableBuilder data section (sst_builder.rs:224-417)                                  */
+/* ------------------------------------------------------------------------------------------- */
+sdb_status orc_encode_sst(const sdb_kv_batch *batch, const sdb_sst_params *params,
+                          const sdb_sst_out *out) {
+    sdb_sst_summary *sm = out->summary;
+    memset(sm, 0, sizeof *sm);
+    sm->first_error_entry = UINT64_MAX;
+    if (params->sst_version != 1 && params->sst_version != 2) return (sdb_status)(sm->status = SDB_INVALID_ARGUMENT);
+    if (params->sst_version == 2 && params->restart_interval == 0) return (sdb_status)(sm->status = SDB_INVALID_ARGUMENT);
+    uint64_t n = batch->n;
+    blk_t b;
+    memset(&b, 0, sizeof b);
+    b.version = params->sst_version;
+    b.block_size = params->block_size;
+    b.restart_interval = params->restart_interval;
+    vbuf enc = {0};
+    uint64_t nblocks = 0, cur_len = 0, cur_first = 0;
+    int64_t cur_index_len = 0;
+    sdb_status st = SDB_OK;
+    uint64_t err_entry = UINT64_MAX;
+    const uint8_t *prev_key = NULL;
+    size_t prev_klen = 0;
+    int has_prev = 0;
+
+#define FINISH_BLOCK()                                                                             \
+    do {                                                                                           \
+        if (nblocks >= out->block_cap) { st = SDB_INVALID_ARGUMENT; goto done; }                    \
+        enc.len = 0;                                                                               \
+        blk_encode(&b, &enc);                                                                      \
+        uint32_t crc = orc_crc32(enc.p, enc.len); /* compress_and_transform, format/sst.rs:541 */   \
+        vb_be(&enc, crc, 4);                                                                       \
+        if (cur_len + enc.len > out->data_cap) { st = SDB_INVALID_ARGUMENT; goto done; }           \
+        memcpy(out->data + cur_len, enc.p, enc.len);                                               \
+        out->block_off[nblocks] = cur_len;                                                         \
+        out->block_first_entry[nblocks] = (uint32_t)cur_first;                                     \
+        out->index_key_len[nblocks] = (uint32_t)cur_index_len;                                     \
+        out->block_stats[3 * nblocks + 0] = b.puts;                                                \
+        out->block_stats[3 * nblocks + 1] = b.deletes;                                             \
+        out->block_stats[3 * nblocks + 2] = b.merges;                                              \
+        sm->num_puts += b.puts; sm->num_deletes += b.deletes; sm->num_merges += b.merges;          \
+        {                                                                                          \
+            uint32_t ne_ = (uint32_t)(b.version == 2 ? b.counter : b.noffs);                       \
+            if (ne_ > sm->max_block_entries) sm->max_block_entries = ne_;                          \
+        }                                                                                          \
+        cur_len += enc.len;                                                                        \
+        nblocks++;                                                                                 \
+        blk_reset(&b);                                                                             \
+    } while (0)
+
+    for (uint64_t i = 0; i < n; i++) {
+        entry_t e;
+        if (!get_entry(batch, i, &e)) { st = SDB_INVALID_ARGUMENT; err_entry = i; goto done; }
+        sm->raw_key_size += e.klen;
+        sm->raw_val_size += e.vlen;
+        /* compute_index_key runs on every entry (sst_builder.rs:228) and panics on an empty or
+         * non-sorted-prefix key (utils.rs:210-216). */
+        int64_t ik = orc_index_key_len(prev_key, prev_klen, has_prev, e.key, e.klen);
+        if (ik < 0) { st = e.klen == 0 ? SDB_EMPTY_KEY : SDB_INVALID_ARGUMENT; err_entry = i; goto done; }
+        if (!blk_would_fit(&b, &e)) {
+            FINISH_BLOCK();
+            cur_index_len = ik;
+            cur_first = i;
+        } else if (i == 0) {
+            cur_index_len = ik;
+            cur_first = 0;
+        }
+        int r = blk_add(&b, &e);
+        if (r < 0) { st = (sdb_status)(-r); err_entry = i; goto done; }
+        prev_key = e.key;
+        prev_klen = e.klen;
+        has_prev = 1;
+    }
+    if (!blk_empty(&b)) FINISH_BLOCK(); /* build(): finish_block (sst_builder.rs:371) */
+    out->block_off[nblocks] = cur_len;
+    out->block_first_entry[nblocks] = (uint32_t)n;
+    sm->data_len = cur_len;
+    sm->num_blocks = nblocks;
+    sm->num_entries = n;
+
+    /* Filters (sst_builder.rs:388-403): one bloom per SST when num_rows >= min_filter_keys. */
+    if (params->bloom_bits_per_key > 0 && n >= params->min_filter_keys) {
+        uint64_t fb = orc_filter_size_bytes(n, params->bloom_bits_per_key);
+        if (fb > out->bloom_cap) { st = SDB_INVALID_ARGUMENT; goto done; }
+        orc_bloom_build(batch->key_bytes, batch->key_off, n, params->bloom_bits_per_key, out->bloom, fb);
+        sm->bloom_len = fb;
+        sm->filter_built = 1;
+        sm->num_probes = orc_optimal_num_probes(params->bloom_bits_per_key);
+    }
+done:
+#undef FINISH_BLOCK
+    blk_free(&b);
+    free(enc.p);
+    sm->status = st;
+    sm->first_error_entry = err_entry;
+    return st;
+}
+
+/* ------------------------------------------------------------------------------------------- */
+/* Decode: validate_checksum -> Block::decode -> ascending DataBlockIterator                    */
+/* ------------------------------------------------------------------------------------------- */
+typedef struct {
+    const uint8_t *blocks;
+    const sdb_decoded_out *out;
+    uint64_t n, key_bytes;
+    int overflow;
+} dec_ctx;
+
+static int emit_entry(dec_ctx *c, const uint8_t *key_a, size_t na, const uint8_t *key_b, size_t nb,
+                      uint64_t val_pos, uint32_t vlen, uint64_t seq, uint8_t flags, int64_t cts,
+                      int64_t ets) {
+    const sdb_decoded_out *o = c->out;
+    if (c->n >= o->cap_entries || c->key_bytes + na + nb > o->key_arena_cap) { c->overflow = 1; return 0; }
+    memcpy(o->key_arena + c->key_bytes, key_a, na);
+    memcpy(o->key_arena + c->key_bytes + na, key_b, nb);
+    o->key_off[c->n] = c->key_bytes;
+    c->key_bytes += na + nb;
+    o->key_off[c->n + 1] = c->key_bytes;
+    o->val_off[c->n] = vlen ? val_pos : 0;
+    o->val_len[c->n] = vlen;
+    o->seq[c->n] = seq;
+    o->flags[c->n] = flags;
+    o->create_ts[c->n] = (flags & SDB_FLAG_HAS_CREATE_TS) ? cts : 0;
+    o->expire_ts[c->n] = (flags & SDB_FLAG_HAS_EXPIRE_TS) ? ets : 0;
+    c->n++;
+    return 1;
+}
+
+static int flags_ok(uint8_t f) { /* decode_flags (row_codec_v2.rs:234-249, row.rs:251-266) */
+    if (f & ~0x0Fu) return 0;
+    if ((f & SDB_FLAG_TOMBSTONE) && (f & SDB_FLAG_MERGE_OPERAND)) return 0;
+    return 1;
+}
+
+/* Decode one block's payload (after CRC strip).  Returns SDB_OK or an error; on error no entries of
+ * this block are kept (caller rewinds). */
+static sdb_status decode_one(dec_ctx *c, uint64_t base, size_t blen, uint16_t version) {
+    const uint8_t *blk = c->blocks + base;
+    if (blen < 2) return SDB_CORRUPT_BLOCK;
+    size_t count = (size_t)rd_be(blk + blen - 2, 2);
+    if (2 + 2 * count > blen) return SDB_CORRUPT_BLOCK;
+    size_t data_end = blen - 2 - 2 * count;
+    const uint8_t *offs = blk + data_end;
+    const uint8_t *d = blk;
+    if (version == 2) {
+        /* BlockIteratorV2 ascending (block_iterator_v2.rs:33-57, 95-113, 235-267) */
+        uint8_t *cur = NULL;
+        size_t curlen = 0, pos = 0;
+        if (count > 0) { /* decode_first_key_at_restart(0): asserts shared == 0 */
+            size_t p = (size_t)rd_be(offs, 2);
+            uint32_t sh, un, vl;
+            if (!rd_varint(d, data_end, &p, &sh) || !rd_varint(d, data_end, &p, &un) ||
+                !rd_varint(d, data_end, &p, &vl) || sh != 0 || p + un > data_end)
+                return SDB_CORRUPT_BLOCK;
+            cur = (uint8_t *)malloc(un ? un : 1);
+            memcpy(cur, d + p, un);
+            curlen = un;
+        }
+        sdb_status st = SDB_OK;
+        while (pos < data_end) {
+            uint32_t sh, un, vl;
+            if (!rd_varint(d, data_end, &pos, &sh) || !rd_varint(d, data_end, &pos, &un) ||
+                !rd_varint(d, data_end, &pos, &vl)) { st = SDB_CORRUPT_BLOCK; break; }
+            if (pos + (size_t)un + (size_t)vl + 9 > data_end || sh > curlen) { st = SDB_CORRUPT_BLOCK; break; }
+            size_t suf = pos;
+            pos += un;
+            uint64_t vpos = base + pos;
+            pos += vl;
+            uint64_t seq = rd_be(d + pos, 8);
+            pos += 8;
+            uint8_t f = d[pos++];
+            if (!flags_ok(f)) { st = SDB_INVALID_ROW_FLAGS; break; }
+            int64_t ets = 0, cts = 0;
+            size_t need = ((f & SDB_FLAG_HAS_EXPIRE_TS) ? 8 : 0) + ((f & SDB_FLAG_HAS_CREATE_TS) ? 8 : 0);
+            if (pos + need > data_end) { st = SDB_CORRUPT_BLOCK; break; }
+            if (f & SDB_FLAG_HAS_EXPIRE_TS) { ets = (int64_t)rd_be(d + pos, 8); pos += 8; }
+            if (f & SDB_FLAG_HAS_CREATE_TS) { cts = (int64_t)rd_be(d + pos, 8); pos += 8; }
+            uint32_t out_vlen = (f & SDB_FLAG_TOMBSTONE) ? 0 : vl;
+            if (!emit_entry(c, cur, sh, d + suf, un, vpos, out_vlen, seq, f, cts, ets)) { st = SDB_INVALID_ARGUMENT; break; }
+            /* current_key = restored key (block_iterator_v2.rs:246) */
+            uint8_t *nk = (uint8_t *)malloc(sh + un ? sh + un : 1);
+            memcpy(nk, cur, sh);
+            memcpy(nk + sh, d + suf, un);
+            free(cur);
+            cur = nk;
+            curlen = (size_t)sh + un;
+        }
+        free(cur);
+        return st;
+    }
+    /* V1: BlockIterator (block_iterator.rs:192-240): entries addressed by the offsets array. */
+    if (count == 0) return SDB_OK;
+    if (data_end < 4) return SDB_CORRUPT_BLOCK;
+    size_t ov = (size_t)rd_be(d, 2), fk = (size_t)rd_be(d + 2, 2);
+    if (ov != 0 || 4 + fk > data_end) return SDB_CORRUPT_BLOCK; /* decode_first_key assert */
+    const uint8_t *first = d + 4;
+    for (size_t i = 0; i < count; i++) {
+        size_t p = (size_t)rd_be(offs + 2 * i, 2);
+        if (p + 4 > data_end) return SDB_CORRUPT_BLOCK;
+        size_t pre = (size_t)rd_be(d + p, 2), sl = (size_t)rd_be(d + p + 2, 2);
+        p += 4;
+        if (p + sl + 9 > data_end) return SDB_CORRUPT_BLOCK;
+        size_t suf = p;
+        p += sl;
+        uint64_t seq = rd_be(d + p, 8);
+        p += 8;
+        uint8_t f = d[p++];
+        if (!flags_ok(f)) return SDB_INVALID_ROW_FLAGS;
+        int64_t ets = 0, cts = 0;
+        size_t need = ((f & SDB_FLAG_HAS_EXPIRE_TS) ? 8 : 0) + ((f & SDB_FLAG_HAS_CREATE_TS) ? 8 : 0);
+        if (p + need > data_end) return SDB_CORRUPT_BLOCK;
+        if (f & SDB_FLAG_HAS_EXPIRE_TS) { ets = (int64_t)rd_be(d + p, 8); p += 8; }
+        if (f & SDB_FLAG_HAS_CREATE_TS) { cts = (int64_t)rd_be(d + p, 8); p += 8; }
+        uint32_t vlen = 0;
+        uint64_t vpos = 0;
+        uint8_t of = f;
+        if (f & SDB_FLAG_TOMBSTONE) {
+            of = (uint8_t)(f & ~SDB_FLAG_HAS_EXPIRE_TS); /* V0 decode drops expire_ts (row.rs:223-231) */
+        } else {
+            if (p + 4 > data_end) return SDB_CORRUPT_BLOCK;
+            vlen = (uint32_t)rd_be(d + p, 4);
+            p += 4;
+            if (p + vlen > data_end) return SDB_CORRUPT_BLOCK;
+            vpos = base + p;
+        }
+        if (pre > fk) return SDB_CORRUPT_BLOCK; /* restore_full_key slices first_key[..prefix] */
+        if (!emit_entry(c, first, pre, d + suf, sl, vpos, vlen, seq, of, cts, ets)) return SDB_INVALID_ARGUMENT;
+    }
+    return SDB_OK;
+}
+
+sdb_status orc_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                             uint16_t sst_version, const sdb_decoded_out *out) {
+    sdb_decode_summary *sm = out->summary;
+    memset(sm, 0, sizeof *sm);
+    if (sst_version != 1 && sst_version != 2) { sm->status = SDB_INVALID_VERSION; return SDB_INVALID_VERSION; }
+    dec_ctx c = {blocks, out, 0, 0, 0};
+    sdb_status first_err = SDB_OK;
+    out->key_off[0] = 0;
+    for (uint64_t k = 0; k < nblocks; k++) {
+        out->block_entry_start[k] = c.n;
+        uint64_t s = block_off[k], e = block_off[k + 1];
+        size_t len = (size_t)(e - s);
+        sdb_status st;
+        uint64_t n0 = c.n, kb0 = c.key_bytes;
+        if (len < 4) st = SDB_CORRUPT_BLOCK;
+        else {
+            uint32_t stored = (uint32_t)rd_be(blocks + e - 4, 4);
+            if (orc_crc32(blocks + s, len - 4) != stored) st = SDB_CHECKSUM_MISMATCH; /* format/sst.rs:1029-1038 */
+            else st = decode_one(&c, s, len - 4, sst_version);
+        }
+        if (st != SDB_OK) {
+            c.n = n0;
+            c.key_bytes = kb0;
+            out->key_off[c.n] = c.key_bytes;
+            if (sm->num_bad_blocks < out->bad_cap) out->bad_block[sm->num_bad_blocks] = (uint32_t)k;
+            sm->num_bad_blocks++;
+            if (first_err == SDB_OK) first_err = st;
+        }
+    }
+    out->block_entry_start[nblocks] = c.n;
+    sm->num_entries = c.n;
+    sm->key_bytes = c.key_bytes;
+    sm->status = first_err;
+    return first_err;
+}
