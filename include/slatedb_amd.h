@@ -258,6 +258,16 @@ sdb_status sdb_decoder_decode_host(sdb_decoder *dec, const uint8_t *blocks,
                                    const uint64_t *block_off, uint64_t nblocks,
                                    uint16_t sst_version, sdb_decode_host_result *result);
 
+/* ---------------------------------------------------------------------------------------------
+ * Diagnostics (bench / profiling only)
+ * ------------------------------------------------------------------------------------------- */
+/* Stage timing of sdb_encode_sst: when enabled, hipEvents are recorded around each kernel stage
+ * (bloom, prep, next, chunk, resolve, emit, emit_slow).  sdb_diag_stage_times synchronises the
+ * recorded events, writes the summed milliseconds per stage into ms[0..max_stages), the number of
+ * encodes measured into *launches, clears the record, and returns the number of stages. */
+void sdb_diag_enable_stage_timing(int on);
+int sdb_diag_stage_times(double *ms, int max_stages, uint64_t *launches);
+
 /* Device query: number of visible HIP devices (0 on a machine without a GPU). */
 int sdb_device_count(void);
 /* Human-readable name of a status code. */

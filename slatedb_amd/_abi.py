@@ -138,9 +138,14 @@ SIGNATURES = {
     "sdb_decoder_destroy": (None, [C.c_void_p]),
     "sdb_decoder_decode_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                           C.c_uint16, C.POINTER(DecodeHostResult)]),
+    "sdb_diag_enable_stage_timing": (None, [C.c_int]),
+    "sdb_diag_stage_times": (C.c_int, [C.POINTER(C.c_double), C.c_int, u64p]),
     "sdb_device_count": (C.c_int, []),
     "sdb_status_name": (C.c_char_p, [C.c_int]),
 }
+
+
+STAGES = ["bloom", "prep", "next", "chunk", "resolve", "emit", "emit_slow"]
 
 
 def bind(lib):

@@ -1,0 +1,684 @@
+// sdb_api.cpp — the C ABI (include/slatedb_amd.h): argument checks, workspace carving, launches,
+// and the host-buffer runtime (device arena + pinned staging + stream per handle).
+//
+// Host side of the drop-in for slatedb's EncodedSsTableBuilder / SsTableFormat::read_blocks
+// (slatedb/src/sst_builder.rs:224-417, format/sst.rs:938-1038).  No CPU fallback: without a HIP
+// device every compute entry point returns SDB_DEVICE_ERROR.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/slatedb_amd.h"
+#include "sdb_decode.h"
+#include "sdb_encode.h"
+
+using namespace sdb;
+
+namespace {
+
+inline hipStream_t S(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+uint16_t num_probes_for(uint32_t bpk) { return (uint16_t)((float)bpk * 0.69f); }  // filter.rs:235-239
+
+uint64_t filter_bytes_for(uint64_t n, uint32_t bpk) {  // filter.rs:65-69 (u32 arithmetic)
+    uint32_t bits = (uint32_t)n * bpk;
+    return bits / 8u + (bits % 8u != 0);
+}
+
+bool device_ok() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return false;
+    return n > 0;
+}
+
+sdb_status check_params(const sdb_sst_params *p) {
+    if (!p) return SDB_INVALID_ARGUMENT;
+    if (p->sst_version != 1 && p->sst_version != 2) return SDB_INVALID_ARGUMENT;
+    if (p->block_size == 0) return SDB_INVALID_ARGUMENT;
+    if (p->sst_version == 2 && p->restart_interval == 0) return SDB_INVALID_ARGUMENT;
+    return SDB_OK;
+}
+
+template <typename T>
+T *carve(void *base, uint64_t off) {
+    return reinterpret_cast<T *>(reinterpret_cast<uint8_t *>(base) + off);
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t sdb_abi_version(void) { return SDB_ABI_VERSION; }
+
+int sdb_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char *sdb_status_name(int s) {
+    switch (s) {
+        case SDB_OK: return "OK";
+        case SDB_EMPTY_KEY: return "EMPTY_KEY";
+        case SDB_EMPTY_BLOCK: return "EMPTY_BLOCK";
+        case SDB_CHECKSUM_MISMATCH: return "CHECKSUM_MISMATCH";
+        case SDB_INVALID_ROW_FLAGS: return "INVALID_ROW_FLAGS";
+        case SDB_INVALID_VERSION: return "INVALID_VERSION";
+        case SDB_LIMIT_EXCEEDED: return "LIMIT_EXCEEDED";
+        case SDB_UNSUPPORTED: return "UNSUPPORTED";
+        case SDB_INVALID_ARGUMENT: return "INVALID_ARGUMENT";
+        case SDB_CORRUPT_BLOCK: return "CORRUPT_BLOCK";
+        case SDB_DEVICE_ERROR: return "DEVICE_ERROR";
+        default: return "UNKNOWN";
+    }
+}
+
+uint64_t sdb_bloom_filter_bytes(uint64_t num_keys, uint32_t bits_per_key) {
+    return filter_bytes_for(num_keys, bits_per_key);
+}
+uint32_t sdb_bloom_num_probes(uint32_t bits_per_key) { return num_probes_for(bits_per_key); }
+
+sdb_status sdb_encode_bounds(uint64_t n, uint64_t total_key_bytes, uint64_t total_val_bytes,
+                             const sdb_sst_params *params, uint64_t *data_cap, uint64_t *block_cap,
+                             uint64_t *bloom_cap) {
+    sdb_status st = check_params(params);
+    if (st) return st;
+    // every row <= 15 B of varints/headers + key + value + 25 B trailer; each entry may be its own
+    // block (+2 offset +2 count +4 crc).  V0 rows: 4 + key + 9 + 16 + 4 + value, +2 offset.
+    if (data_cap) *data_cap = total_key_bytes + total_val_bytes + 64 * n + 64;
+    if (block_cap) *block_cap = n + 1;
+    if (bloom_cap)
+        *bloom_cap = params->bloom_bits_per_key ? ((filter_bytes_for(n, params->bloom_bits_per_key) + 3) & ~3ull) + 16
+                                                : 16;
+    return SDB_OK;
+}
+
+uint64_t sdb_encode_workspace_bytes(uint64_t n, const sdb_sst_params *params) {
+    (void)params;
+    return encode_workspace_layout(n).total;
+}
+
+sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const sdb_sst_out *out,
+                          void *workspace, uint64_t workspace_bytes, void *stream) {
+    if (!b || !out || !out->summary) return SDB_INVALID_ARGUMENT;
+    sdb_status st = check_params(p);
+    if (st) return st;
+    if (!device_ok()) return SDB_DEVICE_ERROR;
+    const uint64_t n = b->n;
+    if (n >= (1ull << 31)) return SDB_LIMIT_EXCEEDED;
+    if (n && (!b->key_bytes || !b->key_off || !b->val_off)) return SDB_INVALID_ARGUMENT;
+    EncodeWorkspace wl = encode_workspace_layout(n);
+    if (!workspace || workspace_bytes < wl.total) return SDB_INVALID_ARGUMENT;
+    const bool want_filter = p->bloom_bits_per_key > 0 && n >= p->min_filter_keys;
+    const uint64_t fb = want_filter ? filter_bytes_for(n, p->bloom_bits_per_key) : 0;
+    if (want_filter && fb && (!out->bloom || out->bloom_cap < fb)) return SDB_INVALID_ARGUMENT;
+    if (n && (!out->data || !out->block_off || !out->block_first_entry || !out->index_key_len ||
+              !out->block_stats))
+        return SDB_INVALID_ARGUMENT;
+
+    EncodeArgs a{};
+    a.key_bytes = b->key_bytes;
+    a.key_off = b->key_off;
+    a.val_bytes = b->val_bytes;
+    a.val_off = b->val_off;
+    a.kind = b->kind;
+    a.seq = b->seq;
+    a.create_ts = b->create_ts;
+    a.expire_ts = b->expire_ts;
+    a.ts_mask = b->ts_mask;
+    a.n = n;
+    a.block_size = p->block_size;
+    a.restart_interval = p->sst_version == 2 ? p->restart_interval : 1;
+    a.version = p->sst_version;
+    a.nchunks = (uint32_t)((n + kChunk - 1) / kChunk);
+    a.lcp = carve<uint32_t>(workspace, wl.lcp);
+    a.s_nr = carve<uint32_t>(workspace, wl.s_nr);
+    a.s_r = carve<uint32_t>(workspace, wl.s_r);
+    a.next = carve<uint32_t>(workspace, wl.next);
+    a.bbytes = carve<uint32_t>(workspace, wl.bbytes);
+    a.tab_exit = carve<uint32_t>(workspace, wl.tab_exit);
+    a.tab_cnt = carve<uint32_t>(workspace, wl.tab_cnt);
+    a.tab_bytes = carve<uint64_t>(workspace, wl.tab_bytes);
+    a.anchor_e = carve<uint32_t>(workspace, wl.anchor_e);
+    a.anchor_blk = carve<uint32_t>(workspace, wl.anchor_blk);
+    a.anchor_byte = carve<uint64_t>(workspace, wl.anchor_byte);
+    a.err = carve<unsigned long long>(workspace, wl.err);
+    a.wmax = carve<uint32_t>(workspace, wl.wmax);
+    a.slow_count = carve<uint32_t>(workspace, wl.slow_count);
+    a.slow_list = carve<uint32_t>(workspace, wl.slow_list);
+    a.out_data = out->data;
+    a.out_block_off = out->block_off;
+    a.out_block_first = out->block_first_entry;
+    a.out_index_key_len = out->index_key_len;
+    a.out_block_stats = out->block_stats;
+    a.data_cap = out->data_cap;
+    a.block_cap = out->block_cap;
+    a.summary = out->summary;
+    a.bloom_len = fb;
+    a.num_probes = want_filter ? num_probes_for(p->bloom_bits_per_key) : 0;
+    a.filter_built = want_filter ? 1 : 0;
+    hipStream_t s = S(stream);
+    if (want_filter) {
+        stage_mark(s, kStBloom, true);
+        if (launch_bloom_build(b->key_bytes, b->key_off, n, a.num_probes, out->bloom, fb, s) != hipSuccess)
+            return SDB_DEVICE_ERROR;
+        stage_mark(s, kStBloom, false);
+    }
+    if (launch_encode(a, s) != hipSuccess) return SDB_DEVICE_ERROR;
+    return SDB_OK;
+}
+
+sdb_status sdb_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
+                           uint32_t bits_per_key, uint8_t *bitmap, uint64_t bitmap_bytes, void *stream) {
+    if (!device_ok()) return SDB_DEVICE_ERROR;
+    uint64_t fb = filter_bytes_for(n, bits_per_key);
+    if (bitmap_bytes < fb || (fb && !bitmap) || (n && (!key_bytes || !key_off))) return SDB_INVALID_ARGUMENT;
+    if (launch_bloom_build(key_bytes, key_off, n, num_probes_for(bits_per_key), bitmap, fb, S(stream)) != hipSuccess)
+        return SDB_DEVICE_ERROR;
+    return SDB_OK;
+}
+
+sdb_status sdb_bloom_might_contain(const uint8_t *bitmap, uint64_t bitmap_bytes, uint32_t num_probes,
+                                   const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
+                                   uint8_t *result, void *stream) {
+    if (!device_ok()) return SDB_DEVICE_ERROR;
+    if (n && (!key_bytes || !key_off || !result)) return SDB_INVALID_ARGUMENT;
+    if (launch_bloom_query(bitmap, bitmap_bytes, num_probes, key_bytes, key_off, n, result, S(stream)) != hipSuccess)
+        return SDB_DEVICE_ERROR;
+    return SDB_OK;
+}
+
+uint64_t sdb_decode_workspace_bytes(uint64_t nblocks) { return decode_workspace_layout(nblocks).total; }
+
+sdb_status sdb_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                             uint16_t sst_version, const sdb_decoded_out *out, void *workspace,
+                             uint64_t workspace_bytes, void *stream) {
+    if (!out || !out->summary || !out->block_entry_start) return SDB_INVALID_ARGUMENT;
+    if (sst_version != 1 && sst_version != 2) return SDB_INVALID_VERSION;  // block_iterator.rs:60-77
+    if (!device_ok()) return SDB_DEVICE_ERROR;
+    DecodeWorkspace wl = decode_workspace_layout(nblocks);
+    if (!workspace || workspace_bytes < wl.total) return SDB_INVALID_ARGUMENT;
+    DecodeArgs a{};
+    a.blocks = blocks;
+    a.block_off = block_off;
+    a.nblocks = nblocks;
+    a.version = sst_version;
+    a.out = *out;
+    a.cnt = carve<uint64_t>(workspace, wl.cnt);
+    a.kbytes = carve<uint64_t>(workspace, wl.kbytes);
+    a.flag = carve<uint8_t>(workspace, wl.flag);
+    a.ent_start = carve<uint64_t>(workspace, wl.ent_start);
+    a.key_start = carve<uint64_t>(workspace, wl.key_start);
+    a.tile_x = carve<uint64_t>(workspace, wl.tile_x);
+    a.tile_y = carve<uint64_t>(workspace, wl.tile_y);
+    a.err = carve<unsigned long long>(workspace, wl.err);
+    a.nbad = carve<unsigned long long>(workspace, wl.nbad);
+    a.bad_block = out->bad_block;
+    a.bad_cap = out->bad_cap;
+    if (launch_decode(a, S(stream)) != hipSuccess) return SDB_DEVICE_ERROR;
+    return SDB_OK;
+}
+
+}  // extern "C"
+
+// =================================================================================================
+// Stage timing (diagnostics)
+// =================================================================================================
+#include <mutex>
+namespace sdb {
+namespace {
+std::mutex g_diag_mu;
+bool g_diag_on = false;
+struct StageRec {
+    int stage;
+    hipEvent_t a, b;
+};
+std::vector<StageRec> g_recs;
+std::vector<hipEvent_t> g_open(kNumStages, nullptr);
+uint64_t g_launches = 0;
+}  // namespace
+bool stage_timing_on() { return g_diag_on; }
+void stage_mark(hipStream_t st, int stage, bool begin) {
+    if (!g_diag_on) return;
+    std::lock_guard<std::mutex> lk(g_diag_mu);
+    hipEvent_t e;
+    hipEventCreate(&e);
+    hipEventRecord(e, st);
+    if (begin) {
+        g_open[stage] = e;
+        if (stage == kStPrep) g_launches++;
+    } else {
+        g_recs.push_back({stage, g_open[stage], e});
+        g_open[stage] = nullptr;
+    }
+}
+}  // namespace sdb
+
+extern "C" {
+void sdb_diag_enable_stage_timing(int on) {
+    std::lock_guard<std::mutex> lk(g_diag_mu);
+    g_diag_on = on != 0;
+}
+int sdb_diag_stage_times(double *ms, int max_stages, uint64_t *launches) {
+    std::lock_guard<std::mutex> lk(g_diag_mu);
+    std::vector<double> acc(kNumStages, 0.0);
+    for (auto &r : g_recs) {
+        hipEventSynchronize(r.b);
+        float t = 0;
+        hipEventElapsedTime(&t, r.a, r.b);
+        acc[r.stage] += t;
+        hipEventDestroy(r.a);
+        hipEventDestroy(r.b);
+    }
+    g_recs.clear();
+    for (int i = 0; i < max_stages && i < kNumStages; i++) ms[i] = acc[i];
+    if (launches) *launches = g_launches;
+    g_launches = 0;
+    return kNumStages;
+}
+}  // extern "C"
+
+// =================================================================================================
+// Host-buffer runtime
+// =================================================================================================
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    uint64_t cap = 0;
+    hipError_t ensure(uint64_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        uint64_t want = std::max<uint64_t>(bytes + bytes / 4, 4096);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    ~DevBuf() {
+        if (p) hipFree(p);
+    }
+};
+struct PinBuf {
+    void *p = nullptr;
+    uint64_t cap = 0;
+    hipError_t ensure(uint64_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        uint64_t want = std::max<uint64_t>(bytes + bytes / 4, 4096);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    ~PinBuf() {
+        if (p) hipHostFree(p);
+    }
+};
+
+}  // namespace
+
+struct sdb_encoder {
+    int device = 0;
+    sdb_sst_params params{};
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {};
+    // device: input, output, workspace
+    DevBuf d_in, d_out, d_ws;
+    PinBuf h_in, h_out;
+};
+
+namespace {
+
+struct InLayout {  // packed input arrays inside one allocation (256-byte aligned pieces)
+    uint64_t key_bytes, key_off, val_bytes, val_off, kind, seq, cts, ets, mask, total;
+};
+InLayout in_layout(uint64_t n, uint64_t kb, uint64_t vb) {
+    InLayout l{};
+    uint64_t off = 0;
+    auto take = [&](uint64_t bytes) {
+        uint64_t r = off;
+        off += (bytes + 255) & ~255ull;
+        return r;
+    };
+    l.key_bytes = take(kb + 16);
+    l.key_off = take(8 * (n + 1));
+    l.val_bytes = take(vb + 16);
+    l.val_off = take(8 * (n + 1));
+    l.kind = take(n + 1);
+    l.seq = take(8 * (n + 1));
+    l.cts = take(8 * (n + 1));
+    l.ets = take(8 * (n + 1));
+    l.mask = take(n + 1);
+    l.total = off;
+    return l;
+}
+struct OutLayout {
+    uint64_t data, block_off, block_first, index_key_len, block_stats, bloom, summary, total;
+};
+OutLayout out_layout(uint64_t data_cap, uint64_t block_cap, uint64_t bloom_cap) {
+    OutLayout l{};
+    uint64_t off = 0;
+    auto take = [&](uint64_t bytes) {
+        uint64_t r = off;
+        off += (bytes + 255) & ~255ull;
+        return r;
+    };
+    l.data = take(data_cap);
+    l.block_off = take(8 * (block_cap + 1));
+    l.block_first = take(4 * (block_cap + 1));
+    l.index_key_len = take(4 * (block_cap + 1));
+    l.block_stats = take(6 * (block_cap + 1));
+    l.bloom = take(bloom_cap);
+    l.summary = take(sizeof(sdb_sst_summary));
+    l.total = off;
+    return l;
+}
+
+}  // namespace
+
+extern "C" {
+
+sdb_encoder *sdb_encoder_create(int device, const sdb_sst_params *params) {
+    if (check_params(params) || !device_ok()) return nullptr;
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    sdb_encoder *e = new sdb_encoder();
+    e->device = device;
+    e->params = *params;
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete e;
+        return nullptr;
+    }
+    for (auto &x : e->ev) hipEventCreate(&x);
+    return e;
+}
+
+void sdb_encoder_destroy(sdb_encoder *e) {
+    if (!e) return;
+    hipSetDevice(e->device);
+    hipStreamSynchronize(e->stream);
+    for (auto &x : e->ev) hipEventDestroy(x);
+    hipStreamDestroy(e->stream);
+    delete e;
+}
+
+sdb_status sdb_encoder_encode_host(sdb_encoder *e, const sdb_kv_batch *hb, sdb_sst_host_result *r) {
+    if (!e || !hb || !r) return SDB_INVALID_ARGUMENT;
+    hipSetDevice(e->device);
+    const uint64_t n = hb->n;
+    const uint64_t k0 = n ? hb->key_off[0] : 0, kb = n ? hb->key_off[n] - k0 : 0;
+    const uint64_t v0 = n ? hb->val_off[0] : 0, vb = n ? hb->val_off[n] - v0 : 0;
+    uint64_t data_cap, block_cap, bloom_cap;
+    sdb_encode_bounds(n, kb, vb, &e->params, &data_cap, &block_cap, &bloom_cap);
+    if (data_cap >= (1ull << 32)) return SDB_LIMIT_EXCEEDED;  // u32 per-block/chunk byte counters
+    InLayout il = in_layout(n, kb, vb);
+    OutLayout ol = out_layout(data_cap, block_cap, bloom_cap);
+    uint64_t wsb = sdb_encode_workspace_bytes(n, &e->params);
+    if (e->h_in.ensure(il.total) || e->d_in.ensure(il.total) || e->h_out.ensure(ol.total) ||
+        e->d_out.ensure(ol.total) || e->d_ws.ensure(wsb))
+        return SDB_DEVICE_ERROR;
+    // marshal the caller's batch into pinned staging (offsets rebased to 0)
+    uint8_t *hi = (uint8_t *)e->h_in.p;
+    if (n) {
+        memcpy(hi + il.key_bytes, hb->key_bytes + k0, kb);
+        memcpy(hi + il.val_bytes, hb->val_bytes ? hb->val_bytes + v0 : hi + il.val_bytes, hb->val_bytes ? vb : 0);
+        uint64_t *ko = (uint64_t *)(hi + il.key_off), *vo = (uint64_t *)(hi + il.val_off);
+        for (uint64_t i = 0; i <= n; i++) {
+            ko[i] = hb->key_off[i] - k0;
+            vo[i] = hb->val_off[i] - v0;
+        }
+        if (hb->kind) memcpy(hi + il.kind, hb->kind, n);
+        if (hb->seq) memcpy(hi + il.seq, hb->seq, 8 * n);
+        if (hb->create_ts) memcpy(hi + il.cts, hb->create_ts, 8 * n);
+        if (hb->expire_ts) memcpy(hi + il.ets, hb->expire_ts, 8 * n);
+        if (hb->ts_mask) memcpy(hi + il.mask, hb->ts_mask, n);
+    }
+    uint8_t *di = (uint8_t *)e->d_in.p, *dout = (uint8_t *)e->d_out.p;
+    hipEventRecord(e->ev[0], e->stream);
+    hipMemcpyAsync(di, hi, il.total, hipMemcpyHostToDevice, e->stream);
+    hipEventRecord(e->ev[1], e->stream);
+    sdb_kv_batch db{};
+    db.n = n;
+    db.key_bytes = di + il.key_bytes;
+    db.key_off = (const uint64_t *)(di + il.key_off);
+    db.val_bytes = di + il.val_bytes;
+    db.val_off = (const uint64_t *)(di + il.val_off);
+    db.kind = hb->kind ? di + il.kind : nullptr;
+    db.seq = hb->seq ? (const uint64_t *)(di + il.seq) : nullptr;
+    db.create_ts = hb->create_ts ? (const int64_t *)(di + il.cts) : nullptr;
+    db.expire_ts = hb->expire_ts ? (const int64_t *)(di + il.ets) : nullptr;
+    db.ts_mask = hb->ts_mask ? di + il.mask : nullptr;
+    sdb_sst_out o{};
+    o.data = dout + ol.data;
+    o.data_cap = data_cap;
+    o.block_off = (uint64_t *)(dout + ol.block_off);
+    o.block_first_entry = (uint32_t *)(dout + ol.block_first);
+    o.index_key_len = (uint32_t *)(dout + ol.index_key_len);
+    o.block_stats = (uint16_t *)(dout + ol.block_stats);
+    o.block_cap = block_cap;
+    o.bloom = dout + ol.bloom;
+    o.bloom_cap = bloom_cap;
+    o.summary = (sdb_sst_summary *)(dout + ol.summary);
+    sdb_status st = sdb_encode_sst(&db, &e->params, &o, e->d_ws.p, e->d_ws.cap, e->stream);
+    if (st) return st;
+    hipEventRecord(e->ev[2], e->stream);
+    // D2H: summary first (sizes), then only the used parts
+    uint8_t *ho = (uint8_t *)e->h_out.p;
+    hipMemcpyAsync(ho + ol.summary, dout + ol.summary, sizeof(sdb_sst_summary), hipMemcpyDeviceToHost, e->stream);
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return SDB_DEVICE_ERROR;
+    sdb_sst_summary sm;
+    memcpy(&sm, ho + ol.summary, sizeof sm);
+    if (sm.status == SDB_OK) {
+        uint64_t nb = sm.num_blocks;
+        hipMemcpyAsync(ho + ol.data, dout + ol.data, sm.data_len, hipMemcpyDeviceToHost, e->stream);
+        hipMemcpyAsync(ho + ol.block_off, dout + ol.block_off, 8 * (nb + 1), hipMemcpyDeviceToHost, e->stream);
+        hipMemcpyAsync(ho + ol.block_first, dout + ol.block_first, 4 * (nb + 1), hipMemcpyDeviceToHost, e->stream);
+        hipMemcpyAsync(ho + ol.index_key_len, dout + ol.index_key_len, 4 * nb, hipMemcpyDeviceToHost, e->stream);
+        hipMemcpyAsync(ho + ol.block_stats, dout + ol.block_stats, 6 * nb, hipMemcpyDeviceToHost, e->stream);
+        if (sm.bloom_len)
+            hipMemcpyAsync(ho + ol.bloom, dout + ol.bloom, sm.bloom_len, hipMemcpyDeviceToHost, e->stream);
+    }
+    hipEventRecord(e->ev[3], e->stream);
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return SDB_DEVICE_ERROR;
+    float t01 = 0, t12 = 0, t23 = 0;
+    hipEventElapsedTime(&t01, e->ev[0], e->ev[1]);
+    hipEventElapsedTime(&t12, e->ev[1], e->ev[2]);
+    hipEventElapsedTime(&t23, e->ev[2], e->ev[3]);
+    r->summary = sm;
+    r->data = ho + ol.data;
+    r->block_off = (const uint64_t *)(ho + ol.block_off);
+    r->block_first_entry = (const uint32_t *)(ho + ol.block_first);
+    r->index_key_len = (const uint32_t *)(ho + ol.index_key_len);
+    r->block_stats = (const uint16_t *)(ho + ol.block_stats);
+    r->bloom = ho + ol.bloom;
+    r->h2d_ms = t01;
+    r->kernel_ms = t12;
+    r->d2h_ms = t23;
+    return (sdb_status)sm.status;
+}
+
+}  // extern "C"
+
+// -------------------------------------------------------------------------------------------------
+// EncodedSsTableBuilder mirror
+// -------------------------------------------------------------------------------------------------
+struct sdb_sst_builder {
+    sdb_encoder *enc = nullptr;
+    std::vector<uint8_t> keys, vals, kind, mask;
+    std::vector<uint64_t> koff{0}, voff{0}, seq;
+    std::vector<int64_t> cts, ets;
+};
+
+extern "C" {
+
+sdb_sst_builder *sdb_sst_builder_new(int device, const sdb_sst_params *params) {
+    sdb_encoder *e = sdb_encoder_create(device, params);
+    if (!e) return nullptr;
+    sdb_sst_builder *b = new sdb_sst_builder();
+    b->enc = e;
+    return b;
+}
+
+void sdb_sst_builder_free(sdb_sst_builder *b) {
+    if (!b) return;
+    sdb_encoder_destroy(b->enc);
+    delete b;
+}
+
+sdb_status sdb_sst_builder_add(sdb_sst_builder *b, const uint8_t *key, uint64_t key_len, uint8_t kind,
+                               const uint8_t *val, uint64_t val_len, uint64_t seq, int32_t has_create_ts,
+                               int64_t create_ts, int32_t has_expire_ts, int64_t expire_ts) {
+    if (!b || kind > SDB_KIND_TOMBSTONE) return SDB_INVALID_ARGUMENT;
+    b->keys.insert(b->keys.end(), key, key + key_len);
+    if (kind != SDB_KIND_TOMBSTONE && val_len) b->vals.insert(b->vals.end(), val, val + val_len);
+    b->koff.push_back(b->keys.size());
+    b->voff.push_back(b->vals.size());
+    b->kind.push_back(kind);
+    b->seq.push_back(seq);
+    b->cts.push_back(create_ts);
+    b->ets.push_back(expire_ts);
+    b->mask.push_back((uint8_t)((has_create_ts ? SDB_TS_CREATE : 0) | (has_expire_ts ? SDB_TS_EXPIRE : 0)));
+    return SDB_OK;
+}
+
+sdb_status sdb_sst_builder_build(sdb_sst_builder *b, sdb_sst_host_result *r) {
+    if (!b) return SDB_INVALID_ARGUMENT;
+    sdb_kv_batch hb{};
+    hb.n = b->kind.size();
+    static const uint8_t zero16[16] = {0};
+    hb.key_bytes = b->keys.empty() ? zero16 : b->keys.data();
+    hb.key_off = b->koff.data();
+    hb.val_bytes = b->vals.empty() ? zero16 : b->vals.data();
+    hb.val_off = b->voff.data();
+    hb.kind = b->kind.data();
+    hb.seq = b->seq.data();
+    hb.create_ts = b->cts.data();
+    hb.expire_ts = b->ets.data();
+    hb.ts_mask = b->mask.data();
+    return sdb_encoder_encode_host(b->enc, &hb, r);
+}
+
+}  // extern "C"
+
+// -------------------------------------------------------------------------------------------------
+// Host decode
+// -------------------------------------------------------------------------------------------------
+struct sdb_decoder {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevBuf d_in, d_out, d_ws;
+    PinBuf h_in, h_out;
+};
+
+extern "C" {
+
+sdb_decoder *sdb_decoder_create(int device) {
+    if (!device_ok() || hipSetDevice(device) != hipSuccess) return nullptr;
+    sdb_decoder *d = new sdb_decoder();
+    d->device = device;
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete d;
+        return nullptr;
+    }
+    return d;
+}
+
+void sdb_decoder_destroy(sdb_decoder *d) {
+    if (!d) return;
+    hipSetDevice(d->device);
+    hipStreamSynchronize(d->stream);
+    hipStreamDestroy(d->stream);
+    delete d;
+}
+
+sdb_status sdb_decoder_decode_host(sdb_decoder *d, const uint8_t *blocks, const uint64_t *block_off,
+                                   uint64_t nblocks, uint16_t sst_version, sdb_decode_host_result *r) {
+    if (!d || !r || (nblocks && (!blocks || !block_off))) return SDB_INVALID_ARGUMENT;
+    hipSetDevice(d->device);
+    const uint64_t b0 = nblocks ? block_off[0] : 0;
+    const uint64_t total = nblocks ? block_off[nblocks] - b0 : 0;
+    // capacities: every row >= 12 bytes; restored keys can exceed encoded bytes (shared prefixes),
+    // bounded by rows x (64 KiB V0 keys) — use a generous first guess and retry once if too small.
+    uint64_t cap_e = total / 12 + 16;
+    uint64_t key_cap = total * 4 + 4096;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        uint64_t off = 0;
+        auto take = [&](uint64_t bytes) {
+            uint64_t rr = off;
+            off += (bytes + 255) & ~255ull;
+            return rr;
+        };
+        uint64_t o_bes = take(8 * (nblocks + 1)), o_ka = take(key_cap), o_ko = take(8 * (cap_e + 1));
+        uint64_t o_vo = take(8 * cap_e), o_vl = take(4 * cap_e), o_seq = take(8 * cap_e), o_fl = take(cap_e);
+        uint64_t o_ct = take(8 * cap_e), o_et = take(8 * cap_e), o_bad = take(4 * (nblocks + 1));
+        uint64_t o_sm = take(sizeof(sdb_decode_summary));
+        uint64_t out_total = off;
+        uint64_t in_total = ((total + 16 + 255) & ~255ull) + 8 * (nblocks + 1);
+        uint64_t wsb = sdb_decode_workspace_bytes(nblocks);
+        if (d->h_in.ensure(in_total) || d->d_in.ensure(in_total) || d->h_out.ensure(out_total) ||
+            d->d_out.ensure(out_total) || d->d_ws.ensure(wsb))
+            return SDB_DEVICE_ERROR;
+        uint8_t *hi = (uint8_t *)d->h_in.p;
+        uint64_t o_boff = (total + 16 + 255) & ~255ull;
+        memcpy(hi, blocks + b0, total);
+        uint64_t *bo = (uint64_t *)(hi + o_boff);
+        for (uint64_t k = 0; k <= nblocks; k++) bo[k] = block_off[k] - b0;
+        uint8_t *di = (uint8_t *)d->d_in.p, *dout = (uint8_t *)d->d_out.p;
+        hipMemcpyAsync(di, hi, in_total, hipMemcpyHostToDevice, d->stream);
+        sdb_decoded_out o{};
+        o.block_entry_start = (uint64_t *)(dout + o_bes);
+        o.key_arena = dout + o_ka;
+        o.key_arena_cap = key_cap;
+        o.key_off = (uint64_t *)(dout + o_ko);
+        o.val_off = (uint64_t *)(dout + o_vo);
+        o.val_len = (uint32_t *)(dout + o_vl);
+        o.seq = (uint64_t *)(dout + o_seq);
+        o.flags = dout + o_fl;
+        o.create_ts = (int64_t *)(dout + o_ct);
+        o.expire_ts = (int64_t *)(dout + o_et);
+        o.cap_entries = cap_e;
+        o.bad_block = (uint32_t *)(dout + o_bad);
+        o.bad_cap = nblocks + 1;
+        o.summary = (sdb_decode_summary *)(dout + o_sm);
+        sdb_status st = sdb_decode_blocks(di, (const uint64_t *)(di + o_boff), nblocks, sst_version, &o, d->d_ws.p,
+                                          d->d_ws.cap, d->stream);
+        if (st) return st;
+        uint8_t *ho = (uint8_t *)d->h_out.p;
+        hipMemcpyAsync(ho, dout, out_total, hipMemcpyDeviceToHost, d->stream);
+        if (hipStreamSynchronize(d->stream) != hipSuccess) return SDB_DEVICE_ERROR;
+        sdb_decode_summary sm;
+        memcpy(&sm, ho + o_sm, sizeof sm);
+        if (sm.status == SDB_INVALID_ARGUMENT && attempt == 0 &&
+            (sm.num_entries > cap_e || sm.key_bytes > key_cap)) {
+            cap_e = sm.num_entries + 16;
+            key_cap = sm.key_bytes + 4096;
+            continue;
+        }
+        // value references are positions in the caller's `blocks` (block_off[0] was rebased to 0)
+        uint64_t *vo_h = (uint64_t *)(ho + o_vo);
+        const uint32_t *vl_h = (const uint32_t *)(ho + o_vl);
+        if (b0)
+            for (uint64_t i = 0; i < sm.num_entries && i < cap_e; i++)
+                if (vl_h[i]) vo_h[i] += b0;
+        r->summary = sm;
+        r->block_entry_start = (const uint64_t *)(ho + o_bes);
+        r->key_arena = ho + o_ka;
+        r->key_off = (const uint64_t *)(ho + o_ko);
+        r->val_off = (const uint64_t *)(ho + o_vo);
+        r->val_len = (const uint32_t *)(ho + o_vl);
+        r->seq = (const uint64_t *)(ho + o_seq);
+        r->flags = ho + o_fl;
+        r->create_ts = (const int64_t *)(ho + o_ct);
+        r->expire_ts = (const int64_t *)(ho + o_et);
+        r->bad_block = (const uint32_t *)(ho + o_bad);
+        return (sdb_status)sm.status;
+    }
+    return SDB_INVALID_ARGUMENT;
+}
+
+}  // extern "C"

@@ -1,0 +1,53 @@
+// sdb_decode.h — kernel arguments of the batched block decoder.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/slatedb_amd.h"
+
+namespace sdb {
+
+struct DecodeArgs {
+    const uint8_t *blocks;
+    const uint64_t *block_off;  // nblocks+1
+    uint64_t nblocks;
+    uint32_t version;
+    sdb_decoded_out out;  // device pointers
+    // workspace
+    uint64_t *cnt, *kbytes;            // per block
+    uint8_t *flag;                     // per block: 1 = sequential V2 walk
+    uint64_t *ent_start, *key_start;   // nblocks+1
+    uint64_t *tile_x, *tile_y;         // per 1024-block tile (+1)
+    unsigned long long *err, *nbad;
+    uint32_t *bad_block;
+    uint64_t bad_cap;
+};
+
+struct DecodeWorkspace {
+    uint64_t cnt, kbytes, flag, ent_start, key_start, tile_x, tile_y, err, nbad, total;
+};
+inline DecodeWorkspace decode_workspace_layout(uint64_t nblocks) {
+    DecodeWorkspace w{};
+    uint64_t off = 0;
+    auto take = [&](uint64_t bytes) {
+        uint64_t r = off;
+        off += (bytes + 255) & ~255ull;
+        return r;
+    };
+    uint64_t nt = (nblocks + 1023) / 1024 + 1;
+    w.cnt = take(8 * (nblocks + 1));
+    w.kbytes = take(8 * (nblocks + 1));
+    w.flag = take(nblocks + 1);
+    w.ent_start = take(8 * (nblocks + 1));
+    w.key_start = take(8 * (nblocks + 1));
+    w.tile_x = take(8 * (nt + 1));
+    w.tile_y = take(8 * (nt + 1));
+    w.err = take(8);
+    w.nbad = take(8);
+    w.total = off;
+    return w;
+}
+
+hipError_t launch_decode(DecodeArgs a, hipStream_t st);
+
+}  // namespace sdb

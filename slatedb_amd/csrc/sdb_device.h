@@ -1,0 +1,262 @@
+// sdb_device.h — device-side building blocks shared by the encode / bloom / decode kernels.
+//
+// gfx950 (CDNA4) only: 64-lane waves, byte work on VALU + LDS, no MFMA.  Nothing here is a port:
+// the reference path is Rust on CPU (slatedb/src/format/*.rs, filter.rs).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/slatedb_amd.h"
+
+#define SDB_DEV __device__ __forceinline__
+
+namespace sdb {
+
+constexpr int kWave = 64;
+
+// ------------------------------------------------------------------------------------------------
+// CRC-32/ISO-HDLC (crc32fast 1.5, reflected poly 0xEDB88320), tables built at compile time.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kPoly = 0xEDB88320u;
+
+struct CrcTables {
+    uint32_t t[8][256];
+};
+constexpr CrcTables make_crc_tables() {
+    CrcTables r{};
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kPoly : (c >> 1);
+        r.t[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; i++)
+        for (int s = 1; s < 8; s++) r.t[s][i] = (r.t[s - 1][i] >> 8) ^ r.t[0][r.t[s - 1][i] & 0xFF];
+    return r;
+}
+
+// multmodp / x2nmodp (GF(2) arithmetic mod P in the reflected representation; "x^1" = 1<<30).
+constexpr uint32_t gf_mul_c(uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
+        }
+        m >>= 1;
+        b = (b & 1) ? (b >> 1) ^ kPoly : b >> 1;
+    }
+    return p;
+}
+// x^(8*nbytes) mod P
+constexpr uint32_t x8n_c(uint64_t nbytes) {
+    uint32_t p = 1u << 31;  // x^0
+    uint32_t sq = 1u << 30; // x^1
+    uint64_t e = nbytes * 8;
+    while (e) {
+        if (e & 1) p = gf_mul_c(sq, p);
+        sq = gf_mul_c(sq, sq);
+        e >>= 1;
+    }
+    return p;
+}
+struct CrcShift64 {   // K[l] = x^(8*64*(63-l)): weight of lane l's 64-byte segment in a 4 KiB window
+    uint32_t k[64];
+    uint32_t window;  // x^(8*4096): shift of the running CRC past one full window
+};
+constexpr CrcShift64 make_shift64() {
+    CrcShift64 r{};
+    for (int l = 0; l < 64; l++) r.k[l] = x8n_c(64ull * (63 - l));
+    r.window = x8n_c(4096);
+    return r;
+}
+
+// Per translation unit (no relocatable device code needed).
+static __constant__ CrcTables c_crc = make_crc_tables();
+static __constant__ CrcShift64 c_shift = make_shift64();
+
+// Runtime GF(2) multiply (branch-free, 32 steps).
+SDB_DEV uint32_t gf_mul(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 31; i >= 0; i--) {
+        p ^= b & (0u - ((a >> i) & 1u));
+        b = (b >> 1) ^ (kPoly & (0u - (b & 1u)));
+    }
+    return p;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Byte helpers
+// ------------------------------------------------------------------------------------------------
+SDB_DEV uint32_t varint_len(uint32_t v) {  // utils.rs:638-645
+    return v < (1u << 7) ? 1 : v < (1u << 14) ? 2 : v < (1u << 21) ? 3 : v < (1u << 28) ? 4 : 5;
+}
+SDB_DEV uint64_t bswap64(uint64_t v) { return __builtin_bswap64(v); }
+
+// Load 8 little-endian bytes at an arbitrary address p, of which only the first `need` (1..8) are
+// required.  Reads only aligned 8-byte words that contain at least one required byte, so it never
+// touches a page that holds no requested byte.  Bytes beyond `need` are unspecified.
+SDB_DEV uint64_t load8(const uint8_t *p, uint32_t need) {
+    uintptr_t a = (uintptr_t)p;
+    uint32_t sh = (uint32_t)(a & 7);
+    const uint64_t *w = (const uint64_t *)(a - sh);
+    uint64_t lo = w[0];
+    if (sh == 0) return lo;
+    uint64_t r = lo >> (8 * sh);
+    if (need > 8 - sh) r |= w[1] << (8 * (8 - sh));
+    return r;
+}
+
+// Longest common prefix of two byte strings (compute_prefix, block_v2.rs:52-75).
+SDB_DEV uint32_t lcp_bytes(const uint8_t *a, uint32_t na, const uint8_t *b, uint32_t nb) {
+    uint32_t n = na < nb ? na : nb, off = 0;
+    while (off < n) {
+        uint32_t need = n - off < 8 ? n - off : 8;
+        uint64_t x = load8(a + off, need) ^ load8(b + off, need);
+        if (need < 8) x &= (~0ull) >> (8 * (8 - need));
+        if (x) return off + (uint32_t)(__builtin_ctzll(x) >> 3);
+        off += need;
+    }
+    return n;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Wave primitives (wave64)
+// ------------------------------------------------------------------------------------------------
+SDB_DEV int lane_id() { return __lane_id(); }
+
+template <typename T>
+SDB_DEV T wave_incl_scan(T v) {
+    const int l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        T o = __shfl_up(v, d, 64);
+        if (l >= d) v += o;
+    }
+    return v;
+}
+template <typename T>
+SDB_DEV T wave_sum(T v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+SDB_DEV uint32_t wave_xor(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v ^= __shfl_xor(v, d, 64);
+    return v;
+}
+SDB_DEV uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        uint32_t o = __shfl_xor(v, d, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Error reporting: the reference stops at the first failing entry, so we keep min(entry<<8|code).
+// ------------------------------------------------------------------------------------------------
+SDB_DEV void report_error(unsigned long long *err_word, uint64_t entry, int code) {
+    atomicMin(err_word, (unsigned long long)((entry << 8) | (uint64_t)code));
+}
+
+// ------------------------------------------------------------------------------------------------
+// CRC of a byte range held in LDS, computed by one wave (64 lanes x 64-byte segments per 4 KiB
+// window, right-aligned so every window but the first is full; zero prefix leaves a zero-init CRC
+// unchanged).  The 0xFFFFFFFF init is folded in by inverting the first 4 message bytes.
+// Returns crc32fast::hash(bytes) in every lane.  `tab` = slicing-by-8 tables in LDS.
+// ------------------------------------------------------------------------------------------------
+SDB_DEV uint32_t lds_read_u32_unaligned(const uint8_t *lds, uint32_t off) {
+    const uint32_t *w = (const uint32_t *)(lds + (off & ~3u));
+    uint32_t sh = off & 3;
+    uint32_t lo = w[0];
+    if (!sh) return lo;
+    uint32_t hi = w[1];
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+SDB_DEV uint32_t crc_slice8(uint32_t c, uint32_t lo, uint32_t hi, const uint32_t (*tab)[256]) {
+    lo ^= c;
+    return tab[7][lo & 0xFF] ^ tab[6][(lo >> 8) & 0xFF] ^ tab[5][(lo >> 16) & 0xFF] ^ tab[4][lo >> 24] ^
+           tab[3][hi & 0xFF] ^ tab[2][(hi >> 8) & 0xFF] ^ tab[1][(hi >> 16) & 0xFF] ^ tab[0][hi >> 24];
+}
+
+// Raw (zero-init, no xorout) CRC of msg[0, len) held in LDS, computed by one wave: 64 lanes x
+// 64-byte segments per 4 KiB window, windows right-aligned so only the first is partial (a zero
+// prefix leaves a zero-init CRC unchanged).  fold_init inverts message bytes [0,4), which turns the
+// raw CRC into update(0xFFFFFFFF, msg).  Reads touch [msg - 3, msg + len + 7] at dword granularity;
+// bytes outside [msg, msg + len) are masked.  Result is returned in every lane.
+SDB_DEV uint32_t wave_crc_raw_lds(const uint8_t *msg, uint32_t len, const uint32_t (*tab)[256],
+                                  bool fold_init) {
+    const int l = lane_id();
+    uint32_t nwin = (len + 4095) >> 12;
+    uint32_t first = len - ((nwin - 1) << 12);  // bytes in the (right-aligned) first window
+    uint32_t acc = 0;
+    const uintptr_t base = (uintptr_t)msg;
+    const uint8_t *b4 = (const uint8_t *)(base & ~(uintptr_t)3);
+    const uint32_t bsh = (uint32_t)(base & 3);
+    for (uint32_t w = 0; w < nwin; w++) {
+        int64_t wend = (int64_t)first + ((int64_t)w << 12);
+        int64_t seg0 = wend - 4096 + 64 * l;  // this lane's 64-byte segment start (message coords)
+        uint32_t c = 0;
+        if (seg0 + 64 > 0) {
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                int64_t s = seg0 + 8 * q;  // 8 bytes [s, s+8)
+                uint32_t lo = 0, hi = 0;
+                if (s + 8 > 0) {
+                    int64_t sc = s < 0 ? 0 : s;
+                    uint32_t off = bsh + (uint32_t)sc;
+                    lo = lds_read_u32_unaligned(b4, off);
+                    hi = lds_read_u32_unaligned(b4, off + 4);
+                    uint64_t v = ((uint64_t)hi << 32) | lo;
+                    if (s < 0) v <<= (uint32_t)(-s) * 8;  // zero the bytes before the message
+                    if (fold_init && s < 4) {             // invert message bytes [0, 4)
+                        int64_t from = -s;
+                        uint64_t m = 0xFFFFFFFFull;
+                        if (from >= 0) m <<= (uint32_t)from * 8;
+                        else m >>= (uint32_t)(-from) * 8;
+                        v ^= m;
+                    }
+                    lo = (uint32_t)v;
+                    hi = (uint32_t)(v >> 32);
+                }
+                c = crc_slice8(c, lo, hi, tab);
+            }
+        }
+        uint32_t win = wave_xor(gf_mul(c_shift.k[l], c));
+        acc = (w == 0) ? win : (gf_mul(c_shift.window, acc) ^ win);
+    }
+    return acc;
+}
+
+// crc32fast::hash(msg[0, len)), len >= 4.
+SDB_DEV uint32_t wave_crc32_lds(const uint8_t *msg, uint32_t len, const uint32_t (*tab)[256]) {
+    return wave_crc_raw_lds(msg, len, tab, true) ^ 0xFFFFFFFFu;
+}
+
+// Block-wide exclusive scan of u64 (blockDim.x <= 1024).  s_w: >= 17 u64 of LDS.
+SDB_DEV uint64_t block_excl_scan_u64(uint64_t v, uint64_t *s_w, uint64_t *total) {
+    const uint32_t tid = threadIdx.x, w = tid >> 6, nw = (blockDim.x + 63) >> 6;
+    uint64_t inc = wave_incl_scan(v);
+    if ((tid & 63) == 63 || tid == blockDim.x - 1) s_w[w] = inc;
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t c = 0;
+        for (uint32_t q = 0; q < nw; q++) {
+            uint64_t t = s_w[q];
+            s_w[q] = c;
+            c += t;
+        }
+        s_w[16] = c;
+    }
+    __syncthreads();
+    uint64_t r = s_w[w] + inc - v;
+    *total = s_w[16];
+    __syncthreads();
+    return r;
+}
+
+}  // namespace sdb

@@ -1,0 +1,115 @@
+// sdb_encode.h — kernel arguments and LDS geometry of the SST encoder.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/slatedb_amd.h"
+
+namespace sdb {
+
+constexpr uint32_t kChunk = 2048;            // entries per chunk (K3 / K5)
+constexpr uint32_t kResolveLds = 96 * 1024;  // LDS budget of the resolve tables (u16 exits)
+constexpr uint32_t kCrcLds = 8 * 1024;       // slicing-by-8 tables
+constexpr uint32_t kImgCap = 4096 + 64;      // LDS block image per wave (fast path)
+constexpr uint32_t kStageCap = 4096 + 64;    // LDS value / key staging per wave
+constexpr uint32_t kMaxRows = 128;           // rows per block on the fast path
+constexpr uint32_t kRowInfoBytes = 40;
+constexpr uint32_t kWaveLds = kImgCap + 2 * kStageCap + kMaxRows * kRowInfoBytes;
+constexpr uint32_t kEmitWaves = 4;
+constexpr uint32_t kEmitWork = kEmitWaves * kWaveLds;  // >= 11 levels x kChunk x 2 B of lifting
+
+struct EncodeArgs {
+    // batch (device)
+    const uint8_t *key_bytes;
+    const uint64_t *key_off;
+    const uint8_t *val_bytes;
+    const uint64_t *val_off;
+    const uint8_t *kind;
+    const uint64_t *seq;
+    const int64_t *create_ts;
+    const int64_t *expire_ts;
+    const uint8_t *ts_mask;
+    uint64_t n;
+    // params
+    uint32_t block_size;
+    uint32_t restart_interval;
+    uint32_t version;
+    uint32_t nchunks;
+    // workspace
+    uint32_t *lcp;
+    uint32_t *s_nr;
+    uint32_t *s_r;
+    uint32_t *next;
+    uint32_t *bbytes;
+    uint32_t *tab_exit;
+    uint32_t *tab_cnt;
+    uint64_t *tab_bytes;
+    uint32_t *anchor_e;     // nchunks+1
+    uint32_t *anchor_blk;   // nchunks+1
+    uint64_t *anchor_byte;  // nchunks+1
+    unsigned long long *err;
+    uint32_t *wmax;
+    uint32_t *slow_count;
+    uint32_t *slow_list;
+    // outputs (device)
+    uint8_t *out_data;
+    uint64_t *out_block_off;
+    uint32_t *out_block_first;
+    uint32_t *out_index_key_len;
+    uint16_t *out_block_stats;
+    uint64_t data_cap, block_cap;
+    sdb_sst_summary *summary;
+    uint64_t bloom_len;
+    uint32_t num_probes, filter_built;
+};
+
+// Workspace layout for n entries (all offsets 256-byte aligned).
+struct EncodeWorkspace {
+    uint64_t lcp, s_nr, s_r, next, bbytes, tab_exit, tab_cnt, tab_bytes;
+    uint64_t anchor_e, anchor_blk, anchor_byte, err, wmax, slow_count, slow_list;
+    uint64_t total;
+};
+inline EncodeWorkspace encode_workspace_layout(uint64_t n) {
+    EncodeWorkspace w{};
+    uint64_t off = 0;
+    auto take = [&](uint64_t bytes) {
+        uint64_t r = off;
+        off += (bytes + 255) & ~255ull;
+        return r;
+    };
+    uint64_t nc = (n + kChunk - 1) / kChunk;
+    w.lcp = take(4 * (n + 1));
+    w.s_nr = take(4 * (n + 1));
+    w.s_r = take(4 * (n + 1));
+    w.next = take(4 * (n + 1));
+    w.bbytes = take(4 * (n + 1));
+    w.tab_exit = take(4 * (n + 1));
+    w.tab_cnt = take(4 * (n + 1));
+    w.tab_bytes = take(8 * (n + 1));
+    w.anchor_e = take(4 * (nc + 2));
+    w.anchor_blk = take(4 * (nc + 2));
+    w.anchor_byte = take(8 * (nc + 2));
+    w.err = take(8);
+    w.wmax = take(4);
+    w.slow_count = take(4);
+    w.slow_list = take(4 * (n + 1));
+    w.total = off;
+    return w;
+}
+
+hipError_t launch_encode(EncodeArgs a, hipStream_t st);
+
+// stage timing (diagnostics)
+enum Stage { kStBloom = 0, kStPrep, kStNext, kStChunk, kStResolve, kStEmit, kStEmitSlow, kNumStages };
+void stage_mark(hipStream_t st, int stage, bool begin);
+bool stage_timing_on();
+
+// bloom (sdb_bloom.hip)
+hipError_t launch_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
+                              uint32_t num_probes, uint8_t *bitmap, uint64_t bitmap_bytes,
+                              hipStream_t st);
+hipError_t launch_bloom_query(const uint8_t *bitmap, uint64_t bitmap_bytes, uint32_t num_probes,
+                              const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
+                              uint8_t *result, hipStream_t st);
+
+}  // namespace sdb

@@ -1,0 +1,361 @@
+"""Host-side front-end of libslatedb_amd.so (ctypes over the C ABI in include/slatedb_amd.h).
+
+Mirrors the reference's surface for this path:
+  * SstBuilder            <- EncodedSsTableBuilder add()/build()/next_block() (sst_builder.rs:224-417)
+  * BloomFilterPolicy     <- FilterPolicy "_bf" / BloomFilterBuilder (filter_policy.rs:170-283,
+                             filter.rs:40-90); encode() = Filter::encode (filter.rs:177-180)
+  * read_blocks()         <- SsTableFormat::read_blocks + DataBlockIterator (format/sst.rs:938-999)
+  * encode_sst_device()   <- the batched device entry point used by bench.py
+
+The HIP library is mandatory: a missing .so or a machine without a HIP device raises; nothing
+falls back to a CPU implementation.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi
+from .batch import Batch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libslatedb_amd.so")
+
+_lib = None
+
+
+class SdbError(RuntimeError):
+    def __init__(self, status, what=""):
+        self.status = status
+        super().__init__("%s: %s" % (what or "slatedb_amd", _abi.STATUS_NAMES.get(status, status)))
+
+
+def lib():
+    """Load libslatedb_amd.so (fails loudly if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libslatedb_amd.so not built: run `python __graft_entry__.py build` "
+                              "(hipcc --offload-arch=gfx950)")
+        _lib = _abi.bind(C.CDLL(LIB_PATH))
+    return _lib
+
+
+def device_count():
+    return lib().sdb_device_count()
+
+
+def require_device():
+    if device_count() <= 0:
+        raise SdbError(_abi.SDB_DEVICE_ERROR, "no HIP device visible")
+
+
+def params(block_size=4096, sst_version=2, restart_interval=16, bloom_bits_per_key=10,
+           min_filter_keys=0):
+    return _abi.SstParams(block_size, sst_version, restart_interval, bloom_bits_per_key,
+                          min_filter_keys)
+
+
+def _u8(ptr, n):
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), (n,)) if n else np.zeros(0, np.uint8)
+
+
+def _arr(ptr, ctype, n, dtype):
+    if not n:
+        return np.zeros(0, dtype)
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ctype)), (n,)).view(dtype)
+
+
+class EncodedSst:
+    """Data section + bloom of one SST (host copies)."""
+
+    def __init__(self, res, params_):
+        sm = res.summary
+        self.status = sm.status
+        self.summary = {f: getattr(sm, f) for f, _ in _abi.SstSummary._fields_}
+        nb = sm.num_blocks if sm.status == 0 else 0
+        self.data = _u8(res.data, sm.data_len if sm.status == 0 else 0).copy()
+        self.block_off = _arr(res.block_off, C.c_uint64, nb + 1 if nb else 0, np.uint64).copy()
+        self.block_first_entry = _arr(res.block_first_entry, C.c_uint32, nb + 1 if nb else 0, np.uint32).copy()
+        self.index_key_len = _arr(res.index_key_len, C.c_uint32, nb, np.uint32).copy()
+        self.block_stats = _arr(res.block_stats, C.c_uint16, 3 * nb, np.uint16).reshape(-1, 3).copy()
+        self.bloom = _u8(res.bloom, sm.bloom_len if sm.status == 0 else 0).copy()
+        self.num_probes = sm.num_probes
+        self.filter_built = bool(sm.filter_built)
+        self.timings_ms = {"h2d": res.h2d_ms, "kernel": res.kernel_ms, "d2h": res.d2h_ms}
+        self.sst_version = params_.sst_version
+        self._next = 0
+
+    @property
+    def num_blocks(self):
+        return len(self.index_key_len)
+
+    def block(self, k):
+        """Encoded block k: Block::encode() ++ crc32 BE (EncodedSsTableBlock.encoded_bytes)."""
+        return self.data[int(self.block_off[k]):int(self.block_off[k + 1])].tobytes()
+
+    def next_block(self):
+        """EncodedSsTableBuilder::next_block (sst_builder.rs:274-276)."""
+        if self._next >= self.num_blocks:
+            return None
+        b = self.block(self._next)
+        self._next += 1
+        return b
+
+    def filter_block(self, name="_bf"):
+        """Composite filter block bytes incl. CRC (format/sst.rs:394-421, 525-554)."""
+        import struct
+        import zlib
+        if not self.filter_built:
+            return b""
+        enc = struct.pack(">H", self.num_probes) + self.bloom.tobytes()
+        comp = struct.pack(">HH", 1, len(name)) + name.encode() + struct.pack(">Q", len(enc)) + enc
+        return comp + struct.pack(">I", zlib.crc32(comp))
+
+
+class Encoder:
+    """Host-buffer encoder (device arena + pinned staging + its own stream)."""
+
+    def __init__(self, prm=None, device=0):
+        require_device()
+        self.params = prm or params()
+        self._h = lib().sdb_encoder_create(device, C.byref(self.params))
+        if not self._h:
+            raise SdbError(_abi.SDB_DEVICE_ERROR, "sdb_encoder_create")
+
+    def encode(self, batch):
+        kb = batch.to_ctypes()
+        res = _abi.SstHostResult()
+        st = lib().sdb_encoder_encode_host(self._h, C.byref(kb), C.byref(res))
+        out = EncodedSst(res, self.params)
+        out.status = st
+        return out
+
+    def close(self):
+        if self._h:
+            lib().sdb_encoder_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class SstBuilder:
+    """EncodedSsTableBuilder mirror: add() entries in order, then build() encodes on the GPU."""
+
+    def __init__(self, prm=None, device=0):
+        require_device()
+        self.params = prm or params()
+        self._h = lib().sdb_sst_builder_new(device, C.byref(self.params))
+        if not self._h:
+            raise SdbError(_abi.SDB_DEVICE_ERROR, "sdb_sst_builder_new")
+
+    def add(self, key, value=b"", seq=0, kind=_abi.KIND_VALUE, create_ts=None, expire_ts=None):
+        key = bytes(key)
+        value = bytes(value or b"")
+        st = lib().sdb_sst_builder_add(self._h, key, len(key), kind, value, len(value), seq,
+                                       create_ts is not None, create_ts or 0, expire_ts is not None,
+                                       expire_ts or 0)
+        if st:
+            raise SdbError(st, "add")
+
+    def add_value(self, key, value, create_ts=None, expire_ts=None):
+        """EncodedSsTableBuilder::add_value (sst_builder.rs:257-272): seq 0."""
+        self.add(key, value, 0, _abi.KIND_VALUE, create_ts, expire_ts)
+
+    def build(self):
+        res = _abi.SstHostResult()
+        st = lib().sdb_sst_builder_build(self._h, C.byref(res))
+        out = EncodedSst(res, self.params)
+        out.status = st
+        return out
+
+    def close(self):
+        if self._h:
+            lib().sdb_sst_builder_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class BloomFilterPolicy:
+    """FilterPolicy "_bf" with whole-key filtering (filter_policy.rs:170-283)."""
+
+    NAME = "_bf"
+
+    def __init__(self, bits_per_key=10):
+        self.bits_per_key = bits_per_key
+
+    def name(self):
+        return self.NAME
+
+    def num_probes(self):
+        return lib().sdb_bloom_num_probes(self.bits_per_key)
+
+    def estimate_size(self, num_keys):
+        return lib().sdb_bloom_filter_bytes(num_keys, self.bits_per_key) + 2
+
+    def build_device(self, key_bytes, key_off, n, stream=None):
+        """Bitmap over device-resident keys -> torch uint8 tensor (device)."""
+        import torch
+        fb = lib().sdb_bloom_filter_bytes(n, self.bits_per_key)
+        bm = torch.empty((fb + 3) // 4 * 4 or 4, dtype=torch.uint8, device=key_bytes.device)
+        st = lib().sdb_bloom_build(key_bytes.data_ptr(), key_off.data_ptr(), n, self.bits_per_key,
+                                   bm.data_ptr(), fb, stream)
+        if st:
+            raise SdbError(st, "sdb_bloom_build")
+        return bm[:fb]
+
+    def build(self, batch_or_keys):
+        """Filter::encode bytes: u16 BE num_probes ++ bitmap (filter.rs:177-180)."""
+        import struct
+        import torch
+        require_device()
+        if isinstance(batch_or_keys, Batch):
+            kbytes, koff = batch_or_keys.key_bytes, batch_or_keys.key_off
+        else:
+            keys = [bytes(k) for k in batch_or_keys]
+            koff = np.zeros(len(keys) + 1, np.uint64)
+            koff[1:] = np.cumsum([len(k) for k in keys]) if keys else []
+            kbytes = np.frombuffer(b"".join(keys) or b"\0", np.uint8)
+        n = len(koff) - 1
+        dk = torch.from_numpy(np.ascontiguousarray(kbytes)).cuda() if kbytes.size else torch.zeros(16, dtype=torch.uint8, device="cuda")
+        do = torch.from_numpy(np.ascontiguousarray(koff).view(np.uint8)).cuda()
+        bm = self.build_device(dk, do, n)
+        torch.cuda.synchronize()
+        return struct.pack(">H", self.num_probes()) + bm.cpu().numpy().tobytes()
+
+
+def might_contain(bitmap, num_probes, keys):
+    """Batched BloomFilter::might_contain over host keys; returns a bool array."""
+    import torch
+    require_device()
+    keys = [bytes(k) for k in keys]
+    koff = np.zeros(len(keys) + 1, np.uint64)
+    koff[1:] = np.cumsum([len(k) for k in keys]) if keys else []
+    kb = np.frombuffer(b"".join(keys) or b"\0", np.uint8).copy()
+    dk = torch.from_numpy(kb).cuda()
+    do = torch.from_numpy(koff.view(np.uint8)).cuda()
+    bm = np.ascontiguousarray(bitmap, np.uint8)
+    dbm = torch.from_numpy(np.concatenate([bm, np.zeros(4, np.uint8)])).cuda()
+    res = torch.zeros(max(len(keys), 1), dtype=torch.uint8, device="cuda")
+    st = lib().sdb_bloom_might_contain(dbm.data_ptr(), bm.size, num_probes, dk.data_ptr(), do.data_ptr(),
+                                       len(keys), res.data_ptr(), None)
+    if st:
+        raise SdbError(st, "sdb_bloom_might_contain")
+    torch.cuda.synchronize()
+    return res.cpu().numpy()[:len(keys)].astype(bool)
+
+
+class Decoded:
+    pass
+
+
+class Decoder:
+    def __init__(self, device=0):
+        require_device()
+        self._h = lib().sdb_decoder_create(device)
+        if not self._h:
+            raise SdbError(_abi.SDB_DEVICE_ERROR, "sdb_decoder_create")
+
+    def decode(self, blocks, block_off, sst_version=2):
+        blocks = np.ascontiguousarray(blocks, np.uint8)
+        block_off = np.ascontiguousarray(block_off, np.uint64)
+        nb = len(block_off) - 1
+        res = _abi.DecodeHostResult()
+        st = lib().sdb_decoder_decode_host(self._h, blocks.ctypes.data if blocks.size else None,
+                                           block_off.ctypes.data, nb, sst_version, C.byref(res))
+        d = Decoded()
+        d.status = st
+        sm = res.summary
+        d.summary = {f: getattr(sm, f) for f, _ in _abi.DecodeSummary._fields_}
+        n = sm.num_entries if st in (0, 3, 4, 9) else 0
+        d.n = n
+        d.block_entry_start = _arr(res.block_entry_start, C.c_uint64, nb + 1, np.uint64).copy()
+        d.key_off = _arr(res.key_off, C.c_uint64, n + 1, np.uint64).copy()
+        d.key_arena = _u8(res.key_arena, sm.key_bytes).copy()
+        d.val_off = _arr(res.val_off, C.c_uint64, n, np.uint64).copy()
+        d.val_len = _arr(res.val_len, C.c_uint32, n, np.uint32).copy()
+        d.seq = _arr(res.seq, C.c_uint64, n, np.uint64).copy()
+        d.flags = _u8(res.flags, n).copy()
+        d.create_ts = _arr(res.create_ts, C.c_int64, n, np.int64).copy()
+        d.expire_ts = _arr(res.expire_ts, C.c_int64, n, np.int64).copy()
+        d.bad_block = _arr(res.bad_block, C.c_uint32, min(sm.num_bad_blocks, nb + 1), np.uint32).copy()
+        return d
+
+    def close(self):
+        if self._h:
+            lib().sdb_decoder_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------------------------------------------
+# Device-resident batched entry point (bench / multi-SST pipelines)
+# ------------------------------------------------------------------------------------------------
+class DeviceSstOutput:
+    """Caller-owned device outputs + workspace for sdb_encode_sst (allocated once, reused)."""
+
+    def __init__(self, n, total_key_bytes, total_val_bytes, prm, device="cuda"):
+        import torch
+        dc, bc, fc = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        st = lib().sdb_encode_bounds(n, total_key_bytes, total_val_bytes, C.byref(prm), C.byref(dc),
+                                     C.byref(bc), C.byref(fc))
+        if st:
+            raise SdbError(st, "sdb_encode_bounds")
+        self.params = prm
+        self.data = torch.empty(dc.value, dtype=torch.uint8, device=device)
+        self.block_off = torch.empty(bc.value + 1, dtype=torch.int64, device=device)
+        self.block_first = torch.empty(bc.value + 1, dtype=torch.int32, device=device)
+        self.index_key_len = torch.empty(bc.value + 1, dtype=torch.int32, device=device)
+        self.block_stats = torch.empty(3 * (bc.value + 1), dtype=torch.int16, device=device)
+        self.bloom = torch.empty(fc.value, dtype=torch.uint8, device=device)
+        self.summary = torch.zeros(C.sizeof(_abi.SstSummary), dtype=torch.uint8, device=device)
+        ws = lib().sdb_encode_workspace_bytes(n, C.byref(prm))
+        self.workspace = torch.empty(max(ws, 256), dtype=torch.uint8, device=device)
+        self.out = _abi.SstOut(self.data.data_ptr(), dc.value, self.block_off.data_ptr(),
+                               self.block_first.data_ptr(), self.index_key_len.data_ptr(),
+                               self.block_stats.data_ptr(), bc.value, self.bloom.data_ptr(), fc.value,
+                               self.summary.data_ptr())
+
+    def summary_host(self):
+        raw = self.summary.cpu().numpy().tobytes()
+        return _abi.SstSummary.from_buffer_copy(raw)
+
+    def to_host(self):
+        sm = self.summary_host()
+        nb = sm.num_blocks
+        r = {
+            "summary": sm,
+            "data": self.data[:sm.data_len].cpu().numpy(),
+            "block_off": self.block_off[:nb + 1].cpu().numpy().view(np.uint64),
+            "block_first_entry": self.block_first[:nb + 1].cpu().numpy().view(np.uint32),
+            "index_key_len": self.index_key_len[:nb].cpu().numpy().view(np.uint32),
+            "block_stats": self.block_stats[:3 * nb].cpu().numpy().view(np.uint16).reshape(-1, 3),
+            "bloom": self.bloom[:sm.bloom_len].cpu().numpy(),
+        }
+        return r
+
+
+def encode_sst_device(dbatch, out, stream=None):
+    """Enqueue one SST encode (device batch -> device outputs) on `stream` (torch stream or None)."""
+    sp = None
+    if stream is not None:
+        sp = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    kb = dbatch.to_ctypes()
+    st = lib().sdb_encode_sst(C.byref(kb), C.byref(out.params), C.byref(out.out), out.workspace.data_ptr(),
+                              out.workspace.numel(), sp)
+    if st:
+        raise SdbError(st, "sdb_encode_sst")

@@ -1,0 +1,280 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle, bit for bit.
+
+Byte/integer work, so the bar is exact equality of every output array: data section (blocks +
+CRC32), block offsets, first entries, index-key lengths, block stats, bloom bitmap, summary
+counters and error codes; decode outputs field by field.  Cases mirror the reference's tests
+(sst_builder.rs:593-1892, format/block_v2.rs:282-630, filter.rs:250-367, sst_iter.rs) plus the
+datasets of SURVEY.md §8d.
+"""
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from slatedb_amd import _abi, datasets
+from slatedb_amd.batch import Batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rt():
+    from slatedb_amd import runtime
+    runtime.require_device()
+    return runtime
+
+
+def encode_both(rt, batch, **kw):
+    prm = O.params(**kw)
+    ref = O.encode_sst(batch, prm)
+    enc = rt.Encoder(rt.params(**kw))
+    got = enc.encode(batch)
+    enc.close()
+    return ref, got
+
+
+def assert_same(ref, got, what=""):
+    assert got.status == ref.status, (what, got.status, ref.status, got.summary)
+    if ref.status != 0:
+        assert got.summary["first_error_entry"] == ref.summary.first_error_entry, what
+        return
+    for f in ("data_len", "num_blocks", "num_entries", "raw_key_size", "raw_val_size", "num_puts",
+              "num_deletes", "num_merges", "bloom_len", "num_probes", "filter_built", "max_block_entries"):
+        if f == "max_block_entries":
+            # device reports the longest candidate block, the oracle the longest actual one
+            assert got.summary[f] >= getattr(ref.summary, f), (what, f)
+            continue
+        assert got.summary[f] == getattr(ref.summary, f), (what, f, got.summary[f], getattr(ref.summary, f))
+    assert np.array_equal(got.block_off, ref.block_off), what
+    assert np.array_equal(got.block_first_entry, ref.block_first_entry), what
+    assert np.array_equal(got.index_key_len, ref.index_key_len), what
+    assert np.array_equal(got.block_stats, ref.block_stats), what
+    if not np.array_equal(got.data, ref.data):
+        bad = np.nonzero(got.data != ref.data)[0]
+        blk = np.searchsorted(ref.block_off, bad[0], side="right") - 1
+        raise AssertionError("%s: data differs at byte %d (block %d), %d bytes differ" % (what, bad[0], blk, len(bad)))
+    assert np.array_equal(got.bloom, ref.bloom), what
+
+
+def ent(key, value=b"", seq=0, kind=0, create=None, expire=None):
+    key = key.encode() if isinstance(key, str) else key
+    value = value.encode() if isinstance(value, str) else value
+    return (key, kind, value, seq, create, expire)
+
+
+# ------------------------------------------------------------------------------------------------
+# encode
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [1, 2, 33, 34, 35, 1000, 20000])
+def test_d1_prefixes(rt, n):
+    ref, got = encode_both(rt, datasets.d1(n=n))
+    assert_same(ref, got, "d1 n=%d" % n)
+
+
+def test_d1_full_64mib(rt):
+    """configs[1]: one 64 MiB L0 SST, bit-exact vs the oracle (578,524 entries, 17,016 blocks)."""
+    b = datasets.d1()
+    ref, got = encode_both(rt, b)
+    assert ref.summary.num_blocks == 17016 and ref.summary.data_len == 68455271
+    assert ref.summary.bloom_len == 723155
+    assert_same(ref, got, "d1 full")
+
+
+def test_d1_seq_desc_and_d2(rt):
+    ref, got = encode_both(rt, datasets.d1(n=50000, seq_desc=True))
+    assert_same(ref, got, "d1 seq desc")
+    ref, got = encode_both(rt, datasets.d2(n=50000))
+    assert_same(ref, got, "d2")
+
+
+@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("block_size", [64, 256, 1024, 4096])
+def test_d3_mixed(rt, version, block_size):
+    b = datasets.d3(n=3000)
+    ref, got = encode_both(rt, b, sst_version=version, block_size=block_size)
+    assert_same(ref, got, "d3 v%d bs%d" % (version, block_size))
+
+
+@pytest.mark.parametrize("ri", [1, 2, 4, 32])
+def test_restart_intervals(rt, ri):
+    ref, got = encode_both(rt, datasets.d3(n=2000), restart_interval=ri, block_size=2048)
+    assert_same(ref, got, "ri=%d" % ri)
+
+
+def test_sst500(rt):
+    from tests.test_oracle_kats import sst500_batch
+    ref, got = encode_both(rt, sst500_batch(), block_size=1024)
+    assert ref.summary.data_len == 21998
+    assert_same(ref, got, "sst500")
+
+
+def test_oversize_and_large_blocks(rt):
+    rng = np.random.default_rng(5)
+    es = []
+    for i in range(300):
+        vlen = 6000 if i % 17 == 0 else int(rng.integers(0, 200))
+        es.append(ent(b"k%06d" % i, bytes(rng.integers(0, 256, vlen, dtype=np.uint8)), i))
+    b = Batch.from_entries(es)
+    for bs in (4096, 16384, 65536):
+        ref, got = encode_both(rt, b, block_size=bs)
+        assert_same(ref, got, "oversize bs=%d" % bs)
+    ref, got = encode_both(rt, b, block_size=4096, sst_version=1)
+    assert_same(ref, got, "oversize v1")
+
+
+def test_long_keys_and_tiny_entries(rt):
+    es = [ent(b"p" * 300 + b"%05d" % i, b"", i) for i in range(500)]
+    ref, got = encode_both(rt, Batch.from_entries(es), block_size=4096)
+    assert_same(ref, got, "long keys")
+    es = [ent(bytes([65 + i % 26]) + struct.pack(">I", i), b"", i) for i in range(5000)]
+    es.sort(key=lambda e: e[0])
+    ref, got = encode_both(rt, Batch.from_entries(es), block_size=4096)
+    assert_same(ref, got, "tiny entries")
+
+
+def test_empty_and_min_filter_keys(rt):
+    ref, got = encode_both(rt, Batch.from_entries([]))
+    assert_same(ref, got, "empty")
+    b = datasets.d1(n=500)
+    ref, got = encode_both(rt, b, min_filter_keys=1000)  # num_rows < min_filter_keys: no filter
+    assert not ref.summary.filter_built
+    assert_same(ref, got, "min_filter_keys")
+    ref, got = encode_both(rt, b, bloom_bits_per_key=0)
+    assert_same(ref, got, "no policy")
+
+
+def test_error_codes(rt):
+    cases = [
+        [ent(b"", "v")],                                  # EmptyKey (block_v2.rs:168)
+        [ent("a", "v"), ent("b", "v"), ent(b"", "v")],    # assert in compute_lower_bound
+        [ent("abc", "v"), ent("ab", "v")],                # out-of-bounds panic in compute_lower_bound
+    ]
+    for es in cases:
+        ref, got = encode_both(rt, Batch.from_entries(es))
+        assert ref.status != 0
+        assert_same(ref, got, "errors")
+    ref, got = encode_both(rt, Batch.from_entries([ent("a", "v"), ent(b"k" * 70000, "v")]), sst_version=1)
+    assert ref.status == _abi.SDB_LIMIT_EXCEEDED
+    assert_same(ref, got, "v1 u16")
+    bad = Batch.from_entries([ent("a", "v"), ent("b", "v")])
+    bad.kind[1] = 7
+    ref, got = encode_both(rt, bad)
+    assert ref.status == _abi.SDB_INVALID_ARGUMENT
+    assert_same(ref, got, "bad kind")
+
+
+def test_builder_mirror(rt):
+    """EncodedSsTableBuilder-style add()/build()/next_block() (sst_builder.rs:224-276)."""
+    b = datasets.d3(n=700)
+    bld = rt.SstBuilder(rt.params(block_size=512))
+    for i in range(b.n):
+        m = int(b.ts_mask[i])
+        bld.add(b.key(i), b.value(i), int(b.seq[i]), int(b.kind[i]),
+                int(b.create_ts[i]) if m & 1 else None, int(b.expire_ts[i]) if m & 2 else None)
+    got = bld.build()
+    ref = O.encode_sst(b, O.params(block_size=512))
+    assert_same(ref, got, "builder")
+    blocks = []
+    while True:
+        x = got.next_block()
+        if x is None:
+            break
+        assert struct.unpack(">I", x[-4:])[0] == zlib.crc32(x[:-4])
+        blocks.append(x)
+    assert b"".join(blocks) == ref.data.tobytes()
+
+
+# ------------------------------------------------------------------------------------------------
+# bloom
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n,bpk", [(1, 10), (7, 10), (1000, 10), (200000, 10), (100000, 7), (5, 1)])
+def test_bloom_bitmap(rt, n, bpk):
+    kb, ko = datasets.c4_keys(n=n, seed=11 + n)
+    ref = O.bloom_build(kb, ko, bpk)
+    got = rt.BloomFilterPolicy(bpk).build(Batch(kb, ko, np.zeros(0, np.uint8), np.zeros(len(ko), np.uint64)))
+    assert got[:2] == struct.pack(">H", O.optimal_num_probes(bpk))
+    assert got[2:] == ref.tobytes()
+
+
+def test_bloom_fp_kat_on_gpu(rt):
+    # filter.rs:331-367 on the device builder + device prober: exactly 870 false positives
+    n = 100000
+    keys = np.arange(n, dtype=">u4").view(np.uint8).copy()
+    off = np.arange(n + 1, dtype=np.uint64) * np.uint64(4)
+    enc = rt.BloomFilterPolicy(10).build(Batch(keys, off, np.zeros(0, np.uint8), np.zeros(n + 1, np.uint64)))
+    bm = np.frombuffer(enc[2:], np.uint8)
+    assert rt.might_contain(bm, 6, [struct.pack(">I", i) for i in range(n)]).all()
+    fp = rt.might_contain(bm, 6, [struct.pack(">I", i) for i in range(n, 2 * n)]).sum()
+    assert fp == 870
+    assert not rt.might_contain(np.zeros(0, np.uint8), 6, [b"x"]).any()  # empty bitmap guard
+
+
+# ------------------------------------------------------------------------------------------------
+# decode
+# ------------------------------------------------------------------------------------------------
+def assert_decode_same(ref, got, what=""):
+    assert got.status == ref.status, (what, got.status, ref.status)
+    assert got.n == ref.n, what
+    assert np.array_equal(got.block_entry_start, ref.block_entry_start), what
+    for f in ("key_off", "val_off", "val_len", "seq", "flags", "create_ts", "expire_ts"):
+        assert np.array_equal(getattr(got, f), getattr(ref, f)), (what, f)
+    assert np.array_equal(got.key_arena, ref.key_arena), what
+    assert sorted(got.bad_block.tolist()) == sorted(ref.bad_block.tolist()), what
+
+
+@pytest.mark.parametrize("version", [1, 2])
+def test_decode_d3(rt, version):
+    b = datasets.d3(n=3000)
+    enc = O.encode_sst(b, O.params(sst_version=version, block_size=1024))
+    ref = O.decode_blocks(enc.data, enc.block_off, version)
+    dec = rt.Decoder()
+    got = dec.decode(enc.data, enc.block_off, version)
+    assert_decode_same(ref, got, "d3 v%d" % version)
+
+
+def test_decode_d1_and_corruption(rt):
+    b = datasets.d1(n=40000)
+    enc = O.encode_sst(b, O.params())
+    dec = rt.Decoder()
+    got = dec.decode(enc.data, enc.block_off, 2)
+    ref = O.decode_blocks(enc.data, enc.block_off, 2)
+    assert_decode_same(ref, got, "d1")
+    data = enc.data.copy()
+    for k in (3, 77, 500):
+        data[int(enc.block_off[k]) + 11] ^= 0x40
+    got = dec.decode(data, enc.block_off, 2)
+    ref = O.decode_blocks(data, enc.block_off, 2)
+    assert ref.status == _abi.SDB_CHECKSUM_MISMATCH
+    assert_decode_same(ref, got, "corrupt")
+
+
+def test_decode_large_blocks_and_flags(rt):
+    rng = np.random.default_rng(9)
+    es = [ent(b"k%06d" % i, bytes(rng.integers(0, 256, 9000 if i % 5 == 0 else 50, dtype=np.uint8)), i)
+          for i in range(200)]
+    enc = O.encode_sst(Batch.from_entries(es), O.params(block_size=65536))
+    dec = rt.Decoder()
+    assert_decode_same(O.decode_blocks(enc.data, enc.block_off, 2), dec.decode(enc.data, enc.block_off, 2), "big")
+    blk = bytearray(O.encode_row(2, 0, b"k", 0, b"v", 7))
+    blk[-1] = 0x10
+    body = bytes(blk) + struct.pack(">HH", 0, 1)
+    body += struct.pack(">I", zlib.crc32(body))
+    arr = np.frombuffer(body, np.uint8)
+    off = np.array([0, len(body)], np.uint64)
+    assert_decode_same(O.decode_blocks(arr, off, 2), dec.decode(arr, off, 2), "flags")
+
+
+def test_device_round_trip_full_d1(rt):
+    """Encode on the GPU, decode on the GPU: size-independent round-trip property at full size."""
+    b = datasets.d1()
+    enc = rt.Encoder(rt.params()).encode(b)
+    assert enc.status == 0
+    d = rt.Decoder().decode(enc.data, enc.block_off, 2)
+    assert d.status == 0 and d.n == b.n
+    assert np.array_equal(d.key_arena, b.key_bytes)
+    assert np.array_equal(d.key_off, b.key_off)
+    assert (d.val_len == 100).all()
+    vals = enc.data[(d.val_off[:, None] + np.arange(100, dtype=np.uint64)).astype(np.int64)]
+    assert np.array_equal(vals.reshape(-1), b.val_bytes)
