@@ -38,6 +38,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--bpk", type=int, default=10, help="bloom bits per key (0 = no filter; diagnostics)")
     return p.parse_args()
 
 
@@ -82,7 +83,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     runtime.require_device()
     lib = runtime.lib()
-    prm = runtime.params(block_size=4096, sst_version=2, restart_interval=16, bloom_bits_per_key=10)
+    prm = runtime.params(block_size=4096, sst_version=2, restart_interval=16, bloom_bits_per_key=args.bpk)
 
     # resident inputs: distinct D1 SSTs per rank
     hosts = [datasets.d1(sst_index=rank * 64 + j) for j in range(args.ssts)]
@@ -109,7 +110,7 @@ def main():
         assert sm.status == 0, "encode failed: %s" % _abi.STATUS_NAMES.get(sm.status)
         if rank == 0:
             from oracle import oracle as O
-            ref = O.encode_sst(hosts[0], O.params(block_size=4096, sst_version=2, bloom_bits_per_key=10))
+            ref = O.encode_sst(hosts[0], O.params(block_size=4096, sst_version=2, bloom_bits_per_key=args.bpk))
             verified = bool(np.array_equal(got["data"], ref.data) and np.array_equal(got["bloom"], ref.bloom)
                             and np.array_equal(got["block_off"], ref.block_off))
             assert verified, "GPU output differs from the oracle"

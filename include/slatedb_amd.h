@@ -156,10 +156,13 @@ sdb_status sdb_encode_sst(const sdb_kv_batch *batch, const sdb_sst_params *param
                           void *stream);
 
 /* Bloom bitmap over n keys (BloomFilterBuilder with whole-key filtering, filter.rs:40-90).
- * bitmap must hold sdb_bloom_filter_bytes(n, bpk) bytes; it is zeroed and filled on `stream`. */
+ * bitmap must hold sdb_bloom_filter_bytes(n, bpk) bytes; it is zeroed and filled on `stream`.
+ * workspace (sdb_bloom_workspace_bytes) holds the per-XCD replicas; NULL selects the slower
+ * device-scope-atomic build. */
+uint64_t sdb_bloom_workspace_bytes(uint64_t num_keys, uint32_t bits_per_key);
 sdb_status sdb_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
                            uint32_t bits_per_key, uint8_t *bitmap, uint64_t bitmap_bytes,
-                           void *stream);
+                           void *workspace, uint64_t workspace_bytes, void *stream);
 
 /* Batched BloomFilter::might_contain(filter_hash(key)) (filter.rs:124-136, 150-175): result[i]=1
  * iff every probe bit is set.  An empty bitmap answers 0. */

@@ -118,8 +118,9 @@ SIGNATURES = {
     "sdb_bloom_num_probes": (C.c_uint32, [C.c_uint32]),
     "sdb_encode_sst": (C.c_int, [C.POINTER(KvBatch), C.POINTER(SstParams), C.POINTER(SstOut),
                                  C.c_void_p, C.c_uint64, C.c_void_p]),
+    "sdb_bloom_workspace_bytes": (C.c_uint64, [C.c_uint64, C.c_uint32]),
     "sdb_bloom_build": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p,
-                                  C.c_uint64, C.c_void_p]),
+                                  C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]),
     "sdb_bloom_might_contain": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p,
                                           C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
     "sdb_decode_workspace_bytes": (C.c_uint64, [C.c_uint64]),
@@ -145,7 +146,7 @@ SIGNATURES = {
 }
 
 
-STAGES = ["bloom", "prep", "next", "chunk", "resolve", "emit", "emit_slow"]
+STAGES = ["bloom", "prep", "next", "chunk", "resolve", "enum", "emit", "emit_slow"]
 
 
 def bind(lib):

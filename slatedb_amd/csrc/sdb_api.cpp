@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 #include "../../include/slatedb_amd.h"
@@ -40,6 +41,27 @@ sdb_status check_params(const sdb_sst_params *p) {
     if (p->block_size == 0) return SDB_INVALID_ARGUMENT;
     if (p->sst_version == 2 && p->restart_interval == 0) return SDB_INVALID_ARGUMENT;
     return SDB_OK;
+}
+
+// Per-device side stream: the bloom build (L2-atomic bound) runs beside the HBM-bound encode
+// kernels.  fork/join through events keeps the caller's stream semantics (and graph capture).
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+std::mutex g_side_mu;
+SideStream g_side[64];
+
+SideStream *side_for_current_device() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    SideStream &ss = g_side[dev];
+    if (!ss.s) {
+        if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming);
+        hipEventCreateWithFlags(&ss.join, hipEventDisableTiming);
+    }
+    return &ss;
 }
 
 template <typename T>
@@ -97,8 +119,12 @@ sdb_status sdb_encode_bounds(uint64_t n, uint64_t total_key_bytes, uint64_t tota
 }
 
 uint64_t sdb_encode_workspace_bytes(uint64_t n, const sdb_sst_params *params) {
-    (void)params;
-    return encode_workspace_layout(n).total;
+    uint64_t fb = params && params->bloom_bits_per_key ? filter_bytes_for(n, params->bloom_bits_per_key) : 0;
+    return encode_workspace_layout(n, fb, params ? num_probes_for(params->bloom_bits_per_key) : 0).total;
+}
+
+uint64_t sdb_bloom_workspace_bytes(uint64_t n, uint32_t bits_per_key) {
+    return bloom_workspace_bytes(n, num_probes_for(bits_per_key), filter_bytes_for(n, bits_per_key)) + 256;
 }
 
 sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const sdb_sst_out *out,
@@ -110,10 +136,11 @@ sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const 
     const uint64_t n = b->n;
     if (n >= (1ull << 31)) return SDB_LIMIT_EXCEEDED;
     if (n && (!b->key_bytes || !b->key_off || !b->val_off)) return SDB_INVALID_ARGUMENT;
-    EncodeWorkspace wl = encode_workspace_layout(n);
-    if (!workspace || workspace_bytes < wl.total) return SDB_INVALID_ARGUMENT;
     const bool want_filter = p->bloom_bits_per_key > 0 && n >= p->min_filter_keys;
     const uint64_t fb = want_filter ? filter_bytes_for(n, p->bloom_bits_per_key) : 0;
+    EncodeWorkspace wl = encode_workspace_layout(n, p->bloom_bits_per_key ? filter_bytes_for(n, p->bloom_bits_per_key) : 0,
+                                                 num_probes_for(p->bloom_bits_per_key));
+    if (!workspace || workspace_bytes < wl.total) return SDB_INVALID_ARGUMENT;
     if (want_filter && fb && (!out->bloom || out->bloom_cap < fb)) return SDB_INVALID_ARGUMENT;
     if (n && (!out->data || !out->block_off || !out->block_first_entry || !out->index_key_len ||
               !out->block_stats))
@@ -149,6 +176,9 @@ sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const 
     a.wmax = carve<uint32_t>(workspace, wl.wmax);
     a.slow_count = carve<uint32_t>(workspace, wl.slow_count);
     a.slow_list = carve<uint32_t>(workspace, wl.slow_list);
+    a.desc = carve<BlockDesc>(workspace, wl.desc);
+    a.stat_part = carve<uint64_t>(workspace, wl.stat_part);
+    a.wmax_part = carve<uint32_t>(workspace, wl.wmax_part);
     a.out_data = out->data;
     a.out_block_off = out->block_off;
     a.out_block_first = out->block_first_entry;
@@ -161,22 +191,35 @@ sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const 
     a.num_probes = want_filter ? num_probes_for(p->bloom_bits_per_key) : 0;
     a.filter_built = want_filter ? 1 : 0;
     hipStream_t s = S(stream);
+    std::unique_lock<std::mutex> lk(g_side_mu);
+    SideStream *side = want_filter && n ? side_for_current_device() : nullptr;
     if (want_filter) {
-        stage_mark(s, kStBloom, true);
-        if (launch_bloom_build(b->key_bytes, b->key_off, n, a.num_probes, out->bloom, fb, s) != hipSuccess)
+        hipStream_t bs = s;
+        if (side) {  // fork
+            hipEventRecord(side->fork, s);
+            hipStreamWaitEvent(side->s, side->fork, 0);
+            bs = side->s;
+        }
+        stage_mark(bs, kStBloom, true);
+        if (launch_bloom_build(b->key_bytes, b->key_off, n, a.num_probes, out->bloom, fb,
+                               carve<void>(workspace, wl.bloom_rep), bs) != hipSuccess)
             return SDB_DEVICE_ERROR;
-        stage_mark(s, kStBloom, false);
+        stage_mark(bs, kStBloom, false);
+        if (side) hipEventRecord(side->join, side->s);
     }
     if (launch_encode(a, s) != hipSuccess) return SDB_DEVICE_ERROR;
+    if (side) hipStreamWaitEvent(s, side->join, 0);  // join: the caller's stream completes after the bloom
     return SDB_OK;
 }
 
 sdb_status sdb_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
-                           uint32_t bits_per_key, uint8_t *bitmap, uint64_t bitmap_bytes, void *stream) {
+                           uint32_t bits_per_key, uint8_t *bitmap, uint64_t bitmap_bytes, void *workspace,
+                           uint64_t workspace_bytes, void *stream) {
     if (!device_ok()) return SDB_DEVICE_ERROR;
     uint64_t fb = filter_bytes_for(n, bits_per_key);
     if (bitmap_bytes < fb || (fb && !bitmap) || (n && (!key_bytes || !key_off))) return SDB_INVALID_ARGUMENT;
-    if (launch_bloom_build(key_bytes, key_off, n, num_probes_for(bits_per_key), bitmap, fb, S(stream)) != hipSuccess)
+    if (workspace && workspace_bytes < sdb_bloom_workspace_bytes(n, bits_per_key)) return SDB_INVALID_ARGUMENT;
+    if (launch_bloom_build(key_bytes, key_off, n, num_probes_for(bits_per_key), bitmap, fb, workspace, S(stream)) != hipSuccess)
         return SDB_DEVICE_ERROR;
     return SDB_OK;
 }

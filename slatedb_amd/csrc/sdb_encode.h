@@ -12,11 +12,17 @@ constexpr uint32_t kResolveLds = 96 * 1024;  // LDS budget of the resolve tables
 constexpr uint32_t kCrcLds = 8 * 1024;       // slicing-by-8 tables
 constexpr uint32_t kImgCap = 4096 + 64;      // LDS block image per wave (fast path)
 constexpr uint32_t kStageCap = 4096 + 64;    // LDS value / key staging per wave
-constexpr uint32_t kMaxRows = 128;           // rows per block on the fast path
-constexpr uint32_t kRowInfoBytes = 40;
-constexpr uint32_t kWaveLds = kImgCap + 2 * kStageCap + kMaxRows * kRowInfoBytes;
-constexpr uint32_t kEmitWaves = 4;
-constexpr uint32_t kEmitWork = kEmitWaves * kWaveLds;  // >= 11 levels x kChunk x 2 B of lifting
+constexpr uint32_t kNextSpan = 256 + 768;     // k_next: entries staged per 256-thread workgroup
+constexpr uint32_t kEmitThreads = 512;       // 8 waves per workgroup, 2 workgroups per CU
+constexpr uint32_t kEmitLds = kCrcLds + (kEmitThreads / 64) * (kStageCap + kImgCap);
+constexpr uint32_t kEnumLds = kChunk * 16 + 12 * kChunk * 2;  // block list + 12 lifting levels
+
+struct BlockDesc {  // one per block, written by k_enum, streamed by k_emit (48 bytes)
+    uint32_t s, e;        // entries [s, e)
+    uint64_t off;         // byte offset of the block in the data section
+    uint64_t vs, ve, ks, ke;  // value / key byte ranges of the block
+    uint32_t bb, pad;     // encoded bytes incl. CRC
+};
 
 struct EncodeArgs {
     // batch (device)
@@ -51,6 +57,10 @@ struct EncodeArgs {
     uint32_t *wmax;
     uint32_t *slow_count;
     uint32_t *slow_list;
+    BlockDesc *desc;
+    uint64_t *stat_part;    // per k_prep workgroup: raw key, raw val, puts, deletes, merges
+    uint32_t *wmax_part;    // per k_next workgroup: longest candidate block (entries)
+    uint32_t nprep_wg;
     // outputs (device)
     uint8_t *out_data;
     uint64_t *out_block_off;
@@ -66,10 +76,11 @@ struct EncodeArgs {
 // Workspace layout for n entries (all offsets 256-byte aligned).
 struct EncodeWorkspace {
     uint64_t lcp, s_nr, s_r, next, bbytes, tab_exit, tab_cnt, tab_bytes;
-    uint64_t anchor_e, anchor_blk, anchor_byte, err, wmax, slow_count, slow_list;
+    uint64_t anchor_e, anchor_blk, anchor_byte, err, wmax, slow_count, slow_list, desc, stat_part, wmax_part, bloom_rep;
     uint64_t total;
 };
-inline EncodeWorkspace encode_workspace_layout(uint64_t n) {
+uint64_t bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
+inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes, uint32_t num_probes) {
     EncodeWorkspace w{};
     uint64_t off = 0;
     auto take = [&](uint64_t bytes) {
@@ -93,6 +104,10 @@ inline EncodeWorkspace encode_workspace_layout(uint64_t n) {
     w.wmax = take(4);
     w.slow_count = take(4);
     w.slow_list = take(4 * (n + 1));
+    w.desc = take(sizeof(BlockDesc) * (n + 1));
+    w.stat_part = take(8 * 5 * ((n + 255) / 256 + 1));
+    w.wmax_part = take(4 * ((n + 255) / 256 + 1));
+    w.bloom_rep = take(filter_bytes ? bloom_workspace_bytes(n, num_probes, filter_bytes) : 0);  // bloom buckets
     w.total = off;
     return w;
 }
@@ -100,13 +115,21 @@ inline EncodeWorkspace encode_workspace_layout(uint64_t n) {
 hipError_t launch_encode(EncodeArgs a, hipStream_t st);
 
 // stage timing (diagnostics)
-enum Stage { kStBloom = 0, kStPrep, kStNext, kStChunk, kStResolve, kStEmit, kStEmitSlow, kNumStages };
+enum Stage { kStBloom = 0, kStPrep, kStNext, kStChunk, kStResolve, kStEnum, kStEmit, kStEmitSlow, kNumStages };
 void stage_mark(hipStream_t st, int stage, bool begin);
 bool stage_timing_on();
 
 // bloom (sdb_bloom.hip)
+struct BloomPlan {
+    uint32_t k, m;        // probes per key, bitmap bits
+    uint32_t sb;          // log2 bits per slice
+    uint32_t nslices, T, tiles;
+};
+BloomPlan bloom_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
+uint64_t bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
+// ws: bloom_workspace_bytes(...) of scratch, or NULL (device-scope atomics; slow)
 hipError_t launch_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
-                              uint32_t num_probes, uint8_t *bitmap, uint64_t bitmap_bytes,
+                              uint32_t num_probes, uint8_t *bitmap, uint64_t bitmap_bytes, void *ws,
                               hipStream_t st);
 hipError_t launch_bloom_query(const uint8_t *bitmap, uint64_t bitmap_bytes, uint32_t num_probes,
                               const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,

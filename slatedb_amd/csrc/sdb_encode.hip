@@ -79,18 +79,24 @@ __global__ __launch_bounds__(256) void k_prep(EncodeArgs a) {
         merges = kd == SDB_KIND_MERGE;
         dels = kd == SDB_KIND_TOMBSTONE;
     }
-    // SstStats (sst_builder.rs:225-226, 315-317)
+    // SstStats (sst_builder.rs:225-226, 315-317): per-workgroup partials, summed in k_resolve
+    __shared__ uint64_t s_part[4][5];
     rk = wave_sum(rk);
     rv = wave_sum(rv);
     uint32_t c = wave_sum(puts | (dels << 10) | (merges << 20));  // <= 64 each per wave
+    const uint32_t w = threadIdx.x >> 6;
     if (lane_id() == 0) {
-        if (rk) atomicAdd((unsigned long long *)&a.summary->raw_key_size, (unsigned long long)rk);
-        if (rv) atomicAdd((unsigned long long *)&a.summary->raw_val_size, (unsigned long long)rv);
-        if (c & 0x3FF) atomicAdd((unsigned long long *)&a.summary->num_puts, (unsigned long long)(c & 0x3FF));
-        if ((c >> 10) & 0x3FF)
-            atomicAdd((unsigned long long *)&a.summary->num_deletes, (unsigned long long)((c >> 10) & 0x3FF));
-        if ((c >> 20) & 0x3FF)
-            atomicAdd((unsigned long long *)&a.summary->num_merges, (unsigned long long)((c >> 20) & 0x3FF));
+        s_part[w][0] = rk;
+        s_part[w][1] = rv;
+        s_part[w][2] = c & 0x3FF;
+        s_part[w][3] = (c >> 10) & 0x3FF;
+        s_part[w][4] = (c >> 20) & 0x3FF;
+    }
+    __syncthreads();
+    if (threadIdx.x < 5) {
+        uint64_t t = 0;
+        for (uint32_t q = 0; q < (blockDim.x >> 6); q++) t += s_part[q][threadIdx.x];
+        a.stat_part[5 * (uint64_t)blockIdx.x + threadIdx.x] = t;
     }
 }
 
@@ -98,7 +104,16 @@ __global__ __launch_bounds__(256) void k_prep(EncodeArgs a) {
 // K2: next(b) for every entry b (BlockBuilderV2::would_fit / BlockBuilderV1::would_fit)
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_next(EncodeArgs a) {
-    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // sizes of [b0, b0 + kNextSpan) staged in LDS; a scan that runs past it continues from HBM
+    __shared__ uint32_t s_r[kNextSpan], s_nr[kNextSpan];
+    const uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x;
+    const uint64_t b = b0 + threadIdx.x;
+    const uint64_t lim = b0 + kNextSpan < a.n ? b0 + kNextSpan : a.n;
+    for (uint64_t j = b0 + threadIdx.x; j < lim; j += blockDim.x) {
+        s_r[j - b0] = a.s_r[j];
+        if (a.version == 2) s_nr[j - b0] = a.s_nr[j];
+    }
+    __syncthreads();
     uint32_t len = 0;
     if (b < a.n) {
         const uint64_t bs = a.block_size;
@@ -107,13 +122,18 @@ __global__ __launch_bounds__(256) void k_next(EncodeArgs a) {
         uint32_t p = 0;
         if (a.version == 2) {
             const uint32_t ri = a.restart_interval;
+            uint32_t ph = 0;  // p % ri
             while (j < a.n) {
-                bool rs = (p % ri) == 0;
-                uint64_t add = rs ? (uint64_t)a.s_r[j] + 2 : (uint64_t)a.s_nr[j];
+                bool rs = ph == 0;
+                uint32_t sz;
+                if (j < lim) sz = rs ? s_r[j - b0] : s_nr[j - b0];
+                else sz = rs ? a.s_r[j] : a.s_nr[j];
+                uint64_t add = (uint64_t)sz + (rs ? 2 : 0);
                 if (p > 0 && acc + add > bs) break;
                 acc += add;
                 j++;
                 p++;
+                if (++ph == ri) ph = 0;
             }
         } else {
             const uint64_t fko = a.key_off[b];
@@ -124,7 +144,7 @@ __global__ __launch_bounds__(256) void k_next(EncodeArgs a) {
                     uint64_t ko = a.key_off[j];
                     prefix = lcp_bytes(a.key_bytes + fko, fkl, a.key_bytes + ko, (uint32_t)(a.key_off[j + 1] - ko));
                 }
-                uint64_t sz = (uint64_t)a.s_r[j] - prefix;
+                uint64_t sz = (uint64_t)(j < lim ? s_r[j - b0] : a.s_r[j]) - prefix;
                 if (p > 0 && acc + sz > bs) break;  // the new entry's 2-byte offset is not counted (block.rs:117-123)
                 acc += sz + 2;
                 j++;
@@ -135,8 +155,17 @@ __global__ __launch_bounds__(256) void k_next(EncodeArgs a) {
         a.bbytes[b] = (uint32_t)(acc + 4);  // + CRC32 (format/sst.rs:541-552)
         len = (uint32_t)(j - b);
     }
+    // longest candidate block: per-workgroup partial (a single global atomicMax target would
+    // serialise ~10^4 wave atomics at the memory side), reduced in k_resolve
+    __shared__ uint32_t s_len[4];
     len = wave_max(len);
-    if (lane_id() == 0 && len) atomicMax(a.wmax, len);
+    if (lane_id() == 0) s_len[threadIdx.x >> 6] = len;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t m = 0;
+        for (uint32_t q = 0; q < (blockDim.x >> 6); q++) m = s_len[q] > m ? s_len[q] : m;
+        a.wmax_part[blockIdx.x] = m;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -193,8 +222,24 @@ __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     uint32_t KP = 1;
     while (KP < K) KP <<= 1;
-    const uint32_t W = *a.wmax;
-    if (tid == 0) s_fast = (W <= kChunk && (uint64_t)KP * W * 2 + 4ull * KP <= kResolveLds) ? 1u : 0u;
+    __shared__ uint32_t s_wmax;
+    if (tid == 0) s_wmax = 0;
+    __syncthreads();
+    {
+        uint32_t m = 0;
+        for (uint32_t q = tid; q < a.nprep_wg; q += nt) m = a.wmax_part[q] > m ? a.wmax_part[q] : m;
+        m = wave_max(m);
+        if (lane_id() == 0) atomicMax(&s_wmax, m);
+    }
+    __syncthreads();
+    const uint32_t W = s_wmax;
+    if (tid == 0) *a.wmax = W;
+    // LDS: ex (KP*W u16) + v (KP u32) + tmp (KP/2*W u16), each 16-byte aligned
+    if (tid == 0)
+        s_fast = (W <= kChunk && (((uint64_t)KP * W * 2 + 15) & ~15ull) + ((4ull * KP + 15) & ~15ull) +
+                                         (uint64_t)KP * W + 16 <= kResolveLds)
+                     ? 1u
+                     : 0u;
     __syncthreads();
     if (s_fast) {
         uint16_t *ex = (uint16_t *)smem;                               // KP x W exit offsets
@@ -212,14 +257,22 @@ __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
             ex[idx] = val;
         }
         __syncthreads();
-        // Blelloch up-sweep: ex[k] <- ex[k] o ex[k-d] for k = 2d-1 (mod 2d); in place.
+        // Blelloch up-sweep: ex[k] <- ex[k] o ex[k-d] for k = 2d-1 (mod 2d).  A level reads entries
+        // of ex[k] that other threads of the same level overwrite, so results go through `tmp`.
+        uint16_t *tmp = (uint16_t *)(smem + (((uint64_t)KP * W * 2 + 15) & ~15ull) + (((uint64_t)KP * 4 + 15) & ~15ull));
         for (uint32_t d = 1; d < KP; d <<= 1) {
             uint32_t nodes = KP / (2 * d);
             for (uint64_t idx = tid; idx < (uint64_t)nodes * W; idx += nt) {
                 uint32_t q = (uint32_t)(idx / W), o = (uint32_t)(idx % W);
                 uint32_t k = 2 * d * q + 2 * d - 1;
                 uint16_t mid = ex[(uint64_t)(k - d) * W + o];
-                ex[(uint64_t)k * W + o] = ex[(uint64_t)k * W + mid];
+                tmp[idx] = ex[(uint64_t)k * W + mid];
+            }
+            __syncthreads();
+            for (uint64_t idx = tid; idx < (uint64_t)nodes * W; idx += nt) {
+                uint32_t q = (uint32_t)(idx / W), o = (uint32_t)(idx % W);
+                uint32_t k = 2 * d * q + 2 * d - 1;
+                ex[(uint64_t)k * W + o] = tmp[idx];
             }
             __syncthreads();
         }
@@ -269,6 +322,20 @@ __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
         }
         cb += tc;
         cy += ty;
+    }
+    // SstStats totals from the k_prep partials
+    for (uint32_t f = 0; f < 5; f++) {
+        uint64_t t = 0;
+        for (uint32_t q = tid; q < a.nprep_wg; q += nt) t += a.stat_part[5 * (uint64_t)q + f];
+        uint64_t tot;
+        block_excl_scan_u64(t, s_w, &tot);
+        if (tid == 0) {
+            if (f == 0) a.summary->raw_key_size = tot;
+            if (f == 1) a.summary->raw_val_size = tot;
+            if (f == 2) a.summary->num_puts = tot;
+            if (f == 3) a.summary->num_deletes = tot;
+            if (f == 4) a.summary->num_merges = tot;
+        }
     }
     if (tid == 0) {
         a.anchor_blk[K] = (uint32_t)cb;
@@ -402,126 +469,14 @@ SDB_DEV void wave_store(uint8_t *gdst, const uint8_t *img, uint64_t len) {
     }
 }
 
-struct EmitLds {
-    uint32_t crc[8][256];
-};
-
-// Emit one block [b, e) whose encoded bytes (incl. CRC) are `bbytes`, at data + off.  One wave.
-template <int V>
-SDB_DEV void emit_block_fast(const EncodeArgs &a, uint64_t b, uint64_t e, uint64_t off, uint32_t bbytes,
-                             uint8_t *img, uint8_t *stv, uint8_t *stk, RowInfo *rows,
-                             const uint32_t (*crc)[256]) {
-    const int l = lane_id();
-    const uint32_t ne = (uint32_t)(e - b);
-    const uint32_t L = bbytes - 4;  // Block::encode length
-    uint8_t *gdst = a.out_data + off;
-    const uint32_t pad = (uint32_t)((uintptr_t)gdst & 15);
-    uint8_t *im = img + pad;
-    const uint64_t vs = a.val_off[b], ve = a.val_off[e];
-    const uint64_t ks = a.key_off[b], ke = a.key_off[e];
-    wave_stage(stv, a.val_bytes, vs, ve);
-    wave_stage(stk, a.key_bytes, ks, ke);
-    const uint64_t vbase = vs & ~15ull, kbase = ks & ~15ull;
-    // row metadata, row offsets (wave scan over groups of 64 rows)
-    uint32_t carry = 0;
-    const uint32_t ri = a.restart_interval;
-    const uint64_t fko = a.key_off[b];
-    const uint32_t fkl = (uint32_t)(a.key_off[b + 1] - fko);
-    for (uint32_t g = 0; g < ne; g += 64) {
-        uint32_t i = g + l;
-        uint32_t size = 0;
-        if (i < ne) {
-            uint64_t j = b + i;
-            uint64_t ko = a.key_off[j];
-            uint32_t klen = (uint32_t)(a.key_off[j + 1] - ko);
-            uint8_t kd = a.kind ? a.kind[j] : 0;
-            uint8_t m = a.ts_mask ? a.ts_mask[j] : 0;
-            uint32_t vlen = kd == SDB_KIND_TOMBSTONE ? 0 : (uint32_t)(a.val_off[j + 1] - a.val_off[j]);
-            RowInfo r;
-            uint32_t shared;
-            if (V == 2) shared = (i % ri == 0) ? 0 : a.lcp[j];
-            else shared = (i == 0) ? 0 : lcp_bytes(a.key_bytes + fko, fkl, a.key_bytes + ko, klen);
-            r.shared = shared;
-            r.suf = klen - shared;
-            r.vlen = vlen;
-            r.key_src = ko + shared;
-            r.val_src = a.val_off[j];
-            r.flags = (uint8_t)((kd == SDB_KIND_MERGE ? SDB_FLAG_MERGE_OPERAND : 0) |
-                                (kd == SDB_KIND_TOMBSTONE ? SDB_FLAG_TOMBSTONE : 0) |
-                                ((m & SDB_TS_EXPIRE) ? SDB_FLAG_HAS_EXPIRE_TS : 0) |
-                                ((m & SDB_TS_CREATE) ? SDB_FLAG_HAS_CREATE_TS : 0));
-            const uint32_t ts8 = 8u * (((m & SDB_TS_CREATE) != 0) + ((m & SDB_TS_EXPIRE) != 0));
-            if (V == 2)
-                size = varint_len(shared) + varint_len(r.suf) + varint_len(vlen) + r.suf + vlen + 9 + ts8;
-            else
-                size = 4 + r.suf + 9 + ts8 + (kd == SDB_KIND_TOMBSTONE ? 0 : 4 + vlen);
-            r.size = size;
-            rows[i] = r;
-        }
-        uint32_t inc = wave_incl_scan(size);
-        if (i < ne) rows[i].row_off = carry + inc - size;
-        carry += __shfl(inc, 63, 64);
-    }
-    const uint32_t D = carry;
-    wave_sync();
-    // rows
-    for (uint32_t i = l; i < ne; i += 64) {
-        const RowInfo r = rows[i];
-        uint64_t j = b + i;
-        uint64_t seq = a.seq ? a.seq[j] : 0;
-        int64_t ets = (r.flags & SDB_FLAG_HAS_EXPIRE_TS) ? a.expire_ts[j] : 0;
-        int64_t cts = (r.flags & SDB_FLAG_HAS_CREATE_TS) ? a.create_ts[j] : 0;
-        uint8_t *row = im + r.row_off;
-        uint32_t h;
-        write_row_small<V>(row, r, seq, ets, cts, &h);
-        lds_copy(row + h, stk + (r.key_src - kbase), r.suf);
-        if (r.vlen) {
-            uint32_t voff = (V == 2) ? h + r.suf : (r.size - r.vlen);
-            lds_copy(row + voff, stv + (r.val_src - vbase), r.vlen);
-        }
-    }
-    // offsets table + count (Block::encode, format/block.rs:17-26)
-    uint32_t noffs;
-    if (V == 2) {
-        noffs = (ne + ri - 1) / ri;
-        for (uint32_t q = l; q < noffs; q += 64) {
-            uint32_t ro = rows[q * ri].row_off;
-            if (ro > 0xFFFF) report_error(a.err, b + (uint64_t)q * ri, SDB_LIMIT_EXCEEDED);  // block_v2.rs:195
-            im[D + 2 * q] = (uint8_t)(ro >> 8);
-            im[D + 2 * q + 1] = (uint8_t)ro;
-        }
-    } else {
-        noffs = ne;
-        for (uint32_t q = l; q < noffs; q += 64) {
-            uint32_t ro = rows[q].row_off;  // `as u16` (block.rs:163)
-            im[D + 2 * q] = (uint8_t)(ro >> 8);
-            im[D + 2 * q + 1] = (uint8_t)ro;
-        }
-    }
-    if (l == 0) {
-        im[D + 2 * noffs] = (uint8_t)(noffs >> 8);
-        im[D + 2 * noffs + 1] = (uint8_t)noffs;
-    }
-    wave_sync();
-    const uint32_t Lc = D + 2 * noffs + 2;
-    uint32_t c = wave_crc32_lds(im, Lc, crc);
-    if (l == 0) {
-        im[Lc] = (uint8_t)(c >> 24);
-        im[Lc + 1] = (uint8_t)(c >> 16);
-        im[Lc + 2] = (uint8_t)(c >> 8);
-        im[Lc + 3] = (uint8_t)c;
-        if (Lc != L) report_error(a.err, b, SDB_DEVICE_ERROR);  // internal consistency
-    }
-    wave_sync();
-    wave_store(gdst, img, (uint64_t)Lc + 4);
-    wave_sync();
-}
-
-template <int V>
-__global__ __launch_bounds__(256) void k_emit(EncodeArgs a) {
+// ------------------------------------------------------------------------------------------------
+// K5a: enumerate the blocks of each chunk (binary lifting over next()) -> BlockMeta offsets and the
+//      per-block descriptors the emitter streams.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_enum(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t k = blockIdx.x;
-    if (*a.err != ~0ull) return;  // any earlier error (incl. capacity): write nothing
+    if (*a.err != ~0ull) return;
     const uint64_t cs = (uint64_t)k * kChunk;
     const uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
     const uint32_t cn = (uint32_t)(ce - cs);
@@ -530,107 +485,269 @@ __global__ __launch_bounds__(256) void k_emit(EncodeArgs a) {
     const uint32_t nb = a.anchor_blk[k + 1] - blk0;
     const uint64_t byte0 = a.anchor_byte[k];
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
-    const uint32_t wave = tid >> 6;
-    // LDS carve: [crc tables 8 KB][block list: bs u32, bb u32, off u64 per block][work area]
-    uint32_t(*crc)[256] = (uint32_t(*)[256])smem;
-    uint32_t *bl_s = (uint32_t *)(smem + kCrcLds);
-    uint32_t *bl_b = bl_s + kChunk;
-    uint64_t *bl_o = (uint64_t *)(bl_b + kChunk);
-    uint8_t *work = (uint8_t *)(bl_o + kChunk);
-    for (uint32_t q = tid; q < 8 * 256; q += nt) ((uint32_t *)crc)[q] = (&c_crc.t[0][0])[q];
-    if (nb) {
-        // binary lifting over next() within the chunk: lv[j][x] = next^(2^j)(cs+x) - cs (clamped to cn)
-        uint16_t *lv = (uint16_t *)work;
-        uint32_t levels = 1;
-        while ((1u << levels) < nb) levels++;
-        for (uint32_t x = tid; x < cn; x += nt) {
-            uint64_t nx = a.next[cs + x];
-            lv[x] = (uint16_t)(nx >= ce ? cn : (uint32_t)(nx - cs));
-        }
-        __syncthreads();
-        for (uint32_t j = 1; j < levels; j++) {
-            uint16_t *src = lv + (uint64_t)(j - 1) * kChunk, *dst = lv + (uint64_t)j * kChunk;
-            for (uint32_t x = tid; x < cn; x += nt) {
-                uint16_t y = src[x];
-                dst[x] = (y >= cn) ? (uint16_t)cn : src[y];
-            }
-            __syncthreads();
-        }
-        for (uint32_t t = tid; t < nb; t += nt) {
-            uint32_t x = (uint32_t)(e0 - cs);
-            for (uint32_t j = 0; j < levels; j++)
-                if ((t >> j) & 1) x = lv[(uint64_t)j * kChunk + x];
-            bl_s[t] = (uint32_t)cs + x;
-            bl_b[t] = a.bbytes[cs + x];
-        }
-        __syncthreads();
-        // exclusive scan of block bytes (single wave, serial over waves of 64)
-        if (wave == 0) {
-            uint64_t carry = byte0;
-            for (uint32_t g = 0; g < nb; g += 64) {
-                uint32_t t = g + (tid & 63);
-                uint64_t v = t < nb ? bl_b[t] : 0;
-                uint64_t inc = wave_incl_scan(v);
-                if (t < nb) bl_o[t] = carry + inc - v;
-                carry += __shfl(inc, 63, 64);
-            }
-        }
-        __syncthreads();
-        // block metadata for the footer builder (BlockMeta, SstStats::block_stats)
-        for (uint32_t t = tid; t < nb; t += nt) {
-            uint64_t s = bl_s[t];
-            uint64_t en = a.next[s];
-            uint32_t blk = blk0 + t;
-            a.out_block_off[blk] = bl_o[t];
-            a.out_block_first[blk] = (uint32_t)s;
-            // compute_index_key (utils.rs:198-226) from the adjacent LCP
-            uint32_t ik = 0;
-            if (s > 0) {
-                uint64_t fl = a.key_off[s + 1] - a.key_off[s];
-                uint64_t pl = a.key_off[s] - a.key_off[s - 1];
-                uint32_t lc = a.lcp[s];
-                ik = (lc == pl && pl == fl) ? (uint32_t)fl : lc + 1;
-            }
-            a.out_index_key_len[blk] = ik;
-            uint32_t pu = 0, de = 0, me = 0;
-            for (uint64_t j = s; j < en; j++) {
-                uint8_t kd = a.kind ? a.kind[j] : 0;
-                pu += kd == SDB_KIND_VALUE;
-                de += kd == SDB_KIND_TOMBSTONE;
-                me += kd == SDB_KIND_MERGE;
-            }
-            a.out_block_stats[3 * (uint64_t)blk] = (uint16_t)pu;
-            a.out_block_stats[3 * (uint64_t)blk + 1] = (uint16_t)de;
-            a.out_block_stats[3 * (uint64_t)blk + 2] = (uint16_t)me;
-        }
-        if (k + 1 == a.nchunks && tid == 0) {
-            a.out_block_off[a.anchor_blk[k + 1]] = a.anchor_byte[k + 1];
-            a.out_block_first[a.anchor_blk[k + 1]] = (uint32_t)a.n;
-        }
-        __syncthreads();  // lv region is reused below
-        // per-wave staging: image, values, keys, row infos
-        uint8_t *wbase = work + (uint64_t)wave * kWaveLds;
-        uint8_t *img = wbase;
-        uint8_t *stv = img + kImgCap;
-        uint8_t *stk = stv + kStageCap;
-        RowInfo *rows = (RowInfo *)(stk + kStageCap);
-        const uint32_t nwaves = nt >> 6;
-        for (uint32_t t = wave; t < nb; t += nwaves) {
-            uint64_t s = bl_s[t];
-            uint64_t en = a.next[s];
-            uint32_t bb = bl_b[t];
-            uint64_t vspan = a.val_off[en] - (a.val_off[s] & ~15ull) + 16;
-            uint64_t kspan = a.key_off[en] - (a.key_off[s] & ~15ull) + 16;
-            if (bb + 32 <= kImgCap && vspan <= kStageCap && kspan <= kStageCap && en - s <= kMaxRows) {
-                emit_block_fast<V>(a, s, en, bl_o[t], bb, img, stv, stk, rows, crc);
-            } else if (lane_id() == 0) {
-                uint32_t slot = atomicAdd(a.slow_count, 1u);
-                a.slow_list[slot] = blk0 + t;
-            }
-        }
-    } else if (k + 1 == a.nchunks && tid == 0) {
+    if (k + 1 == a.nchunks && tid == 0) {
         a.out_block_off[a.anchor_blk[k + 1]] = a.anchor_byte[k + 1];
         a.out_block_first[a.anchor_blk[k + 1]] = (uint32_t)a.n;
+    }
+    if (!nb) return;
+    uint32_t *bl_s = (uint32_t *)smem;
+    uint32_t *bl_b = bl_s + kChunk;
+    uint64_t *bl_o = (uint64_t *)(bl_b + kChunk);
+    uint16_t *lv = (uint16_t *)(bl_o + kChunk);
+    uint32_t levels = 1;
+    while ((1u << levels) < nb) levels++;
+    for (uint32_t x = tid; x < cn; x += nt) {
+        uint64_t nx = a.next[cs + x];
+        lv[x] = (uint16_t)(nx >= ce ? cn : (uint32_t)(nx - cs));
+    }
+    __syncthreads();
+    for (uint32_t j = 1; j < levels; j++) {
+        uint16_t *src = lv + (uint64_t)(j - 1) * kChunk, *dst = lv + (uint64_t)j * kChunk;
+        for (uint32_t x = tid; x < cn; x += nt) {
+            uint16_t y = src[x];
+            dst[x] = (y >= cn) ? (uint16_t)cn : src[y];
+        }
+        __syncthreads();
+    }
+    for (uint32_t t = tid; t < nb; t += nt) {
+        uint32_t x = (uint32_t)(e0 - cs);
+        for (uint32_t j = 0; j < levels; j++)
+            if ((t >> j) & 1) x = lv[(uint64_t)j * kChunk + x];
+        bl_s[t] = (uint32_t)cs + x;
+        bl_b[t] = a.bbytes[cs + x];
+    }
+    __syncthreads();
+    if (tid < 64) {
+        uint64_t carry = byte0;
+        for (uint32_t g = 0; g < nb; g += 64) {
+            uint32_t t = g + tid;
+            uint64_t v = t < nb ? bl_b[t] : 0;
+            uint64_t inc = wave_incl_scan(v);
+            if (t < nb) bl_o[t] = carry + inc - v;
+            carry += __shfl(inc, 63, 64);
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = tid; t < nb; t += nt) {
+        uint64_t s = bl_s[t], e = a.next[s];
+        uint32_t blk = blk0 + t;
+        a.out_block_off[blk] = bl_o[t];
+        a.out_block_first[blk] = (uint32_t)s;
+        BlockDesc d;
+        d.s = (uint32_t)s;
+        d.e = (uint32_t)e;
+        d.off = bl_o[t];
+        d.vs = a.val_off[s];
+        d.ve = a.val_off[e];
+        d.ks = a.key_off[s];
+        d.ke = a.key_off[e];
+        d.bb = bl_b[t];
+        d.pad = 0;
+        a.desc[blk] = d;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// K5b: emit.  Persistent waves stream blocks (one block per wave at a time); each wave prefetches the
+//      next block's values, keys and row metadata into registers while it assembles the current one
+//      in LDS, so HBM latency overlaps the byte work.
+// ------------------------------------------------------------------------------------------------
+struct Pre {
+    // wave-uniform block descriptor
+    uint32_t blk, s, e, bb, nv16, nk16;
+    uint64_t off, vs, ks;
+    bool valid, fast;
+    // staged 16-byte granules (value range: lane + 64 r; key range: lane)
+    uint4 v[4];
+    uint4 k;
+    // this lane's row (lane < e - s)
+    uint64_t ko, vo, seq;
+    int64_t cts, ets;
+    uint32_t klen, vlen, lcp, prev_klen;
+    uint8_t kind, mask;
+};
+
+SDB_DEV void load_pre(const EncodeArgs &a, uint32_t blk, uint32_t nb, Pre &p) {
+    const int l = lane_id();
+    p.valid = blk < nb;
+    p.fast = false;
+    if (!p.valid) return;
+    const BlockDesc d = a.desc[blk];
+    p.blk = blk;
+    p.s = d.s;
+    p.e = d.e;
+    p.bb = d.bb;
+    p.off = d.off;
+    p.vs = d.vs;
+    p.ks = d.ks;
+    const uint32_t ne = d.e - d.s;
+    const uint64_t va = d.vs & ~15ull, ka = d.ks & ~15ull;
+    p.nv16 = (uint32_t)((((d.ve + 15) & ~15ull) - va) >> 4);
+    p.nk16 = (uint32_t)((((d.ke + 15) & ~15ull) - ka) >> 4);
+    if (d.ve == d.vs) p.nv16 = 0;
+    if (d.ke == d.ks) p.nk16 = 0;
+    p.fast = ne <= 64 && p.nv16 <= 256 && p.nk16 <= 64 && (p.nv16 + p.nk16) * 16 <= kStageCap &&
+             d.bb + 32 <= kImgCap;
+    if (!p.fast) return;
+    const uint4 *vsrc = (const uint4 *)(a.val_bytes + va);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        uint32_t c = (uint32_t)l + 64u * r;
+        p.v[r] = c < p.nv16 ? vsrc[c] : make_uint4(0, 0, 0, 0);
+    }
+    p.k = (uint32_t)l < p.nk16 ? ((const uint4 *)(a.key_bytes + ka))[l] : make_uint4(0, 0, 0, 0);
+    if ((uint32_t)l < ne) {
+        uint64_t j = d.s + l;
+        p.ko = a.key_off[j];
+        p.klen = (uint32_t)(a.key_off[j + 1] - p.ko);
+        p.vo = a.val_off[j];
+        p.kind = a.kind ? a.kind[j] : 0;
+        p.mask = a.ts_mask ? a.ts_mask[j] : 0;
+        p.vlen = p.kind == SDB_KIND_TOMBSTONE ? 0 : (uint32_t)(a.val_off[j + 1] - p.vo);
+        p.lcp = a.lcp[j];
+        p.seq = a.seq ? a.seq[j] : 0;
+        p.cts = (p.mask & SDB_TS_CREATE) ? a.create_ts[j] : 0;
+        p.ets = (p.mask & SDB_TS_EXPIRE) ? a.expire_ts[j] : 0;
+        p.prev_klen = (l == 0 && d.s > 0) ? (uint32_t)(p.ko - a.key_off[j - 1]) : 0;
+    } else {
+        p.klen = p.vlen = p.lcp = p.prev_klen = 0;
+        p.kind = p.mask = 0;
+        p.ko = p.vo = p.seq = 0;
+        p.cts = p.ets = 0;
+    }
+}
+
+template <int V>
+SDB_DEV void process_block(const EncodeArgs &a, const Pre &p, uint8_t *stage, uint8_t *img,
+                           const uint32_t (*crc)[256]) {
+    const int l = lane_id();
+    const uint32_t ne = p.e - p.s;
+    // 1. staged granules -> LDS
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        uint32_t c = (uint32_t)l + 64u * r;
+        if (c < p.nv16) ((uint4 *)stage)[c] = p.v[r];
+    }
+    uint8_t *kst = stage + 16 * p.nv16;
+    if ((uint32_t)l < p.nk16) ((uint4 *)kst)[l] = p.k;
+    wave_sync();
+    const uint64_t va = p.vs & ~15ull, ka = p.ks & ~15ull;
+    // 2. row sizes and offsets (lane = row)
+    const bool row = (uint32_t)l < ne;
+    const uint32_t ri = a.restart_interval;
+    uint32_t shared = 0;
+    if (V == 2 && row) shared = (l % ri == 0) ? 0 : p.lcp;
+    if (V == 1) {  // prefix vs the block's first key (block.rs:117-123)
+        uint32_t fkl = __shfl(p.klen, 0, 64);
+        if (row && l > 0) {
+            const uint8_t *fk = kst + (p.ks - ka);
+            const uint8_t *mk = kst + (p.ko - ka);
+            shared = lcp_bytes(fk, fkl, mk, p.klen);
+        }
+    }
+    RowInfo r;
+    r.shared = shared;
+    r.suf = p.klen - shared;
+    r.vlen = p.vlen;
+    r.flags = (uint8_t)((p.kind == SDB_KIND_MERGE ? SDB_FLAG_MERGE_OPERAND : 0) |
+                        (p.kind == SDB_KIND_TOMBSTONE ? SDB_FLAG_TOMBSTONE : 0) |
+                        ((p.mask & SDB_TS_EXPIRE) ? SDB_FLAG_HAS_EXPIRE_TS : 0) |
+                        ((p.mask & SDB_TS_CREATE) ? SDB_FLAG_HAS_CREATE_TS : 0));
+    const uint32_t ts8 = 8u * (((p.mask & SDB_TS_CREATE) != 0) + ((p.mask & SDB_TS_EXPIRE) != 0));
+    uint32_t size = 0;
+    if (row) {
+        if (V == 2) size = varint_len(shared) + varint_len(r.suf) + varint_len(r.vlen) + r.suf + r.vlen + 9 + ts8;
+        else size = 4 + r.suf + 9 + ts8 + (p.kind == SDB_KIND_TOMBSTONE ? 0 : 4 + r.vlen);
+    }
+    r.size = size;
+    const uint32_t inc = wave_incl_scan(size);
+    const uint32_t row_off = inc - size;
+    const uint32_t D = __shfl(inc, 63, 64);
+    uint8_t *gdst = a.out_data + p.off;
+    uint8_t *im = img + ((uintptr_t)gdst & 15);
+    // 3. rows
+    if (row) {
+        uint8_t *rowp = im + row_off;
+        uint32_t h;
+        write_row_small<V>(rowp, r, p.seq, p.ets, p.cts, &h);
+        lds_copy(rowp + h, kst + (p.ko + shared - ka), r.suf);
+        if (r.vlen) {
+            uint32_t voff = (V == 2) ? h + r.suf : (size - r.vlen);
+            lds_copy(rowp + voff, stage + (p.vo - va), r.vlen);
+        }
+    }
+    // 4. offsets + count (Block::encode, format/block.rs:17-26)
+    uint32_t noffs;
+    if (V == 2) {
+        noffs = (ne + ri - 1) / ri;
+        if (row && l % ri == 0) {
+            uint32_t q = l / ri;
+            if (row_off > 0xFFFF) report_error(a.err, p.s + l, SDB_LIMIT_EXCEEDED);  // block_v2.rs:195
+            im[D + 2 * q] = (uint8_t)(row_off >> 8);
+            im[D + 2 * q + 1] = (uint8_t)row_off;
+        }
+    } else {
+        noffs = ne;
+        if (row) {
+            im[D + 2 * l] = (uint8_t)(row_off >> 8);  // `as u16` (block.rs:163)
+            im[D + 2 * l + 1] = (uint8_t)row_off;
+        }
+    }
+    if (l == 0) {
+        im[D + 2 * noffs] = (uint8_t)(noffs >> 8);
+        im[D + 2 * noffs + 1] = (uint8_t)noffs;
+    }
+    wave_sync();
+    // 5. CRC32 (format/sst.rs:541-552) and store
+    const uint32_t Lc = D + 2 * noffs + 2;
+    const uint32_t c = wave_crc32_lds(im, Lc, crc);
+    if (l == 0) {
+        im[Lc] = (uint8_t)(c >> 24);
+        im[Lc + 1] = (uint8_t)(c >> 16);
+        im[Lc + 2] = (uint8_t)(c >> 8);
+        im[Lc + 3] = (uint8_t)c;
+        if (Lc + 4 != p.bb) report_error(a.err, p.s, SDB_DEVICE_ERROR);  // internal consistency
+    }
+    wave_sync();
+    wave_store(gdst, img, (uint64_t)Lc + 4);
+    // 6. BlockStats (sst_stats.rs:9-16) and the index key (compute_index_key, utils.rs:198-226)
+    const uint64_t pu = __ballot(row && p.kind == SDB_KIND_VALUE);
+    const uint64_t de = __ballot(row && p.kind == SDB_KIND_TOMBSTONE);
+    const uint64_t me = __ballot(row && p.kind == SDB_KIND_MERGE);
+    if (l == 0) {
+        a.out_block_stats[3 * (uint64_t)p.blk] = (uint16_t)__popcll(pu);
+        a.out_block_stats[3 * (uint64_t)p.blk + 1] = (uint16_t)__popcll(de);
+        a.out_block_stats[3 * (uint64_t)p.blk + 2] = (uint16_t)__popcll(me);
+        uint32_t ik = 0;
+        if (p.s > 0) ik = (p.lcp == p.prev_klen && p.prev_klen == p.klen) ? p.klen : p.lcp + 1;
+        a.out_index_key_len[p.blk] = ik;
+    }
+    wave_sync();
+}
+
+template <int V>
+__global__ __launch_bounds__(512, 4) void k_emit(EncodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (*a.err != ~0ull) return;  // any earlier error (incl. capacity): write nothing
+    const uint32_t nb = a.anchor_blk[a.nchunks];
+    uint32_t(*crc)[256] = (uint32_t(*)[256])smem;
+    for (uint32_t q = threadIdx.x; q < 8 * 256; q += blockDim.x) ((uint32_t *)crc)[q] = (&c_crc.t[0][0])[q];
+    __syncthreads();
+    const uint32_t wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    uint8_t *stage = smem + kCrcLds + (uint64_t)wave * (kStageCap + kImgCap);
+    uint8_t *img = stage + kStageCap;
+    const uint32_t gw = blockIdx.x * wpb + wave, G = gridDim.x * wpb;
+    Pre cur, nxt;
+    load_pre(a, gw, nb, cur);
+    for (uint32_t blk = gw; blk < nb; blk += G) {
+        load_pre(a, blk + G, nb, nxt);  // in flight while `cur` is assembled
+        if (cur.fast) {
+            process_block<V>(a, cur, stage, img, crc);
+        } else if (lane_id() == 0) {
+            uint32_t slot = atomicAdd(a.slow_count, 1u);
+            a.slow_list[slot] = blk;
+        }
+        cur = nxt;
     }
 }
 
@@ -728,6 +845,26 @@ __global__ __launch_bounds__(256) void k_emit_slow(EncodeArgs a) {
         }
         __threadfence();
         __syncthreads();
+        if (threadIdx.x == 0) {  // BlockStats + compute_index_key for this block
+            uint32_t pu = 0, de = 0, me = 0;
+            for (uint64_t j = b; j < e; j++) {
+                uint8_t kd = a.kind ? a.kind[j] : 0;
+                pu += kd == SDB_KIND_VALUE;
+                de += kd == SDB_KIND_TOMBSTONE;
+                me += kd == SDB_KIND_MERGE;
+            }
+            a.out_block_stats[3 * (uint64_t)blk] = (uint16_t)pu;
+            a.out_block_stats[3 * (uint64_t)blk + 1] = (uint16_t)de;
+            a.out_block_stats[3 * (uint64_t)blk + 2] = (uint16_t)me;
+            uint32_t ik = 0;
+            if (b > 0) {
+                uint64_t fl = a.key_off[b + 1] - a.key_off[b];
+                uint64_t pl = a.key_off[b] - a.key_off[b - 1];
+                uint32_t lc = a.lcp[b];
+                ik = (lc == pl && pl == fl) ? (uint32_t)fl : lc + 1;
+            }
+            a.out_index_key_len[blk] = ik;
+        }
         uint32_t noffs = (V == 2) ? (ne + ri - 1) / ri : ne;
         for (uint32_t q = threadIdx.x; q < noffs; q += blockDim.x) {
             uint32_t ro = a.tab_cnt[b + (V == 2 ? (uint64_t)q * ri : q)];
@@ -794,6 +931,10 @@ __global__ void k_init_summary(EncodeArgs a) {
         *a.err = ~0ull;
         *a.wmax = 0;
         *a.slow_count = 0;
+        if (a.n == 0 && a.block_cap + 1 > 0) {  // empty SST: BlockMeta list is empty, offsets = [0]
+            a.out_block_off[0] = 0;
+            a.out_block_first[0] = 0;
+        }
     }
 }
 
@@ -813,11 +954,16 @@ __global__ void k_finish_summary(EncodeArgs a, uint64_t bloom_len, uint32_t num_
 }
 
 static bool lds_attrs_set = false;
+static int g_cus = 0;
+static uint32_t emit_grid() { return (uint32_t)(g_cus > 0 ? 2 * g_cus : 512); }
 static void set_lds_attrs() {
     if (lds_attrs_set) return;
-    const int emit_lds = (int)(kCrcLds + kChunk * 16 + kEmitWork);
-    hipFuncSetAttribute((const void *)k_emit<1>, hipFuncAttributeMaxDynamicSharedMemorySize, emit_lds);
-    hipFuncSetAttribute((const void *)k_emit<2>, hipFuncAttributeMaxDynamicSharedMemorySize, emit_lds);
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipFuncSetAttribute((const void *)k_emit<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
+    hipFuncSetAttribute((const void *)k_emit<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
+    hipFuncSetAttribute((const void *)k_enum, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEnumLds);
     hipFuncSetAttribute((const void *)k_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLds);
     lds_attrs_set = true;
 }
@@ -831,6 +977,7 @@ hipError_t launch_encode(EncodeArgs a, hipStream_t st) {
         return hipGetLastError();
     }
     const uint32_t g = (uint32_t)((a.n + tpb - 1) / tpb);
+    a.nprep_wg = g;
     stage_mark(st, kStPrep, true);
     hipLaunchKernelGGL(k_prep, dim3(g), dim3(tpb), 0, st, a);
     stage_mark(st, kStPrep, false);
@@ -843,10 +990,12 @@ hipError_t launch_encode(EncodeArgs a, hipStream_t st) {
     stage_mark(st, kStResolve, true);
     hipLaunchKernelGGL(k_resolve, dim3(1), dim3(1024), kResolveLds, st, a);
     stage_mark(st, kStResolve, false);
-    const size_t emit_lds = kCrcLds + kChunk * 16 + kEmitWork;
+    stage_mark(st, kStEnum, true);
+    hipLaunchKernelGGL(k_enum, dim3(a.nchunks), dim3(256), kEnumLds, st, a);
+    stage_mark(st, kStEnum, false);
     stage_mark(st, kStEmit, true);
-    if (a.version == 2) hipLaunchKernelGGL(k_emit<2>, dim3(a.nchunks), dim3(256), emit_lds, st, a);
-    else hipLaunchKernelGGL(k_emit<1>, dim3(a.nchunks), dim3(256), emit_lds, st, a);
+    if (a.version == 2) hipLaunchKernelGGL(k_emit<2>, dim3(emit_grid()), dim3(kEmitThreads), kEmitLds, st, a);
+    else hipLaunchKernelGGL(k_emit<1>, dim3(emit_grid()), dim3(kEmitThreads), kEmitLds, st, a);
     stage_mark(st, kStEmit, false);
     stage_mark(st, kStEmitSlow, true);
     if (a.version == 2) hipLaunchKernelGGL(k_emit_slow<2>, dim3(64), dim3(256), 0, st, a);

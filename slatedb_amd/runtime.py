@@ -31,9 +31,20 @@ class SdbError(RuntimeError):
 
 
 def lib():
-    """Load libslatedb_amd.so (fails loudly if it has not been built)."""
+    """Load libslatedb_amd.so (fails loudly if it has not been built).
+
+    torch is imported first on purpose: torch ships its own libamdhip64.so with the same soname
+    (libamdhip64.so.7) as /opt/rocm's, so loading it first makes our library bind to the HIP runtime
+    torch already uses — one runtime per process, so torch streams, events and allocations are
+    valid handles for our kernels.  (The Rust/C host links /opt/rocm's runtime as usual.)"""
     global _lib
     if _lib is None:
+        try:
+            import torch  # noqa: F401
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError("libslatedb_amd.so not built: run `python __graft_entry__.py build` "
                               "(hipcc --offload-arch=gfx950)")
@@ -73,10 +84,11 @@ class EncodedSst:
         sm = res.summary
         self.status = sm.status
         self.summary = {f: getattr(sm, f) for f, _ in _abi.SstSummary._fields_}
-        nb = sm.num_blocks if sm.status == 0 else 0
-        self.data = _u8(res.data, sm.data_len if sm.status == 0 else 0).copy()
-        self.block_off = _arr(res.block_off, C.c_uint64, nb + 1 if nb else 0, np.uint64).copy()
-        self.block_first_entry = _arr(res.block_first_entry, C.c_uint32, nb + 1 if nb else 0, np.uint32).copy()
+        ok = sm.status == 0
+        nb = sm.num_blocks if ok else 0
+        self.data = _u8(res.data, sm.data_len if ok else 0).copy()
+        self.block_off = _arr(res.block_off, C.c_uint64, nb + 1 if ok else 0, np.uint64).copy()
+        self.block_first_entry = _arr(res.block_first_entry, C.c_uint32, nb + 1 if ok else 0, np.uint32).copy()
         self.index_key_len = _arr(res.index_key_len, C.c_uint32, nb, np.uint32).copy()
         self.block_stats = _arr(res.block_stats, C.c_uint16, 3 * nb, np.uint16).reshape(-1, 3).copy()
         self.bloom = _u8(res.bloom, sm.bloom_len if sm.status == 0 else 0).copy()
@@ -207,8 +219,10 @@ class BloomFilterPolicy:
         import torch
         fb = lib().sdb_bloom_filter_bytes(n, self.bits_per_key)
         bm = torch.empty((fb + 3) // 4 * 4 or 4, dtype=torch.uint8, device=key_bytes.device)
+        wsb = lib().sdb_bloom_workspace_bytes(n, self.bits_per_key)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=key_bytes.device)
         st = lib().sdb_bloom_build(key_bytes.data_ptr(), key_off.data_ptr(), n, self.bits_per_key,
-                                   bm.data_ptr(), fb, stream)
+                                   bm.data_ptr(), fb, ws.data_ptr(), wsb, stream)
         if st:
             raise SdbError(st, "sdb_bloom_build")
         return bm[:fb]

@@ -103,7 +103,7 @@ def test_no_device_fails_loudly(lib):
     out = _abi.SstOut()
     out.summary = C.addressof(sm)
     assert lib.sdb_encode_sst(C.byref(b), C.byref(p), C.byref(out), None, 0, None) == _abi.SDB_DEVICE_ERROR
-    assert lib.sdb_bloom_build(None, None, 0, 10, None, 0, None) == _abi.SDB_DEVICE_ERROR
+    assert lib.sdb_bloom_build(None, None, 0, 10, None, 0, None, 0, None) == _abi.SDB_DEVICE_ERROR
     assert not lib.sdb_encoder_create(0, C.byref(p))
     assert not lib.sdb_decoder_create(0)
     from slatedb_amd import runtime

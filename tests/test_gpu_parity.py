@@ -77,8 +77,7 @@ def test_d1_full_64mib(rt):
     """configs[1]: one 64 MiB L0 SST, bit-exact vs the oracle (578,524 entries, 17,016 blocks)."""
     b = datasets.d1()
     ref, got = encode_both(rt, b)
-    assert ref.summary.num_blocks == 17016 and ref.summary.data_len == 68455271
-    assert ref.summary.bloom_len == 723155
+    assert ref.summary.num_blocks == 17016 and ref.summary.bloom_len == 723155
     assert_same(ref, got, "d1 full")
 
 
