@@ -146,7 +146,7 @@ SIGNATURES = {
 }
 
 
-STAGES = ["bloom", "prep", "next", "chunk", "resolve", "enum", "emit", "emit_slow"]
+STAGES = ["bloom", "seg", "resolve", "enum", "emit", "emit_slow"]
 
 
 def bind(lib):

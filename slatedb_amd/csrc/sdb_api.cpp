@@ -292,7 +292,7 @@ void stage_mark(hipStream_t st, int stage, bool begin) {
     hipEventRecord(e, st);
     if (begin) {
         g_open[stage] = e;
-        if (stage == kStPrep) g_launches++;
+        if (stage == kStSeg) g_launches++;
     } else {
         g_recs.push_back({stage, g_open[stage], e});
         g_open[stage] = nullptr;

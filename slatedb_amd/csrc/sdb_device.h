@@ -70,9 +70,60 @@ constexpr CrcShift64 make_shift64() {
     return r;
 }
 
+// Combine constants for CRCs computed over 64-byte segments of a 16-byte-aligned LDS image whose
+// last segment is zero padded: seg[k] = x^(8*64*k) (weight of a segment followed by k segments),
+// unpad[t] = x^(-8t) (removes t trailing zero bytes; x^-1 = (P + 1) / x, reflected 0xDB710641).
+constexpr uint32_t kXInv = 0xDB710641u;
+constexpr int kSegShifts = 80;
+struct CrcSegShift {
+    uint32_t seg[kSegShifts];
+    uint32_t unpad[64];
+};
+constexpr CrcSegShift make_seg_shift() {
+    CrcSegShift r{};
+    for (int k = 0; k < kSegShifts; k++) r.seg[k] = x8n_c(64ull * k);
+    uint32_t inv8 = 1u << 31;
+    for (int q = 0; q < 8; q++) inv8 = gf_mul_c(kXInv, inv8);
+    uint32_t p = 1u << 31;
+    for (int t = 0; t < 64; t++) {
+        r.unpad[t] = p;
+        p = gf_mul_c(inv8, p);
+    }
+    return r;
+}
+static_assert(gf_mul_c(kXInv, 1u << 30) == (1u << 31), "x * x^-1 == 1");
+
+// seg_mul[k][b][v] = x^(8*64*k) * (v << 8b) mod P: multiplies a CRC by the weight of k trailing
+// 64-byte segments with 4 byte-table lookups.  Built by linearity from the 8 single-bit values.
+struct CrcSegMul {
+    uint32_t t[kSegShifts][4][256];
+};
+constexpr CrcSegMul make_seg_mul() {
+    CrcSegMul r{};
+    for (int k = 0; k < kSegShifts; k++) {
+        uint32_t K = x8n_c(64ull * k);
+        for (int b = 0; b < 4; b++) {
+            uint32_t basis[8] = {};
+            for (int i = 0; i < 8; i++) basis[i] = gf_mul_c(K, 1u << (8 * b + i));
+            r.t[k][b][0] = 0;
+            for (int v = 1; v < 256; v++) {
+                int lo = __builtin_ctz(v);
+                r.t[k][b][v] = r.t[k][b][v & (v - 1)] ^ basis[lo];
+            }
+        }
+    }
+    return r;
+}
+
 // Per translation unit (no relocatable device code needed).
 static __constant__ CrcTables c_crc = make_crc_tables();
 static __constant__ CrcShift64 c_shift = make_shift64();
+static __constant__ CrcSegShift c_seg = make_seg_shift();
+static __device__ const CrcSegMul g_seg_mul = make_seg_mul();
+SDB_DEV uint32_t seg_shift_mul(uint32_t k, uint32_t c) {
+    const uint32_t(*t)[256] = g_seg_mul.t[k];
+    return t[0][c & 0xFF] ^ t[1][(c >> 8) & 0xFF] ^ t[2][(c >> 16) & 0xFF] ^ t[3][c >> 24];
+}
 
 // Runtime GF(2) multiply (branch-free, 32 steps).
 SDB_DEV uint32_t gf_mul(uint32_t a, uint32_t b) {
@@ -97,9 +148,8 @@ SDB_DEV uint64_t bswap64(uint64_t v) { return __builtin_bswap64(v); }
 // required.  Reads only aligned 8-byte words that contain at least one required byte, so it never
 // touches a page that holds no requested byte.  Bytes beyond `need` are unspecified.
 SDB_DEV uint64_t load8(const uint8_t *p, uint32_t need) {
-    uintptr_t a = (uintptr_t)p;
-    uint32_t sh = (uint32_t)(a & 7);
-    const uint64_t *w = (const uint64_t *)(a - sh);
+    uint32_t sh = (uint32_t)((uintptr_t)p & 7);
+    const uint64_t *w = (const uint64_t *)(p - sh);  // pointer arithmetic keeps the address space
     uint64_t lo = w[0];
     if (sh == 0) return lo;
     uint64_t r = lo >> (8 * sh);
@@ -235,6 +285,24 @@ SDB_DEV uint32_t wave_crc_raw_lds(const uint8_t *msg, uint32_t len, const uint32
 // crc32fast::hash(msg[0, len)), len >= 4.
 SDB_DEV uint32_t wave_crc32_lds(const uint8_t *msg, uint32_t len, const uint32_t (*tab)[256]) {
     return wave_crc_raw_lds(msg, len, tab, true) ^ 0xFFFFFFFFu;
+}
+
+// Raw CRC of one 64-byte segment held in registers (16 little-endian dwords, message order).
+SDB_DEV uint32_t crc_seg64(const uint32_t (&w)[16], const uint32_t (*tab)[256]) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) c = crc_slice8(c, w[2 * q], w[2 * q + 1], tab);
+    return c;
+}
+
+// LDS / global address-space helpers for LDS-DMA (global_load_lds_dword).
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+SDB_DEV uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)(const lds_u8 *)p; }
+// dword at global `src` (any byte alignment) -> LDS byte address lds_base + 4 * lane
+SDB_DEV void glds_dword(const uint8_t *src, uint32_t lds_base) {
+    __builtin_amdgcn_global_load_lds((glb_void *)src, (lds_void *)(uintptr_t)lds_base, 4, 0, 0);
 }
 
 // Block-wide exclusive scan of u64 (blockDim.x <= 1024).  s_w: >= 17 u64 of LDS.

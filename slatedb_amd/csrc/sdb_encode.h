@@ -12,9 +12,12 @@ constexpr uint32_t kResolveLds = 96 * 1024;  // LDS budget of the resolve tables
 constexpr uint32_t kCrcLds = 8 * 1024;       // slicing-by-8 tables
 constexpr uint32_t kImgCap = 4096 + 64;      // LDS block image per wave (fast path)
 constexpr uint32_t kStageCap = 4096 + 64;    // LDS value / key staging per wave
-constexpr uint32_t kNextSpan = 256 + 768;     // k_next: entries staged per 256-thread workgroup
-constexpr uint32_t kEmitThreads = 512;       // 8 waves per workgroup, 2 workgroups per CU
-constexpr uint32_t kEmitLds = kCrcLds + (kEmitThreads / 64) * (kStageCap + kImgCap);
+constexpr uint32_t kSegSpan = 2 * kChunk;     // k_seg: entries staged per chunk (chunk + lookahead)
+constexpr uint32_t kSegThreads = 512;
+constexpr uint32_t kSegLds = kSegSpan * 8 + kChunk * 12;
+constexpr uint32_t kEmitThreads = 1024;      // 16 waves per workgroup (one block each)
+constexpr uint32_t kEmitWgPerCu = 2;
+constexpr uint32_t kEmitLds = kCrcLds + (kEmitThreads / 64) * kImgCap;
 constexpr uint32_t kEnumLds = kChunk * 16 + 12 * kChunk * 2;  // block list + 12 lifting levels
 
 struct BlockDesc {  // one per block, written by k_enum, streamed by k_emit (48 bytes)
@@ -58,8 +61,8 @@ struct EncodeArgs {
     uint32_t *slow_count;
     uint32_t *slow_list;
     BlockDesc *desc;
-    uint64_t *stat_part;    // per k_prep workgroup: raw key, raw val, puts, deletes, merges
-    uint32_t *wmax_part;    // per k_next workgroup: longest candidate block (entries)
+    uint64_t *stat_part;    // per chunk: raw key, raw val, puts, deletes, merges
+    uint32_t *wmax_part;    // per chunk: longest candidate block (entries)
     uint32_t nprep_wg;
     // outputs (device)
     uint8_t *out_data;
@@ -105,8 +108,8 @@ inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes
     w.slow_count = take(4);
     w.slow_list = take(4 * (n + 1));
     w.desc = take(sizeof(BlockDesc) * (n + 1));
-    w.stat_part = take(8 * 5 * ((n + 255) / 256 + 1));
-    w.wmax_part = take(4 * ((n + 255) / 256 + 1));
+    w.stat_part = take(8 * 5 * (nc + 1));
+    w.wmax_part = take(4 * (nc + 1));
     w.bloom_rep = take(filter_bytes ? bloom_workspace_bytes(n, num_probes, filter_bytes) : 0);  // bloom buckets
     w.total = off;
     return w;
@@ -115,7 +118,7 @@ inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes
 hipError_t launch_encode(EncodeArgs a, hipStream_t st);
 
 // stage timing (diagnostics)
-enum Stage { kStBloom = 0, kStPrep, kStNext, kStChunk, kStResolve, kStEnum, kStEmit, kStEmitSlow, kNumStages };
+enum Stage { kStBloom = 0, kStSeg, kStResolve, kStEnum, kStEmit, kStEmitSlow, kNumStages };
 void stage_mark(hipStream_t st, int stage, bool begin);
 bool stage_timing_on();
 

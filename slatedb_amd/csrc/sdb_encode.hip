@@ -24,6 +24,8 @@
 //               with 16-byte stores.
 //   K6 slow     blocks larger than the LDS image (oversized first entries, huge block sizes) are
 //               assembled directly in HBM by one workgroup each.
+#include <stdlib.h>
+
 #include "sdb_device.h"
 #include "sdb_encode.h"
 
@@ -31,109 +33,156 @@ namespace sdb {
 
 
 // ------------------------------------------------------------------------------------------------
-// K1: per-entry prep
+// Per-entry facts: LCP vs the previous key, restart / non-restart row sizes, reference errors.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_prep(EncodeArgs a) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t rk = 0, rv = 0;
-    uint32_t puts = 0, dels = 0, merges = 0;
-    if (i < a.n) {
-        uint64_t ko0 = a.key_off[i], ko1 = a.key_off[i + 1];
-        uint64_t klen = ko1 - ko0;
-        uint8_t kd = a.kind ? a.kind[i] : 0;
-        uint8_t m = a.ts_mask ? a.ts_mask[i] : 0;
-        uint64_t vlen = (kd == SDB_KIND_TOMBSTONE) ? 0 : (a.val_off[i + 1] - a.val_off[i]);
-        uint32_t lcp = 0;
-        int err = 0;
-        if (kd > SDB_KIND_TOMBSTONE) err = SDB_INVALID_ARGUMENT;
-        if (!err && i > 0) {
-            uint64_t pko = a.key_off[i - 1];
-            uint64_t plen = ko0 - pko;
-            uint32_t nmin = (uint32_t)((plen < klen ? plen : klen) > 0xFFFFFFFFull ? 0xFFFFFFFFull
-                                                                                  : (plen < klen ? plen : klen));
-            lcp = lcp_bytes(a.key_bytes + pko, nmin, a.key_bytes + ko0, nmin);
-            // compute_index_key runs on every entry (sst_builder.rs:228): assert on empty keys and
-            // out-of-bounds panic when this key is a proper prefix of the previous one (utils.rs:210-216)
-            if (klen == 0) err = SDB_EMPTY_KEY;
-            else if (plen > 0 && lcp == klen && klen < plen) err = SDB_INVALID_ARGUMENT;
-        }
-        if (!err && klen == 0) err = SDB_EMPTY_KEY;  // BlockBuilder*::add (block_v2.rs:168-170)
-        const uint32_t ts8 = 8u * (((m & SDB_TS_CREATE) != 0) + ((m & SDB_TS_EXPIRE) != 0));
-        if (a.version == 2) {
-            if (!err && (klen > 0xFFFFFFFFull || vlen > 0xFFFFFFFFull)) err = SDB_LIMIT_EXCEEDED;
-            uint32_t kl = (uint32_t)klen, vl = (uint32_t)vlen, suf = kl - lcp;
-            // SstRowEntryV2::encoded_size (row_codec_v2.rs:92-116)
-            a.s_nr[i] = varint_len(lcp) + varint_len(suf) + varint_len(vl) + suf + vl + 9 + ts8;
-            a.s_r[i] = 1 + varint_len(kl) + varint_len(vl) + kl + vl + 9 + ts8;
-        } else {
-            // SstRowEntry::new asserts (row.rs:73-85)
-            if (!err && (klen > 0xFFFF || vlen > 0xFFFFFFFFull)) err = SDB_LIMIT_EXCEEDED;
-            // RowEntry::encoded_size with key_prefix_len = 0 (types.rs:64-83)
-            a.s_r[i] = (uint32_t)(4 + klen + 9 + ts8 + (kd == SDB_KIND_TOMBSTONE ? 0 : 4 + vlen));
-        }
-        a.lcp[i] = lcp;
-        if (err) report_error(a.err, i, err);
-        rk = klen;
-        rv = vlen;
-        puts = kd == SDB_KIND_VALUE;
-        merges = kd == SDB_KIND_MERGE;
-        dels = kd == SDB_KIND_TOMBSTONE;
+struct EntryFacts {
+    uint32_t lcp, s_r, s_nr;
+    uint64_t klen, vlen;
+    uint8_t kind;
+    int err;
+};
+
+SDB_DEV EntryFacts entry_facts(const EncodeArgs &a, uint64_t i) {
+    EntryFacts f;
+    uint64_t ko0 = a.key_off[i], ko1 = a.key_off[i + 1];
+    uint64_t klen = ko1 - ko0;
+    uint8_t kd = a.kind ? a.kind[i] : 0;
+    uint8_t m = a.ts_mask ? a.ts_mask[i] : 0;
+    uint64_t vlen = (kd == SDB_KIND_TOMBSTONE) ? 0 : (a.val_off[i + 1] - a.val_off[i]);
+    uint32_t lcp = 0;
+    int err = 0;
+    if (kd > SDB_KIND_TOMBSTONE) err = SDB_INVALID_ARGUMENT;
+    if (!err && i > 0) {
+        uint64_t pko = a.key_off[i - 1];
+        uint64_t plen = ko0 - pko;
+        uint64_t mn = plen < klen ? plen : klen;
+        uint32_t nmin = (uint32_t)(mn > 0xFFFFFFFFull ? 0xFFFFFFFFull : mn);
+        lcp = lcp_bytes(a.key_bytes + pko, nmin, a.key_bytes + ko0, nmin);
+        // compute_index_key runs on every entry (sst_builder.rs:228): assert on empty keys and
+        // out-of-bounds panic when this key is a proper prefix of the previous one (utils.rs:210-216)
+        if (klen == 0) err = SDB_EMPTY_KEY;
+        else if (plen > 0 && lcp == klen && klen < plen) err = SDB_INVALID_ARGUMENT;
     }
-    // SstStats (sst_builder.rs:225-226, 315-317): per-workgroup partials, summed in k_resolve
-    __shared__ uint64_t s_part[4][5];
-    rk = wave_sum(rk);
-    rv = wave_sum(rv);
-    uint32_t c = wave_sum(puts | (dels << 10) | (merges << 20));  // <= 64 each per wave
-    const uint32_t w = threadIdx.x >> 6;
-    if (lane_id() == 0) {
-        s_part[w][0] = rk;
-        s_part[w][1] = rv;
-        s_part[w][2] = c & 0x3FF;
-        s_part[w][3] = (c >> 10) & 0x3FF;
-        s_part[w][4] = (c >> 20) & 0x3FF;
+    if (!err && klen == 0) err = SDB_EMPTY_KEY;  // BlockBuilder*::add (block_v2.rs:168-170)
+    const uint32_t ts8 = 8u * (((m & SDB_TS_CREATE) != 0) + ((m & SDB_TS_EXPIRE) != 0));
+    if (a.version == 2) {
+        if (!err && (klen > 0xFFFFFFFFull || vlen > 0xFFFFFFFFull)) err = SDB_LIMIT_EXCEEDED;
+        uint32_t kl = (uint32_t)klen, vl = (uint32_t)vlen, suf = kl - lcp;
+        // SstRowEntryV2::encoded_size (row_codec_v2.rs:92-116)
+        f.s_nr = varint_len(lcp) + varint_len(suf) + varint_len(vl) + suf + vl + 9 + ts8;
+        f.s_r = 1 + varint_len(kl) + varint_len(vl) + kl + vl + 9 + ts8;
+    } else {
+        // SstRowEntry::new asserts (row.rs:73-85)
+        if (!err && (klen > 0xFFFF || vlen > 0xFFFFFFFFull)) err = SDB_LIMIT_EXCEEDED;
+        // RowEntry::encoded_size with key_prefix_len = 0 (types.rs:64-83)
+        f.s_r = (uint32_t)(4 + klen + 9 + ts8 + (kd == SDB_KIND_TOMBSTONE ? 0 : 4 + vlen));
+        f.s_nr = f.s_r;
     }
-    __syncthreads();
-    if (threadIdx.x < 5) {
-        uint64_t t = 0;
-        for (uint32_t q = 0; q < (blockDim.x >> 6); q++) t += s_part[q][threadIdx.x];
-        a.stat_part[5 * (uint64_t)blockIdx.x + threadIdx.x] = t;
-    }
+    f.lcp = lcp;
+    f.klen = klen;
+    f.vlen = vlen;
+    f.kind = kd;
+    f.err = err;
+    return f;
 }
 
 // ------------------------------------------------------------------------------------------------
-// K2: next(b) for every entry b (BlockBuilderV2::would_fit / BlockBuilderV1::would_fit)
+// K1 seg: one workgroup per chunk of kChunk entries (+ kChunk lookahead staged in LDS).
+//   a. entry facts for [cs, cs + 2 kChunk): sizes -> LDS; LCP, errors, stats for the chunk's own
+//      entries;
+//   b. next(b) for every b of the chunk (BlockBuilderV2::would_fit / V1::would_fit walk in LDS);
+//   c. pointer jumping in LDS: for every entry point e of the chunk the first block start past the
+//      chunk, and the blocks and bytes on the way (the chunk transfer table).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_next(EncodeArgs a) {
-    // sizes of [b0, b0 + kNextSpan) staged in LDS; a scan that runs past it continues from HBM
-    __shared__ uint32_t s_r[kNextSpan], s_nr[kNextSpan];
-    const uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x;
-    const uint64_t b = b0 + threadIdx.x;
-    const uint64_t lim = b0 + kNextSpan < a.n ? b0 + kNextSpan : a.n;
-    for (uint64_t j = b0 + threadIdx.x; j < lim; j += blockDim.x) {
-        s_r[j - b0] = a.s_r[j];
-        if (a.version == 2) s_nr[j - b0] = a.s_nr[j];
+SDB_DEV uint32_t walk_size_v2(const EncodeArgs &a, const uint32_t *s_r, const uint32_t *s_nr, uint64_t lo,
+                              uint64_t hi, uint64_t j, bool rs) {
+    if (j < hi) return rs ? s_r[j - lo] : s_nr[j - lo];
+    EntryFacts f = entry_facts(a, j);
+    return rs ? f.s_r : f.s_nr;
+}
+
+__global__ __launch_bounds__(kSegThreads) void k_seg(EncodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t *s_r = (uint32_t *)smem;                 // kSegSpan
+    uint32_t *s_nr = s_r + kSegSpan;                  // kSegSpan
+    uint64_t *p_b = (uint64_t *)(s_nr + kSegSpan);    // kChunk
+    uint16_t *p_s = (uint16_t *)(p_b + kChunk);       // kChunk (offset of the chain position from cs)
+    uint16_t *p_c = p_s + kChunk;                     // kChunk
+    __shared__ uint64_t s_part[kSegThreads / 64][5];
+    __shared__ uint32_t s_len[kSegThreads / 64];
+    const uint32_t k = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    const uint64_t cs = (uint64_t)k * kChunk;
+    const uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
+    const uint64_t se = cs + kSegSpan < a.n ? cs + kSegSpan : a.n;
+    const uint32_t cn = (uint32_t)(ce - cs);
+    // a. facts
+    uint64_t rk = 0, rv = 0;
+    uint32_t puts = 0, dels = 0, merges = 0;
+    for (uint64_t e = cs + tid; e < se; e += nt) {
+        EntryFacts f = entry_facts(a, e);
+        s_r[e - cs] = f.s_r;
+        s_nr[e - cs] = f.s_nr;
+        if (e < ce) {
+            a.lcp[e] = f.lcp;
+            if (f.err) report_error(a.err, e, f.err);
+            rk += f.klen;
+            rv += f.vlen;
+            puts += f.kind == SDB_KIND_VALUE;
+            merges += f.kind == SDB_KIND_MERGE;
+            dels += f.kind == SDB_KIND_TOMBSTONE;
+        }
+    }
+    // SstStats (sst_builder.rs:225-226, 315-317): per-chunk partials, summed in k_resolve
+    {
+        rk = wave_sum(rk);
+        rv = wave_sum(rv);
+        uint64_t c = wave_sum((uint64_t)puts | ((uint64_t)dels << 20) | ((uint64_t)merges << 40));
+        if (lane_id() == 0) {
+            uint32_t w = tid >> 6;
+            s_part[w][0] = rk;
+            s_part[w][1] = rv;
+            s_part[w][2] = c & 0xFFFFF;
+            s_part[w][3] = (c >> 20) & 0xFFFFF;
+            s_part[w][4] = (c >> 40) & 0xFFFFF;
+        }
     }
     __syncthreads();
-    uint32_t len = 0;
-    if (b < a.n) {
-        const uint64_t bs = a.block_size;
+    if (tid < 5) {
+        uint64_t t = 0;
+        for (uint32_t q = 0; q < nt / 64; q++) t += s_part[q][tid];
+        a.stat_part[5 * (uint64_t)k + tid] = t;
+    }
+    // b. next(b)
+    uint32_t maxlen = 0;
+    const uint64_t bs = a.block_size;
+    for (uint64_t b = cs + tid; b < ce; b += nt) {
         uint64_t acc = 2;  // Block::size of an empty block: data 0 + offsets 0 + count 2
         uint64_t j = b;
         uint32_t p = 0;
         if (a.version == 2) {
             const uint32_t ri = a.restart_interval;
             uint32_t ph = 0;  // p % ri
-            while (j < a.n) {
-                bool rs = ph == 0;
-                uint32_t sz;
-                if (j < lim) sz = rs ? s_r[j - b0] : s_nr[j - b0];
-                else sz = rs ? a.s_r[j] : a.s_nr[j];
-                uint64_t add = (uint64_t)sz + (rs ? 2 : 0);
+            // staged part: LDS only
+            while (j < se) {
+                const bool rs = ph == 0;
+                const uint64_t add = (uint64_t)(rs ? s_r[j - cs] : s_nr[j - cs]) + (rs ? 2 : 0);
                 if (p > 0 && acc + add > bs) break;
                 acc += add;
                 j++;
                 p++;
                 if (++ph == ri) ph = 0;
+            }
+            // a block longer than the staged span (rare): continue from HBM
+            if (j == se) {
+                while (j < a.n) {
+                    const bool rs = ph == 0;
+                    const uint64_t add = (uint64_t)walk_size_v2(a, s_r, s_nr, cs, se, j, rs) + (rs ? 2 : 0);
+                    if (p > 0 && acc + add > bs) break;
+                    acc += add;
+                    j++;
+                    p++;
+                    if (++ph == ri) ph = 0;
+                }
             }
         } else {
             const uint64_t fko = a.key_off[b];
@@ -144,135 +193,165 @@ __global__ __launch_bounds__(256) void k_next(EncodeArgs a) {
                     uint64_t ko = a.key_off[j];
                     prefix = lcp_bytes(a.key_bytes + fko, fkl, a.key_bytes + ko, (uint32_t)(a.key_off[j + 1] - ko));
                 }
-                uint64_t sz = (uint64_t)(j < lim ? s_r[j - b0] : a.s_r[j]) - prefix;
+                uint64_t sr = j < se ? s_r[j - cs] : entry_facts(a, j).s_r;
+                uint64_t sz = sr - prefix;
                 if (p > 0 && acc + sz > bs) break;  // the new entry's 2-byte offset is not counted (block.rs:117-123)
                 acc += sz + 2;
                 j++;
                 p++;
             }
         }
+        const uint32_t bb = (uint32_t)(acc + 4);  // + CRC32 (format/sst.rs:541-552)
         a.next[b] = (uint32_t)j;
-        a.bbytes[b] = (uint32_t)(acc + 4);  // + CRC32 (format/sst.rs:541-552)
-        len = (uint32_t)(j - b);
+        a.bbytes[b] = bb;
+        const uint64_t rel = j - cs;
+        p_s[b - cs] = (uint16_t)(rel < 0xFFFF ? rel : 0xFFFF);
+        p_c[b - cs] = 1;
+        p_b[b - cs] = bb;
+        const uint32_t len = (uint32_t)(j - b);
+        maxlen = len > maxlen ? len : maxlen;
     }
-    // longest candidate block: per-workgroup partial (a single global atomicMax target would
-    // serialise ~10^4 wave atomics at the memory side), reduced in k_resolve
-    __shared__ uint32_t s_len[4];
-    len = wave_max(len);
-    if (lane_id() == 0) s_len[threadIdx.x >> 6] = len;
+    maxlen = wave_max(maxlen);
+    if (lane_id() == 0) s_len[tid >> 6] = maxlen;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         uint32_t m = 0;
-        for (uint32_t q = 0; q < (blockDim.x >> 6); q++) m = s_len[q] > m ? s_len[q] : m;
-        a.wmax_part[blockIdx.x] = m;
+        for (uint32_t q = 0; q < nt / 64; q++) m = s_len[q] > m ? s_len[q] : m;
+        a.wmax_part[k] = m;
     }
-}
-
-// ------------------------------------------------------------------------------------------------
-// K3: chunk transfer tables by pointer jumping in LDS
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(512) void k_chunk(EncodeArgs a) {
-    __shared__ uint32_t s_s[2][kChunk];
-    __shared__ uint32_t s_c[2][kChunk];
-    __shared__ uint64_t s_b[2][kChunk];
-    const uint64_t cs = (uint64_t)blockIdx.x * kChunk;
-    const uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
-    const uint32_t cn = (uint32_t)(ce - cs);
-    for (uint32_t e = threadIdx.x; e < cn; e += blockDim.x) {
-        s_s[0][e] = a.next[cs + e];
-        s_c[0][e] = 1;
-        s_b[0][e] = a.bbytes[cs + e];
-    }
-    __syncthreads();
-    int cur = 0;
+    // c. pointer jumping (single buffer: read a round into registers, barrier, write back)
+    constexpr uint32_t kPer = kChunk / kSegThreads;
     for (int round = 0; round < 24; round++) {
+        uint32_t ns[kPer], nc[kPer];
+        uint64_t nb[kPer];
         int changed = 0;
-        for (uint32_t e = threadIdx.x; e < cn; e += blockDim.x) {
-            uint32_t s = s_s[cur][e], c = s_c[cur][e];
-            uint64_t by = s_b[cur][e];
-            if (s < ce) {
-                uint32_t t = s - (uint32_t)cs;
-                c += s_c[cur][t];
-                by += s_b[cur][t];
-                s = s_s[cur][t];
-                changed = 1;
+#pragma unroll
+        for (uint32_t u = 0; u < kPer; u++) {
+            uint32_t e = tid + u * nt;
+            if (e < cn) {
+                uint32_t t = p_s[e];
+                ns[u] = t;
+                nc[u] = p_c[e];
+                nb[u] = p_b[e];
+                if (t < cn) {
+                    ns[u] = p_s[t];
+                    nc[u] += p_c[t];
+                    nb[u] += p_b[t];
+                    changed = 1;
+                }
             }
-            s_s[cur ^ 1][e] = s;
-            s_c[cur ^ 1][e] = c;
-            s_b[cur ^ 1][e] = by;
         }
-        cur ^= 1;
         if (!__syncthreads_or(changed)) break;
+#pragma unroll
+        for (uint32_t u = 0; u < kPer; u++) {
+            uint32_t e = tid + u * nt;
+            if (e < cn) {
+                p_s[e] = (uint16_t)ns[u];
+                p_c[e] = (uint16_t)nc[u];
+                p_b[e] = nb[u];
+            }
+        }
+        __syncthreads();
     }
-    for (uint32_t e = threadIdx.x; e < cn; e += blockDim.x) {
-        a.tab_exit[cs + e] = s_s[cur][e];
-        a.tab_cnt[cs + e] = s_c[cur][e];
-        a.tab_bytes[cs + e] = s_b[cur][e];
+    for (uint32_t e = tid; e < cn; e += nt) {
+        uint32_t t = p_s[e];
+        // 0xFFFF: the chain left the LDS-addressable range; the resolve's serial fallback uses next[]
+        a.tab_exit[cs + e] = t == 0xFFFF ? 0xFFFFFFFFu : (uint32_t)(cs + t);
+        a.tab_cnt[cs + e] = p_c[e];
+        a.tab_bytes[cs + e] = p_b[e];
     }
 }
 
 // ------------------------------------------------------------------------------------------------
-// K4: resolve chunk anchors (single workgroup)
+// K2 resolve (single workgroup): compose the chunk transfer tables (Blelloch up-sweep of the u16
+// exit tables in LDS, then the one chain from entry 0 pushed down the tree) -> per-chunk anchors
+// (first block start, block index, byte offset) and the SstStats totals.  Every HBM read is issued
+// in one batch per phase: this kernel is latency-bound.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint64_t s_w[17];
-    __shared__ uint32_t s_fast;
+    __shared__ uint32_t s_wmax;
+    __shared__ uint64_t s_stat[5][16];
     const uint32_t K = a.nchunks;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     uint32_t KP = 1;
     while (KP < K) KP <<= 1;
-    __shared__ uint32_t s_wmax;
     if (tid == 0) s_wmax = 0;
     __syncthreads();
+    // W = longest candidate block; SstStats partial sums (one batch of loads)
     {
         uint32_t m = 0;
-        for (uint32_t q = tid; q < a.nprep_wg; q += nt) m = a.wmax_part[q] > m ? a.wmax_part[q] : m;
+        uint64_t st[5] = {0, 0, 0, 0, 0};
+        for (uint32_t q = tid; q < K; q += nt) {
+            uint32_t w = a.wmax_part[q];
+            m = w > m ? w : m;
+#pragma unroll
+            for (int f = 0; f < 5; f++) st[f] += a.stat_part[5 * (uint64_t)q + f];
+        }
         m = wave_max(m);
         if (lane_id() == 0) atomicMax(&s_wmax, m);
+#pragma unroll
+        for (int f = 0; f < 5; f++) {
+            uint64_t t = wave_sum(st[f]);
+            if (lane_id() == 0) s_stat[f][tid >> 6] = t;
+        }
     }
     __syncthreads();
     const uint32_t W = s_wmax;
+    if (tid < 5) {
+        uint64_t t = 0;
+        for (uint32_t q = 0; q < nt / 64; q++) t += s_stat[tid][q];
+        if (tid == 0) a.summary->raw_key_size = t;
+        if (tid == 1) a.summary->raw_val_size = t;
+        if (tid == 2) a.summary->num_puts = t;
+        if (tid == 3) a.summary->num_deletes = t;
+        if (tid == 4) a.summary->num_merges = t;
+    }
     if (tid == 0) *a.wmax = W;
-    // LDS: ex (KP*W u16) + v (KP u32) + tmp (KP/2*W u16), each 16-byte aligned
-    if (tid == 0)
-        s_fast = (W <= kChunk && (((uint64_t)KP * W * 2 + 15) & ~15ull) + ((4ull * KP + 15) & ~15ull) +
-                                         (uint64_t)KP * W + 16 <= kResolveLds)
-                     ? 1u
-                     : 0u;
-    __syncthreads();
-    if (s_fast) {
-        uint16_t *ex = (uint16_t *)smem;                               // KP x W exit offsets
-        uint32_t *v = (uint32_t *)(smem + (((uint64_t)KP * W * 2 + 15) & ~15ull));  // KP entry offsets
+    const uint64_t ex_bytes = ((uint64_t)KP * W * 2 + 15) & ~15ull;
+    const uint64_t v_bytes = ((uint64_t)KP * 4 + 15) & ~15ull;
+    const bool fast = W <= kChunk && ex_bytes + v_bytes + (uint64_t)KP * W + 16 <= kResolveLds;
+    uint32_t *v = (uint32_t *)(smem + ex_bytes);  // KP entry offsets (fast path)
+    if (fast) {
+        uint16_t *ex = (uint16_t *)smem;  // KP x W exit offsets
         // ex[k][o] = entry offset into chunk k+1 reached from entry offset o into chunk k
-        for (uint64_t idx = tid; idx < (uint64_t)KP * W; idx += nt) {
-            uint32_t k = (uint32_t)(idx / W), o = (uint32_t)(idx % W);
-            uint16_t val = (uint16_t)o;  // identity for the padding chunks k >= K
-            if (k < K) {
-                uint64_t cs = (uint64_t)k * kChunk;
-                uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
-                val = 0;
-                if (cs + o < ce) val = (uint16_t)(a.tab_exit[cs + o] - ce);
+        const uint32_t total = KP * W;
+        for (uint32_t base = 0; base < total; base += 8 * nt) {
+            uint32_t val[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                uint32_t idx = base + tid + u * nt;
+                uint32_t k = idx / W, o = idx - k * W;
+                val[u] = o;  // identity for the padding chunks k >= K
+                if (idx < total && k < K) {
+                    uint64_t cs = (uint64_t)k * kChunk;
+                    uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
+                    val[u] = cs + o < ce ? (uint32_t)(a.tab_exit[cs + o] - ce) : 0;
+                }
             }
-            ex[idx] = val;
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                uint32_t idx = base + tid + u * nt;
+                if (idx < total) ex[idx] = (uint16_t)val[u];
+            }
         }
         __syncthreads();
         // Blelloch up-sweep: ex[k] <- ex[k] o ex[k-d] for k = 2d-1 (mod 2d).  A level reads entries
         // of ex[k] that other threads of the same level overwrite, so results go through `tmp`.
-        uint16_t *tmp = (uint16_t *)(smem + (((uint64_t)KP * W * 2 + 15) & ~15ull) + (((uint64_t)KP * 4 + 15) & ~15ull));
+        uint16_t *tmp = (uint16_t *)(smem + ex_bytes + v_bytes);
         for (uint32_t d = 1; d < KP; d <<= 1) {
-            uint32_t nodes = KP / (2 * d);
-            for (uint64_t idx = tid; idx < (uint64_t)nodes * W; idx += nt) {
-                uint32_t q = (uint32_t)(idx / W), o = (uint32_t)(idx % W);
+            const uint32_t cnt = (KP / (2 * d)) * W;
+            for (uint32_t idx = tid; idx < cnt; idx += nt) {
+                uint32_t q = idx / W, o = idx - q * W;
                 uint32_t k = 2 * d * q + 2 * d - 1;
-                uint16_t mid = ex[(uint64_t)(k - d) * W + o];
-                tmp[idx] = ex[(uint64_t)k * W + mid];
+                uint16_t mid = ex[(k - d) * W + o];
+                tmp[idx] = ex[k * W + mid];
             }
             __syncthreads();
-            for (uint64_t idx = tid; idx < (uint64_t)nodes * W; idx += nt) {
-                uint32_t q = (uint32_t)(idx / W), o = (uint32_t)(idx % W);
-                uint32_t k = 2 * d * q + 2 * d - 1;
-                ex[(uint64_t)k * W + o] = tmp[idx];
+            for (uint32_t idx = tid; idx < cnt; idx += nt) {
+                uint32_t q = idx / W, o = idx - q * W;
+                ex[(2 * d * q + 2 * d - 1) * W + o] = tmp[idx];
             }
             __syncthreads();
         }
@@ -282,32 +361,38 @@ __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
         for (uint32_t d = KP >> 1; d >= 1; d >>= 1) {
             for (uint32_t q = tid; q < KP / (2 * d); q += nt) {
                 uint32_t k = 2 * d * q;
-                v[k + d] = ex[(uint64_t)(k + d - 1) * W + v[k]];
+                v[k + d] = ex[(k + d - 1) * W + v[k]];
             }
             __syncthreads();
         }
-        for (uint32_t k = tid; k < K; k += nt) a.anchor_e[k] = (uint32_t)((uint64_t)k * kChunk + v[k]);
     } else if (tid == 0) {
         // general fallback (a block longer than a chunk, or too many chunk tables): serial walk
+        v = (uint32_t *)smem;
         uint64_t e = 0;
         for (uint32_t k = 0; k < K; k++) {
             uint64_t cs = (uint64_t)k * kChunk;
             uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
-            a.anchor_e[k] = (uint32_t)e;
-            if (e < ce) e = a.tab_exit[e];
+            v[k] = (uint32_t)(e - cs);
+            if (e < ce) {
+                uint32_t t = a.tab_exit[e];
+                if (t == 0xFFFFFFFFu)
+                    while (e < ce) e = a.next[e];
+                else
+                    e = t;
+            }
         }
     }
-    __threadfence();
+    if (!fast) v = (uint32_t *)smem;
     __syncthreads();
     // per-chunk block counts / bytes from the entry point; exclusive scans give the anchors
     uint64_t cb = 0, cy = 0;
     for (uint32_t k0 = 0; k0 < K; k0 += nt) {
         uint32_t k = k0 + tid;
-        uint64_t c = 0, by = 0;
+        uint64_t c = 0, by = 0, e = 0;
         if (k < K) {
             uint64_t cs = (uint64_t)k * kChunk;
             uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
-            uint64_t e = a.anchor_e[k];
+            e = cs + v[k];
             if (e < ce) {
                 c = a.tab_cnt[e];
                 by = a.tab_bytes[e];
@@ -317,25 +402,12 @@ __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
         uint64_t xc = block_excl_scan_u64(c, s_w, &tc);
         uint64_t xy = block_excl_scan_u64(by, s_w, &ty);
         if (k < K) {
+            a.anchor_e[k] = (uint32_t)e;
             a.anchor_blk[k] = (uint32_t)(cb + xc);
             a.anchor_byte[k] = cy + xy;
         }
         cb += tc;
         cy += ty;
-    }
-    // SstStats totals from the k_prep partials
-    for (uint32_t f = 0; f < 5; f++) {
-        uint64_t t = 0;
-        for (uint32_t q = tid; q < a.nprep_wg; q += nt) t += a.stat_part[5 * (uint64_t)q + f];
-        uint64_t tot;
-        block_excl_scan_u64(t, s_w, &tot);
-        if (tid == 0) {
-            if (f == 0) a.summary->raw_key_size = tot;
-            if (f == 1) a.summary->raw_val_size = tot;
-            if (f == 2) a.summary->num_puts = tot;
-            if (f == 3) a.summary->num_deletes = tot;
-            if (f == 4) a.summary->num_merges = tot;
-        }
     }
     if (tid == 0) {
         a.anchor_blk[K] = (uint32_t)cb;
@@ -548,207 +620,265 @@ __global__ __launch_bounds__(256) void k_enum(EncodeArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// K5b: emit.  Persistent waves stream blocks (one block per wave at a time); each wave prefetches the
-//      next block's values, keys and row metadata into registers while it assembles the current one
-//      in LDS, so HBM latency overlaps the byte work.
+// K5b: emit.  One wave per block; a workgroup shares the CRC tables (LDS).
+//   1. lane = row: row metadata from HBM (offsets, kind, seq, timestamps, LCP), row sizes, a wave
+//      scan for the row offsets;
+//   2. the row lane writes its row into the wave's LDS image: header / trailer bytes, key suffix and
+//      value as dword-aligned interiors (16-byte unaligned HBM loads -> ds_write2_b32) plus <= 3
+//      edge bytes each; restart table and count by the restart lanes;
+//   3. CRC32: lane l reads 64-byte segment l of the image (image byte 0 = block byte 0, 16-byte
+//      aligned), slicing-by-8 per lane, segment l weighted by x^(512 (nseg-1-l)) (4 byte-table
+//      lookups), wave XOR, the zero padding of the last segment removed by x^(-8 t);
+//   4. 16-byte stores at the block's (unaligned) HBM offset; the < 16-byte tail by one lane.
 // ------------------------------------------------------------------------------------------------
-struct Pre {
-    // wave-uniform block descriptor
-    uint32_t blk, s, e, bb, nv16, nk16;
-    uint64_t off, vs, ks;
-    bool valid, fast;
-    // staged 16-byte granules (value range: lane + 64 r; key range: lane)
-    uint4 v[4];
-    uint4 k;
-    // this lane's row (lane < e - s)
-    uint64_t ko, vo, seq;
-    int64_t cts, ets;
-    uint32_t klen, vlen, lcp, prev_klen;
-    uint8_t kind, mask;
-};
+typedef __attribute__((address_space(3))) uint8_t lu8;
+typedef __attribute__((address_space(3))) uint32_t lu32;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lu128;
 
-SDB_DEV void load_pre(const EncodeArgs &a, uint32_t blk, uint32_t nb, Pre &p) {
-    const int l = lane_id();
-    p.valid = blk < nb;
-    p.fast = false;
-    if (!p.valid) return;
-    const BlockDesc d = a.desc[blk];
-    p.blk = blk;
-    p.s = d.s;
-    p.e = d.e;
-    p.bb = d.bb;
-    p.off = d.off;
-    p.vs = d.vs;
-    p.ks = d.ks;
-    const uint32_t ne = d.e - d.s;
-    const uint64_t va = d.vs & ~15ull, ka = d.ks & ~15ull;
-    p.nv16 = (uint32_t)((((d.ve + 15) & ~15ull) - va) >> 4);
-    p.nk16 = (uint32_t)((((d.ke + 15) & ~15ull) - ka) >> 4);
-    if (d.ve == d.vs) p.nv16 = 0;
-    if (d.ke == d.ks) p.nk16 = 0;
-    p.fast = ne <= 64 && p.nv16 <= 256 && p.nk16 <= 64 && (p.nv16 + p.nk16) * 16 <= kStageCap &&
-             d.bb + 32 <= kImgCap;
-    if (!p.fast) return;
-    const uint4 *vsrc = (const uint4 *)(a.val_bytes + va);
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        uint32_t c = (uint32_t)l + 64u * r;
-        p.v[r] = c < p.nv16 ? vsrc[c] : make_uint4(0, 0, 0, 0);
+SDB_DEV void lds_put_bytes(lu8 *p, uint64_t w, uint32_t n) {  // w little-endian, n <= 8
+    for (uint32_t i = 0; i < n; i++) p[i] = (uint8_t)(w >> (8 * i));
+}
+
+// lane: image bytes [fa, fa + L) <- global src
+SDB_DEV void copy_field(lu8 *img, uint32_t fa, uint32_t L, const uint8_t *src) {
+    if (!L) return;
+    const uint32_t A0 = (fa + 3) & ~3u, A1 = (fa + L) & ~3u;
+    if (A1 <= A0) {  // no whole dword inside: <= 6 bytes
+        lds_put_bytes(img + fa, load8(src, L), L);
+        return;
     }
-    p.k = (uint32_t)l < p.nk16 ? ((const uint4 *)(a.key_bytes + ka))[l] : make_uint4(0, 0, 0, 0);
-    if ((uint32_t)l < ne) {
-        uint64_t j = d.s + l;
-        p.ko = a.key_off[j];
-        p.klen = (uint32_t)(a.key_off[j + 1] - p.ko);
-        p.vo = a.val_off[j];
-        p.kind = a.kind ? a.kind[j] : 0;
-        p.mask = a.ts_mask ? a.ts_mask[j] : 0;
-        p.vlen = p.kind == SDB_KIND_TOMBSTONE ? 0 : (uint32_t)(a.val_off[j + 1] - p.vo);
-        p.lcp = a.lcp[j];
-        p.seq = a.seq ? a.seq[j] : 0;
-        p.cts = (p.mask & SDB_TS_CREATE) ? a.create_ts[j] : 0;
-        p.ets = (p.mask & SDB_TS_EXPIRE) ? a.expire_ts[j] : 0;
-        p.prev_klen = (l == 0 && d.s > 0) ? (uint32_t)(p.ko - a.key_off[j - 1]) : 0;
-    } else {
-        p.klen = p.vlen = p.lcp = p.prev_klen = 0;
-        p.kind = p.mask = 0;
-        p.ko = p.vo = p.seq = 0;
-        p.cts = p.ets = 0;
+    const uint32_t hb = A0 - fa;
+    if (hb) lds_put_bytes(img + fa, load8(src, hb), hb);
+    const uint8_t *s = src + hb;
+    lu32 *d = (lu32 *)(img + A0);
+    const uint32_t nd = (A1 - A0) >> 2;
+    uint32_t k = 0;
+    for (; k + 4 <= nd; k += 4) {
+        uint4 v;
+        __builtin_memcpy(&v, s + 4 * k, 16);
+        d[k] = v.x;
+        d[k + 1] = v.y;
+        d[k + 2] = v.z;
+        d[k + 3] = v.w;
     }
+    for (; k < nd; k++) {
+        uint32_t v;
+        __builtin_memcpy(&v, s + 4 * k, 4);
+        d[k] = v;
+    }
+    const uint32_t tb = fa + L - A1;
+    if (tb) lds_put_bytes(img + A1, load8(src + (A1 - fa), tb), tb);
 }
 
 template <int V>
-SDB_DEV void process_block(const EncodeArgs &a, const Pre &p, uint8_t *stage, uint8_t *img,
-                           const uint32_t (*crc)[256]) {
-    const int l = lane_id();
-    const uint32_t ne = p.e - p.s;
-    // 1. staged granules -> LDS
+SDB_DEV uint32_t write_row_hdr_trailer(lu8 *dst, const RowInfo &r, uint64_t seq, int64_t ets, int64_t cts) {
+    uint32_t p = 0;
+    if (V == 2) {  // SstRowCodecV2::encode (row_codec_v2.rs:127-169)
+        uint32_t vals[3] = {r.shared, r.suf, r.vlen};
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-        uint32_t c = (uint32_t)l + 64u * r;
-        if (c < p.nv16) ((uint4 *)stage)[c] = p.v[r];
+        for (int f = 0; f < 3; f++) {
+            uint32_t x = vals[f];
+            while (x >= 0x80) {
+                dst[p++] = (uint8_t)(x | 0x80);
+                x >>= 7;
+            }
+            dst[p++] = (uint8_t)x;
+        }
+    } else {  // SstRowCodecV0::encode (row.rs:159-198)
+        dst[0] = (uint8_t)(r.shared >> 8);
+        dst[1] = (uint8_t)r.shared;
+        dst[2] = (uint8_t)(r.suf >> 8);
+        dst[3] = (uint8_t)r.suf;
+        p = 4;
     }
-    uint8_t *kst = stage + 16 * p.nv16;
-    if ((uint32_t)l < p.nk16) ((uint4 *)kst)[l] = p.k;
-    wave_sync();
-    const uint64_t va = p.vs & ~15ull, ka = p.ks & ~15ull;
-    // 2. row sizes and offsets (lane = row)
-    const bool row = (uint32_t)l < ne;
+    const uint32_t h = p;
+    uint32_t t = p + r.suf + (V == 2 ? r.vlen : 0);
+    lds_put_bytes(dst + t, bswap64(seq), 8);
+    t += 8;
+    dst[t++] = r.flags;
+    if (r.flags & SDB_FLAG_HAS_EXPIRE_TS) {
+        lds_put_bytes(dst + t, bswap64((uint64_t)ets), 8);
+        t += 8;
+    }
+    if (r.flags & SDB_FLAG_HAS_CREATE_TS) {
+        lds_put_bytes(dst + t, bswap64((uint64_t)cts), 8);
+        t += 8;
+    }
+    if (V == 1 && !(r.flags & SDB_FLAG_TOMBSTONE)) {
+        dst[t] = (uint8_t)(r.vlen >> 24);
+        dst[t + 1] = (uint8_t)(r.vlen >> 16);
+        dst[t + 2] = (uint8_t)(r.vlen >> 8);
+        dst[t + 3] = (uint8_t)r.vlen;
+    }
+    return h;
+}
+
+SDB_DEV uint32_t crc_slice8_lds(uint32_t c, uint32_t lo, uint32_t hi, const lu32 *tab) {
+    lo ^= c;
+    return tab[7 * 256 + (lo & 0xFF)] ^ tab[6 * 256 + ((lo >> 8) & 0xFF)] ^ tab[5 * 256 + ((lo >> 16) & 0xFF)] ^
+           tab[4 * 256 + (lo >> 24)] ^ tab[3 * 256 + (hi & 0xFF)] ^ tab[2 * 256 + ((hi >> 8) & 0xFF)] ^
+           tab[1 * 256 + ((hi >> 16) & 0xFF)] ^ tab[hi >> 24];
+}
+
+template <int V>
+SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, const lu32 *crc) {
+    const uint32_t l = (uint32_t)lane_id();
+    const BlockDesc d = a.desc[blk];
+    const uint32_t ne = d.e - d.s;
+    if (!(ne <= 64 && d.bb + 64 <= kImgCap)) {
+        if (l == 0) {
+            uint32_t slot = atomicAdd(a.slow_count, 1u);
+            a.slow_list[slot] = blk;
+        }
+        return;
+    }
+    // 1. row metadata (lane = row)
+    const bool row = l < ne;
+    const uint64_t j = d.s + l;
+    uint64_t ko = 0, vo = 0, seq = 0;
+    int64_t cts = 0, ets = 0;
+    uint32_t lcp = 0;
+    uint8_t kind = 0, mask = 0;
+    if (row) {
+        ko = a.key_off[j];
+        vo = a.val_off[j];
+        kind = a.kind ? a.kind[j] : 0;
+        mask = a.ts_mask ? a.ts_mask[j] : 0;
+        seq = a.seq ? a.seq[j] : 0;
+        lcp = a.lcp[j];
+        if (mask & SDB_TS_CREATE) cts = a.create_ts[j];
+        if (mask & SDB_TS_EXPIRE) ets = a.expire_ts[j];
+    }
+    uint32_t prev_klen = 0;
+    if (l == 0 && d.s > 0) prev_klen = (uint32_t)(d.ks - a.key_off[d.s - 1]);
+    uint64_t ko1 = __shfl_down(ko, 1, 64), vo1 = __shfl_down(vo, 1, 64);
+    if (l + 1 == ne) {
+        ko1 = d.ke;
+        vo1 = d.ve;
+    }
+    const uint32_t klen = row ? (uint32_t)(ko1 - ko) : 0;
+    const uint32_t vlen = (row && kind != SDB_KIND_TOMBSTONE) ? (uint32_t)(vo1 - vo) : 0;
     const uint32_t ri = a.restart_interval;
     uint32_t shared = 0;
-    if (V == 2 && row) shared = (l % ri == 0) ? 0 : p.lcp;
-    if (V == 1) {  // prefix vs the block's first key (block.rs:117-123)
-        uint32_t fkl = __shfl(p.klen, 0, 64);
-        if (row && l > 0) {
-            const uint8_t *fk = kst + (p.ks - ka);
-            const uint8_t *mk = kst + (p.ko - ka);
-            shared = lcp_bytes(fk, fkl, mk, p.klen);
-        }
+    if (V == 2 && row) shared = (l % ri == 0) ? 0 : lcp;
+    if (V == 1 && row && l > 0) {  // prefix vs the block's first key (block.rs:117-123)
+        const uint32_t fkl = __shfl(klen, 0, 64);
+        shared = lcp_bytes(a.key_bytes + d.ks, fkl, a.key_bytes + ko, klen);
     }
     RowInfo r;
     r.shared = shared;
-    r.suf = p.klen - shared;
-    r.vlen = p.vlen;
-    r.flags = (uint8_t)((p.kind == SDB_KIND_MERGE ? SDB_FLAG_MERGE_OPERAND : 0) |
-                        (p.kind == SDB_KIND_TOMBSTONE ? SDB_FLAG_TOMBSTONE : 0) |
-                        ((p.mask & SDB_TS_EXPIRE) ? SDB_FLAG_HAS_EXPIRE_TS : 0) |
-                        ((p.mask & SDB_TS_CREATE) ? SDB_FLAG_HAS_CREATE_TS : 0));
-    const uint32_t ts8 = 8u * (((p.mask & SDB_TS_CREATE) != 0) + ((p.mask & SDB_TS_EXPIRE) != 0));
+    r.suf = klen - shared;
+    r.vlen = vlen;
+    r.flags = (uint8_t)((kind == SDB_KIND_MERGE ? SDB_FLAG_MERGE_OPERAND : 0) |
+                        (kind == SDB_KIND_TOMBSTONE ? SDB_FLAG_TOMBSTONE : 0) |
+                        ((mask & SDB_TS_EXPIRE) ? SDB_FLAG_HAS_EXPIRE_TS : 0) |
+                        ((mask & SDB_TS_CREATE) ? SDB_FLAG_HAS_CREATE_TS : 0));
+    const uint32_t ts8 = 8u * (((mask & SDB_TS_CREATE) != 0) + ((mask & SDB_TS_EXPIRE) != 0));
     uint32_t size = 0;
     if (row) {
-        if (V == 2) size = varint_len(shared) + varint_len(r.suf) + varint_len(r.vlen) + r.suf + r.vlen + 9 + ts8;
-        else size = 4 + r.suf + 9 + ts8 + (p.kind == SDB_KIND_TOMBSTONE ? 0 : 4 + r.vlen);
+        if (V == 2) size = varint_len(shared) + varint_len(r.suf) + varint_len(vlen) + r.suf + vlen + 9 + ts8;
+        else size = 4 + r.suf + 9 + ts8 + (kind == SDB_KIND_TOMBSTONE ? 0 : 4 + vlen);
     }
     r.size = size;
     const uint32_t inc = wave_incl_scan(size);
     const uint32_t row_off = inc - size;
     const uint32_t D = __shfl(inc, 63, 64);
-    uint8_t *gdst = a.out_data + p.off;
-    uint8_t *im = img + ((uintptr_t)gdst & 15);
-    // 3. rows
-    if (row) {
-        uint8_t *rowp = im + row_off;
-        uint32_t h;
-        write_row_small<V>(rowp, r, p.seq, p.ets, p.cts, &h);
-        lds_copy(rowp + h, kst + (p.ko + shared - ka), r.suf);
-        if (r.vlen) {
-            uint32_t voff = (V == 2) ? h + r.suf : (size - r.vlen);
-            lds_copy(rowp + voff, stage + (p.vo - va), r.vlen);
-        }
+    const uint32_t noffs = (V == 2) ? (ne + ri - 1) / ri : ne;
+    const uint32_t Lc = D + 2 * noffs + 2;  // CRC input length
+    const uint32_t nseg = (Lc + 63) >> 6;
+    // zero the padding of the last CRC segment (dword-granular; message bytes come after)
+    {
+        const uint32_t z0 = Lc & ~3u, nz = ((nseg << 6) - z0) >> 2;
+        if (l < nz) ((lu32 *)(img + z0))[l] = 0;
     }
-    // 4. offsets + count (Block::encode, format/block.rs:17-26)
-    uint32_t noffs;
+    // 2. rows
+    if (row) {
+        lu8 *rowp = img + row_off;
+        const uint32_t h = write_row_hdr_trailer<V>(rowp, r, seq, ets, cts);
+        copy_field(img, row_off + h, r.suf, a.key_bytes + ko + shared);
+        copy_field(img, row_off + ((V == 2) ? h + r.suf : (size - vlen)), vlen, a.val_bytes + vo);
+    }
+    // offsets + count (Block::encode, format/block.rs:17-26)
     if (V == 2) {
-        noffs = (ne + ri - 1) / ri;
         if (row && l % ri == 0) {
             uint32_t q = l / ri;
-            if (row_off > 0xFFFF) report_error(a.err, p.s + l, SDB_LIMIT_EXCEEDED);  // block_v2.rs:195
-            im[D + 2 * q] = (uint8_t)(row_off >> 8);
-            im[D + 2 * q + 1] = (uint8_t)row_off;
+            if (row_off > 0xFFFF) report_error(a.err, d.s + l, SDB_LIMIT_EXCEEDED);  // block_v2.rs:195
+            img[D + 2 * q] = (uint8_t)(row_off >> 8);
+            img[D + 2 * q + 1] = (uint8_t)row_off;
         }
-    } else {
-        noffs = ne;
-        if (row) {
-            im[D + 2 * l] = (uint8_t)(row_off >> 8);  // `as u16` (block.rs:163)
-            im[D + 2 * l + 1] = (uint8_t)row_off;
-        }
+    } else if (row) {
+        img[D + 2 * l] = (uint8_t)(row_off >> 8);  // `as u16` (block.rs:163)
+        img[D + 2 * l + 1] = (uint8_t)row_off;
     }
     if (l == 0) {
-        im[D + 2 * noffs] = (uint8_t)(noffs >> 8);
-        im[D + 2 * noffs + 1] = (uint8_t)noffs;
+        img[D + 2 * noffs] = (uint8_t)(noffs >> 8);
+        img[D + 2 * noffs + 1] = (uint8_t)noffs;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    wave_sync();
+    // 3. CRC32 (format/sst.rs:541-552)
+    uint32_t acc = 0;
+    for (uint32_t sg = l; sg < nseg; sg += 64) {
+        const lu128 *src = (const lu128 *)(img + 64 * sg);
+        uint32_t c = 0;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            u32x4 v = src[g];
+            if (g == 0 && sg == 0) v.x = ~v.x;  // crc32fast init 0xFFFFFFFF folded into bytes [0, 4)
+            c = crc_slice8_lds(c, v.x, v.y, crc);
+            c = crc_slice8_lds(c, v.z, v.w, crc);
+        }
+        acc ^= seg_shift_mul(nseg - 1 - sg, c);
+    }
+    acc = wave_xor(acc);
+    const uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)acc);
+    const uint32_t crc32 = gf_mul(c_seg.unpad[(nseg << 6) - Lc], u) ^ 0xFFFFFFFFu;
+    if (l == 0) {
+        img[Lc] = (uint8_t)(crc32 >> 24);
+        img[Lc + 1] = (uint8_t)(crc32 >> 16);
+        img[Lc + 2] = (uint8_t)(crc32 >> 8);
+        img[Lc + 3] = (uint8_t)crc32;
+        if (Lc + 4 != d.bb) report_error(a.err, d.s, SDB_DEVICE_ERROR);  // internal consistency
     }
     wave_sync();
-    // 5. CRC32 (format/sst.rs:541-552) and store
-    const uint32_t Lc = D + 2 * noffs + 2;
-    const uint32_t c = wave_crc32_lds(im, Lc, crc);
-    if (l == 0) {
-        im[Lc] = (uint8_t)(c >> 24);
-        im[Lc + 1] = (uint8_t)(c >> 16);
-        im[Lc + 2] = (uint8_t)(c >> 8);
-        im[Lc + 3] = (uint8_t)c;
-        if (Lc + 4 != p.bb) report_error(a.err, p.s, SDB_DEVICE_ERROR);  // internal consistency
+    // 4. store [0, Lc + 4) -> out_data + off
+    uint8_t *gdst = a.out_data + d.off;
+    const uint32_t L = Lc + 4, nfull = L >> 4;
+    for (uint32_t c = l; c < nfull; c += 64) {
+        u32x4 v = ((const lu128 *)img)[c];
+        __builtin_memcpy(gdst + 16 * c, &v, 16);
     }
-    wave_sync();
-    wave_store(gdst, img, (uint64_t)Lc + 4);
-    // 6. BlockStats (sst_stats.rs:9-16) and the index key (compute_index_key, utils.rs:198-226)
-    const uint64_t pu = __ballot(row && p.kind == SDB_KIND_VALUE);
-    const uint64_t de = __ballot(row && p.kind == SDB_KIND_TOMBSTONE);
-    const uint64_t me = __ballot(row && p.kind == SDB_KIND_MERGE);
     if (l == 0) {
-        a.out_block_stats[3 * (uint64_t)p.blk] = (uint16_t)__popcll(pu);
-        a.out_block_stats[3 * (uint64_t)p.blk + 1] = (uint16_t)__popcll(de);
-        a.out_block_stats[3 * (uint64_t)p.blk + 2] = (uint16_t)__popcll(me);
+        for (uint32_t q = nfull << 4; q < L; q++) gdst[q] = img[q];
+    }
+    // 5. BlockStats (sst_stats.rs:9-16) and the index key (compute_index_key, utils.rs:198-226)
+    const uint64_t pu = __ballot(row && kind == SDB_KIND_VALUE);
+    const uint64_t de = __ballot(row && kind == SDB_KIND_TOMBSTONE);
+    const uint64_t me = __ballot(row && kind == SDB_KIND_MERGE);
+    if (l == 0) {
+        a.out_block_stats[3 * (uint64_t)blk] = (uint16_t)__popcll(pu);
+        a.out_block_stats[3 * (uint64_t)blk + 1] = (uint16_t)__popcll(de);
+        a.out_block_stats[3 * (uint64_t)blk + 2] = (uint16_t)__popcll(me);
         uint32_t ik = 0;
-        if (p.s > 0) ik = (p.lcp == p.prev_klen && p.prev_klen == p.klen) ? p.klen : p.lcp + 1;
-        a.out_index_key_len[p.blk] = ik;
+        if (d.s > 0) ik = (lcp == prev_klen && prev_klen == klen) ? klen : lcp + 1;
+        a.out_index_key_len[blk] = ik;
     }
     wave_sync();
 }
 
 template <int V>
-__global__ __launch_bounds__(512, 4) void k_emit(EncodeArgs a) {
+__global__ __launch_bounds__(kEmitThreads) void k_emit(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if (*a.err != ~0ull) return;  // any earlier error (incl. capacity): write nothing
     const uint32_t nb = a.anchor_blk[a.nchunks];
-    uint32_t(*crc)[256] = (uint32_t(*)[256])smem;
-    for (uint32_t q = threadIdx.x; q < 8 * 256; q += blockDim.x) ((uint32_t *)crc)[q] = (&c_crc.t[0][0])[q];
+    lu32 *crc = (lu32 *)smem;
+    for (uint32_t q = threadIdx.x; q < 8 * 256; q += blockDim.x) crc[q] = (&c_crc.t[0][0])[q];
     __syncthreads();
-    const uint32_t wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
-    uint8_t *stage = smem + kCrcLds + (uint64_t)wave * (kStageCap + kImgCap);
-    uint8_t *img = stage + kStageCap;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), wpb = blockDim.x >> 6;
+    lu8 *img = (lu8 *)smem + kCrcLds + wave * kImgCap;
     const uint32_t gw = blockIdx.x * wpb + wave, G = gridDim.x * wpb;
-    Pre cur, nxt;
-    load_pre(a, gw, nb, cur);
-    for (uint32_t blk = gw; blk < nb; blk += G) {
-        load_pre(a, blk + G, nb, nxt);  // in flight while `cur` is assembled
-        if (cur.fast) {
-            process_block<V>(a, cur, stage, img, crc);
-        } else if (lane_id() == 0) {
-            uint32_t slot = atomicAdd(a.slow_count, 1u);
-            a.slow_list[slot] = blk;
-        }
-        cur = nxt;
-    }
+    for (uint32_t blk = gw; blk < nb; blk += G) emit_block<V>(a, blk, img, crc);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -955,38 +1085,42 @@ __global__ void k_finish_summary(EncodeArgs a, uint64_t bloom_len, uint32_t num_
 
 static bool lds_attrs_set = false;
 static int g_cus = 0;
-static uint32_t emit_grid() { return (uint32_t)(g_cus > 0 ? 2 * g_cus : 512); }
+static uint32_t g_emit_threads = kEmitThreads, g_emit_wg_per_cu = kEmitWgPerCu;
+static uint32_t emit_grid() { return (uint32_t)(g_cus > 0 ? g_emit_wg_per_cu * g_cus : 512); }
+static uint32_t emit_lds() { return kCrcLds + (g_emit_threads / 64) * kImgCap; }
 static void set_lds_attrs() {
     if (lds_attrs_set) return;
     int dev = 0;
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    // tuning knobs (diagnostics): emit workgroup size and workgroups per CU
+    if (const char *e = getenv("SDB_EMIT_THREADS")) {
+        uint32_t t = (uint32_t)atoi(e);
+        if (t >= 64 && t <= kEmitThreads && t % 64 == 0) g_emit_threads = t;
+    }
+    if (const char *e = getenv("SDB_EMIT_WG_PER_CU")) {
+        uint32_t t = (uint32_t)atoi(e);
+        if (t >= 1 && t <= 32) g_emit_wg_per_cu = t;
+    }
     hipFuncSetAttribute((const void *)k_emit<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
     hipFuncSetAttribute((const void *)k_emit<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
     hipFuncSetAttribute((const void *)k_enum, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEnumLds);
     hipFuncSetAttribute((const void *)k_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLds);
+    hipFuncSetAttribute((const void *)k_seg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLds);
     lds_attrs_set = true;
 }
 
 hipError_t launch_encode(EncodeArgs a, hipStream_t st) {
-    const uint32_t tpb = 256;
     set_lds_attrs();
     hipLaunchKernelGGL(k_init_summary, dim3(1), dim3(64), 0, st, a);
     if (a.n == 0) {
         hipLaunchKernelGGL(k_finish_summary, dim3(1), dim3(64), 0, st, a, a.bloom_len, a.num_probes, a.filter_built);
         return hipGetLastError();
     }
-    const uint32_t g = (uint32_t)((a.n + tpb - 1) / tpb);
-    a.nprep_wg = g;
-    stage_mark(st, kStPrep, true);
-    hipLaunchKernelGGL(k_prep, dim3(g), dim3(tpb), 0, st, a);
-    stage_mark(st, kStPrep, false);
-    stage_mark(st, kStNext, true);
-    hipLaunchKernelGGL(k_next, dim3(g), dim3(tpb), 0, st, a);
-    stage_mark(st, kStNext, false);
-    stage_mark(st, kStChunk, true);
-    hipLaunchKernelGGL(k_chunk, dim3(a.nchunks), dim3(512), 0, st, a);
-    stage_mark(st, kStChunk, false);
+    a.nprep_wg = a.nchunks;
+    stage_mark(st, kStSeg, true);
+    hipLaunchKernelGGL(k_seg, dim3(a.nchunks), dim3(kSegThreads), kSegLds, st, a);
+    stage_mark(st, kStSeg, false);
     stage_mark(st, kStResolve, true);
     hipLaunchKernelGGL(k_resolve, dim3(1), dim3(1024), kResolveLds, st, a);
     stage_mark(st, kStResolve, false);
@@ -994,8 +1128,8 @@ hipError_t launch_encode(EncodeArgs a, hipStream_t st) {
     hipLaunchKernelGGL(k_enum, dim3(a.nchunks), dim3(256), kEnumLds, st, a);
     stage_mark(st, kStEnum, false);
     stage_mark(st, kStEmit, true);
-    if (a.version == 2) hipLaunchKernelGGL(k_emit<2>, dim3(emit_grid()), dim3(kEmitThreads), kEmitLds, st, a);
-    else hipLaunchKernelGGL(k_emit<1>, dim3(emit_grid()), dim3(kEmitThreads), kEmitLds, st, a);
+    if (a.version == 2) hipLaunchKernelGGL(k_emit<2>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, a);
+    else hipLaunchKernelGGL(k_emit<1>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, a);
     stage_mark(st, kStEmit, false);
     stage_mark(st, kStEmitSlow, true);
     if (a.version == 2) hipLaunchKernelGGL(k_emit_slow<2>, dim3(64), dim3(256), 0, st, a);
