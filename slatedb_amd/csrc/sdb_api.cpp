@@ -161,6 +161,11 @@ sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const 
     a.restart_interval = p->sst_version == 2 ? p->restart_interval : 1;
     a.version = p->sst_version;
     a.nchunks = (uint32_t)((n + kChunk - 1) / kChunk);
+    {   // a block holds at most (block_size - 2) / 12 + 1 entries (smallest row: 12 bytes in V2, 13 in V1);
+        // blocks longer than the lookahead continue from HBM inside k_seg
+        uint64_t look = (uint64_t)p->block_size / 12 + 2;
+        a.seg_look = (uint32_t)(look < kSegLook ? look : kSegLook);
+    }
     a.lcp = carve<uint32_t>(workspace, wl.lcp);
     a.s_nr = carve<uint32_t>(workspace, wl.s_nr);
     a.s_r = carve<uint32_t>(workspace, wl.s_r);

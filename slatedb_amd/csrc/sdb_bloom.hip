@@ -87,7 +87,9 @@ __global__ __launch_bounds__(256) void k_bloom_atomic(const uint8_t *__restrict_
 //                 ORs them into an LDS copy of the slice, writes the slice with plain stores.
 // Deterministic (the bitmap is an OR), no global atomics, no bitmap memset.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(512) void k_bloom_tile(const uint8_t *__restrict__ key_bytes,
+constexpr uint32_t kBloomTile = 512, kBloomTileThreads = 256;  // keys / threads per tile workgroup
+
+__global__ __launch_bounds__(kBloomTileThreads) void k_bloom_tile(const uint8_t *__restrict__ key_bytes,
                                                     const uint64_t *__restrict__ key_off, uint64_t n,
                                                     BloomPlan pl, uint32_t *region, uint32_t *cnt,
                                                     uint32_t *off) {
@@ -218,8 +220,12 @@ BloomPlan bloom_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes) {
     while ((((uint64_t)pl.m + (1ull << pl.sb) - 1) >> pl.sb) > 1024) pl.sb++;
     pl.nslices = (uint32_t)(((uint64_t)pl.m + (1ull << pl.sb) - 1) >> pl.sb);
     if (pl.nslices == 0) pl.nslices = 1;
-    uint32_t T = 12288 / pl.k;
-    if (T > 2048) T = 2048;
+    // small tiles for parallelism, but at most ~4096 tiles so k_bloom_set's per-slice tile table
+    // stays small; a tile's probes (T * k u32) must fit the tile kernel's LDS
+    uint64_t T64 = (n + 4095) / 4096;
+    if (T64 < kBloomTile) T64 = kBloomTile;
+    const uint32_t tmax = 12288 / pl.k;
+    uint32_t T = (uint32_t)(T64 < tmax ? T64 : tmax);
     if (T < 64) T = 64;
     pl.T = T;
     pl.tiles = (uint32_t)((n + T - 1) / T);
@@ -263,7 +269,7 @@ hipError_t launch_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off,
     uint64_t region_b = (((uint64_t)pl.tiles * pl.T * pl.k * 4) + 255) & ~255ull;
     uint64_t mat_b = (((uint64_t)pl.tiles * pl.nslices * 4) + 255) & ~255ull;
     uint32_t *region = (uint32_t *)w, *cnt = (uint32_t *)(w + region_b), *off = (uint32_t *)(w + region_b + mat_b);
-    hipLaunchKernelGGL(k_bloom_tile, dim3(pl.tiles), dim3(512), tile_lds(pl), st, key_bytes, key_off, n, pl, region,
+    hipLaunchKernelGGL(k_bloom_tile, dim3(pl.tiles), dim3(kBloomTileThreads), tile_lds(pl), st, key_bytes, key_off, n, pl, region,
                        cnt, off);
     hipLaunchKernelGGL(k_bloom_set, dim3(pl.nslices), dim3(1024), set_lds(pl), st, region, cnt, off, pl, bitmap,
                        bitmap_bytes);

@@ -11,13 +11,14 @@ constexpr uint32_t kChunk = 2048;            // entries per chunk (K3 / K5)
 constexpr uint32_t kResolveLds = 96 * 1024;  // LDS budget of the resolve tables (u16 exits)
 constexpr uint32_t kCrcLds = 8 * 1024;       // slicing-by-8 tables
 constexpr uint32_t kImgCap = 4096 + 64;      // LDS block image per wave (fast path)
-constexpr uint32_t kStageCap = 4096 + 64;    // LDS value / key staging per wave
-constexpr uint32_t kSegSpan = 2 * kChunk;     // k_seg: entries staged per chunk (chunk + lookahead)
-constexpr uint32_t kSegThreads = 512;
+constexpr uint32_t kStageCap = 4096;         // LDS value staging per wave (LDS-DMA, 1 KiB per instruction)
+constexpr uint32_t kSegLook = 1024;           // k_seg: max lookahead entries staged past the chunk
+constexpr uint32_t kSegSpan = kChunk + kSegLook;
+constexpr uint32_t kSegThreads = 1024;
 constexpr uint32_t kSegLds = kSegSpan * 8 + kChunk * 12;
-constexpr uint32_t kEmitThreads = 1024;      // 16 waves per workgroup (one block each)
+constexpr uint32_t kEmitThreads = 512;       // 8 waves per workgroup (one block each)
 constexpr uint32_t kEmitWgPerCu = 2;
-constexpr uint32_t kEmitLds = kCrcLds + (kEmitThreads / 64) * kImgCap;
+constexpr uint32_t kEmitLds = kCrcLds + (kEmitThreads / 64) * (kImgCap + kStageCap);
 constexpr uint32_t kEnumLds = kChunk * 16 + 12 * kChunk * 2;  // block list + 12 lifting levels
 
 struct BlockDesc {  // one per block, written by k_enum, streamed by k_emit (48 bytes)
@@ -44,6 +45,7 @@ struct EncodeArgs {
     uint32_t restart_interval;
     uint32_t version;
     uint32_t nchunks;
+    uint32_t seg_look;      // lookahead entries staged by k_seg (covers the longest possible block)
     // workspace
     uint32_t *lcp;
     uint32_t *s_nr;

@@ -113,7 +113,7 @@ __global__ __launch_bounds__(kSegThreads) void k_seg(EncodeArgs a) {
     const uint32_t k = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
     const uint64_t cs = (uint64_t)k * kChunk;
     const uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
-    const uint64_t se = cs + kSegSpan < a.n ? cs + kSegSpan : a.n;
+    const uint64_t se = ce + a.seg_look < a.n ? ce + a.seg_look : a.n;
     const uint32_t cn = (uint32_t)(ce - cs);
     // a. facts
     uint64_t rk = 0, rv = 0;
@@ -671,6 +671,35 @@ SDB_DEV void copy_field(lu8 *img, uint32_t fa, uint32_t L, const uint8_t *src) {
     if (tb) lds_put_bytes(img + A1, load8(src + (A1 - fa), tb), tb);
 }
 
+// lane: image bytes [fa, fa + L) <- stage bytes [sa, sa + L) (both LDS, any alignment): dword
+// interior by aligned reads + v_alignbyte, <= 3 + 3 edge bytes bytewise.
+SDB_DEV void lds_move(lu8 *img, uint32_t fa, const lu8 *stage, uint32_t sa, uint32_t L) {
+    if (!L) return;
+    const uint32_t A0 = (fa + 3) & ~3u, A1 = (fa + L) & ~3u;
+    if (A1 <= A0) {
+        for (uint32_t i = 0; i < L; i++) img[fa + i] = stage[sa + i];
+        return;
+    }
+    const uint32_t hb = A0 - fa;
+    for (uint32_t i = 0; i < hb; i++) img[fa + i] = stage[sa + i];
+    const uint32_t s0 = sa + hb, sh = s0 & 3, nd = (A1 - A0) >> 2;
+    const lu32 *sw = (const lu32 *)(stage + (s0 & ~3u));
+    lu32 *dw = (lu32 *)(img + A0);
+    if (sh == 0) {
+#pragma unroll 1
+        for (uint32_t k = 0; k < nd; k++) dw[k] = sw[k];
+    } else {
+        uint32_t lo = sw[0];
+#pragma unroll 1
+        for (uint32_t k = 0; k < nd; k++) {
+            const uint32_t hi = sw[k + 1];
+            dw[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+            lo = hi;
+        }
+    }
+    for (uint32_t i = A1 - fa; i < L; i++) img[fa + i] = stage[sa + i];
+}
+
 template <int V>
 SDB_DEV uint32_t write_row_hdr_trailer(lu8 *dst, const RowInfo &r, uint64_t seq, int64_t ets, int64_t cts) {
     uint32_t p = 0;
@@ -722,11 +751,13 @@ SDB_DEV uint32_t crc_slice8_lds(uint32_t c, uint32_t lo, uint32_t hi, const lu32
 }
 
 template <int V>
-SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, const lu32 *crc) {
+SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, lu8 *stage, const lu32 *crc) {
     const uint32_t l = (uint32_t)lane_id();
     const BlockDesc d = a.desc[blk];
     const uint32_t ne = d.e - d.s;
-    if (!(ne <= 64 && d.bb + 64 <= kImgCap)) {
+    const uint64_t va = d.vs & ~15ull;
+    const uint32_t nv16 = d.ve > d.vs ? (uint32_t)((d.ve - va + 15) >> 4) : 0;
+    if (!(ne <= 64 && d.bb + 64 <= kImgCap && nv16 <= kStageCap / 16)) {
         if (l == 0) {
             uint32_t slot = atomicAdd(a.slow_count, 1u);
             a.slow_list[slot] = blk;
@@ -752,6 +783,18 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, const lu32 
     }
     uint32_t prev_klen = 0;
     if (l == 0 && d.s > 0) prev_klen = (uint32_t)(d.ks - a.key_off[d.s - 1]);
+    // the block's value bytes -> stage (coalesced LDS-DMA, 1 KiB per wave instruction; lanes past
+    // the range reload the last granule into unused stage slots so the instruction count is fixed)
+    if (nv16) {
+        const uint32_t stage_lds = lds_addr((const void *)stage);
+#pragma unroll
+        for (uint32_t q = 0; q < kStageCap / 1024; q++) {
+            uint32_t g = 64 * q + l;
+            g = g < nv16 ? g : nv16 - 1;
+            __builtin_amdgcn_global_load_lds((glb_void *)(a.val_bytes + va + 16 * (uint64_t)g),
+                                             (lds_void *)(uintptr_t)(stage_lds + 1024 * q), 16, 0, 0);
+        }
+    }
     uint64_t ko1 = __shfl_down(ko, 1, 64), vo1 = __shfl_down(vo, 1, 64);
     if (l + 1 == ne) {
         ko1 = d.ke;
@@ -793,12 +836,16 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, const lu32 
         if (l < nz) ((lu32 *)(img + z0))[l] = 0;
     }
     // 2. rows
+    uint32_t vdst = 0;
     if (row) {
         lu8 *rowp = img + row_off;
         const uint32_t h = write_row_hdr_trailer<V>(rowp, r, seq, ets, cts);
         copy_field(img, row_off + h, r.suf, a.key_bytes + ko + shared);
-        copy_field(img, row_off + ((V == 2) ? h + r.suf : (size - vlen)), vlen, a.val_bytes + vo);
+        vdst = row_off + ((V == 2) ? h + r.suf : (size - vlen));
     }
+    __builtin_amdgcn_s_waitcnt(0);  // stage landed (LDS-DMA counts on vmcnt)
+    wave_sync();
+    if (row) lds_move(img, vdst, stage, (uint32_t)(vo - va), vlen);
     // offsets + count (Block::encode, format/block.rs:17-26)
     if (V == 2) {
         if (row && l % ri == 0) {
@@ -868,7 +915,7 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, const lu32 
 }
 
 template <int V>
-__global__ __launch_bounds__(kEmitThreads) void k_emit(EncodeArgs a) {
+__global__ __launch_bounds__(kEmitThreads, 4) void k_emit(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if (*a.err != ~0ull) return;  // any earlier error (incl. capacity): write nothing
     const uint32_t nb = a.anchor_blk[a.nchunks];
@@ -876,9 +923,10 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(EncodeArgs a) {
     for (uint32_t q = threadIdx.x; q < 8 * 256; q += blockDim.x) crc[q] = (&c_crc.t[0][0])[q];
     __syncthreads();
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), wpb = blockDim.x >> 6;
-    lu8 *img = (lu8 *)smem + kCrcLds + wave * kImgCap;
+    lu8 *img = (lu8 *)smem + kCrcLds + wave * (kImgCap + kStageCap);
+    lu8 *stage = img + kImgCap;
     const uint32_t gw = blockIdx.x * wpb + wave, G = gridDim.x * wpb;
-    for (uint32_t blk = gw; blk < nb; blk += G) emit_block<V>(a, blk, img, crc);
+    for (uint32_t blk = gw; blk < nb; blk += G) emit_block<V>(a, blk, img, stage, crc);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1087,7 +1135,7 @@ static bool lds_attrs_set = false;
 static int g_cus = 0;
 static uint32_t g_emit_threads = kEmitThreads, g_emit_wg_per_cu = kEmitWgPerCu;
 static uint32_t emit_grid() { return (uint32_t)(g_cus > 0 ? g_emit_wg_per_cu * g_cus : 512); }
-static uint32_t emit_lds() { return kCrcLds + (g_emit_threads / 64) * kImgCap; }
+static uint32_t emit_lds() { return kCrcLds + (g_emit_threads / 64) * (kImgCap + kStageCap); }
 static void set_lds_attrs() {
     if (lds_attrs_set) return;
     int dev = 0;

@@ -20,6 +20,9 @@ from .batch import Batch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libslatedb_amd.so")
+# tuning experiments only: an alternative in-tree build of the same library
+if os.environ.get("SDB_LIBRARY"):
+    LIB_PATH = os.path.join(HERE, os.path.basename(os.environ["SDB_LIBRARY"]))
 
 _lib = None
 
