@@ -167,8 +167,7 @@ sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const 
         a.seg_look = (uint32_t)(look < kSegLook ? look : kSegLook);
     }
     a.lcp = carve<uint32_t>(workspace, wl.lcp);
-    a.s_nr = carve<uint32_t>(workspace, wl.s_nr);
-    a.s_r = carve<uint32_t>(workspace, wl.s_r);
+    a.row_scratch = carve<uint32_t>(workspace, wl.row_scratch);
     a.next = carve<uint32_t>(workspace, wl.next);
     a.bbytes = carve<uint32_t>(workspace, wl.bbytes);
     a.tab_exit = carve<uint32_t>(workspace, wl.tab_exit);

@@ -115,10 +115,27 @@ constexpr CrcSegMul make_seg_mul() {
     return r;
 }
 
+// mul256[b][v] = x^(8*32) * (v << 8b) mod P: shifts a CRC past 32 zero bytes (4 byte-table lookups).
+struct CrcMul256 {
+    uint32_t t[4][256];
+};
+constexpr CrcMul256 make_mul256() {
+    CrcMul256 r{};
+    const uint32_t K = x8n_c(32);
+    for (int b = 0; b < 4; b++) {
+        uint32_t basis[8] = {};
+        for (int i = 0; i < 8; i++) basis[i] = gf_mul_c(K, 1u << (8 * b + i));
+        r.t[b][0] = 0;
+        for (int v = 1; v < 256; v++) r.t[b][v] = r.t[b][v & (v - 1)] ^ basis[__builtin_ctz(v)];
+    }
+    return r;
+}
+
 // Per translation unit (no relocatable device code needed).
 static __constant__ CrcTables c_crc = make_crc_tables();
 static __constant__ CrcShift64 c_shift = make_shift64();
 static __constant__ CrcSegShift c_seg = make_seg_shift();
+static __constant__ CrcMul256 c_mul256 = make_mul256();
 static __device__ const CrcSegMul g_seg_mul = make_seg_mul();
 SDB_DEV uint32_t seg_shift_mul(uint32_t k, uint32_t c) {
     const uint32_t(*t)[256] = g_seg_mul.t[k];
@@ -175,34 +192,68 @@ SDB_DEV uint32_t lcp_bytes(const uint8_t *a, uint32_t na, const uint8_t *b, uint
 // ------------------------------------------------------------------------------------------------
 SDB_DEV int lane_id() { return __lane_id(); }
 
+// DPP (GFX9 data-parallel primitives): register-to-register lane moves on the VALU, no LDS round
+// trip (ds_bpermute-based __shfl costs an LDS latency per step).
+constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114, kDppRowShr8 = 0x118;
+constexpr int kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143, kDppWaveShl1 = 0x130, kDppWaveShr1 = 0x138;
+
+template <int CTRL, int ROWS = 0xF>
+SDB_DEV uint32_t dpp32(uint32_t v) {  // lanes whose source is invalid / masked get 0
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xF, false);
+}
+template <int CTRL, int ROWS = 0xF>
+SDB_DEV uint64_t dpp64(uint64_t v) {
+    return (uint64_t)dpp32<CTRL, ROWS>((uint32_t)v) | ((uint64_t)dpp32<CTRL, ROWS>((uint32_t)(v >> 32)) << 32);
+}
+template <int CTRL, int ROWS = 0xF>
+SDB_DEV uint32_t dpp(uint32_t v) { return dpp32<CTRL, ROWS>(v); }
+template <int CTRL, int ROWS = 0xF>
+SDB_DEV uint64_t dpp(uint64_t v) { return dpp64<CTRL, ROWS>(v); }
+
+// Inclusive wave scan with an associative, identity-0 operator (row Kogge-Stone + row broadcasts).
+template <typename T, typename Op>
+SDB_DEV T wave_incl_scan_op(T v, Op op) {
+    v = op(v, dpp<kDppRowShr1>(v));
+    v = op(v, dpp<kDppRowShr2>(v));
+    v = op(v, dpp<kDppRowShr4>(v));
+    v = op(v, dpp<kDppRowShr8>(v));
+    v = op(v, dpp<kDppRowBcast15, 0xA>(v));
+    v = op(v, dpp<kDppRowBcast31, 0xC>(v));
+    return v;
+}
+template <typename T>
+SDB_DEV T wave_readlane(T v, int lane) {
+    if constexpr (sizeof(T) == 8) {
+        uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+        uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane);
+        return (T)(((uint64_t)hi << 32) | lo);
+    } else {
+        return (T)__builtin_amdgcn_readlane((int)v, lane);
+    }
+}
 template <typename T>
 SDB_DEV T wave_incl_scan(T v) {
-    const int l = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        T o = __shfl_up(v, d, 64);
-        if (l >= d) v += o;
-    }
-    return v;
+    return wave_incl_scan_op(v, [](T x, T y) { return x + y; });
 }
 template <typename T>
-SDB_DEV T wave_sum(T v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
+SDB_DEV T wave_sum(T v) {  // every lane gets the total
+    return wave_readlane(wave_incl_scan(v), 63);
 }
 SDB_DEV uint32_t wave_xor(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v ^= __shfl_xor(v, d, 64);
-    return v;
+    return wave_readlane(wave_incl_scan_op(v, [](uint32_t x, uint32_t y) { return x ^ y; }), 63);
 }
 SDB_DEV uint32_t wave_max(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        uint32_t o = __shfl_xor(v, d, 64);
-        v = o > v ? o : v;
-    }
-    return v;
+    return wave_readlane(wave_incl_scan_op(v, [](uint32_t x, uint32_t y) { return x > y ? x : y; }), 63);
+}
+// lane l gets lane l + 1's value (lane 63 gets 0)
+template <typename T>
+SDB_DEV T wave_next_lane(T v) {
+    return dpp<kDppWaveShl1>(v);
+}
+// lane l gets lane l - 1's value (lane 0 gets 0)
+template <typename T>
+SDB_DEV T wave_prev_lane(T v) {
+    return dpp<kDppWaveShr1>(v);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -9,16 +9,19 @@ namespace sdb {
 
 constexpr uint32_t kChunk = 2048;            // entries per chunk (K3 / K5)
 constexpr uint32_t kResolveLds = 96 * 1024;  // LDS budget of the resolve tables (u16 exits)
-constexpr uint32_t kCrcLds = 8 * 1024;       // slicing-by-8 tables
+constexpr uint32_t kCrcLds = 12 * 1024;      // slicing-by-8 tables + x^256 byte tables
 constexpr uint32_t kImgCap = 4096 + 64;      // LDS block image per wave (fast path)
-constexpr uint32_t kStageCap = 4096;         // LDS value staging per wave (LDS-DMA, 1 KiB per instruction)
+constexpr uint32_t kStageCap = 4096;         // value staging per wave (LDS-DMA, 1 KiB per instruction), in place
+constexpr uint32_t kStageGuard = 64;         // LDS bytes before each image the value stage may use
+constexpr uint32_t kKeyStageCap = 1024;      // key staging per wave
 constexpr uint32_t kSegLook = 1024;           // k_seg: max lookahead entries staged past the chunk
 constexpr uint32_t kSegSpan = kChunk + kSegLook;
 constexpr uint32_t kSegThreads = 1024;
-constexpr uint32_t kSegLds = kSegSpan * 8 + kChunk * 12;
-constexpr uint32_t kEmitThreads = 512;       // 8 waves per workgroup (one block each)
+constexpr uint32_t kSegLds = (3 * kSegSpan + 4) * 4 + kChunk * 6;
+constexpr uint32_t kEmitThreads = 640;       // 10 waves per workgroup (one block each), 2 per CU
 constexpr uint32_t kEmitWgPerCu = 2;
-constexpr uint32_t kEmitLds = kCrcLds + (kEmitThreads / 64) * (kImgCap + kStageCap);
+constexpr uint32_t kEmitWaveLds = kStageGuard + kImgCap + 16 + kKeyStageCap + 64 * 16;  // guard, image, key stage, spans
+constexpr uint32_t kEmitLds = kCrcLds + (kEmitThreads / 64) * kEmitWaveLds;
 constexpr uint32_t kEnumLds = kChunk * 16 + 12 * kChunk * 2;  // block list + 12 lifting levels
 
 struct BlockDesc {  // one per block, written by k_enum, streamed by k_emit (48 bytes)
@@ -48,8 +51,7 @@ struct EncodeArgs {
     uint32_t seg_look;      // lookahead entries staged by k_seg (covers the longest possible block)
     // workspace
     uint32_t *lcp;
-    uint32_t *s_nr;
-    uint32_t *s_r;
+    uint32_t *row_scratch;  // per entry: row offsets of slow-path blocks
     uint32_t *next;
     uint32_t *bbytes;
     uint32_t *tab_exit;
@@ -80,7 +82,7 @@ struct EncodeArgs {
 
 // Workspace layout for n entries (all offsets 256-byte aligned).
 struct EncodeWorkspace {
-    uint64_t lcp, s_nr, s_r, next, bbytes, tab_exit, tab_cnt, tab_bytes;
+    uint64_t lcp, row_scratch, next, bbytes, tab_exit, tab_cnt, tab_bytes;
     uint64_t anchor_e, anchor_blk, anchor_byte, err, wmax, slow_count, slow_list, desc, stat_part, wmax_part, bloom_rep;
     uint64_t total;
 };
@@ -95,13 +97,12 @@ inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes
     };
     uint64_t nc = (n + kChunk - 1) / kChunk;
     w.lcp = take(4 * (n + 1));
-    w.s_nr = take(4 * (n + 1));
-    w.s_r = take(4 * (n + 1));
+    w.row_scratch = take(4 * (n + 1));
     w.next = take(4 * (n + 1));
     w.bbytes = take(4 * (n + 1));
-    w.tab_exit = take(4 * (n + 1));
-    w.tab_cnt = take(4 * (n + 1));
-    w.tab_bytes = take(8 * (n + 1));
+    w.tab_exit = take(4 * (nc * kSegLook + 1));   // per chunk: seg_look candidate entry points
+    w.tab_cnt = take(4 * (nc * kSegLook + 1));
+    w.tab_bytes = take(8 * (nc * kSegLook + 1));
     w.anchor_e = take(4 * (nc + 2));
     w.anchor_blk = take(4 * (nc + 2));
     w.anchor_byte = take(8 * (nc + 2));
@@ -141,3 +142,4 @@ hipError_t launch_bloom_query(const uint8_t *bitmap, uint64_t bitmap_bytes, uint
                               uint8_t *result, hipStream_t st);
 
 }  // namespace sdb
+static_assert(sdb::kSegSpan % sdb::kSegThreads == 0 && sdb::kChunk % 64 == 0, "k_seg geometry");

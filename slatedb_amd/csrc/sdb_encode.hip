@@ -31,6 +31,37 @@
 
 namespace sdb {
 
+// Phase timestamps (diagnostic builds with -DSDB_PHASE_TIMING): per workgroup of the instrumented
+// kernel, s_memtime at each phase mark of thread 0 -> g_phase[blockIdx][mark].  A mark adds its own
+// barrier in timing builds only: it never stands in for a barrier the algorithm needs.
+#ifdef SDB_PHASE_TIMING
+__device__ uint64_t g_phase[1024][8];
+#define PHASE_MARK(i)                                                              \
+    do {                                                                           \
+        __syncthreads();                                                           \
+        if (threadIdx.x == 0 && blockIdx.x < 1024) g_phase[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+__device__ uint64_t g_wave_phase[8192][8];
+#define WAVE_T(var)                                     \
+    uint64_t var = __builtin_amdgcn_s_memtime();        \
+    __builtin_amdgcn_s_waitcnt(0xC07F) /* lgkmcnt(0) */
+#define PHASE_MARK_AT(slot, i)                                                        \
+    do {                                                                          \
+        __syncthreads();                                                          \
+        if (threadIdx.x == 0) g_phase[slot][i] = __builtin_amdgcn_s_memtime();   \
+    } while (0)
+#else
+#define PHASE_MARK(i) \
+    do {              \
+    } while (0)
+#define PHASE_MARK_AT(slot, i) \
+    do {                       \
+    } while (0)
+#define WAVE_T(var) \
+    do {            \
+    } while (0)
+#endif
+
 
 // ------------------------------------------------------------------------------------------------
 // Per-entry facts: LCP vs the previous key, restart / non-restart row sizes, reference errors.
@@ -42,22 +73,61 @@ struct EntryFacts {
     int err;
 };
 
-SDB_DEV EntryFacts entry_facts(const EncodeArgs &a, uint64_t i) {
+// The facts are computed in three steps so a thread can issue the loads of several entries before
+// it waits: offsets/flags, then the first 16 bytes of this and the previous key, then the rest.
+struct FactsIn {
+    uint64_t pko, ko0, ko1, vo0, vo1;
+    uint64_t pk0, pk1, ck0, ck1;  // first 16 bytes of the previous / this key (masked by length later)
+    uint8_t kd, m;
+};
+
+SDB_DEV void facts_load_offsets(const EncodeArgs &a, uint64_t i, FactsIn &in) {
+    in.ko0 = a.key_off[i];
+    in.ko1 = a.key_off[i + 1];
+    in.pko = i > 0 ? a.key_off[i - 1] : in.ko0;
+    in.vo0 = a.val_off[i];
+    in.vo1 = a.val_off[i + 1];
+    in.kd = a.kind ? a.kind[i] : 0;
+    in.m = a.ts_mask ? a.ts_mask[i] : 0;
+}
+
+SDB_DEV void facts_load_keys(const EncodeArgs &a, FactsIn &in) {
+    const uint64_t klen = in.ko1 - in.ko0, plen = in.ko0 - in.pko;
+    uint64_t n = klen < plen ? klen : plen;
+    n = n < 16 ? n : 16;
+    in.pk0 = in.ck0 = in.pk1 = in.ck1 = 0;
+    if (n) {
+        const uint32_t n0 = (uint32_t)(n < 8 ? n : 8);
+        in.pk0 = load8(a.key_bytes + in.pko, n0);
+        in.ck0 = load8(a.key_bytes + in.ko0, n0);
+        if (n > 8) {
+            in.pk1 = load8(a.key_bytes + in.pko + 8, (uint32_t)(n - 8));
+            in.ck1 = load8(a.key_bytes + in.ko0 + 8, (uint32_t)(n - 8));
+        }
+    }
+}
+
+SDB_DEV EntryFacts facts_finish(const EncodeArgs &a, uint64_t i, const FactsIn &in) {
     EntryFacts f;
-    uint64_t ko0 = a.key_off[i], ko1 = a.key_off[i + 1];
-    uint64_t klen = ko1 - ko0;
-    uint8_t kd = a.kind ? a.kind[i] : 0;
-    uint8_t m = a.ts_mask ? a.ts_mask[i] : 0;
-    uint64_t vlen = (kd == SDB_KIND_TOMBSTONE) ? 0 : (a.val_off[i + 1] - a.val_off[i]);
+    const uint64_t klen = in.ko1 - in.ko0;
+    const uint8_t kd = in.kd, m = in.m;
+    const uint64_t vlen = (kd == SDB_KIND_TOMBSTONE) ? 0 : (in.vo1 - in.vo0);
     uint32_t lcp = 0;
     int err = 0;
     if (kd > SDB_KIND_TOMBSTONE) err = SDB_INVALID_ARGUMENT;
     if (!err && i > 0) {
-        uint64_t pko = a.key_off[i - 1];
-        uint64_t plen = ko0 - pko;
-        uint64_t mn = plen < klen ? plen : klen;
-        uint32_t nmin = (uint32_t)(mn > 0xFFFFFFFFull ? 0xFFFFFFFFull : mn);
-        lcp = lcp_bytes(a.key_bytes + pko, nmin, a.key_bytes + ko0, nmin);
+        const uint64_t plen = in.ko0 - in.pko;
+        const uint64_t mn = plen < klen ? plen : klen;
+        const uint32_t nmin = (uint32_t)(mn > 0xFFFFFFFFull ? 0xFFFFFFFFull : mn);
+        // compute_prefix (block_v2.rs:52-75) on the preloaded 16 bytes, then on from HBM
+        const uint32_t n0 = nmin < 8 ? nmin : 8, n1 = nmin < 16 ? nmin - n0 : 8;
+        uint64_t x0 = in.pk0 ^ in.ck0, x1 = in.pk1 ^ in.ck1;
+        if (n0 < 8) x0 &= (1ull << (8 * n0)) - 1;
+        if (n1 < 8) x1 &= (1ull << (8 * n1)) - 1;
+        if (x0) lcp = __builtin_ctzll(x0) >> 3;
+        else if (x1) lcp = 8 + (__builtin_ctzll(x1) >> 3);
+        else if (nmin <= 16) lcp = nmin;
+        else lcp = 16 + lcp_bytes(a.key_bytes + in.pko + 16, nmin - 16, a.key_bytes + in.ko0 + 16, nmin - 16);
         // compute_index_key runs on every entry (sst_builder.rs:228): assert on empty keys and
         // out-of-bounds panic when this key is a proper prefix of the previous one (utils.rs:210-216)
         if (klen == 0) err = SDB_EMPTY_KEY;
@@ -86,42 +156,127 @@ SDB_DEV EntryFacts entry_facts(const EncodeArgs &a, uint64_t i) {
     return f;
 }
 
+SDB_DEV EntryFacts entry_facts(const EncodeArgs &a, uint64_t i) {
+    FactsIn in;
+    facts_load_offsets(a, i, in);
+    facts_load_keys(a, in);
+    return facts_finish(a, i, in);
+}
+
 // ------------------------------------------------------------------------------------------------
-// K1 seg: one workgroup per chunk of kChunk entries (+ kChunk lookahead staged in LDS).
-//   a. entry facts for [cs, cs + 2 kChunk): sizes -> LDS; LCP, errors, stats for the chunk's own
-//      entries;
-//   b. next(b) for every b of the chunk (BlockBuilderV2::would_fit / V1::would_fit walk in LDS);
-//   c. pointer jumping in LDS: for every entry point e of the chunk the first block start past the
-//      chunk, and the blocks and bytes on the way (the chunk transfer table).
+// K1 seg: one workgroup per chunk of kChunk entries, plus a lookahead of seg_look entries (the
+// longest block a chunk entry can start) staged in LDS.
+//   a. entry facts for the staged span: LCP, errors and stats of the chunk's own entries; row sizes
+//      clamped to block_size + 16 (a clamped entry never fits after another one, exactly like the
+//      real one) -> LDS;
+//   b. V2: P = exclusive prefix of the non-restart sizes, R = prefix of the restart surcharges along
+//      each residue class mod restart_interval.  size(b, e) of a block [b, e) is then O(1):
+//        2 + P[e] - P[b] + R[last restart] - R[b - ri];
+//   c. next(b) = the largest e with size(b, e) <= block_size (at least b + 1): a search started at
+//      the estimate block_size / (mean row size) that steps by the size formula (BlockBuilderV2::
+//      would_fit, block_v2.rs:151-164: adding an entry keeps the block within block_size);
+//      V1 (prefixes against the block's first key) keeps the entry-by-entry walk;
+//   d. chains from the seg_look candidate entry points at the chunk start, walked in LDS to the first
+//      block start past the chunk: exit, blocks and bytes per candidate (the chunk transfer table).
 // ------------------------------------------------------------------------------------------------
-SDB_DEV uint32_t walk_size_v2(const EncodeArgs &a, const uint32_t *s_r, const uint32_t *s_nr, uint64_t lo,
-                              uint64_t hi, uint64_t j, bool rs) {
-    if (j < hi) return rs ? s_r[j - lo] : s_nr[j - lo];
+SDB_DEV uint32_t walk_size_v2(const EncodeArgs &a, uint64_t j, bool rs) {
     EntryFacts f = entry_facts(a, j);
     return rs ? f.s_r : f.s_nr;
 }
 
-__global__ __launch_bounds__(kSegThreads) void k_seg(EncodeArgs a) {
+__global__ __launch_bounds__(kSegThreads, 8) void k_seg(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint32_t *s_r = (uint32_t *)smem;                 // kSegSpan
-    uint32_t *s_nr = s_r + kSegSpan;                  // kSegSpan
-    uint64_t *p_b = (uint64_t *)(s_nr + kSegSpan);    // kChunk
-    uint16_t *p_s = (uint16_t *)(p_b + kChunk);       // kChunk (offset of the chain position from cs)
-    uint16_t *p_c = p_s + kChunk;                     // kChunk
+    uint32_t *s_r = (uint32_t *)smem;          // kSegSpan: true restart-row sizes (V1: row sizes)
+    uint32_t *s_P = s_r + kSegSpan;            // kSegSpan + 4: prefix of clamped non-restart sizes
+    uint32_t *s_R = s_P + kSegSpan + 4;        // kSegSpan: residue-class prefix of restart surcharges
+    uint32_t *s_bb = s_R + kSegSpan;           // kChunk: encoded block bytes for blocks starting here
+    uint16_t *s_nx = (uint16_t *)(s_bb + kChunk);  // kChunk: next(b) - cs (0xFFFF: out of range)
     __shared__ uint64_t s_part[kSegThreads / 64][5];
     __shared__ uint32_t s_len[kSegThreads / 64];
+    __shared__ uint64_t s_w[17];
     const uint32_t k = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
     const uint64_t cs = (uint64_t)k * kChunk;
     const uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
     const uint64_t se = ce + a.seg_look < a.n ? ce + a.seg_look : a.n;
-    const uint32_t cn = (uint32_t)(ce - cs);
+    const uint32_t cn = (uint32_t)(ce - cs), sn = (uint32_t)(se - cs);
+    const uint64_t bs = a.block_size;
+    const uint32_t clampv = (uint32_t)(bs + 16);
+    // prefix sums of clamped sizes stay < 2^32 for block sizes up to 1 MiB; beyond that (and for V1)
+    // next() walks entry by entry
+    const bool v2 = a.version == 2 && bs <= (1u << 20);
+    const uint32_t ri = a.restart_interval;
+    PHASE_MARK(0);
     // a. facts
     uint64_t rk = 0, rv = 0;
     uint32_t puts = 0, dels = 0, merges = 0;
-    for (uint64_t e = cs + tid; e < se; e += nt) {
-        EntryFacts f = entry_facts(a, e);
-        s_r[e - cs] = f.s_r;
-        s_nr[e - cs] = f.s_nr;
+    // lanes hold consecutive entries, so the next / previous entry's offsets and key prefix come
+    // from the neighbour lane (DPP); lanes 0 / 63 load theirs
+    constexpr uint32_t kPerT = kSegSpan / kSegThreads;
+    struct Own {
+        uint64_t ko, vo, k0, k1;
+        uint8_t kd, m;
+    } own[kPerT];
+    const uint32_t lane = (uint32_t)lane_id();
+#pragma unroll
+    for (uint32_t u = 0; u < kPerT; u++) {
+        const uint32_t x = tid + u * nt;
+        if (x < sn) {
+            const uint64_t e = cs + x;
+            own[u].ko = a.key_off[e];
+            own[u].vo = a.val_off[e];
+            own[u].kd = a.kind ? a.kind[e] : 0;
+            own[u].m = a.ts_mask ? a.ts_mask[e] : 0;
+        }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kPerT; u++) {
+        const uint32_t x = tid + u * nt;
+        own[u].k0 = own[u].k1 = 0;
+        if (x < sn) {
+            const uint64_t e = cs + x;
+            const uint64_t kl = a.key_off[e + 1] - own[u].ko;  // L1 hit: the neighbour's load
+            const uint32_t n = (uint32_t)(kl < 16 ? kl : 16);
+            if (n) own[u].k0 = load8(a.key_bytes + own[u].ko, n < 8 ? n : 8);
+            if (n > 8) own[u].k1 = load8(a.key_bytes + own[u].ko + 8, n - 8);
+        }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kPerT; u++) {
+        const uint32_t x = tid + u * nt;
+        const uint64_t e = cs + x;
+        FactsIn in;
+        in.ko0 = own[u].ko;
+        in.vo0 = own[u].vo;
+        in.kd = own[u].kd;
+        in.m = own[u].m;
+        in.ck0 = own[u].k0;
+        in.ck1 = own[u].k1;
+        in.ko1 = wave_next_lane(own[u].ko);
+        in.vo1 = wave_next_lane(own[u].vo);
+        in.pko = wave_prev_lane(own[u].ko);
+        in.pk0 = wave_prev_lane(own[u].k0);
+        in.pk1 = wave_prev_lane(own[u].k1);
+        if (x < sn) {
+            if (lane == 63 || x + 1 == sn) {
+                in.ko1 = a.key_off[e + 1];
+                in.vo1 = a.val_off[e + 1];
+            }
+            if (lane == 0) {
+                in.pko = e > 0 ? a.key_off[e - 1] : in.ko0;
+                const uint64_t pl = in.ko0 - in.pko;
+                const uint32_t n = (uint32_t)(pl < 16 ? pl : 16);
+                in.pk0 = n ? load8(a.key_bytes + in.pko, n < 8 ? n : 8) : 0;
+                in.pk1 = n > 8 ? load8(a.key_bytes + in.pko + 8, n - 8) : 0;
+            }
+        }
+        if (x >= sn) continue;
+        EntryFacts f = facts_finish(a, e, in);
+        s_r[x] = f.s_r;
+        if (v2) {
+            const uint32_t cr = f.s_r < clampv ? f.s_r : clampv, cnr = f.s_nr < clampv ? f.s_nr : clampv;
+            s_P[x] = cnr;
+            s_R[x] = cr + 2 - cnr;  // restart row: restart size + its 2-byte offset, instead of cnr
+        }
         if (e < ce) {
             a.lcp[e] = f.lcp;
             if (f.err) report_error(a.err, e, f.err);
@@ -152,39 +307,103 @@ __global__ __launch_bounds__(kSegThreads) void k_seg(EncodeArgs a) {
         for (uint32_t q = 0; q < nt / 64; q++) t += s_part[q][tid];
         a.stat_part[5 * (uint64_t)k + tid] = t;
     }
-    // b. next(b)
+    PHASE_MARK(1);
+    // b. prefix sums (V2)
+    if (v2) {
+        uint64_t carry = 0;
+        for (uint32_t x0 = 0; x0 < sn; x0 += nt) {
+            const uint32_t x = x0 + tid;
+            const uint64_t v = x < sn ? s_P[x] : 0;
+            uint64_t tot;
+            const uint64_t ex = block_excl_scan_u64(v, s_w, &tot);
+            if (x < sn) s_P[x] = (uint32_t)(carry + ex);
+            carry += tot;
+        }
+        if (tid == 0) s_P[sn] = (uint32_t)carry;
+        PHASE_MARK(2);
+        // R[x] = sum of surcharges at x, x - ri, x - 2 ri, ... (Hillis-Steele along each residue class)
+        for (uint32_t stride = ri; stride < sn; stride <<= 1) {
+            uint32_t nv[kPerT];
+#pragma unroll
+            for (uint32_t u = 0; u < kPerT; u++) {
+                const uint32_t x = tid + u * nt;
+                nv[u] = (x < sn && x >= stride) ? s_R[x] + s_R[x - stride] : (x < sn ? s_R[x] : 0);
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t u = 0; u < kPerT; u++) {
+                const uint32_t x = tid + u * nt;
+                if (x < sn) s_R[x] = nv[u];
+            }
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    PHASE_MARK(3);
+    // c. next(b)
     uint32_t maxlen = 0;
-    const uint64_t bs = a.block_size;
-    for (uint64_t b = cs + tid; b < ce; b += nt) {
-        uint64_t acc = 2;  // Block::size of an empty block: data 0 + offsets 0 + count 2
-        uint64_t j = b;
-        uint32_t p = 0;
-        if (a.version == 2) {
-            const uint32_t ri = a.restart_interval;
-            uint32_t ph = 0;  // p % ri
-            // staged part: LDS only
-            while (j < se) {
+    for (uint32_t x = tid; x < cn; x += nt) {
+        const uint64_t b = cs + x;
+        uint64_t j;        // next(b)
+        uint64_t bytes;    // Block::size of [b, j) (+ CRC below)
+        if (v2) {
+            // size(b, e) for b < e <= sn (clamped sizes; exact whenever it is <= block_size)
+            const uint32_t Pb = s_P[x];
+            const uint32_t Rb = x >= ri ? s_R[x - ri] : 0;
+            auto size_of = [&](uint32_t e) -> uint64_t {
+                const uint32_t last = x + ((e - 1 - x) / ri) * ri;  // last restart row of [x, e)
+                return 2ull + (s_P[e] - Pb) + (s_R[last] - Rb);
+            };
+            // start from an estimate and step (sizes are positive, so size(b, e) grows with e)
+            uint32_t lo = x + 1;  // size(b, lo) may exceed block_size: a one-entry block
+            uint32_t e = lo;
+            {
+                const uint32_t w = (x + 64 < sn ? x + 64 : sn) - x;
+                const uint32_t mean = (s_P[x + w] - Pb) / w + 1;
+                uint32_t est = x + (uint32_t)(bs / mean);
+                e = est < lo ? lo : (est > sn ? sn : est);
+            }
+            if (size_of(e) <= bs) {
+                while (e < sn && size_of(e + 1) <= bs) e++;
+            } else {
+                while (e > lo && size_of(e) > bs) e--;
+            }
+            j = cs + e;
+            if (e == lo) bytes = 2ull + s_r[x] + 2;  // single row: its true size
+            else bytes = size_of(e);
+            if (e == sn && se < a.n) {
+                // the block may continue past the staged span (only for blocks longer than
+                // seg_look, i.e. never when seg_look bounds the longest block): walk on from HBM
+                uint64_t acc = bytes;
+                uint32_t p = e - x, ph = p % ri;
+                while (j < a.n) {
+                    const bool rs = ph == 0;
+                    const uint64_t add = (uint64_t)walk_size_v2(a, j, rs) + (rs ? 2 : 0);
+                    if (acc + add > bs) break;
+                    acc += add;
+                    j++;
+                    if (++ph == ri) ph = 0;
+                }
+                bytes = acc;
+            }
+        } else if (a.version == 2) {  // huge blocks: V2 walk with sizes from HBM
+            uint64_t acc = 2;
+            j = b;
+            uint32_t p = 0, ph = 0;
+            while (j < a.n) {
                 const bool rs = ph == 0;
-                const uint64_t add = (uint64_t)(rs ? s_r[j - cs] : s_nr[j - cs]) + (rs ? 2 : 0);
+                const uint64_t add = (uint64_t)walk_size_v2(a, j, rs) + (rs ? 2 : 0);
                 if (p > 0 && acc + add > bs) break;
                 acc += add;
                 j++;
                 p++;
                 if (++ph == ri) ph = 0;
             }
-            // a block longer than the staged span (rare): continue from HBM
-            if (j == se) {
-                while (j < a.n) {
-                    const bool rs = ph == 0;
-                    const uint64_t add = (uint64_t)walk_size_v2(a, s_r, s_nr, cs, se, j, rs) + (rs ? 2 : 0);
-                    if (p > 0 && acc + add > bs) break;
-                    acc += add;
-                    j++;
-                    p++;
-                    if (++ph == ri) ph = 0;
-                }
-            }
+            bytes = acc;
         } else {
+            uint64_t acc = 2;
+            j = b;
+            uint32_t p = 0;
             const uint64_t fko = a.key_off[b];
             const uint32_t fkl = (uint32_t)(a.key_off[b + 1] - fko);
             while (j < a.n) {
@@ -200,14 +419,14 @@ __global__ __launch_bounds__(kSegThreads) void k_seg(EncodeArgs a) {
                 j++;
                 p++;
             }
+            bytes = acc;
         }
-        const uint32_t bb = (uint32_t)(acc + 4);  // + CRC32 (format/sst.rs:541-552)
+        const uint32_t bb = (uint32_t)(bytes + 4);  // + CRC32 (format/sst.rs:541-552)
         a.next[b] = (uint32_t)j;
         a.bbytes[b] = bb;
+        s_bb[x] = bb;
         const uint64_t rel = j - cs;
-        p_s[b - cs] = (uint16_t)(rel < 0xFFFF ? rel : 0xFFFF);
-        p_c[b - cs] = 1;
-        p_b[b - cs] = bb;
+        s_nx[x] = (uint16_t)(rel < 0xFFFF ? rel : 0xFFFF);
         const uint32_t len = (uint32_t)(j - b);
         maxlen = len > maxlen ? len : maxlen;
     }
@@ -219,47 +438,24 @@ __global__ __launch_bounds__(kSegThreads) void k_seg(EncodeArgs a) {
         for (uint32_t q = 0; q < nt / 64; q++) m = s_len[q] > m ? s_len[q] : m;
         a.wmax_part[k] = m;
     }
-    // c. pointer jumping (single buffer: read a round into registers, barrier, write back)
-    constexpr uint32_t kPer = kChunk / kSegThreads;
-    for (int round = 0; round < 24; round++) {
-        uint32_t ns[kPer], nc[kPer];
-        uint64_t nb[kPer];
-        int changed = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < kPer; u++) {
-            uint32_t e = tid + u * nt;
-            if (e < cn) {
-                uint32_t t = p_s[e];
-                ns[u] = t;
-                nc[u] = p_c[e];
-                nb[u] = p_b[e];
-                if (t < cn) {
-                    ns[u] = p_s[t];
-                    nc[u] += p_c[t];
-                    nb[u] += p_b[t];
-                    changed = 1;
-                }
-            }
+    PHASE_MARK(4);
+    // d. chains from the candidate entry points [cs, cs + seg_look)
+    const uint32_t Wc = a.seg_look;
+    for (uint32_t c = tid; c < Wc; c += nt) {
+        uint32_t e = c, cnt = 0;
+        uint64_t by = 0;
+        while (e < cn) {
+            by += s_bb[e];
+            cnt++;
+            e = s_nx[e];
         }
-        if (!__syncthreads_or(changed)) break;
-#pragma unroll
-        for (uint32_t u = 0; u < kPer; u++) {
-            uint32_t e = tid + u * nt;
-            if (e < cn) {
-                p_s[e] = (uint16_t)ns[u];
-                p_c[e] = (uint16_t)nc[u];
-                p_b[e] = nb[u];
-            }
-        }
-        __syncthreads();
+        const uint64_t t = (uint64_t)k * Wc + c;
+        // 0xFFFFFFFF: the exit is beyond the u16 range (resolve then walks next[])
+        a.tab_exit[t] = c >= cn ? (uint32_t)ce : (e == 0xFFFF ? 0xFFFFFFFFu : (uint32_t)(cs + e));
+        a.tab_cnt[t] = cnt;
+        a.tab_bytes[t] = by;
     }
-    for (uint32_t e = tid; e < cn; e += nt) {
-        uint32_t t = p_s[e];
-        // 0xFFFF: the chain left the LDS-addressable range; the resolve's serial fallback uses next[]
-        a.tab_exit[cs + e] = t == 0xFFFF ? 0xFFFFFFFFu : (uint32_t)(cs + t);
-        a.tab_cnt[cs + e] = p_c[e];
-        a.tab_bytes[cs + e] = p_b[e];
-    }
+    PHASE_MARK(5);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -279,6 +475,7 @@ __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
     while (KP < K) KP <<= 1;
     if (tid == 0) s_wmax = 0;
     __syncthreads();
+    PHASE_MARK_AT(1023, 0);
     // W = longest candidate block; SstStats partial sums (one batch of loads)
     {
         uint32_t m = 0;
@@ -311,8 +508,9 @@ __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
     if (tid == 0) *a.wmax = W;
     const uint64_t ex_bytes = ((uint64_t)KP * W * 2 + 15) & ~15ull;
     const uint64_t v_bytes = ((uint64_t)KP * 4 + 15) & ~15ull;
-    const bool fast = W <= kChunk && ex_bytes + v_bytes + (uint64_t)KP * W + 16 <= kResolveLds;
+    const bool fast = W <= a.seg_look && ex_bytes + v_bytes + (uint64_t)KP * W + 16 <= kResolveLds;
     uint32_t *v = (uint32_t *)(smem + ex_bytes);  // KP entry offsets (fast path)
+    PHASE_MARK_AT(1023, 1);
     if (fast) {
         uint16_t *ex = (uint16_t *)smem;  // KP x W exit offsets
         // ex[k][o] = entry offset into chunk k+1 reached from entry offset o into chunk k
@@ -327,7 +525,7 @@ __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
                 if (idx < total && k < K) {
                     uint64_t cs = (uint64_t)k * kChunk;
                     uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
-                    val[u] = cs + o < ce ? (uint32_t)(a.tab_exit[cs + o] - ce) : 0;
+                    val[u] = cs + o < ce ? (uint32_t)(a.tab_exit[(uint64_t)k * a.seg_look + o] - ce) : 0;
                 }
             }
 #pragma unroll
@@ -337,6 +535,7 @@ __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
             }
         }
         __syncthreads();
+        PHASE_MARK_AT(1023, 2);
         // Blelloch up-sweep: ex[k] <- ex[k] o ex[k-d] for k = 2d-1 (mod 2d).  A level reads entries
         // of ex[k] that other threads of the same level overwrite, so results go through `tmp`.
         uint16_t *tmp = (uint16_t *)(smem + ex_bytes + v_bytes);
@@ -355,6 +554,7 @@ __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
             }
             __syncthreads();
         }
+        PHASE_MARK_AT(1023, 3);
         // down-sweep of the single chain that starts at entry 0
         if (tid == 0) v[0] = 0;
         __syncthreads();
@@ -366,24 +566,28 @@ __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
             __syncthreads();
         }
     } else if (tid == 0) {
-        // general fallback (a block longer than a chunk, or too many chunk tables): serial walk
+        // general fallback (blocks longer than the staged lookahead, or too many chunk tables):
+        // serial walk of the chain; per-chunk counts / bytes stashed in the tab_* slot of offset 0
         v = (uint32_t *)smem;
         uint64_t e = 0;
         for (uint32_t k = 0; k < K; k++) {
             uint64_t cs = (uint64_t)k * kChunk;
             uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
             v[k] = (uint32_t)(e - cs);
-            if (e < ce) {
-                uint32_t t = a.tab_exit[e];
-                if (t == 0xFFFFFFFFu)
-                    while (e < ce) e = a.next[e];
-                else
-                    e = t;
+            uint32_t cnt = 0;
+            uint64_t by = 0;
+            while (e < ce) {
+                by += a.bbytes[e];
+                cnt++;
+                e = a.next[e];
             }
+            a.tab_cnt[(uint64_t)k * a.seg_look] = cnt;
+            a.tab_bytes[(uint64_t)k * a.seg_look] = by;
         }
     }
     if (!fast) v = (uint32_t *)smem;
     __syncthreads();
+    PHASE_MARK_AT(1023, 4);
     // per-chunk block counts / bytes from the entry point; exclusive scans give the anchors
     uint64_t cb = 0, cy = 0;
     for (uint32_t k0 = 0; k0 < K; k0 += nt) {
@@ -394,8 +598,9 @@ __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
             uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
             e = cs + v[k];
             if (e < ce) {
-                c = a.tab_cnt[e];
-                by = a.tab_bytes[e];
+                const uint64_t t = (uint64_t)k * a.seg_look + (fast ? v[k] : 0);
+                c = a.tab_cnt[t];
+                by = a.tab_bytes[t];
             }
         }
         uint64_t tc, ty;
@@ -418,6 +623,7 @@ __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
         a.summary->num_entries = a.n;
         if (cb > a.block_cap || cy > a.data_cap) report_error(a.err, 0, SDB_INVALID_ARGUMENT);
     }
+    PHASE_MARK_AT(1023, 5);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -596,7 +802,7 @@ __global__ __launch_bounds__(256) void k_enum(EncodeArgs a) {
             uint64_t v = t < nb ? bl_b[t] : 0;
             uint64_t inc = wave_incl_scan(v);
             if (t < nb) bl_o[t] = carry + inc - v;
-            carry += __shfl(inc, 63, 64);
+            carry += wave_readlane(inc, 63);
         }
     }
     __syncthreads();
@@ -671,33 +877,84 @@ SDB_DEV void copy_field(lu8 *img, uint32_t fa, uint32_t L, const uint8_t *src) {
     if (tb) lds_put_bytes(img + A1, load8(src + (A1 - fa), tb), tb);
 }
 
-// lane: image bytes [fa, fa + L) <- stage bytes [sa, sa + L) (both LDS, any alignment): dword
-// interior by aligned reads + v_alignbyte, <= 3 + 3 edge bytes bytewise.
-SDB_DEV void lds_move(lu8 *img, uint32_t fa, const lu8 *stage, uint32_t sa, uint32_t L) {
-    if (!L) return;
-    const uint32_t A0 = (fa + 3) & ~3u, A1 = (fa + L) & ~3u;
-    if (A1 <= A0) {
-        for (uint32_t i = 0; i < L; i++) img[fa + i] = stage[sa + i];
-        return;
-    }
-    const uint32_t hb = A0 - fa;
-    for (uint32_t i = 0; i < hb; i++) img[fa + i] = stage[sa + i];
-    const uint32_t s0 = sa + hb, sh = s0 & 3, nd = (A1 - A0) >> 2;
-    const lu32 *sw = (const lu32 *)(stage + (s0 & ~3u));
-    lu32 *dw = (lu32 *)(img + A0);
-    if (sh == 0) {
-#pragma unroll 1
-        for (uint32_t k = 0; k < nd; k++) dw[k] = sw[k];
-    } else {
-        uint32_t lo = sw[0];
-#pragma unroll 1
-        for (uint32_t k = 0; k < nd; k++) {
-            const uint32_t hi = sw[k + 1];
-            dw[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
-            lo = hi;
+// Key-suffix + value copy into the block image.  A row's copy span is [F0, F1): from its key suffix
+// (rounded down to a dword) to the end of its value (rounded up).  Each image dword of the span is
+// produced by one lane from two aligned LDS dwords + v_alignbyte, reading the key stage for the
+// dwords that hold only key bytes and the value stage for all others.  Bytes of those dwords that
+// belong to the row's header / trailer, and the <= 3 key bytes that share a dword with value or
+// trailer bytes, come out as garbage and are overwritten by the row lane's literal writes, which are
+// issued after all copies (DS instructions of one wave execute in order).
+//
+// The value stage overlaps the image (value byte x of the block is staged at image byte
+// x - 64 - (vs & 15) + 64 ... see stage_base): every value is staged at or below its image position
+// (a row's header/key/trailer bytes only push it right; the 64-byte guard covers row 0), so copying
+// rows in decreasing order never reads a clobbered byte as long as each row is read before it is
+// written: a batch of spans of <= 32 dwords reads all of them before writing any; longer spans go
+// one row at a time, 64 dwords per pass, passes top-down (a row's image bytes sit >= 52 bytes above
+// its staged bytes, so a pass never overwrites the stage of a lower pass).
+struct SpanCopy {
+    uint32_t a;   // F0 >> 2 | nd << 16: first image dword and dword count of the span
+    uint32_t jk;  // leading dwords taken from the key stage
+    uint32_t kb;  // LDS byte address (key stage) of image byte F0, as if the key extended left
+    uint32_t vb;  // LDS byte address (value stage) of image byte F0, as if the value extended left
+};
+typedef __attribute__((address_space(3))) SpanCopy lSpanCopy;
+
+SDB_DEV uint32_t span_src(uint32_t j, uint32_t jk, uint32_t kb, uint32_t vb) {
+    const uint32_t off = (j < jk ? kb : vb) + 4 * j;
+    const lu32 *w = (const lu32 *)(uintptr_t)(off & ~3u);
+    return __builtin_amdgcn_alignbyte(w[1], w[0], off & 3);
+}
+
+SDB_DEV void copy_spans(lu8 *img, const lSpanCopy *tab, uint32_t ne) {
+    const uint32_t l = (uint32_t)lane_id(), half = l >> 5, j0 = l & 31;
+    lu32 *dw = (lu32 *)img;
+    constexpr uint32_t kB = 4;  // row pairs per batch
+    for (uint32_t p0 = 0; p0 < ne; p0 += 2 * kB) {
+        uint32_t f0[kB], nd[kB], jk[kB], kb[kB], vb[kB];
+        uint32_t mx = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kB; q++) {
+            const uint32_t i = p0 + 2 * q + half;  // rows in decreasing order
+            nd[q] = 0;
+            f0[q] = jk[q] = kb[q] = vb[q] = 0;
+            if (i < ne) {
+                const uint32_t r = ne - 1 - i;
+                const uint32_t ta = tab[r].a;
+                f0[q] = ta & 0xFFFF;
+                nd[q] = ta >> 16;
+                jk[q] = tab[r].jk;
+                kb[q] = tab[r].kb;
+                vb[q] = tab[r].vb;
+            }
+            mx = nd[q] > mx ? nd[q] : mx;
+        }
+        mx = wave_max(mx);
+        if (mx <= 32) {
+            // every span of the batch fits one pass: all reads, then all writes
+            uint32_t v[kB];
+#pragma unroll
+            for (uint32_t q = 0; q < kB; q++)
+                if (j0 < nd[q]) v[q] = span_src(j0, jk[q], kb[q], vb[q]);
+#pragma unroll
+            for (uint32_t q = 0; q < kB; q++)
+                if (j0 < nd[q]) dw[f0[q] + j0] = v[q];
+        } else {
+            // long spans: one row at a time (decreasing), 64 dwords per pass, passes top-down
+            for (uint32_t i = p0; i < p0 + 2 * kB && i < ne; i++) {
+                const uint32_t r = ne - 1 - i;
+                const uint32_t ta = tab[r].a, rjk = tab[r].jk, rkb = tab[r].kb, rvb = tab[r].vb;
+                const uint32_t rf0 = ta & 0xFFFF, rnd = ta >> 16;
+                for (uint32_t c = (rnd + 63) >> 6; c-- > 0;) {
+                    const uint32_t j = 64 * c + l;
+                    uint32_t v = 0;
+                    if (j < rnd) v = span_src(j, rjk, rkb, rvb);
+                    wave_sync();
+                    if (j < rnd) dw[rf0 + j] = v;
+                }
+            }
         }
     }
-    for (uint32_t i = A1 - fa; i < L; i++) img[fa + i] = stage[sa + i];
 }
 
 template <int V>
@@ -743,59 +1000,98 @@ SDB_DEV uint32_t write_row_hdr_trailer(lu8 *dst, const RowInfo &r, uint64_t seq,
     return h;
 }
 
+// 4 * byte SEL of w in one VALU op (SDWA operand select): the LDS byte offset of a table entry.
+template <int SEL>
+SDB_DEV uint32_t bytex4(uint32_t w) {
+    uint32_t r;
+    if constexpr (SEL == 0)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+            : "=v"(r) : "v"(w));
+    else if constexpr (SEL == 1)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+            : "=v"(r) : "v"(w));
+    else if constexpr (SEL == 2)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+            : "=v"(r) : "v"(w));
+    else
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+            : "=v"(r) : "v"(w));
+    return r;
+}
+// k_emit keeps the tables at LDS address 0 (its only LDS is the dynamic region, checked at entry),
+// so a lookup is ds_read_b32 <byte offset>, offset:<table * 1024> with no address add.
+template <int T>
+SDB_DEV uint32_t crc_tab(const lu32 *, uint32_t off4) {
+    return *(const lu32 *)(uintptr_t)(T * 1024 + off4);
+}
+// slicing-by-8 step over the 8 message bytes (lo, hi), tables at LDS `tab` (8 x 256 u32)
 SDB_DEV uint32_t crc_slice8_lds(uint32_t c, uint32_t lo, uint32_t hi, const lu32 *tab) {
     lo ^= c;
-    return tab[7 * 256 + (lo & 0xFF)] ^ tab[6 * 256 + ((lo >> 8) & 0xFF)] ^ tab[5 * 256 + ((lo >> 16) & 0xFF)] ^
-           tab[4 * 256 + (lo >> 24)] ^ tab[3 * 256 + (hi & 0xFF)] ^ tab[2 * 256 + ((hi >> 8) & 0xFF)] ^
-           tab[1 * 256 + ((hi >> 16) & 0xFF)] ^ tab[hi >> 24];
+    const uint32_t x = crc_tab<7>(tab, bytex4<0>(lo)) ^ crc_tab<6>(tab, bytex4<1>(lo)) ^ crc_tab<5>(tab, bytex4<2>(lo));
+    const uint32_t y = crc_tab<4>(tab, bytex4<3>(lo)) ^ crc_tab<3>(tab, bytex4<0>(hi)) ^ crc_tab<2>(tab, bytex4<1>(hi));
+    const uint32_t z = crc_tab<1>(tab, bytex4<2>(hi)) ^ crc_tab<0>(tab, bytex4<3>(hi));
+    return x ^ y ^ z;
+}
+
+// x^256 * c (the x^(8*32) shift of a CRC) from the 4 byte tables at LDS 8 KiB (k_emit layout)
+SDB_DEV uint32_t crc_mul256_lds(uint32_t c) {
+    return crc_tab<8>(nullptr, bytex4<0>(c)) ^ crc_tab<9>(nullptr, bytex4<1>(c)) ^ crc_tab<10>(nullptr, bytex4<2>(c)) ^
+           crc_tab<11>(nullptr, bytex4<3>(c));
 }
 
 template <int V>
-SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, lu8 *stage, const lu32 *crc) {
+SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, lu8 *kst, lSpanCopy *rtab, const lu32 *crc,
+                        uint64_t *ph) {
+    WAVE_T(t0);
     const uint32_t l = (uint32_t)lane_id();
     const BlockDesc d = a.desc[blk];
     const uint32_t ne = d.e - d.s;
-    const uint64_t va = d.vs & ~15ull;
+    const uint64_t va = d.vs & ~15ull, ka = d.ks & ~15ull;
     const uint32_t nv16 = d.ve > d.vs ? (uint32_t)((d.ve - va + 15) >> 4) : 0;
-    if (!(ne <= 64 && d.bb + 64 <= kImgCap && nv16 <= kStageCap / 16)) {
+    const uint32_t nk16 = (uint32_t)((d.ke - ka + 15) >> 4);
+    if (!(ne <= 64 && d.bb + 64 <= kImgCap && nv16 <= kStageCap / 16 && nk16 <= kKeyStageCap / 16)) {
         if (l == 0) {
             uint32_t slot = atomicAdd(a.slow_count, 1u);
             a.slow_list[slot] = blk;
         }
         return;
     }
-    // 1. row metadata (lane = row)
-    const bool row = l < ne;
-    const uint64_t j = d.s + l;
-    uint64_t ko = 0, vo = 0, seq = 0;
-    int64_t cts = 0, ets = 0;
-    uint32_t lcp = 0;
-    uint8_t kind = 0, mask = 0;
-    if (row) {
-        ko = a.key_off[j];
-        vo = a.val_off[j];
-        kind = a.kind ? a.kind[j] : 0;
-        mask = a.ts_mask ? a.ts_mask[j] : 0;
-        seq = a.seq ? a.seq[j] : 0;
-        lcp = a.lcp[j];
-        if (mask & SDB_TS_CREATE) cts = a.create_ts[j];
-        if (mask & SDB_TS_EXPIRE) ets = a.expire_ts[j];
-    }
-    uint32_t prev_klen = 0;
-    if (l == 0 && d.s > 0) prev_klen = (uint32_t)(d.ks - a.key_off[d.s - 1]);
-    // the block's value bytes -> stage (coalesced LDS-DMA, 1 KiB per wave instruction; lanes past
-    // the range reload the last granule into unused stage slots so the instruction count is fixed)
+    // value stage: value byte x lands at LDS (img - kStageGuard) + (x - va), i.e. at or below its
+    // image position (see copy_spans); keys land in the key stage
+    const uint32_t vstage = lds_addr((const void *)img) - kStageGuard;
+    const uint32_t kstage = lds_addr((const void *)kst);
+    // 0. LDS-DMA of the block's values and keys (1 KiB per wave instruction; lanes past the range
+    //    reload the last granule into an unused slot so the instruction count is fixed)
     if (nv16) {
-        const uint32_t stage_lds = lds_addr((const void *)stage);
 #pragma unroll
         for (uint32_t q = 0; q < kStageCap / 1024; q++) {
             uint32_t g = 64 * q + l;
             g = g < nv16 ? g : nv16 - 1;
             __builtin_amdgcn_global_load_lds((glb_void *)(a.val_bytes + va + 16 * (uint64_t)g),
-                                             (lds_void *)(uintptr_t)(stage_lds + 1024 * q), 16, 0, 0);
+                                             (lds_void *)(uintptr_t)(vstage + 1024 * q), 16, 0, 0);
         }
     }
-    uint64_t ko1 = __shfl_down(ko, 1, 64), vo1 = __shfl_down(vo, 1, 64);
+#pragma unroll
+    for (uint32_t q = 0; q < kKeyStageCap / 1024; q++) {
+        uint32_t g = 64 * q + l;
+        g = g < nk16 ? g : nk16 - 1;
+        __builtin_amdgcn_global_load_lds((glb_void *)(a.key_bytes + ka + 16 * (uint64_t)g),
+                                         (lds_void *)(uintptr_t)(kstage + 1024 * q), 16, 0, 0);
+    }
+    // 1. row metadata (lane = row)
+    const bool row = l < ne;
+    const uint64_t j = d.s + (row ? l : 0);
+    const uint64_t ko = a.key_off[j], vo = a.val_off[j];
+    const uint64_t seq = a.seq ? a.seq[j] : 0;
+    const uint32_t lcp = a.lcp[j];
+    const uint8_t kind = row && a.kind ? a.kind[j] : 0;
+    const uint8_t mask = row && a.ts_mask ? a.ts_mask[j] : 0;
+    int64_t cts = 0, ets = 0;
+    if (mask & SDB_TS_CREATE) cts = a.create_ts[j];
+    if (mask & SDB_TS_EXPIRE) ets = a.expire_ts[j];
+    uint32_t prev_klen = 0;
+    if (l == 0 && d.s > 0) prev_klen = (uint32_t)(d.ks - a.key_off[d.s - 1]);
+    uint64_t ko1 = wave_next_lane(ko), vo1 = wave_next_lane(vo);
     if (l + 1 == ne) {
         ko1 = d.ke;
         vo1 = d.ve;
@@ -806,7 +1102,7 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, lu8 *stage,
     uint32_t shared = 0;
     if (V == 2 && row) shared = (l % ri == 0) ? 0 : lcp;
     if (V == 1 && row && l > 0) {  // prefix vs the block's first key (block.rs:117-123)
-        const uint32_t fkl = __shfl(klen, 0, 64);
+        const uint32_t fkl = wave_readlane(klen, 0);
         shared = lcp_bytes(a.key_bytes + d.ks, fkl, a.key_bytes + ko, klen);
     }
     RowInfo r;
@@ -818,35 +1114,54 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, lu8 *stage,
                         ((mask & SDB_TS_EXPIRE) ? SDB_FLAG_HAS_EXPIRE_TS : 0) |
                         ((mask & SDB_TS_CREATE) ? SDB_FLAG_HAS_CREATE_TS : 0));
     const uint32_t ts8 = 8u * (((mask & SDB_TS_CREATE) != 0) + ((mask & SDB_TS_EXPIRE) != 0));
-    uint32_t size = 0;
+    uint32_t size = 0, h = 0;
     if (row) {
-        if (V == 2) size = varint_len(shared) + varint_len(r.suf) + varint_len(vlen) + r.suf + vlen + 9 + ts8;
-        else size = 4 + r.suf + 9 + ts8 + (kind == SDB_KIND_TOMBSTONE ? 0 : 4 + vlen);
+        if (V == 2) {
+            h = varint_len(shared) + varint_len(r.suf) + varint_len(vlen);
+            size = h + r.suf + vlen + 9 + ts8;
+        } else {
+            h = 4;
+            size = 4 + r.suf + 9 + ts8 + (kind == SDB_KIND_TOMBSTONE ? 0 : 4 + vlen);
+        }
     }
     r.size = size;
     const uint32_t inc = wave_incl_scan(size);
     const uint32_t row_off = inc - size;
-    const uint32_t D = __shfl(inc, 63, 64);
+    const uint32_t D = wave_readlane(inc, 63);
     const uint32_t noffs = (V == 2) ? (ne + ri - 1) / ri : ne;
     const uint32_t Lc = D + 2 * noffs + 2;  // CRC input length
     const uint32_t nseg = (Lc + 63) >> 6;
-    // zero the padding of the last CRC segment (dword-granular; message bytes come after)
-    {
-        const uint32_t z0 = Lc & ~3u, nz = ((nseg << 6) - z0) >> 2;
-        if (l < nz) ((lu32 *)(img + z0))[l] = 0;
-    }
-    // 2. rows
-    uint32_t vdst = 0;
+    // copy span of the row: key suffix .. value end
+    const uint32_t kstart = row_off + h, kend = kstart + r.suf;
+    const uint32_t vstart = (V == 2) ? kend : row_off + size - vlen;
+    const uint32_t vend = vlen ? vstart + vlen : kend;
     if (row) {
-        lu8 *rowp = img + row_off;
-        const uint32_t h = write_row_hdr_trailer<V>(rowp, r, seq, ets, cts);
-        copy_field(img, row_off + h, r.suf, a.key_bytes + ko + shared);
-        vdst = row_off + ((V == 2) ? h + r.suf : (size - vlen));
+        const uint32_t F0 = kstart & ~3u, F1 = (vend + 3) & ~3u;
+        SpanCopy sc;
+        sc.a = (F0 >> 2) | (((F1 - F0) >> 2) << 16);
+        sc.jk = (kend - F0) >> 2;
+        sc.kb = kstage + (uint32_t)(ko + shared - ka) - (kstart - F0);
+        sc.vb = vstage + (uint32_t)(vo - va) - (vstart - F0);
+        rtab[l].a = sc.a;
+        rtab[l].jk = sc.jk;
+        rtab[l].kb = sc.kb;
+        rtab[l].vb = sc.vb;
     }
-    __builtin_amdgcn_s_waitcnt(0);  // stage landed (LDS-DMA counts on vmcnt)
+    WAVE_T(t1);
+    __builtin_amdgcn_s_waitcnt(0);  // stages landed (LDS-DMA counts on vmcnt)
     wave_sync();
-    if (row) lds_move(img, vdst, stage, (uint32_t)(vo - va), vlen);
-    // offsets + count (Block::encode, format/block.rs:17-26)
+    WAVE_T(t2);
+    // 2. key suffixes + values (cooperative)
+    copy_spans(img, rtab, ne);
+    WAVE_T(t3);
+    // 3. literals: header, the key bytes sharing a dword with non-key bytes, trailer; then the
+    //    restart table, count and the zero padding of the last CRC segment
+    if (row) {
+        write_row_hdr_trailer<V>(img + row_off, r, seq, ets, cts);
+        const uint32_t kj = (kend & ~3u) > kstart ? (kend & ~3u) : kstart;  // first key byte not
+        for (uint32_t x = kj; x < kend; x++)                                 // in a key dword
+            img[x] = kst[(uint32_t)(ko + shared - ka) + (x - kstart)];
+    }
     if (V == 2) {
         if (row && l % ri == 0) {
             uint32_t q = l / ri;
@@ -858,24 +1173,32 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, lu8 *stage,
         img[D + 2 * l] = (uint8_t)(row_off >> 8);  // `as u16` (block.rs:163)
         img[D + 2 * l + 1] = (uint8_t)row_off;
     }
-    if (l == 0) {
-        img[D + 2 * noffs] = (uint8_t)(noffs >> 8);
-        img[D + 2 * noffs + 1] = (uint8_t)noffs;
+    {
+        const uint32_t z0 = (Lc + 3) & ~3u, nz = ((nseg << 6) - z0) >> 2;
+        if (l < nz) ((lu32 *)(img + z0))[l] = 0;
+        if (l == 0) {
+            img[D + 2 * noffs] = (uint8_t)(noffs >> 8);
+            img[D + 2 * noffs + 1] = (uint8_t)noffs;
+            for (uint32_t x = Lc; x < z0; x++) img[x] = 0;
+        }
     }
-    __builtin_amdgcn_s_waitcnt(0);
     wave_sync();
-    // 3. CRC32 (format/sst.rs:541-552)
+    WAVE_T(t4);
+    // 4. CRC32 (format/sst.rs:541-552): lane l = 64-byte segment l, two 32-byte chains
     uint32_t acc = 0;
     for (uint32_t sg = l; sg < nseg; sg += 64) {
         const lu128 *src = (const lu128 *)(img + 64 * sg);
-        uint32_t c = 0;
-#pragma unroll
-        for (int g = 0; g < 4; g++) {
-            u32x4 v = src[g];
-            if (g == 0 && sg == 0) v.x = ~v.x;  // crc32fast init 0xFFFFFFFF folded into bytes [0, 4)
-            c = crc_slice8_lds(c, v.x, v.y, crc);
-            c = crc_slice8_lds(c, v.z, v.w, crc);
-        }
+        u32x4 v0 = src[0], v1 = src[1], v2 = src[2], v3 = src[3];
+        if (sg == 0) v0.x = ~v0.x;  // crc32fast init 0xFFFFFFFF folded into bytes [0, 4)
+        uint32_t ca = crc_slice8_lds(0, v0.x, v0.y, crc), cb = crc_slice8_lds(0, v2.x, v2.y, crc);
+        ca = crc_slice8_lds(ca, v0.z, v0.w, crc);
+        cb = crc_slice8_lds(cb, v2.z, v2.w, crc);
+        ca = crc_slice8_lds(ca, v1.x, v1.y, crc);
+        cb = crc_slice8_lds(cb, v3.x, v3.y, crc);
+        ca = crc_slice8_lds(ca, v1.z, v1.w, crc);
+        cb = crc_slice8_lds(cb, v3.z, v3.w, crc);
+        // raw(seg) = raw(first 32) * x^256 + raw(last 32)
+        const uint32_t c = crc_mul256_lds(ca) ^ cb;
         acc ^= seg_shift_mul(nseg - 1 - sg, c);
     }
     acc = wave_xor(acc);
@@ -889,7 +1212,8 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, lu8 *stage,
         if (Lc + 4 != d.bb) report_error(a.err, d.s, SDB_DEVICE_ERROR);  // internal consistency
     }
     wave_sync();
-    // 4. store [0, Lc + 4) -> out_data + off
+    WAVE_T(t5);
+    // 5. store [0, Lc + 4) -> out_data + off
     uint8_t *gdst = a.out_data + d.off;
     const uint32_t L = Lc + 4, nfull = L >> 4;
     for (uint32_t c = l; c < nfull; c += 64) {
@@ -899,7 +1223,17 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, lu8 *stage,
     if (l == 0) {
         for (uint32_t q = nfull << 4; q < L; q++) gdst[q] = img[q];
     }
-    // 5. BlockStats (sst_stats.rs:9-16) and the index key (compute_index_key, utils.rs:198-226)
+    WAVE_T(t6);
+#ifdef SDB_PHASE_TIMING
+    ph[0] += t1 - t0;
+    ph[1] += t2 - t1;
+    ph[2] += t3 - t2;
+    ph[3] += t4 - t3;
+    ph[4] += t5 - t4;
+    ph[5] += t6 - t5;
+    ph[6] += 1;
+#endif
+    // 6. BlockStats (sst_stats.rs:9-16) and the index key (compute_index_key, utils.rs:198-226)
     const uint64_t pu = __ballot(row && kind == SDB_KIND_VALUE);
     const uint64_t de = __ballot(row && kind == SDB_KIND_TOMBSTONE);
     const uint64_t me = __ballot(row && kind == SDB_KIND_MERGE);
@@ -915,18 +1249,30 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, lu8 *stage,
 }
 
 template <int V>
-__global__ __launch_bounds__(kEmitThreads, 4) void k_emit(EncodeArgs a) {
+__global__ __launch_bounds__(kEmitThreads, 5) void k_emit(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if (*a.err != ~0ull) return;  // any earlier error (incl. capacity): write nothing
     const uint32_t nb = a.anchor_blk[a.nchunks];
     lu32 *crc = (lu32 *)smem;
+    if (lds_addr((const void *)smem) != 0) {  // crc_tab / crc_mul256_lds assume LDS address 0
+        if (threadIdx.x == 0) report_error(a.err, 0, SDB_DEVICE_ERROR);
+        return;
+    }
     for (uint32_t q = threadIdx.x; q < 8 * 256; q += blockDim.x) crc[q] = (&c_crc.t[0][0])[q];
+    for (uint32_t q = threadIdx.x; q < 4 * 256; q += blockDim.x) crc[8 * 256 + q] = (&c_mul256.t[0][0])[q];
     __syncthreads();
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), wpb = blockDim.x >> 6;
-    lu8 *img = (lu8 *)smem + kCrcLds + wave * (kImgCap + kStageCap);
-    lu8 *stage = img + kImgCap;
+    lu8 *wbase = (lu8 *)smem + kCrcLds + wave * kEmitWaveLds;
+    lu8 *img = wbase + kStageGuard;
+    lu8 *kst = img + kImgCap + 16;
+    lSpanCopy *rtab = (lSpanCopy *)(kst + kKeyStageCap);
     const uint32_t gw = blockIdx.x * wpb + wave, G = gridDim.x * wpb;
-    for (uint32_t blk = gw; blk < nb; blk += G) emit_block<V>(a, blk, img, stage, crc);
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t blk = gw; blk < nb; blk += G) emit_block<V>(a, blk, img, kst, rtab, crc, ph);
+#ifdef SDB_PHASE_TIMING
+    if (lane_id() == 0 && gw < 8192)
+        for (int i = 0; i < 8; i++) g_wave_phase[gw][i] = ph[i];
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1016,8 +1362,8 @@ __global__ __launch_bounds__(256) void k_emit_slow(EncodeArgs a) {
             }
             __syncthreads();
             // offsets table entries for this round are written after D is known: store row offsets
-            // temporarily in the workspace `lcp` is still needed, so stash into tab_cnt (per entry)
-            if (i < ne) a.tab_cnt[b + i] = (uint32_t)s_off[threadIdx.x];
+            // temporarily in the workspace `lcp` is still needed, so stash into row_scratch (per entry)
+            if (i < ne) a.row_scratch[b + i] = (uint32_t)s_off[threadIdx.x];
             D = s_off[blockDim.x - 1] + s_size[blockDim.x - 1];
             __syncthreads();
         }
@@ -1045,7 +1391,7 @@ __global__ __launch_bounds__(256) void k_emit_slow(EncodeArgs a) {
         }
         uint32_t noffs = (V == 2) ? (ne + ri - 1) / ri : ne;
         for (uint32_t q = threadIdx.x; q < noffs; q += blockDim.x) {
-            uint32_t ro = a.tab_cnt[b + (V == 2 ? (uint64_t)q * ri : q)];
+            uint32_t ro = a.row_scratch[b + (V == 2 ? (uint64_t)q * ri : q)];
             dst[D + 2 * q] = (uint8_t)(ro >> 8);
             dst[D + 2 * q + 1] = (uint8_t)ro;
         }
@@ -1131,11 +1477,20 @@ __global__ void k_finish_summary(EncodeArgs a, uint64_t bloom_len, uint32_t num_
     }
 }
 
+#ifdef SDB_PHASE_TIMING
+extern "C" int sdb_diag_wave_phase(uint64_t *out, int nwaves) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_phase), sizeof(uint64_t) * 8 * nwaves) == hipSuccess ? 0 : -1;
+}
+extern "C" int sdb_diag_phase_times(uint64_t *out, int nblocks) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(uint64_t) * 8 * nblocks) == hipSuccess ? 0 : -1;
+}
+#endif
+
 static bool lds_attrs_set = false;
 static int g_cus = 0;
 static uint32_t g_emit_threads = kEmitThreads, g_emit_wg_per_cu = kEmitWgPerCu;
 static uint32_t emit_grid() { return (uint32_t)(g_cus > 0 ? g_emit_wg_per_cu * g_cus : 512); }
-static uint32_t emit_lds() { return kCrcLds + (g_emit_threads / 64) * (kImgCap + kStageCap); }
+static uint32_t emit_lds() { return kCrcLds + (g_emit_threads / 64) * kEmitWaveLds; }
 static void set_lds_attrs() {
     if (lds_attrs_set) return;
     int dev = 0;
