@@ -1,0 +1,184 @@
+"""Secondary measurements for BASELINE.json configs[2..3] and the host-memory (E2E) encode path.
+
+  python scripts/bench_configs.py [--decode] [--bloom] [--e2e] [--reps R]
+
+Prints one JSON line per measurement.  Not the headline bench (bench.py is); these numbers feed
+DESIGN.md:
+  decode  configs[2]: 16 D1 SSTs (suffix 0..15) encoded on the GPU, their 272,256 blocks decoded in
+          one sdb_decode_blocks launch sequence (device-resident in and out); also 2 MiB ranges.
+          Algorithmic bytes = encoded bytes read + Σ(|k| + 8 + 1 + 8·ts) + value refs are not
+          counted.
+  bloom   configs[3]: 10 M sorted random 16 B keys, 10 bits/key; bitmap bit-exact vs the oracle.
+  e2e     configs[1] from pinned host memory: sdb_encoder_encode_host (H2D + kernels + D2H).
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from slatedb_amd import _abi, datasets, runtime  # noqa: E402
+
+PEAK = 8000.0
+
+
+def timed(fn, reps, stream):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def decode_bench(reps):
+    lib = runtime.lib()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(device=dev)
+    prm = runtime.params(block_size=4096, sst_version=2, bloom_bits_per_key=0)
+    chunks, offs, keys, nent = [], [], [], 0
+    base = 0
+    for j in range(16):
+        h = datasets.d1(sst_index=j)
+        db = h.to_device(dev)
+        out = runtime.DeviceSstOutput(h.n, h.logical_bytes(), h.logical_bytes(), prm, device=dev)
+        runtime.encode_sst_device(db, out)
+        torch.cuda.synchronize()
+        sm = out.summary_host()
+        assert sm.status == 0
+        chunks.append(out.data[:sm.data_len].clone())
+        bo = out.block_off[:sm.num_blocks + 1].clone()
+        offs.append(bo[:-1] + base if j < 15 else bo + base)
+        base += sm.data_len
+        keys.append(h.key_bytes)
+        nent += h.n
+        del db, out
+    blocks = torch.cat(chunks)
+    block_off = torch.cat(offs)
+    nb = block_off.numel() - 1
+    kbytes = int(sum(k.size for k in keys))
+    o = lambda n, dt: torch.empty(n, dtype=dt, device=dev)
+    bes, ka, ko = o(nb + 1, torch.int64), o(kbytes + 16, torch.uint8), o(nent + 1, torch.int64)
+    vo, vl, sq = o(nent, torch.int64), o(nent, torch.int32), o(nent, torch.int64)
+    fl, ct, et = o(nent, torch.uint8), o(nent, torch.int64), o(nent, torch.int64)
+    bad, smy = o(nb + 1, torch.int32), torch.zeros(64, dtype=torch.uint8, device=dev)
+    dout = _abi.DecodedOut(bes.data_ptr(), ka.data_ptr(), kbytes + 16, ko.data_ptr(), vo.data_ptr(),
+                           vl.data_ptr(), sq.data_ptr(), fl.data_ptr(), ct.data_ptr(), et.data_ptr(), nent,
+                           bad.data_ptr(), nb + 1, smy.data_ptr())
+    wsb = lib.sdb_decode_workspace_bytes(nb)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+
+    def run(b0=0, b1=nb):
+        st = lib.sdb_decode_blocks(blocks.data_ptr(), block_off[b0:].data_ptr(), b1 - b0, 2, C.byref(dout),
+                                   ws.data_ptr(), wsb, s.cuda_stream)
+        assert st == 0, st
+
+    with torch.cuda.stream(s):
+        ms = timed(run, reps, s)
+    torch.cuda.synchronize()
+    sm = _abi.DecodeSummary.from_buffer_copy(smy.cpu().numpy().tobytes()[:C.sizeof(_abi.DecodeSummary)])
+    ok = sm.status == 0 and sm.num_entries == nent and sm.num_bad_blocks == 0
+    ok = ok and np.array_equal(ka[:kbytes].cpu().numpy(), np.concatenate(keys))
+    enc = int(blocks.numel())
+    alg = enc + nent * (16 + 8 + 1 + 8)  # encoded bytes + Σ(|k| + 8 + 1 + 8·ts) (val refs 8)
+    gbs = alg / (ms * 1e-3) / 1e9
+    print(json.dumps({"what": "decode configs[2]", "blocks": nb, "entries": nent, "encoded_bytes": enc,
+                      "ms": round(ms, 4), "GiB_per_s_encoded": round(enc / (ms * 1e-3) / 2**30, 2),
+                      "algorithmic_bytes": alg, "achieved_GBps": round(gbs, 1), "frac": round(gbs / PEAK, 4),
+                      "verified_keys": bool(ok)}), flush=True)
+    # 2 MiB ranged-GET granularity (≈ 520 blocks per call), launched back to back
+    per = 520
+    ranges = [(b, min(nb, b + per)) for b in range(0, nb, per)]
+
+    def run_ranges():
+        for b0, b1 in ranges:
+            run(b0, b1)
+
+    with torch.cuda.stream(s):
+        ms2 = timed(run_ranges, max(1, reps // 4), s)
+    print(json.dumps({"what": "decode configs[2] at 2 MiB granularity", "calls": len(ranges), "ms": round(ms2, 4),
+                      "GiB_per_s_encoded": round(enc / (ms2 * 1e-3) / 2**30, 2)}), flush=True)
+
+
+def bloom_bench(reps):
+    from oracle import oracle as O
+    lib = runtime.lib()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(device=dev)
+    kb, ko = datasets.c4_keys()
+    n = len(ko) - 1
+    dk = torch.from_numpy(kb).to(dev)
+    do = torch.from_numpy(ko.view(np.uint8)).to(dev)
+    fb = lib.sdb_bloom_filter_bytes(n, 10)
+    bm = torch.empty(fb + 16, dtype=torch.uint8, device=dev)
+    wsb = lib.sdb_bloom_workspace_bytes(n, 10)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+
+    def run():
+        st = lib.sdb_bloom_build(dk.data_ptr(), do.data_ptr(), n, 10, bm.data_ptr(), fb, ws.data_ptr(), wsb,
+                                 s.cuda_stream)
+        assert st == 0
+
+    with torch.cuda.stream(s):
+        ms = timed(run, reps, s)
+    got = bm[:fb].cpu().numpy()
+    t0 = time.perf_counter()
+    ref = O.bloom_build(kb, ko, 10)
+    cpu_s = time.perf_counter() - t0
+    ok = np.array_equal(got, np.frombuffer(bytes(ref), np.uint8) if not isinstance(ref, np.ndarray) else ref)
+    alg = n * 16 + fb
+    gbs = alg / (ms * 1e-3) / 1e9
+    print(json.dumps({"what": "bloom configs[3]", "keys": n, "bitmap_bytes": fb, "ms": round(ms, 4),
+                      "Mkeys_per_s": round(n / (ms * 1e-3) / 1e6, 1), "algorithmic_bytes": alg,
+                      "achieved_GBps": round(gbs, 1), "frac": round(gbs / PEAK, 4), "bit_exact": bool(ok),
+                      "oracle_1thread_s": round(cpu_s, 3)}), flush=True)
+
+
+def e2e_bench(reps):
+    h = datasets.d1(sst_index=0)
+    enc = runtime.Encoder(runtime.params(block_size=4096, sst_version=2, bloom_bits_per_key=10))
+    for _ in range(2):
+        enc.encode(h)
+    ev = []
+    for _ in range(reps):
+        r = enc.encode(h)
+        assert r.status == 0
+        ev.append(r.timings_ms)
+    med = {k: round(float(np.median([e[k] for e in ev])), 4) for k in ev[0]}
+    ms = sum(med.values())
+    print(json.dumps({"what": "e2e configs[1] host->host (pageable batch -> pinned staging, H2D + kernels + D2H)",
+                      "ms": round(ms, 3), "GiB_per_s_logical": round(h.logical_bytes() / (ms * 1e-3) / 2**30, 2),
+                      "events_ms_median": med, "num_blocks": r.num_blocks}), flush=True)
+    enc.close()
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--decode", action="store_true")
+    p.add_argument("--bloom", action="store_true")
+    p.add_argument("--e2e", action="store_true")
+    p.add_argument("--reps", type=int, default=20)
+    a = p.parse_args()
+    allp = not (a.decode or a.bloom or a.e2e)
+    torch.cuda.set_device(0)
+    runtime.require_device()
+    if a.bloom or allp:
+        bloom_bench(a.reps)
+    if a.decode or allp:
+        decode_bench(a.reps)
+    if a.e2e or allp:
+        e2e_bench(a.reps)
+
+
+if __name__ == "__main__":
+    main()
