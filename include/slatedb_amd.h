@@ -84,8 +84,8 @@ typedef struct sdb_kv_batch {
     const uint64_t *val_off;    /* n+1 */
     const uint8_t *kind;        /* n; NULL = all SDB_KIND_VALUE */
     const uint64_t *seq;        /* n; NULL = all 0 */
-    const int64_t *create_ts;   /* n; read only where ts_mask & SDB_TS_CREATE */
-    const int64_t *expire_ts;   /* n; read only where ts_mask & SDB_TS_EXPIRE */
+    const int64_t *create_ts;   /* n (NULL = none); used where ts_mask & SDB_TS_CREATE, any entry may be read */
+    const int64_t *expire_ts;   /* n (NULL = none); used where ts_mask & SDB_TS_EXPIRE, any entry may be read */
     const uint8_t *ts_mask;     /* n; NULL = no timestamps */
 } sdb_kv_batch;
 

@@ -47,3 +47,14 @@ per = w[:, :6].sum(axis=0) / w[:, 6].sum()
 for n, v in zip(names, per):
     print("  %-16s %8.0f" % (n, v))
 print("  total            %8.0f  (per-wave total mean %.0f)" % (per.sum(), w[:, :6].sum(axis=1).mean()))
+
+rb = (C.c_uint64 * (4 * 8192))()
+cdll.sdb_diag_wave_rt.argtypes = [C.c_void_p, C.c_int]
+assert cdll.sdb_diag_wave_rt(C.addressof(rb), 8192) == 0
+r = np.frombuffer(rb, dtype=np.uint64).reshape(8192, 4).astype(np.int64)
+r = r[r[:, 1] > 0][:len(w)]
+st, en = (r[:, 0] - r[:, 0].min()) / 100.0, (r[:, 1] - r[:, 0].min()) / 100.0  # 100 MHz -> us
+clk = (r[:, 3] - r[:, 2]) / np.maximum(r[:, 1] - r[:, 0], 1) * 100.0
+print("k_emit waves (us from first start): start p50 %.1f p90 %.1f max %.1f; end p10 %.1f p50 %.1f max %.1f; "
+      "wave duration p50 %.1f; shader clock %.0f MHz (median)" % (np.percentile(st, 50), np.percentile(st, 90), st.max(),
+      np.percentile(en, 10), np.percentile(en, 50), en.max(), np.median(en - st), np.median(clk)))

@@ -183,6 +183,8 @@ sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const 
     a.desc = carve<BlockDesc>(workspace, wl.desc);
     a.stat_part = carve<uint64_t>(workspace, wl.stat_part);
     a.wmax_part = carve<uint32_t>(workspace, wl.wmax_part);
+    a.err_part = carve<unsigned long long>(workspace, wl.err_part);
+    a.done = carve<uint32_t>(workspace, wl.done);
     a.out_data = out->data;
     a.out_block_off = out->block_off;
     a.out_block_first = out->block_first_entry;

@@ -131,7 +131,28 @@ constexpr CrcMul256 make_mul256() {
     return r;
 }
 
+// tree[s][b][v] = x^(8*64*2^s) * (v << 8b) mod P, s = 0..5: the wave combine of 64 segment CRCs in
+// 6 pairwise steps (left segment run shifted past a right run of 2^s 64-byte segments).
+constexpr int kTreeSteps = 6;
+struct CrcTree {
+    uint32_t t[kTreeSteps][4][256];
+};
+constexpr CrcTree make_tree() {
+    CrcTree r{};
+    for (int s = 0; s < kTreeSteps; s++) {
+        const uint32_t K = x8n_c(64ull << s);
+        for (int b = 0; b < 4; b++) {
+            uint32_t basis[8] = {};
+            for (int i = 0; i < 8; i++) basis[i] = gf_mul_c(K, 1u << (8 * b + i));
+            r.t[s][b][0] = 0;
+            for (int v = 1; v < 256; v++) r.t[s][b][v] = r.t[s][b][v & (v - 1)] ^ basis[__builtin_ctz(v)];
+        }
+    }
+    return r;
+}
+
 // Per translation unit (no relocatable device code needed).
+static __device__ const CrcTree g_tree = make_tree();
 static __constant__ CrcTables c_crc = make_crc_tables();
 static __constant__ CrcShift64 c_shift = make_shift64();
 static __constant__ CrcSegShift c_seg = make_seg_shift();

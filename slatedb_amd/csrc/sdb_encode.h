@@ -9,7 +9,7 @@ namespace sdb {
 
 constexpr uint32_t kChunk = 2048;            // entries per chunk (K3 / K5)
 constexpr uint32_t kResolveLds = 96 * 1024;  // LDS budget of the resolve tables (u16 exits)
-constexpr uint32_t kCrcLds = 12 * 1024;      // slicing-by-8 tables + x^256 byte tables
+constexpr uint32_t kCrcLds = 36 * 1024;      // slicing-by-8 tables + x^256 byte tables + 6 combine-tree steps
 constexpr uint32_t kImgCap = 4096 + 64;      // LDS block image per wave (fast path)
 constexpr uint32_t kStageCap = 4096;         // value staging per wave (LDS-DMA, 1 KiB per instruction), in place
 constexpr uint32_t kStageGuard = 64;         // LDS bytes before each image the value stage may use
@@ -18,13 +18,13 @@ constexpr uint32_t kSegLook = 1024;           // k_seg: max lookahead entries st
 constexpr uint32_t kSegSpan = kChunk + kSegLook;
 constexpr uint32_t kSegThreads = 1024;
 constexpr uint32_t kSegLds = (3 * kSegSpan + 4) * 4 + kChunk * 6;
-constexpr uint32_t kEmitThreads = 640;       // 10 waves per workgroup (one block each), 2 per CU
-constexpr uint32_t kEmitWgPerCu = 2;
+constexpr uint32_t kEmitThreads = 1024;      // 16 waves per workgroup (two blocks in flight each), 1 per CU
+constexpr uint32_t kEmitWgPerCu = 1;
 constexpr uint32_t kEmitWaveLds = kStageGuard + kImgCap + 16 + kKeyStageCap + 64 * 16;  // guard, image, key stage, spans
 constexpr uint32_t kEmitLds = kCrcLds + (kEmitThreads / 64) * kEmitWaveLds;
 constexpr uint32_t kEnumLds = kChunk * 16 + 12 * kChunk * 2;  // block list + 12 lifting levels
 
-struct BlockDesc {  // one per block, written by k_enum, streamed by k_emit (48 bytes)
+struct BlockDesc {  // one per block, written by k_enum, streamed by k_emit (56 bytes)
     uint32_t s, e;        // entries [s, e)
     uint64_t off;         // byte offset of the block in the data section
     uint64_t vs, ve, ks, ke;  // value / key byte ranges of the block
@@ -67,6 +67,8 @@ struct EncodeArgs {
     BlockDesc *desc;
     uint64_t *stat_part;    // per chunk: raw key, raw val, puts, deletes, merges
     uint32_t *wmax_part;    // per chunk: longest candidate block (entries)
+    unsigned long long *err_part;  // per chunk: min (entry << 8 | code) of k_seg's checks (~0: none)
+    uint32_t *done;         // k_emit workgroups finished (the last one writes the summary)
     uint32_t nprep_wg;
     // outputs (device)
     uint8_t *out_data;
@@ -84,6 +86,7 @@ struct EncodeArgs {
 struct EncodeWorkspace {
     uint64_t lcp, row_scratch, next, bbytes, tab_exit, tab_cnt, tab_bytes;
     uint64_t anchor_e, anchor_blk, anchor_byte, err, wmax, slow_count, slow_list, desc, stat_part, wmax_part, bloom_rep;
+    uint64_t err_part, done;
     uint64_t total;
 };
 uint64_t bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
@@ -113,6 +116,8 @@ inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes
     w.desc = take(sizeof(BlockDesc) * (n + 1));
     w.stat_part = take(8 * 5 * (nc + 1));
     w.wmax_part = take(4 * (nc + 1));
+    w.err_part = take(8 * (nc + 1));
+    w.done = take(4);
     w.bloom_rep = take(filter_bytes ? bloom_workspace_bytes(n, num_probes, filter_bytes) : 0);  // bloom buckets
     w.total = off;
     return w;

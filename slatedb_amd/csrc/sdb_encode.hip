@@ -42,6 +42,7 @@ __device__ uint64_t g_phase[1024][8];
         if (threadIdx.x == 0 && blockIdx.x < 1024) g_phase[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 __device__ uint64_t g_wave_phase[8192][8];
+__device__ uint64_t g_wave_rt[8192][4];  // k_emit per wave: s_memrealtime start/end, s_memtime start/end
 #define WAVE_T(var)                                     \
     uint64_t var = __builtin_amdgcn_s_memtime();        \
     __builtin_amdgcn_s_waitcnt(0xC07F) /* lgkmcnt(0) */
@@ -194,7 +195,10 @@ __global__ __launch_bounds__(kSegThreads, 8) void k_seg(EncodeArgs a) {
     __shared__ uint64_t s_part[kSegThreads / 64][5];
     __shared__ uint32_t s_len[kSegThreads / 64];
     __shared__ uint64_t s_w[17];
+    __shared__ unsigned long long s_err;
     const uint32_t k = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    if (tid == 0) s_err = ~0ull;
+    __syncthreads();
     const uint64_t cs = (uint64_t)k * kChunk;
     const uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
     const uint64_t se = ce + a.seg_look < a.n ? ce + a.seg_look : a.n;
@@ -279,7 +283,7 @@ __global__ __launch_bounds__(kSegThreads, 8) void k_seg(EncodeArgs a) {
         }
         if (e < ce) {
             a.lcp[e] = f.lcp;
-            if (f.err) report_error(a.err, e, f.err);
+            if (f.err) atomicMin(&s_err, (unsigned long long)((e << 8) | (uint64_t)f.err));
             rk += f.klen;
             rv += f.vlen;
             puts += f.kind == SDB_KIND_VALUE;
@@ -307,6 +311,7 @@ __global__ __launch_bounds__(kSegThreads, 8) void k_seg(EncodeArgs a) {
         for (uint32_t q = 0; q < nt / 64; q++) t += s_part[q][tid];
         a.stat_part[5 * (uint64_t)k + tid] = t;
     }
+    if (tid == 0) a.err_part[k] = s_err;  // every chunk writes its slot: no initialisation needed
     PHASE_MARK(1);
     // b. prefix sums (V2)
     if (v2) {
@@ -469,25 +474,33 @@ __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
     __shared__ uint64_t s_w[17];
     __shared__ uint32_t s_wmax;
     __shared__ uint64_t s_stat[5][16];
+    __shared__ unsigned long long s_err;
     const uint32_t K = a.nchunks;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     uint32_t KP = 1;
     while (KP < K) KP <<= 1;
-    if (tid == 0) s_wmax = 0;
+    if (tid == 0) {
+        s_wmax = 0;
+        s_err = ~0ull;
+    }
     __syncthreads();
     PHASE_MARK_AT(1023, 0);
     // W = longest candidate block; SstStats partial sums (one batch of loads)
     {
         uint32_t m = 0;
         uint64_t st[5] = {0, 0, 0, 0, 0};
+        unsigned long long em = ~0ull;
         for (uint32_t q = tid; q < K; q += nt) {
             uint32_t w = a.wmax_part[q];
             m = w > m ? w : m;
+            const unsigned long long ep = a.err_part[q];
+            em = ep < em ? ep : em;
 #pragma unroll
             for (int f = 0; f < 5; f++) st[f] += a.stat_part[5 * (uint64_t)q + f];
         }
         m = wave_max(m);
         if (lane_id() == 0) atomicMax(&s_wmax, m);
+        if (em != ~0ull) atomicMin(&s_err, em);
 #pragma unroll
         for (int f = 0; f < 5; f++) {
             uint64_t t = wave_sum(st[f]);
@@ -505,7 +518,20 @@ __global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
         if (tid == 3) a.summary->num_deletes = t;
         if (tid == 4) a.summary->num_merges = t;
     }
-    if (tid == 0) *a.wmax = W;
+    if (tid == 0) {
+        // the encode's device-side state for the later kernels (this kernel runs alone)
+        *a.wmax = W;
+        *a.err = s_err;
+        *a.slow_count = 0;
+        *a.done = 0;
+        sdb_sst_summary *sm = a.summary;
+        sm->bloom_len = 0;
+        sm->num_probes = 0;
+        sm->filter_built = 0;
+        sm->status = 0;
+        sm->max_block_entries = 0;
+        sm->first_error_entry = ~0ull;
+    }
     const uint64_t ex_bytes = ((uint64_t)KP * W * 2 + 15) & ~15ull;
     const uint64_t v_bytes = ((uint64_t)KP * 4 + 15) & ~15ull;
     const bool fast = W <= a.seg_look && ex_bytes + v_bytes + (uint64_t)KP * W + 16 <= kResolveLds;
@@ -747,6 +773,15 @@ SDB_DEV void wave_store(uint8_t *gdst, const uint8_t *img, uint64_t len) {
     }
 }
 
+// Blocks k_emit assembles in its per-wave LDS image; the rest take the workgroup slow path.
+SDB_DEV bool emit_fast(const BlockDesc &d) {
+    const uint32_t ne = d.e - d.s;
+    const uint64_t va = d.vs & ~15ull, ka = d.ks & ~15ull;
+    const uint32_t nv16 = d.ve > d.vs ? (uint32_t)((d.ve - va + 15) >> 4) : 0;
+    const uint32_t nk16 = (uint32_t)((d.ke - ka + 15) >> 4);
+    return ne <= 64 && d.bb + 64 <= kImgCap && nv16 <= kStageCap / 16 && nk16 <= kKeyStageCap / 16;
+}
+
 // ------------------------------------------------------------------------------------------------
 // K5a: enumerate the blocks of each chunk (binary lifting over next()) -> BlockMeta offsets and the
 //      per-block descriptors the emitter streams.
@@ -822,6 +857,7 @@ __global__ __launch_bounds__(256) void k_enum(EncodeArgs a) {
         d.bb = bl_b[t];
         d.pad = 0;
         a.desc[blk] = d;
+        if (!emit_fast(d)) a.slow_list[atomicAdd(a.slow_count, 1u)] = blk;
     }
 }
 
@@ -920,12 +956,12 @@ SDB_DEV void copy_spans(lu8 *img, const lSpanCopy *tab, uint32_t ne) {
             f0[q] = jk[q] = kb[q] = vb[q] = 0;
             if (i < ne) {
                 const uint32_t r = ne - 1 - i;
-                const uint32_t ta = tab[r].a;
-                f0[q] = ta & 0xFFFF;
-                nd[q] = ta >> 16;
-                jk[q] = tab[r].jk;
-                kb[q] = tab[r].kb;
-                vb[q] = tab[r].vb;
+                const u32x4 t = *(const lu128 *)&tab[r];  // one 16-byte broadcast read
+                f0[q] = t.x & 0xFFFF;
+                nd[q] = t.x >> 16;
+                jk[q] = t.y;
+                kb[q] = t.z;
+                vb[q] = t.w;
             }
             mx = nd[q] > mx ? nd[q] : mx;
         }
@@ -1039,58 +1075,104 @@ SDB_DEV uint32_t crc_mul256_lds(uint32_t c) {
            crc_tab<11>(nullptr, bytex4<3>(c));
 }
 
-template <int V>
-SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, lu8 *kst, lSpanCopy *rtab, const lu32 *crc,
-                        uint64_t *ph) {
-    WAVE_T(t0);
+// Everything one block needs from HBM, loaded into registers one block ahead (software pipeline):
+// the block's value / key granules (lane l holds granules l, 64 + l, ...) and the row metadata
+// (lane = row).  Plain loads only: the compute phase of the current block issues no global load,
+// so the compiler's in-order vmcnt waits never drain the prefetch early.
+struct EmitPre {
+    uint4 vg[kStageCap / 1024];
+    uint4 kg[kKeyStageCap / 1024];
+    uint64_t ko, vo, seq;
+    int64_t cts, ets;
+    uint64_t pko;  // lane 0: key_off[s - 1] (previous key, index-key rule)
+    uint32_t lcp;
+    uint32_t kind, mask;
+};
+
+SDB_DEV BlockDesc desc_from_lanes(uint32_t dv) {  // lanes 0..13 hold the 14 dwords of a BlockDesc
+    uint32_t w[14];
+#pragma unroll
+    for (int i = 0; i < 14; i++) w[i] = (uint32_t)__builtin_amdgcn_readlane((int)dv, i);
+    BlockDesc d;
+    d.s = w[0];
+    d.e = w[1];
+    d.off = w[2] | ((uint64_t)w[3] << 32);
+    d.vs = w[4] | ((uint64_t)w[5] << 32);
+    d.ve = w[6] | ((uint64_t)w[7] << 32);
+    d.ks = w[8] | ((uint64_t)w[9] << 32);
+    d.ke = w[10] | ((uint64_t)w[11] << 32);
+    d.bb = w[12];
+    d.pad = w[13];
+    return d;
+}
+static_assert(sizeof(BlockDesc) == 56, "BlockDesc is 14 dwords");
+
+
+SDB_DEV void emit_prefetch(const EncodeArgs &a, const BlockDesc &d, EmitPre &p) {
     const uint32_t l = (uint32_t)lane_id();
-    const BlockDesc d = a.desc[blk];
     const uint32_t ne = d.e - d.s;
     const uint64_t va = d.vs & ~15ull, ka = d.ks & ~15ull;
     const uint32_t nv16 = d.ve > d.vs ? (uint32_t)((d.ve - va + 15) >> 4) : 0;
     const uint32_t nk16 = (uint32_t)((d.ke - ka + 15) >> 4);
-    if (!(ne <= 64 && d.bb + 64 <= kImgCap && nv16 <= kStageCap / 16 && nk16 <= kKeyStageCap / 16)) {
-        if (l == 0) {
-            uint32_t slot = atomicAdd(a.slow_count, 1u);
-            a.slow_list[slot] = blk;
-        }
-        return;
-    }
+    const uint4 *vsrc = (const uint4 *)(a.val_bytes + va), *ksrc = (const uint4 *)(a.key_bytes + ka);
+#if !defined(SDB_EXP_NO_VALUE_LOAD)
+#pragma unroll
+    for (uint32_t q = 0; q < kStageCap / 1024; q++)
+        if (64 * q + l < nv16) p.vg[q] = vsrc[64 * q + l];
+#endif
+#pragma unroll
+    for (uint32_t q = 0; q < kKeyStageCap / 1024; q++)
+        if (64 * q + l < nk16) p.kg[q] = ksrc[64 * q + l];
+    const bool row = l < ne;
+    const uint64_t j = d.s + (row ? l : 0);
+    p.ko = a.key_off[j];
+    p.vo = a.val_off[j];
+    p.seq = a.seq ? a.seq[j] : 0;
+    p.lcp = a.lcp[j];
+    p.kind = a.kind ? a.kind[j] : 0;      // rows >= ne read entry s (masked at use)
+    p.mask = a.ts_mask ? a.ts_mask[j] : 0;
+    // unconditional loads (selected by the mask at use): a load whose address or predicate hangs on
+    // another prefetched value would make the compiler wait for the whole prefetch here
+    p.cts = a.create_ts ? a.create_ts[j] : 0;
+    p.ets = a.expire_ts ? a.expire_ts[j] : 0;
+    p.pko = (l == 0 && d.s > 0) ? a.key_off[d.s - 1] : 0;
+}
+
+// x^(8*64*2^s) * c from the 4 byte tables of tree step s (LDS 12 KiB + s * 4 KiB, k_emit layout)
+template <int S>
+SDB_DEV uint32_t crc_tree_mul(uint32_t c) {
+    return crc_tab<12 + 4 * S>(nullptr, bytex4<0>(c)) ^ crc_tab<13 + 4 * S>(nullptr, bytex4<1>(c)) ^
+           crc_tab<14 + 4 * S>(nullptr, bytex4<2>(c)) ^ crc_tab<15 + 4 * S>(nullptr, bytex4<3>(c));
+}
+
+template <int V>
+SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, const EmitPre &p, lu8 *img,
+                        lu8 *kst, lSpanCopy *rtab, const lu32 *crc, uint64_t *ph) {
+    WAVE_T(t0);
+    const uint32_t l = (uint32_t)lane_id();
+    const uint32_t ne = d.e - d.s;
+    const uint64_t va = d.vs & ~15ull, ka = d.ks & ~15ull;
+    const uint32_t nv16 = d.ve > d.vs ? (uint32_t)((d.ve - va + 15) >> 4) : 0;
+    const uint32_t nk16 = (uint32_t)((d.ke - ka + 15) >> 4);
     // value stage: value byte x lands at LDS (img - kStageGuard) + (x - va), i.e. at or below its
     // image position (see copy_spans); keys land in the key stage
     const uint32_t vstage = lds_addr((const void *)img) - kStageGuard;
     const uint32_t kstage = lds_addr((const void *)kst);
-    // 0. LDS-DMA of the block's values and keys (1 KiB per wave instruction; lanes past the range
-    //    reload the last granule into an unused slot so the instruction count is fixed)
-    if (nv16) {
+    // 0. prefetched granules -> LDS stages
 #pragma unroll
-        for (uint32_t q = 0; q < kStageCap / 1024; q++) {
-            uint32_t g = 64 * q + l;
-            g = g < nv16 ? g : nv16 - 1;
-            __builtin_amdgcn_global_load_lds((glb_void *)(a.val_bytes + va + 16 * (uint64_t)g),
-                                             (lds_void *)(uintptr_t)(vstage + 1024 * q), 16, 0, 0);
-        }
-    }
+    for (uint32_t q = 0; q < kStageCap / 1024; q++)
+        if (64 * q + l < nv16) *(lu128 *)(uintptr_t)(vstage + 16 * (64 * q + l)) = *(const u32x4 *)&p.vg[q];
 #pragma unroll
-    for (uint32_t q = 0; q < kKeyStageCap / 1024; q++) {
-        uint32_t g = 64 * q + l;
-        g = g < nk16 ? g : nk16 - 1;
-        __builtin_amdgcn_global_load_lds((glb_void *)(a.key_bytes + ka + 16 * (uint64_t)g),
-                                         (lds_void *)(uintptr_t)(kstage + 1024 * q), 16, 0, 0);
-    }
+    for (uint32_t q = 0; q < kKeyStageCap / 1024; q++)
+        if (64 * q + l < nk16) *(lu128 *)(uintptr_t)(kstage + 16 * (64 * q + l)) = *(const u32x4 *)&p.kg[q];
     // 1. row metadata (lane = row)
     const bool row = l < ne;
-    const uint64_t j = d.s + (row ? l : 0);
-    const uint64_t ko = a.key_off[j], vo = a.val_off[j];
-    const uint64_t seq = a.seq ? a.seq[j] : 0;
-    const uint32_t lcp = a.lcp[j];
-    const uint8_t kind = row && a.kind ? a.kind[j] : 0;
-    const uint8_t mask = row && a.ts_mask ? a.ts_mask[j] : 0;
-    int64_t cts = 0, ets = 0;
-    if (mask & SDB_TS_CREATE) cts = a.create_ts[j];
-    if (mask & SDB_TS_EXPIRE) ets = a.expire_ts[j];
+    const uint64_t ko = p.ko, vo = p.vo, seq = p.seq;
+    const uint32_t lcp = p.lcp;
+    const uint8_t kind = row ? (uint8_t)p.kind : 0, mask = row ? (uint8_t)p.mask : 0;
+    const int64_t cts = (mask & SDB_TS_CREATE) ? p.cts : 0, ets = (mask & SDB_TS_EXPIRE) ? p.ets : 0;
     uint32_t prev_klen = 0;
-    if (l == 0 && d.s > 0) prev_klen = (uint32_t)(d.ks - a.key_off[d.s - 1]);
+    if (l == 0 && d.s > 0) prev_klen = (uint32_t)(d.ks - p.pko);
     uint64_t ko1 = wave_next_lane(ko), vo1 = wave_next_lane(vo);
     if (l + 1 == ne) {
         ko1 = d.ke;
@@ -1101,9 +1183,14 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, lu8 *kst, l
     const uint32_t ri = a.restart_interval;
     uint32_t shared = 0;
     if (V == 2 && row) shared = (l % ri == 0) ? 0 : lcp;
-    if (V == 1 && row && l > 0) {  // prefix vs the block's first key (block.rs:117-123)
+    if (V == 1) {  // prefix vs the block's first key (block.rs:117-123), from the key stage
+        wave_sync();
         const uint32_t fkl = wave_readlane(klen, 0);
-        shared = lcp_bytes(a.key_bytes + d.ks, fkl, a.key_bytes + ko, klen);
+        if (row && l > 0) {
+            const lu8 *f = kst + (uint32_t)(d.ks - ka), *c = kst + (uint32_t)(ko - ka);
+            const uint32_t mn = fkl < klen ? fkl : klen;
+            while (shared < mn && f[shared] == c[shared]) shared++;
+        }
     }
     RowInfo r;
     r.shared = shared;
@@ -1148,8 +1235,7 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, lu8 *kst, l
         rtab[l].vb = sc.vb;
     }
     WAVE_T(t1);
-    __builtin_amdgcn_s_waitcnt(0);  // stages landed (LDS-DMA counts on vmcnt)
-    wave_sync();
+    wave_sync();  // stages + span table written (DS instructions of one wave complete in order)
     WAVE_T(t2);
     // 2. key suffixes + values (cooperative)
     copy_spans(img, rtab, ne);
@@ -1184,26 +1270,39 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, lu8 *kst, l
     }
     wave_sync();
     WAVE_T(t4);
-    // 4. CRC32 (format/sst.rs:541-552): lane l = 64-byte segment l, two 32-byte chains
-    uint32_t acc = 0;
-    for (uint32_t sg = l; sg < nseg; sg += 64) {
-        const lu128 *src = (const lu128 *)(img + 64 * sg);
-        u32x4 v0 = src[0], v1 = src[1], v2 = src[2], v3 = src[3];
-        if (sg == 0) v0.x = ~v0.x;  // crc32fast init 0xFFFFFFFF folded into bytes [0, 4)
-        uint32_t ca = crc_slice8_lds(0, v0.x, v0.y, crc), cb = crc_slice8_lds(0, v2.x, v2.y, crc);
-        ca = crc_slice8_lds(ca, v0.z, v0.w, crc);
-        cb = crc_slice8_lds(cb, v2.z, v2.w, crc);
-        ca = crc_slice8_lds(ca, v1.x, v1.y, crc);
-        cb = crc_slice8_lds(cb, v3.x, v3.y, crc);
-        ca = crc_slice8_lds(ca, v1.z, v1.w, crc);
-        cb = crc_slice8_lds(cb, v3.z, v3.w, crc);
-        // raw(seg) = raw(first 32) * x^256 + raw(last 32)
-        const uint32_t c = crc_mul256_lds(ca) ^ cb;
-        acc ^= seg_shift_mul(nseg - 1 - sg, c);
+    // 4. CRC32 (format/sst.rs:541-552).  Segments are right-aligned on the lanes: lane l holds
+    //    64-byte segment l - (64 - nseg), two 32-byte slicing-by-8 chains each; lanes before the
+    //    first segment hold 0 (leading zero bytes leave a raw CRC unchanged).  Six pairwise tree
+    //    steps combine them (lane 0 ends with the whole image), then the zero padding of the last
+    //    segment is removed by x^(-8 t).
+    uint32_t c = 0;
+    {
+        const int sg = (int)l - (64 - (int)nseg);
+        if (sg >= 0) {
+            const lu128 *src = (const lu128 *)(img + 64 * sg);
+            u32x4 v0 = src[0], v1 = src[1], v2 = src[2], v3 = src[3];
+            if (sg == 0) v0.x = ~v0.x;  // crc32fast init 0xFFFFFFFF folded into bytes [0, 4)
+            uint32_t ca = crc_slice8_lds(0, v0.x, v0.y, crc), cb = crc_slice8_lds(0, v2.x, v2.y, crc);
+            ca = crc_slice8_lds(ca, v0.z, v0.w, crc);
+            cb = crc_slice8_lds(cb, v2.z, v2.w, crc);
+            ca = crc_slice8_lds(ca, v1.x, v1.y, crc);
+            cb = crc_slice8_lds(cb, v3.x, v3.y, crc);
+            ca = crc_slice8_lds(ca, v1.z, v1.w, crc);
+            cb = crc_slice8_lds(cb, v3.z, v3.w, crc);
+            c = crc_mul256_lds(ca) ^ cb;  // raw(seg) = raw(first 32) * x^256 + raw(last 32)
+        }
     }
-    acc = wave_xor(acc);
-    const uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)acc);
-    const uint32_t crc32 = gf_mul(c_seg.unpad[(nseg << 6) - Lc], u) ^ 0xFFFFFFFFu;
+    // partner = lane + 2^s: DPP row_shl inside a row, then permlane16 / permlane32 swaps (only the
+    // lanes with bit s clear use the result)
+    c = crc_tree_mul<0>(c) ^ dpp32<0x101>(c);
+    c = crc_tree_mul<1>(c) ^ dpp32<0x102>(c);
+    c = crc_tree_mul<2>(c) ^ dpp32<0x104>(c);
+    c = crc_tree_mul<3>(c) ^ dpp32<0x108>(c);
+    c = crc_tree_mul<4>(c) ^ (uint32_t)__builtin_amdgcn_permlane16_swap(c, c, false, false)[1];
+    c = crc_tree_mul<5>(c) ^ (uint32_t)__builtin_amdgcn_permlane32_swap(c, c, false, false)[1];
+    const uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+    const uint32_t pad = (uint32_t)__builtin_amdgcn_readfirstlane((int)((nseg << 6) - Lc));
+    const uint32_t crc32 = gf_mul(c_seg.unpad[pad], u) ^ 0xFFFFFFFFu;
     if (l == 0) {
         img[Lc] = (uint8_t)(crc32 >> 24);
         img[Lc + 1] = (uint8_t)(crc32 >> 16);
@@ -1215,14 +1314,17 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, lu8 *kst, l
     WAVE_T(t5);
     // 5. store [0, Lc + 4) -> out_data + off
     uint8_t *gdst = a.out_data + d.off;
+#if defined(SDB_EXP_ALIGNED_STORE)
+    gdst = (uint8_t *)((uintptr_t)gdst & ~(uintptr_t)15);  // experiment: wrong bytes, aligned stores
+#endif
     const uint32_t L = Lc + 4, nfull = L >> 4;
-    for (uint32_t c = l; c < nfull; c += 64) {
-        u32x4 v = ((const lu128 *)img)[c];
-        __builtin_memcpy(gdst + 16 * c, &v, 16);
+#if !defined(SDB_EXP_NO_STORE)
+    for (uint32_t cc = l; cc < nfull; cc += 64) {
+        u32x4 v = ((const lu128 *)img)[cc];
+        __builtin_memcpy(gdst + 16 * cc, &v, 16);
     }
-    if (l == 0) {
-        for (uint32_t q = nfull << 4; q < L; q++) gdst[q] = img[q];
-    }
+    if (l < (L & 15)) gdst[(nfull << 4) + l] = img[(nfull << 4) + l];
+#endif
     WAVE_T(t6);
 #ifdef SDB_PHASE_TIMING
     ph[0] += t1 - t0;
@@ -1248,44 +1350,113 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, lu8 *img, lu8 *kst, l
     wave_sync();
 }
 
+// One wave per block, blocks strided over the grid's waves; each wave runs a two-stage software
+// pipeline: while block i is assembled, CRC'd and stored from LDS, block i + 1's granules and row
+// metadata are in flight into registers, and block i + 2's descriptor behind them.
 template <int V>
-__global__ __launch_bounds__(kEmitThreads, 5) void k_emit(EncodeArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    if (*a.err != ~0ull) return;  // any earlier error (incl. capacity): write nothing
-    const uint32_t nb = a.anchor_blk[a.nchunks];
-    lu32 *crc = (lu32 *)smem;
-    if (lds_addr((const void *)smem) != 0) {  // crc_tab / crc_mul256_lds assume LDS address 0
-        if (threadIdx.x == 0) report_error(a.err, 0, SDB_DEVICE_ERROR);
-        return;
+SDB_DEV void emit_slow_blocks(const EncodeArgs &a, uint8_t *scratch, const uint32_t (*s_crc)[256]);
+
+// SstStats / status of the encode, written by the last k_emit workgroup to finish.
+SDB_DEV void finish_summary(const EncodeArgs &a) {
+    sdb_sst_summary *s = a.summary;
+    const unsigned long long e = atomicOr(a.err, 0ull);  // device-scope read of the error word
+    s->max_block_entries = *a.wmax;
+    s->bloom_len = a.bloom_len;
+    s->num_probes = a.num_probes;
+    s->filter_built = a.filter_built;
+    if (e != ~0ull) {
+        s->status = (int32_t)(e & 0xFF);
+        s->first_error_entry = e >> 8;
     }
-    for (uint32_t q = threadIdx.x; q < 8 * 256; q += blockDim.x) crc[q] = (&c_crc.t[0][0])[q];
-    for (uint32_t q = threadIdx.x; q < 4 * 256; q += blockDim.x) crc[8 * 256 + q] = (&c_mul256.t[0][0])[q];
-    __syncthreads();
+}
+
+// One wave per block, blocks strided over the grid's waves; each wave runs a two-stage software
+// pipeline: while block i is assembled, CRC'd and stored from LDS, block i + 1's granules and row
+// metadata are in flight into registers, and block i + 2's descriptor behind them.  Blocks that do
+// not fit the LDS image (k_enum's slow list) are done first, one workgroup each.  The last
+// workgroup to finish writes the summary.
+template <int V>
+__global__ __launch_bounds__(kEmitThreads, 1) void k_emit(EncodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+#ifdef SDB_PHASE_TIMING
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime(), mt0 = __builtin_amdgcn_s_memtime();
+#endif
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), wpb = blockDim.x >> 6;
-    lu8 *wbase = (lu8 *)smem + kCrcLds + wave * kEmitWaveLds;
-    lu8 *img = wbase + kStageGuard;
-    lu8 *kst = img + kImgCap + 16;
-    lSpanCopy *rtab = (lSpanCopy *)(kst + kKeyStageCap);
     const uint32_t gw = blockIdx.x * wpb + wave, G = gridDim.x * wpb;
+    const uint32_t l = (uint32_t)lane_id();
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t blk = gw; blk < nb; blk += G) emit_block<V>(a, blk, img, kst, rtab, crc, ph);
+    bool run = *a.err == ~0ull;  // any earlier error (incl. capacity): write nothing
+    if (run && lds_addr((const void *)smem) != 0) {  // crc_tab / crc_mul256_lds / crc_tree_mul assume LDS address 0
+        if (threadIdx.x == 0) report_error(a.err, 0, SDB_DEVICE_ERROR);
+        run = false;
+    }
+    if (run) {
+        lu32 *crc = (lu32 *)smem;
+        for (uint32_t q = threadIdx.x; q < 8 * 256; q += blockDim.x) crc[q] = (&c_crc.t[0][0])[q];
+        for (uint32_t q = threadIdx.x; q < 4 * 256; q += blockDim.x) crc[8 * 256 + q] = (&c_mul256.t[0][0])[q];
+        for (uint32_t q = threadIdx.x; q < kTreeSteps * 4 * 256; q += blockDim.x) crc[12 * 256 + q] = (&g_tree.t[0][0][0])[q];
+        __syncthreads();
+        emit_slow_blocks<V>(a, (uint8_t *)smem + kCrcLds, (const uint32_t(*)[256])smem);
+        __syncthreads();
+        const uint32_t nb = a.anchor_blk[a.nchunks];
+        lu8 *wbase = (lu8 *)smem + kCrcLds + wave * kEmitWaveLds;
+        lu8 *img = wbase + kStageGuard;
+        lu8 *kst = img + kImgCap + 16;
+        lSpanCopy *rtab = (lSpanCopy *)(kst + kKeyStageCap);
+        const uint32_t *dw = (const uint32_t *)a.desc;
+        uint32_t blk = gw;
+        if (blk < nb) {
+            // prologue: block gw's descriptor, its prefetch, and block gw + G's descriptor
+            BlockDesc dn = desc_from_lanes(l < 14 ? dw[14 * (uint64_t)blk + l] : 0);
+            EmitPre pn;
+            bool fn = emit_fast(dn);
+            if (fn) emit_prefetch(a, dn, pn);
+            uint32_t dv = (blk + G < nb && l < 14) ? dw[14 * (uint64_t)(blk + G) + l] : 0;
+            for (; blk < nb; blk += G) {
+                const BlockDesc d = dn;
+                const EmitPre p = pn;
+                const bool fast = fn;
+                if (blk + G < nb) {  // issue block blk + G (and blk + 2G's descriptor)
+                    dn = desc_from_lanes(dv);
+                    fn = emit_fast(dn);
+                    if (fn) emit_prefetch(a, dn, pn);
+                    dv = (blk + 2 * G < nb && l < 14) ? dw[14 * (uint64_t)(blk + 2 * G) + l] : 0;
+                }
+                if (fast) emit_block<V>(a, blk, d, p, img, kst, rtab, crc, ph);  // slow blocks: done above
+            }
+        }
+    }
 #ifdef SDB_PHASE_TIMING
     if (lane_id() == 0 && gw < 8192)
         for (int i = 0; i < 8; i++) g_wave_phase[gw][i] = ph[i];
+    const uint64_t rt1 = __builtin_amdgcn_s_memrealtime(), mt1 = __builtin_amdgcn_s_memtime();
+    if (lane_id() == 0 && gw < 8192) {
+        g_wave_rt[gw][0] = rt0;
+        g_wave_rt[gw][1] = rt1;
+        g_wave_rt[gw][2] = mt0;
+        g_wave_rt[gw][3] = mt1;
+    }
 #endif
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(a.done, 1u) == gridDim.x - 1) {
+            __threadfence();
+            finish_summary(a);
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
 // K6: slow path for blocks that do not fit the LDS image: assemble straight into HBM.
 // ------------------------------------------------------------------------------------------------
 template <int V>
-__global__ __launch_bounds__(256) void k_emit_slow(EncodeArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_crc[8][256];
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[4096 + 64];  // window at +16
+SDB_DEV void emit_slow_blocks(const EncodeArgs &a, uint8_t *scratch, const uint32_t (*s_crc)[256]) {
+    // LDS scratch (the wave images, unused until the fast loop): window, row sizes, row offsets
+    uint8_t *s_win = scratch;  // 4096 + 64, window at +16
+    uint64_t *s_size = (uint64_t *)(scratch + 8192);
+    uint64_t *s_off = (uint64_t *)(scratch + 8192 + 8 * kEmitThreads);
     const uint32_t nslow = *a.slow_count;
-    if (a.anchor_blk[a.nchunks] > a.block_cap || a.anchor_byte[a.nchunks] > a.data_cap) return;
-    for (uint32_t q = threadIdx.x; q < 8 * 256; q += blockDim.x) ((uint32_t *)s_crc)[q] = (&c_crc.t[0][0])[q];
-    __syncthreads();
     for (uint32_t it = blockIdx.x; it < nslow; it += gridDim.x) {
         const uint32_t blk = a.slow_list[it];
         const uint64_t b = a.out_block_first[blk];
@@ -1300,8 +1471,6 @@ __global__ __launch_bounds__(256) void k_emit_slow(EncodeArgs a) {
         for (uint32_t i0 = 0; i0 < ne; i0 += blockDim.x) {
             uint32_t i = i0 + threadIdx.x;
             // each thread writes its own row; row offsets need a prefix sum -> do it serially per round
-            __shared__ uint64_t s_size[256];
-            __shared__ uint64_t s_off[256];
             RowInfo r;
             uint64_t seq = 0;
             int64_t ets = 0, cts = 0;
@@ -1431,8 +1600,6 @@ __global__ __launch_bounds__(256) void k_emit_slow(EncodeArgs a) {
 
 template __global__ void k_emit<1>(EncodeArgs);
 template __global__ void k_emit<2>(EncodeArgs);
-template __global__ void k_emit_slow<1>(EncodeArgs);
-template __global__ void k_emit_slow<2>(EncodeArgs);
 
 // ------------------------------------------------------------------------------------------------
 // Launcher
@@ -1481,6 +1648,13 @@ __global__ void k_finish_summary(EncodeArgs a, uint64_t bloom_len, uint32_t num_
 extern "C" int sdb_diag_wave_phase(uint64_t *out, int nwaves) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_phase), sizeof(uint64_t) * 8 * nwaves) == hipSuccess ? 0 : -1;
 }
+extern "C" int sdb_diag_wave_rt(uint64_t *out, int nwaves) {
+#ifdef SDB_PHASE_TIMING
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_rt), sizeof(uint64_t) * 4 * nwaves) == hipSuccess ? 0 : -1;
+#else
+    return -1;
+#endif
+}
 extern "C" int sdb_diag_phase_times(uint64_t *out, int nblocks) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(uint64_t) * 8 * nblocks) == hipSuccess ? 0 : -1;
 }
@@ -1515,8 +1689,8 @@ static void set_lds_attrs() {
 
 hipError_t launch_encode(EncodeArgs a, hipStream_t st) {
     set_lds_attrs();
-    hipLaunchKernelGGL(k_init_summary, dim3(1), dim3(64), 0, st, a);
     if (a.n == 0) {
+        hipLaunchKernelGGL(k_init_summary, dim3(1), dim3(64), 0, st, a);
         hipLaunchKernelGGL(k_finish_summary, dim3(1), dim3(64), 0, st, a, a.bloom_len, a.num_probes, a.filter_built);
         return hipGetLastError();
     }
@@ -1534,11 +1708,6 @@ hipError_t launch_encode(EncodeArgs a, hipStream_t st) {
     if (a.version == 2) hipLaunchKernelGGL(k_emit<2>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, a);
     else hipLaunchKernelGGL(k_emit<1>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, a);
     stage_mark(st, kStEmit, false);
-    stage_mark(st, kStEmitSlow, true);
-    if (a.version == 2) hipLaunchKernelGGL(k_emit_slow<2>, dim3(64), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(k_emit_slow<1>, dim3(64), dim3(256), 0, st, a);
-    stage_mark(st, kStEmitSlow, false);
-    hipLaunchKernelGGL(k_finish_summary, dim3(1), dim3(64), 0, st, a, a.bloom_len, a.num_probes, a.filter_built);
     return hipGetLastError();
 }
 
