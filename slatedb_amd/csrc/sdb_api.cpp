@@ -185,6 +185,15 @@ sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const 
     a.wmax_part = carve<uint32_t>(workspace, wl.wmax_part);
     a.err_part = carve<unsigned long long>(workspace, wl.err_part);
     a.done = carve<uint32_t>(workspace, wl.done);
+    a.gtab_exit = carve<uint32_t>(workspace, wl.gtab_exit);
+    a.gtab_cnt = carve<uint32_t>(workspace, wl.gtab_cnt);
+    a.gtab_bytes = carve<uint64_t>(workspace, wl.gtab_bytes);
+    a.mode = carve<uint32_t>(workspace, wl.mode);
+    {   // chunks per group: about sqrt(nchunks), so k_enum walks <= ~2 sqrt(nchunks) tables
+        uint32_t g = 16;
+        while ((uint64_t)g * g < a.nchunks) g++;
+        a.group = g;
+    }
     a.out_data = out->data;
     a.out_block_off = out->block_off;
     a.out_block_first = out->block_first_entry;

@@ -23,6 +23,9 @@ constexpr uint32_t kEmitWgPerCu = 1;
 constexpr uint32_t kEmitWaveLds = kStageGuard + kImgCap + 16 + kKeyStageCap + 64 * 16;  // guard, image, key stage, spans
 constexpr uint32_t kEmitLds = kCrcLds + (kEmitThreads / 64) * kEmitWaveLds;
 constexpr uint32_t kEnumLds = kChunk * 16 + 12 * kChunk * 2;  // block list + 12 lifting levels
+constexpr uint32_t kEnumTabLds = 12 * kChunk * 2;  // k_enum's table walk (aliases the lifting levels)
+constexpr uint32_t kGroupThreads = 1024;
+constexpr uint32_t kGroupLds = kResolveLds;         // group tables, or the single-workgroup resolve
 
 struct BlockDesc {  // one per block, written by k_enum, streamed by k_emit (56 bytes)
     uint32_t s, e;        // entries [s, e)
@@ -68,6 +71,11 @@ struct EncodeArgs {
     uint64_t *stat_part;    // per chunk: raw key, raw val, puts, deletes, merges
     uint32_t *wmax_part;    // per chunk: longest candidate block (entries)
     unsigned long long *err_part;  // per chunk: min (entry << 8 | code) of k_seg's checks (~0: none)
+    uint32_t *gtab_exit;    // per group of kGroup chunks, seg_look candidates: composed transfer table
+    uint32_t *gtab_cnt;
+    uint64_t *gtab_bytes;
+    uint32_t *mode;         // k_group -> k_enum: 1 = compose the tables, 0 = anchors were walked
+    uint32_t group;         // chunks per group (host: ~sqrt(nchunks))
     uint32_t *done;         // k_emit workgroups finished (the last one writes the summary)
     uint32_t nprep_wg;
     // outputs (device)
@@ -86,7 +94,7 @@ struct EncodeArgs {
 struct EncodeWorkspace {
     uint64_t lcp, row_scratch, next, bbytes, tab_exit, tab_cnt, tab_bytes;
     uint64_t anchor_e, anchor_blk, anchor_byte, err, wmax, slow_count, slow_list, desc, stat_part, wmax_part, bloom_rep;
-    uint64_t err_part, done;
+    uint64_t err_part, done, gtab_exit, gtab_cnt, gtab_bytes, mode;
     uint64_t total;
 };
 uint64_t bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
@@ -118,6 +126,10 @@ inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes
     w.wmax_part = take(4 * (nc + 1));
     w.err_part = take(8 * (nc + 1));
     w.done = take(4);
+    w.gtab_exit = take(4 * (nc * kSegLook + 1));  // one table per group (<= one per chunk)
+    w.gtab_cnt = take(4 * (nc * kSegLook + 1));
+    w.gtab_bytes = take(8 * (nc * kSegLook + 1));
+    w.mode = take(4);
     w.bloom_rep = take(filter_bytes ? bloom_workspace_bytes(n, num_probes, filter_bytes) : 0);  // bloom buckets
     w.total = off;
     return w;
@@ -135,6 +147,7 @@ struct BloomPlan {
     uint32_t k, m;        // probes per key, bitmap bits
     uint32_t sb;          // log2 bits per slice
     uint32_t nslices, T, tiles;
+    uint64_t mmod;        // Lemire fastmod constant: floor((2^64 - 1) / m) + 1
 };
 BloomPlan bloom_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
 uint64_t bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes);

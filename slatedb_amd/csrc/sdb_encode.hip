@@ -444,8 +444,25 @@ __global__ __launch_bounds__(kSegThreads, 8) void k_seg(EncodeArgs a) {
         a.wmax_part[k] = m;
     }
     PHASE_MARK(4);
-    // d. chains from the candidate entry points [cs, cs + seg_look)
-    const uint32_t Wc = a.seg_look;
+    // d. chains from the candidate entry points [cs, cs + Wc).  A block that starts before cs and
+    //    reaches past cs + x holds the non-restart rows [cs, cs + x], so (V2, clamped sizes <= true
+    //    sizes) sum(s_nr[cs .. cs + x]) <= block_size - 2: entry points lie in [cs, cs + x_max + 1].
+    __shared__ uint32_t s_wc;
+    if (tid == 0) {
+        uint32_t wc = a.seg_look;
+        if (v2) {
+            uint32_t lo = 0, hi = sn;  // largest x in [0, sn] with P[x] - P[0] <= bs - 2
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if ((uint64_t)(s_P[mid] - s_P[0]) + 2 <= bs) lo = mid;
+                else hi = mid - 1;
+            }
+            wc = lo + 1 < wc ? lo + 1 : wc;
+        }
+        s_wc = wc;
+    }
+    __syncthreads();
+    const uint32_t Wc = s_wc;
     for (uint32_t c = tid; c < Wc; c += nt) {
         uint32_t e = c, cnt = 0;
         uint64_t by = 0;
@@ -454,7 +471,7 @@ __global__ __launch_bounds__(kSegThreads, 8) void k_seg(EncodeArgs a) {
             cnt++;
             e = s_nx[e];
         }
-        const uint64_t t = (uint64_t)k * Wc + c;
+        const uint64_t t = (uint64_t)k * a.seg_look + c;
         // 0xFFFFFFFF: the exit is beyond the u16 range (resolve then walks next[])
         a.tab_exit[t] = c >= cn ? (uint32_t)ce : (e == 0xFFFF ? 0xFFFFFFFFu : (uint32_t)(cs + e));
         a.tab_cnt[t] = cnt;
@@ -464,192 +481,139 @@ __global__ __launch_bounds__(kSegThreads, 8) void k_seg(EncodeArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// K2 resolve (single workgroup): compose the chunk transfer tables (Blelloch up-sweep of the u16
-// exit tables in LDS, then the one chain from entry 0 pushed down the tree) -> per-chunk anchors
-// (first block start, block index, byte offset) and the SstStats totals.  Every HBM read is issued
-// in one batch per phase: this kernel is latency-bound.
+// K2 group: compose the chunk transfer tables of each group of a.group consecutive chunks (one
+// workgroup per group): for every candidate entry offset o < W into the group's first chunk, the
+// exit offset into the chunk after the group and the blocks / bytes on the way.  k_enum then walks
+// the group tables and its own group's chunk tables from entry 0 (<= ~2 sqrt(nchunks) steps).
+// Workgroup 0 also reduces the per-chunk SstStats / error partials and initialises the device
+// state the later kernels use.  When the tables cannot describe the chain (blocks longer than
+// the staged lookahead) or do not fit k_enum's LDS, workgroup 0 walks next() serially instead and
+// writes every chunk's anchors (mode 0).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_resolve(EncodeArgs a) {
+__global__ __launch_bounds__(kGroupThreads) void k_group(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ uint64_t s_w[17];
-    __shared__ uint32_t s_wmax;
-    __shared__ uint64_t s_stat[5][16];
+    __shared__ uint32_t s_W;
     __shared__ unsigned long long s_err;
-    const uint32_t K = a.nchunks;
+    __shared__ uint64_t s_stat[5][kGroupThreads / 64];
+    const uint32_t K = a.nchunks, g = blockIdx.x, G = a.group, ngroups = gridDim.x;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
-    uint32_t KP = 1;
-    while (KP < K) KP <<= 1;
     if (tid == 0) {
-        s_wmax = 0;
+        s_W = 0;
         s_err = ~0ull;
     }
     __syncthreads();
-    PHASE_MARK_AT(1023, 0);
-    // W = longest candidate block; SstStats partial sums (one batch of loads)
     {
         uint32_t m = 0;
-        uint64_t st[5] = {0, 0, 0, 0, 0};
         unsigned long long em = ~0ull;
+        uint64_t st[5] = {0, 0, 0, 0, 0};
         for (uint32_t q = tid; q < K; q += nt) {
-            uint32_t w = a.wmax_part[q];
+            const uint32_t w = a.wmax_part[q];
             m = w > m ? w : m;
-            const unsigned long long ep = a.err_part[q];
-            em = ep < em ? ep : em;
+            if (g == 0) {
+                const unsigned long long ep = a.err_part[q];
+                em = ep < em ? ep : em;
 #pragma unroll
-            for (int f = 0; f < 5; f++) st[f] += a.stat_part[5 * (uint64_t)q + f];
+                for (int f = 0; f < 5; f++) st[f] += a.stat_part[5 * (uint64_t)q + f];
+            }
         }
         m = wave_max(m);
-        if (lane_id() == 0) atomicMax(&s_wmax, m);
-        if (em != ~0ull) atomicMin(&s_err, em);
+        if (lane_id() == 0) atomicMax(&s_W, m);
+        if (g == 0) {
+            if (em != ~0ull) atomicMin(&s_err, em);
 #pragma unroll
-        for (int f = 0; f < 5; f++) {
-            uint64_t t = wave_sum(st[f]);
-            if (lane_id() == 0) s_stat[f][tid >> 6] = t;
+            for (int f = 0; f < 5; f++) {
+                const uint64_t t = wave_sum(st[f]);
+                if (lane_id() == 0) s_stat[f][tid >> 6] = t;
+            }
         }
     }
     __syncthreads();
-    const uint32_t W = s_wmax;
-    if (tid < 5) {
-        uint64_t t = 0;
-        for (uint32_t q = 0; q < nt / 64; q++) t += s_stat[tid][q];
-        if (tid == 0) a.summary->raw_key_size = t;
-        if (tid == 1) a.summary->raw_val_size = t;
-        if (tid == 2) a.summary->num_puts = t;
-        if (tid == 3) a.summary->num_deletes = t;
-        if (tid == 4) a.summary->num_merges = t;
-    }
-    if (tid == 0) {
-        // the encode's device-side state for the later kernels (this kernel runs alone)
+    const uint32_t W = s_W;
+    const bool fast = W >= 1 && W <= a.seg_look && (uint64_t)W * (ngroups + G) * 16 + 64 <= kEnumTabLds;
+    if (g == 0 && tid == 0) {
+        // device state for k_enum / k_emit (this kernel runs alone on the stream)
         *a.wmax = W;
         *a.err = s_err;
         *a.slow_count = 0;
         *a.done = 0;
+        *a.mode = fast ? 1u : 0u;
         sdb_sst_summary *sm = a.summary;
+        uint64_t t[5];
+        for (int f = 0; f < 5; f++) {
+            t[f] = 0;
+            for (uint32_t q = 0; q < nt / 64; q++) t[f] += s_stat[f][q];
+        }
+        sm->raw_key_size = t[0];
+        sm->raw_val_size = t[1];
+        sm->num_puts = t[2];
+        sm->num_deletes = t[3];
+        sm->num_merges = t[4];
+        sm->num_entries = a.n;
         sm->bloom_len = 0;
         sm->num_probes = 0;
         sm->filter_built = 0;
         sm->status = 0;
         sm->max_block_entries = 0;
         sm->first_error_entry = ~0ull;
-    }
-    const uint64_t ex_bytes = ((uint64_t)KP * W * 2 + 15) & ~15ull;
-    const uint64_t v_bytes = ((uint64_t)KP * 4 + 15) & ~15ull;
-    const bool fast = W <= a.seg_look && ex_bytes + v_bytes + (uint64_t)KP * W + 16 <= kResolveLds;
-    uint32_t *v = (uint32_t *)(smem + ex_bytes);  // KP entry offsets (fast path)
-    PHASE_MARK_AT(1023, 1);
-    if (fast) {
-        uint16_t *ex = (uint16_t *)smem;  // KP x W exit offsets
-        // ex[k][o] = entry offset into chunk k+1 reached from entry offset o into chunk k
-        const uint32_t total = KP * W;
-        for (uint32_t base = 0; base < total; base += 8 * nt) {
-            uint32_t val[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                uint32_t idx = base + tid + u * nt;
-                uint32_t k = idx / W, o = idx - k * W;
-                val[u] = o;  // identity for the padding chunks k >= K
-                if (idx < total && k < K) {
-                    uint64_t cs = (uint64_t)k * kChunk;
-                    uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
-                    val[u] = cs + o < ce ? (uint32_t)(a.tab_exit[(uint64_t)k * a.seg_look + o] - ce) : 0;
+        if (!fast) {
+            // serial walk of the block chain (one next() step per block), anchors for every chunk
+            uint64_t e = 0, blk = 0, by = 0;
+            for (uint32_t k = 0; k < K; k++) {
+                const uint64_t cs = (uint64_t)k * kChunk, ce = cs + kChunk < a.n ? cs + kChunk : a.n;
+                a.anchor_e[k] = (uint32_t)e;
+                a.anchor_blk[k] = (uint32_t)blk;
+                a.anchor_byte[k] = by;
+                while (e < ce) {
+                    by += a.bbytes[e];
+                    blk++;
+                    e = a.next[e];
                 }
             }
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                uint32_t idx = base + tid + u * nt;
-                if (idx < total) ex[idx] = (uint16_t)val[u];
-            }
-        }
-        __syncthreads();
-        PHASE_MARK_AT(1023, 2);
-        // Blelloch up-sweep: ex[k] <- ex[k] o ex[k-d] for k = 2d-1 (mod 2d).  A level reads entries
-        // of ex[k] that other threads of the same level overwrite, so results go through `tmp`.
-        uint16_t *tmp = (uint16_t *)(smem + ex_bytes + v_bytes);
-        for (uint32_t d = 1; d < KP; d <<= 1) {
-            const uint32_t cnt = (KP / (2 * d)) * W;
-            for (uint32_t idx = tid; idx < cnt; idx += nt) {
-                uint32_t q = idx / W, o = idx - q * W;
-                uint32_t k = 2 * d * q + 2 * d - 1;
-                uint16_t mid = ex[(k - d) * W + o];
-                tmp[idx] = ex[k * W + mid];
-            }
-            __syncthreads();
-            for (uint32_t idx = tid; idx < cnt; idx += nt) {
-                uint32_t q = idx / W, o = idx - q * W;
-                ex[(2 * d * q + 2 * d - 1) * W + o] = tmp[idx];
-            }
-            __syncthreads();
-        }
-        PHASE_MARK_AT(1023, 3);
-        // down-sweep of the single chain that starts at entry 0
-        if (tid == 0) v[0] = 0;
-        __syncthreads();
-        for (uint32_t d = KP >> 1; d >= 1; d >>= 1) {
-            for (uint32_t q = tid; q < KP / (2 * d); q += nt) {
-                uint32_t k = 2 * d * q;
-                v[k + d] = ex[(k + d - 1) * W + v[k]];
-            }
-            __syncthreads();
-        }
-    } else if (tid == 0) {
-        // general fallback (blocks longer than the staged lookahead, or too many chunk tables):
-        // serial walk of the chain; per-chunk counts / bytes stashed in the tab_* slot of offset 0
-        v = (uint32_t *)smem;
-        uint64_t e = 0;
-        for (uint32_t k = 0; k < K; k++) {
-            uint64_t cs = (uint64_t)k * kChunk;
-            uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
-            v[k] = (uint32_t)(e - cs);
-            uint32_t cnt = 0;
-            uint64_t by = 0;
-            while (e < ce) {
-                by += a.bbytes[e];
-                cnt++;
-                e = a.next[e];
-            }
-            a.tab_cnt[(uint64_t)k * a.seg_look] = cnt;
-            a.tab_bytes[(uint64_t)k * a.seg_look] = by;
+            a.anchor_e[K] = (uint32_t)a.n;
+            a.anchor_blk[K] = (uint32_t)blk;
+            a.anchor_byte[K] = by;
+            sm->num_blocks = blk;
+            sm->data_len = by;
+            if (blk > a.block_cap || by > a.data_cap) report_error(a.err, 0, SDB_INVALID_ARGUMENT);
         }
     }
-    if (!fast) v = (uint32_t *)smem;
+    if (!fast) return;
+    // this group's chunk tables -> LDS (exit offsets clamped into [0, W): candidates past a chunk's
+    // own bound are never entry points, their stale slots only need to stay in range)
+    const uint32_t k0 = g * G, k1 = k0 + G < K ? k0 + G : K, nk = k1 - k0;
+    uint16_t *ex = (uint16_t *)smem;                                 // nk x W
+    uint32_t *cn_ = (uint32_t *)(smem + ((2 * nk * W + 15) & ~15u)); // nk x W
+    uint64_t *by_ = (uint64_t *)((uint8_t *)cn_ + ((4 * nk * W + 15) & ~15u));
+    for (uint32_t idx = tid; idx < nk * W; idx += nt) {
+        const uint32_t j = idx / W, o = idx - j * W, k = k0 + j;
+        const uint64_t cs = (uint64_t)k * kChunk, ce = cs + kChunk < a.n ? cs + kChunk : a.n;
+        uint32_t x = 0, c = 0;
+        uint64_t b = 0;
+        if (cs + o < ce) {
+            const uint64_t t = (uint64_t)k * a.seg_look + o;
+            const uint32_t te = a.tab_exit[t];
+            x = te >= ce && te - ce < W ? (uint32_t)(te - ce) : W - 1;
+            c = a.tab_cnt[t];
+            b = a.tab_bytes[t];
+        }
+        ex[idx] = (uint16_t)x;
+        cn_[idx] = c;
+        by_[idx] = b;
+    }
     __syncthreads();
-    PHASE_MARK_AT(1023, 4);
-    // per-chunk block counts / bytes from the entry point; exclusive scans give the anchors
-    uint64_t cb = 0, cy = 0;
-    for (uint32_t k0 = 0; k0 < K; k0 += nt) {
-        uint32_t k = k0 + tid;
-        uint64_t c = 0, by = 0, e = 0;
-        if (k < K) {
-            uint64_t cs = (uint64_t)k * kChunk;
-            uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
-            e = cs + v[k];
-            if (e < ce) {
-                const uint64_t t = (uint64_t)k * a.seg_look + (fast ? v[k] : 0);
-                c = a.tab_cnt[t];
-                by = a.tab_bytes[t];
-            }
+    for (uint32_t o = tid; o < W; o += nt) {
+        uint32_t e = o, c = 0;
+        uint64_t b = 0;
+        for (uint32_t j = 0; j < nk; j++) {
+            c += cn_[j * W + e];
+            b += by_[j * W + e];
+            e = ex[j * W + e];
         }
-        uint64_t tc, ty;
-        uint64_t xc = block_excl_scan_u64(c, s_w, &tc);
-        uint64_t xy = block_excl_scan_u64(by, s_w, &ty);
-        if (k < K) {
-            a.anchor_e[k] = (uint32_t)e;
-            a.anchor_blk[k] = (uint32_t)(cb + xc);
-            a.anchor_byte[k] = cy + xy;
-        }
-        cb += tc;
-        cy += ty;
+        const uint64_t t = (uint64_t)g * a.seg_look + o;
+        a.gtab_exit[t] = e;
+        a.gtab_cnt[t] = c;
+        a.gtab_bytes[t] = b;
     }
-    if (tid == 0) {
-        a.anchor_blk[K] = (uint32_t)cb;
-        a.anchor_byte[K] = cy;
-        a.anchor_e[K] = (uint32_t)a.n;
-        a.summary->num_blocks = cb;
-        a.summary->data_len = cy;
-        a.summary->num_entries = a.n;
-        if (cb > a.block_cap || cy > a.data_cap) report_error(a.err, 0, SDB_INVALID_ARGUMENT);
-    }
-    PHASE_MARK_AT(1023, 5);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -788,25 +752,98 @@ SDB_DEV bool emit_fast(const BlockDesc &d) {
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_enum(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t k = blockIdx.x;
+    __shared__ uint64_t s_anc[4];  // entry point, first block, first byte, blocks of this chunk
+    const uint32_t k = blockIdx.x, K = a.nchunks;
     if (*a.err != ~0ull) return;
     const uint64_t cs = (uint64_t)k * kChunk;
     const uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
     const uint32_t cn = (uint32_t)(ce - cs);
-    const uint64_t e0 = a.anchor_e[k];
-    const uint32_t blk0 = a.anchor_blk[k];
-    const uint32_t nb = a.anchor_blk[k + 1] - blk0;
-    const uint64_t byte0 = a.anchor_byte[k];
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
-    if (k + 1 == a.nchunks && tid == 0) {
-        a.out_block_off[a.anchor_blk[k + 1]] = a.anchor_byte[k + 1];
-        a.out_block_first[a.anchor_blk[k + 1]] = (uint32_t)a.n;
-    }
-    if (!nb) return;
     uint32_t *bl_s = (uint32_t *)smem;
     uint32_t *bl_b = bl_s + kChunk;
     uint64_t *bl_o = (uint64_t *)(bl_b + kChunk);
     uint16_t *lv = (uint16_t *)(bl_o + kChunk);
+    if (*a.mode) {
+        // walk the group tables of the groups before this chunk's, then this group's chunk tables
+        // (k's own last: its block count), from entry 0.  Tables -> LDS first (one batch of loads).
+        const uint32_t W = *a.wmax, G = a.group, g = k / G, k0 = g * G, nc = k - k0 + 1;
+        const uint32_t ntab = g + nc;
+        const uint32_t tb4 = (4 * ntab * W + 15) & ~15u;
+        uint32_t *t_ex = (uint32_t *)lv;                 // ntab x W each
+        uint32_t *t_cn = (uint32_t *)((uint8_t *)lv + tb4);
+        uint64_t *t_by = (uint64_t *)((uint8_t *)lv + 2 * tb4);
+        for (uint32_t idx = tid; idx < ntab * W; idx += nt) {
+            const uint32_t q = idx / W, o = idx - q * W;
+            uint32_t x, c;
+            uint64_t b;
+            if (q < g) {
+                const uint64_t t = (uint64_t)q * a.seg_look + o;
+                x = a.gtab_exit[t];
+                c = a.gtab_cnt[t];
+                b = a.gtab_bytes[t];
+            } else {
+                const uint32_t kk = k0 + (q - g);
+                const uint64_t ccs = (uint64_t)kk * kChunk, cce = ccs + kChunk < a.n ? ccs + kChunk : a.n;
+                x = 0;
+                c = 0;
+                b = 0;
+                if (ccs + o < cce) {
+                    const uint64_t t = (uint64_t)kk * a.seg_look + o;
+                    const uint32_t te = a.tab_exit[t];
+                    x = te >= cce ? te - (uint32_t)cce : 0;
+                    c = a.tab_cnt[t];
+                    b = a.tab_bytes[t];
+                }
+            }
+            t_ex[idx] = x < W ? x : W - 1;
+            t_cn[idx] = c;
+            t_by[idx] = b;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t e = 0;
+            uint64_t blk = 0, by = 0;
+            for (uint32_t q = 0; q + 1 < ntab; q++) {
+                blk += t_cn[q * W + e];
+                by += t_by[q * W + e];
+                e = t_ex[q * W + e];
+            }
+            const uint32_t q = ntab - 1;  // chunk k itself
+            s_anc[0] = cs + e;
+            s_anc[1] = blk;
+            s_anc[2] = by;
+            s_anc[3] = cs + e < ce ? t_cn[q * W + e] : 0;
+            if (k + 1 == K) {  // totals (the chain's last blocks are this chunk's)
+                const uint64_t tb = blk + s_anc[3], ty = by + (cs + e < ce ? t_by[q * W + e] : 0);
+                a.anchor_blk[K] = (uint32_t)tb;
+                a.anchor_byte[K] = ty;
+                a.anchor_e[K] = (uint32_t)a.n;
+                a.summary->num_blocks = tb;
+                a.summary->data_len = ty;
+                if (tb > a.block_cap || ty > a.data_cap) report_error(a.err, 0, SDB_INVALID_ARGUMENT);
+            }
+        }
+        __syncthreads();
+    } else if (tid == 0) {
+        s_anc[0] = a.anchor_e[k];
+        s_anc[1] = a.anchor_blk[k];
+        s_anc[2] = a.anchor_byte[k];
+        s_anc[3] = a.anchor_blk[k + 1] - a.anchor_blk[k];
+    }
+    __syncthreads();
+    const uint64_t e0 = s_anc[0];
+    const uint32_t blk0 = (uint32_t)s_anc[1];
+    const uint32_t nb = (uint32_t)s_anc[3];
+    const uint64_t byte0 = s_anc[2];
+    if (blk0 + (uint64_t)nb > a.block_cap) {  // capacity: the last chunk reports it
+        if (tid == 0) report_error(a.err, 0, SDB_INVALID_ARGUMENT);
+        return;
+    }
+    if (k + 1 == K && tid == 0) {
+        a.out_block_off[blk0 + nb] = a.anchor_byte[K];
+        a.out_block_first[blk0 + nb] = (uint32_t)a.n;
+    }
+    if (!nb) return;
     uint32_t levels = 1;
     while ((1u << levels) < nb) levels++;
     for (uint32_t x = tid; x < cn; x += nt) {
@@ -1682,7 +1719,7 @@ static void set_lds_attrs() {
     hipFuncSetAttribute((const void *)k_emit<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
     hipFuncSetAttribute((const void *)k_emit<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
     hipFuncSetAttribute((const void *)k_enum, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEnumLds);
-    hipFuncSetAttribute((const void *)k_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLds);
+    hipFuncSetAttribute((const void *)k_group, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGroupLds);
     hipFuncSetAttribute((const void *)k_seg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLds);
     lds_attrs_set = true;
 }
@@ -1699,7 +1736,7 @@ hipError_t launch_encode(EncodeArgs a, hipStream_t st) {
     hipLaunchKernelGGL(k_seg, dim3(a.nchunks), dim3(kSegThreads), kSegLds, st, a);
     stage_mark(st, kStSeg, false);
     stage_mark(st, kStResolve, true);
-    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(1024), kResolveLds, st, a);
+    hipLaunchKernelGGL(k_group, dim3((a.nchunks + a.group - 1) / a.group), dim3(kGroupThreads), kGroupLds, st, a);
     stage_mark(st, kStResolve, false);
     stage_mark(st, kStEnum, true);
     hipLaunchKernelGGL(k_enum, dim3(a.nchunks), dim3(256), kEnumLds, st, a);
