@@ -58,3 +58,10 @@ clk = (r[:, 3] - r[:, 2]) / np.maximum(r[:, 1] - r[:, 0], 1) * 100.0
 print("k_emit waves (us from first start): start p50 %.1f p90 %.1f max %.1f; end p10 %.1f p50 %.1f max %.1f; "
       "wave duration p50 %.1f; shader clock %.0f MHz (median)" % (np.percentile(st, 50), np.percentile(st, 90), st.max(),
       np.percentile(en, 10), np.percentile(en, 50), en.max(), np.median(en - st), np.median(clk)))
+
+eb = (C.c_uint64 * (8 * 1024))()
+cdll.sdb_diag_enum_phase.argtypes = [C.c_void_p, C.c_int]
+assert cdll.sdb_diag_enum_phase(C.addressof(eb), 1024) == 0
+t = np.frombuffer(eb, dtype=np.uint64).reshape(1024, 8)[:nb].astype(np.int64)
+d = np.diff(t[:, :6], axis=1)
+print("k_enum phases (ticks) mean/max: " + "  ".join("%d->%d %.0f/%.0f" % (i, i + 1, d[:, i].mean(), d[:, i].max()) for i in range(5)))

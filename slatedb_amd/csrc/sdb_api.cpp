@@ -14,7 +14,7 @@
 
 #include "../../include/slatedb_amd.h"
 #include "sdb_decode.h"
-#include "sdb_encode.h"
+#include "sdb_bloom.h"
 
 using namespace sdb;
 
@@ -41,27 +41,6 @@ sdb_status check_params(const sdb_sst_params *p) {
     if (p->block_size == 0) return SDB_INVALID_ARGUMENT;
     if (p->sst_version == 2 && p->restart_interval == 0) return SDB_INVALID_ARGUMENT;
     return SDB_OK;
-}
-
-// Per-device side stream: the bloom build (L2-atomic bound) runs beside the HBM-bound encode
-// kernels.  fork/join through events keeps the caller's stream semantics (and graph capture).
-struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-std::mutex g_side_mu;
-SideStream g_side[64];
-
-SideStream *side_for_current_device() {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    SideStream &ss = g_side[dev];
-    if (!ss.s) {
-        if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-        hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming);
-        hipEventCreateWithFlags(&ss.join, hipEventDisableTiming);
-    }
-    return &ss;
 }
 
 template <typename T>
@@ -206,24 +185,28 @@ sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const 
     a.num_probes = want_filter ? num_probes_for(p->bloom_bits_per_key) : 0;
     a.filter_built = want_filter ? 1 : 0;
     hipStream_t s = S(stream);
-    std::unique_lock<std::mutex> lk(g_side_mu);
-    SideStream *side = want_filter && n ? side_for_current_device() : nullptr;
-    if (want_filter) {
-        hipStream_t bs = s;
-        if (side) {  // fork
-            hipEventRecord(side->fork, s);
-            hipStreamWaitEvent(side->s, side->fork, 0);
-            bs = side->s;
+    if (want_filter && n) {
+        // the bloom runs inside the encode kernels (k_seg hashes, k_group bins, k_enum fills) when the
+        // binned build fits; otherwise it is built on the stream before the encode
+        const BloomPlan pl = bloom_plan(n, a.num_probes, fb);
+        if (bloom_plan_fits(pl, n) && bloom_fill_lds(pl) <= 64 * 1024) {
+            a.bloom_fused = 1;
+            a.hd = carve<uint64_t>(workspace, wl.hd);
+            a.bpl = pl;
+            a.bq = bloom_queues(carve<void>(workspace, wl.bloom_rep), n, pl);
+            a.bloom_out = out->bloom;
+        } else {
+            stage_mark(s, kStBloom, true);
+            if (launch_bloom_build(b->key_bytes, b->key_off, n, a.num_probes, out->bloom, fb,
+                                   carve<void>(workspace, wl.bloom_rep), s) != hipSuccess)
+                return SDB_DEVICE_ERROR;
+            stage_mark(s, kStBloom, false);
         }
-        stage_mark(bs, kStBloom, true);
-        if (launch_bloom_build(b->key_bytes, b->key_off, n, a.num_probes, out->bloom, fb,
-                               carve<void>(workspace, wl.bloom_rep), bs) != hipSuccess)
+    } else if (want_filter) {
+        if (launch_bloom_build(b->key_bytes, b->key_off, n, a.num_probes, out->bloom, fb, nullptr, s) != hipSuccess)
             return SDB_DEVICE_ERROR;
-        stage_mark(bs, kStBloom, false);
-        if (side) hipEventRecord(side->join, side->s);
     }
     if (launch_encode(a, s) != hipSuccess) return SDB_DEVICE_ERROR;
-    if (side) hipStreamWaitEvent(s, side->join, 0);  // join: the caller's stream completes after the bloom
     return SDB_OK;
 }
 
@@ -740,3 +723,9 @@ sdb_status sdb_decoder_decode_host(sdb_decoder *d, const uint8_t *blocks, const 
 }
 
 }  // extern "C"
+
+// Diagnostics: byte offset of the bloom queue region (cursors first) inside sdb_encode_sst's workspace.
+extern "C" uint64_t sdb_diag_bloom_ws_offset(uint64_t n, const sdb_sst_params *p) {
+    uint64_t fb = p && p->bloom_bits_per_key ? filter_bytes_for(n, p->bloom_bits_per_key) : 0;
+    return sdb::encode_workspace_layout(n, fb, p ? num_probes_for(p->bloom_bits_per_key) : 0).bloom_rep;
+}

@@ -25,7 +25,21 @@ constexpr uint32_t kEmitLds = kCrcLds + (kEmitThreads / 64) * kEmitWaveLds;
 constexpr uint32_t kEnumLds = kChunk * 16 + 12 * kChunk * 2;  // block list + 12 lifting levels
 constexpr uint32_t kEnumTabLds = 12 * kChunk * 2;  // k_enum's table walk (aliases the lifting levels)
 constexpr uint32_t kGroupThreads = 1024;
+constexpr uint32_t kEnumThreads = 1024;
 constexpr uint32_t kGroupLds = kResolveLds;         // group tables, or the single-workgroup resolve
+
+// bloom build plan (sdb_bloom.hip): 2^sb-bit slices, T-key binning tiles
+struct BloomPlan {
+    uint32_t k, m;        // probes per key, bitmap bits
+    uint32_t sb;          // log2 bits per slice
+    uint32_t nslices, T, tiles;
+    uint64_t mmod;        // Lemire fastmod constant: floor((2^64 - 1) / m) + 1
+};
+struct BloomQueues {
+    uint32_t *cursor;  // nslices * kShards (+1: the overflow flag)
+    uint32_t *queue;   // (nslices * kShards) x cap probes
+    uint32_t cap;
+};
 
 struct BlockDesc {  // one per block, written by k_enum, streamed by k_emit (56 bytes)
     uint32_t s, e;        // entries [s, e)
@@ -76,6 +90,12 @@ struct EncodeArgs {
     uint64_t *gtab_bytes;
     uint32_t *mode;         // k_group -> k_enum: 1 = compose the tables, 0 = anchors were walked
     uint32_t group;         // chunks per group (host: ~sqrt(nchunks))
+    // bloom fused into the encode: k_seg hashes (-> hd), k_group bins, k_enum fills
+    uint32_t bloom_fused;
+    uint64_t *hd;           // per entry: h0 | d0 << 32 (first probe, first step)
+    BloomPlan bpl;
+    BloomQueues bq;
+    uint8_t *bloom_out;
     uint32_t *done;         // k_emit workgroups finished (the last one writes the summary)
     uint32_t nprep_wg;
     // outputs (device)
@@ -94,7 +114,7 @@ struct EncodeArgs {
 struct EncodeWorkspace {
     uint64_t lcp, row_scratch, next, bbytes, tab_exit, tab_cnt, tab_bytes;
     uint64_t anchor_e, anchor_blk, anchor_byte, err, wmax, slow_count, slow_list, desc, stat_part, wmax_part, bloom_rep;
-    uint64_t err_part, done, gtab_exit, gtab_cnt, gtab_bytes, mode;
+    uint64_t err_part, done, gtab_exit, gtab_cnt, gtab_bytes, mode, hd;
     uint64_t total;
 };
 uint64_t bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
@@ -130,6 +150,7 @@ inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes
     w.gtab_cnt = take(4 * (nc * kSegLook + 1));
     w.gtab_bytes = take(8 * (nc * kSegLook + 1));
     w.mode = take(4);
+    w.hd = take(filter_bytes ? 8 * (n + 1) : 0);
     w.bloom_rep = take(filter_bytes ? bloom_workspace_bytes(n, num_probes, filter_bytes) : 0);  // bloom buckets
     w.total = off;
     return w;
@@ -143,12 +164,7 @@ void stage_mark(hipStream_t st, int stage, bool begin);
 bool stage_timing_on();
 
 // bloom (sdb_bloom.hip)
-struct BloomPlan {
-    uint32_t k, m;        // probes per key, bitmap bits
-    uint32_t sb;          // log2 bits per slice
-    uint32_t nslices, T, tiles;
-    uint64_t mmod;        // Lemire fastmod constant: floor((2^64 - 1) / m) + 1
-};
+
 BloomPlan bloom_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
 uint64_t bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
 // ws: bloom_workspace_bytes(...) of scratch, or NULL (device-scope atomics; slow)

@@ -26,8 +26,7 @@
 //               assembled directly in HBM by one workgroup each.
 #include <stdlib.h>
 
-#include "sdb_device.h"
-#include "sdb_encode.h"
+#include "sdb_bloom.h"
 
 namespace sdb {
 
@@ -42,6 +41,12 @@ __device__ uint64_t g_phase[1024][8];
         if (threadIdx.x == 0 && blockIdx.x < 1024) g_phase[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 __device__ uint64_t g_wave_phase[8192][8];
+__device__ uint64_t g_phase_enum[1024][8];
+#define PHASE_MARK_E(i)                                                                  \
+    do {                                                                                 \
+        __syncthreads();                                                                 \
+        if (threadIdx.x == 0 && blockIdx.x < 1024) g_phase_enum[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 __device__ uint64_t g_wave_rt[8192][4];  // k_emit per wave: s_memrealtime start/end, s_memtime start/end
 #define WAVE_T(var)                                     \
     uint64_t var = __builtin_amdgcn_s_memtime();        \
@@ -57,6 +62,9 @@ __device__ uint64_t g_wave_rt[8192][4];  // k_emit per wave: s_memrealtime start
     } while (0)
 #define PHASE_MARK_AT(slot, i) \
     do {                       \
+    } while (0)
+#define PHASE_MARK_E(i) \
+    do {                \
     } while (0)
 #define WAVE_T(var) \
     do {            \
@@ -189,16 +197,17 @@ __global__ __launch_bounds__(kSegThreads, 8) void k_seg(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t *s_r = (uint32_t *)smem;          // kSegSpan: true restart-row sizes (V1: row sizes)
     uint32_t *s_P = s_r + kSegSpan;            // kSegSpan + 4: prefix of clamped non-restart sizes
-    uint32_t *s_R = s_P + kSegSpan + 4;        // kSegSpan: residue-class prefix of restart surcharges
+    uint32_t *s_R = s_P + kSegSpan + 4;        // kSegSpan: restart surcharge of each entry
     uint32_t *s_bb = s_R + kSegSpan;           // kChunk: encoded block bytes for blocks starting here
     uint16_t *s_nx = (uint16_t *)(s_bb + kChunk);  // kChunk: next(b) - cs (0xFFFF: out of range)
     __shared__ uint64_t s_part[kSegThreads / 64][5];
     __shared__ uint32_t s_len[kSegThreads / 64];
-    __shared__ uint64_t s_w[17];
     __shared__ unsigned long long s_err;
     const uint32_t k = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
     if (tid == 0) s_err = ~0ull;
     __syncthreads();
+    if (a.bloom_fused && k == 0)  // the bloom queue cursors for k_group's binning
+        for (uint32_t i = tid; i <= a.bpl.nslices * kShards; i += nt) a.bq.cursor[i] = 0;
     const uint64_t cs = (uint64_t)k * kChunk;
     const uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
     const uint64_t se = ce + a.seg_look < a.n ? ce + a.seg_look : a.n;
@@ -213,65 +222,60 @@ __global__ __launch_bounds__(kSegThreads, 8) void k_seg(EncodeArgs a) {
     // a. facts
     uint64_t rk = 0, rv = 0;
     uint32_t puts = 0, dels = 0, merges = 0;
-    // lanes hold consecutive entries, so the next / previous entry's offsets and key prefix come
-    // from the neighbour lane (DPP); lanes 0 / 63 load theirs
+    // lanes hold consecutive entries.  Two rounds of loads: (1) the entry's and the next entry's
+    // offsets (lane 0 also the previous key's offset), kind, ts mask; (2) the first 16 bytes of the
+    // key (lane 0 also of the previous key).  The previous key's prefix of lanes 1..63 comes from the
+    // neighbour lane (DPP).
     constexpr uint32_t kPerT = kSegSpan / kSegThreads;
-    struct Own {
-        uint64_t ko, vo, k0, k1;
-        uint8_t kd, m;
-    } own[kPerT];
+    FactsIn fin[kPerT];
     const uint32_t lane = (uint32_t)lane_id();
 #pragma unroll
     for (uint32_t u = 0; u < kPerT; u++) {
         const uint32_t x = tid + u * nt;
+        FactsIn &in = fin[u];
+        in.ko0 = in.ko1 = in.vo0 = in.vo1 = in.pko = 0;
+        in.kd = in.m = 0;
         if (x < sn) {
             const uint64_t e = cs + x;
-            own[u].ko = a.key_off[e];
-            own[u].vo = a.val_off[e];
-            own[u].kd = a.kind ? a.kind[e] : 0;
-            own[u].m = a.ts_mask ? a.ts_mask[e] : 0;
+            in.ko0 = a.key_off[e];
+            in.ko1 = a.key_off[e + 1];
+            in.vo0 = a.val_off[e];
+            in.vo1 = a.val_off[e + 1];
+            in.kd = a.kind ? a.kind[e] : 0;
+            in.m = a.ts_mask ? a.ts_mask[e] : 0;
+            if (lane == 0 && e > 0) in.pko = a.key_off[e - 1];
         }
     }
 #pragma unroll
     for (uint32_t u = 0; u < kPerT; u++) {
         const uint32_t x = tid + u * nt;
-        own[u].k0 = own[u].k1 = 0;
+        FactsIn &in = fin[u];
+        in.ck0 = in.ck1 = in.pk0 = in.pk1 = 0;
         if (x < sn) {
-            const uint64_t e = cs + x;
-            const uint64_t kl = a.key_off[e + 1] - own[u].ko;  // L1 hit: the neighbour's load
+            const uint64_t kl = in.ko1 - in.ko0;
             const uint32_t n = (uint32_t)(kl < 16 ? kl : 16);
-            if (n) own[u].k0 = load8(a.key_bytes + own[u].ko, n < 8 ? n : 8);
-            if (n > 8) own[u].k1 = load8(a.key_bytes + own[u].ko + 8, n - 8);
+            if (n) in.ck0 = load8(a.key_bytes + in.ko0, n < 8 ? n : 8);
+            if (n > 8) in.ck1 = load8(a.key_bytes + in.ko0 + 8, n - 8);
+            if (lane == 0 && cs + x > 0) {
+                const uint64_t pl = in.ko0 - in.pko;
+                const uint32_t pn = (uint32_t)(pl < 16 ? pl : 16);
+                if (pn) in.pk0 = load8(a.key_bytes + in.pko, pn < 8 ? pn : 8);
+                if (pn > 8) in.pk1 = load8(a.key_bytes + in.pko + 8, pn - 8);
+            }
         }
     }
 #pragma unroll
     for (uint32_t u = 0; u < kPerT; u++) {
         const uint32_t x = tid + u * nt;
         const uint64_t e = cs + x;
-        FactsIn in;
-        in.ko0 = own[u].ko;
-        in.vo0 = own[u].vo;
-        in.kd = own[u].kd;
-        in.m = own[u].m;
-        in.ck0 = own[u].k0;
-        in.ck1 = own[u].k1;
-        in.ko1 = wave_next_lane(own[u].ko);
-        in.vo1 = wave_next_lane(own[u].vo);
-        in.pko = wave_prev_lane(own[u].ko);
-        in.pk0 = wave_prev_lane(own[u].k0);
-        in.pk1 = wave_prev_lane(own[u].k1);
-        if (x < sn) {
-            if (lane == 63 || x + 1 == sn) {
-                in.ko1 = a.key_off[e + 1];
-                in.vo1 = a.val_off[e + 1];
-            }
-            if (lane == 0) {
-                in.pko = e > 0 ? a.key_off[e - 1] : in.ko0;
-                const uint64_t pl = in.ko0 - in.pko;
-                const uint32_t n = (uint32_t)(pl < 16 ? pl : 16);
-                in.pk0 = n ? load8(a.key_bytes + in.pko, n < 8 ? n : 8) : 0;
-                in.pk1 = n > 8 ? load8(a.key_bytes + in.pko + 8, n - 8) : 0;
-            }
+        FactsIn &in = fin[u];
+        const uint64_t pko = wave_prev_lane(in.ko0), pk0 = wave_prev_lane(in.ck0), pk1 = wave_prev_lane(in.ck1);
+        if (lane != 0) {
+            in.pko = pko;
+            in.pk0 = pk0;
+            in.pk1 = pk1;
+        } else if (e == 0) {
+            in.pko = in.ko0;
         }
         if (x >= sn) continue;
         EntryFacts f = facts_finish(a, e, in);
@@ -280,6 +284,12 @@ __global__ __launch_bounds__(kSegThreads, 8) void k_seg(EncodeArgs a) {
             const uint32_t cr = f.s_r < clampv ? f.s_r : clampv, cnr = f.s_nr < clampv ? f.s_nr : clampv;
             s_P[x] = cnr;
             s_R[x] = cr + 2 - cnr;  // restart row: restart size + its 2-byte offset, instead of cnr
+        }
+        if (a.bloom_fused && e < ce) {  // filter_hash (filter.rs:196-204) -> first probe / step
+            const uint64_t kl = in.ko1 - in.ko0;
+            const uint64_t h = kl == 16 ? siphash13_16(in.ck0, in.ck1) : siphash13(a.key_bytes + in.ko0, kl);
+            a.hd[e] = (uint64_t)fastmod_u32((uint32_t)h, a.bpl.mmod, a.bpl.m) |
+                      ((uint64_t)fastmod_u32((uint32_t)(h >> 32), a.bpl.mmod, a.bpl.m) << 32);
         }
         if (e < ce) {
             a.lcp[e] = f.lcp;
@@ -313,35 +323,34 @@ __global__ __launch_bounds__(kSegThreads, 8) void k_seg(EncodeArgs a) {
     }
     if (tid == 0) a.err_part[k] = s_err;  // every chunk writes its slot: no initialisation needed
     PHASE_MARK(1);
-    // b. prefix sums (V2)
+    // b. P = exclusive prefix of the clamped non-restart sizes (V2): one block scan of the three
+    //    strided rows (entry x = tid + u * nt); the restart surcharges stay per entry (s_R)
     if (v2) {
-        uint64_t carry = 0;
-        for (uint32_t x0 = 0; x0 < sn; x0 += nt) {
-            const uint32_t x = x0 + tid;
-            const uint64_t v = x < sn ? s_P[x] : 0;
-            uint64_t tot;
-            const uint64_t ex = block_excl_scan_u64(v, s_w, &tot);
-            if (x < sn) s_P[x] = (uint32_t)(carry + ex);
-            carry += tot;
+        __shared__ uint32_t s_wt[kPerT * (kSegThreads / 64) + 1];
+        const uint32_t wv = tid >> 6;
+        uint32_t v[kPerT], inc[kPerT];
+#pragma unroll
+        for (uint32_t u = 0; u < kPerT; u++) {
+            const uint32_t x = tid + u * nt;
+            v[u] = x < sn ? s_P[x] : 0;
+            inc[u] = wave_incl_scan(v[u]);
+            if (lane == 63) s_wt[u * (nt >> 6) + wv] = inc[u];
         }
-        if (tid == 0) s_P[sn] = (uint32_t)carry;
+        __syncthreads();
+        if (tid < 64) {
+            const uint32_t nw = kPerT * (nt >> 6);
+            const uint32_t t = tid < nw ? s_wt[tid] : 0, it = wave_incl_scan(t);
+            __builtin_amdgcn_wave_barrier();
+            if (tid < nw) s_wt[tid] = it - t;
+            if (tid == 63) s_P[sn] = it;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < kPerT; u++) {
+            const uint32_t x = tid + u * nt;
+            if (x < sn) s_P[x] = s_wt[u * (nt >> 6) + wv] + inc[u] - v[u];
+        }
         PHASE_MARK(2);
-        // R[x] = sum of surcharges at x, x - ri, x - 2 ri, ... (Hillis-Steele along each residue class)
-        for (uint32_t stride = ri; stride < sn; stride <<= 1) {
-            uint32_t nv[kPerT];
-#pragma unroll
-            for (uint32_t u = 0; u < kPerT; u++) {
-                const uint32_t x = tid + u * nt;
-                nv[u] = (x < sn && x >= stride) ? s_R[x] + s_R[x - stride] : (x < sn ? s_R[x] : 0);
-            }
-            __syncthreads();
-#pragma unroll
-            for (uint32_t u = 0; u < kPerT; u++) {
-                const uint32_t x = tid + u * nt;
-                if (x < sn) s_R[x] = nv[u];
-            }
-            __syncthreads();
-        }
     }
     __syncthreads();
     PHASE_MARK(3);
@@ -354,10 +363,10 @@ __global__ __launch_bounds__(kSegThreads, 8) void k_seg(EncodeArgs a) {
         if (v2) {
             // size(b, e) for b < e <= sn (clamped sizes; exact whenever it is <= block_size)
             const uint32_t Pb = s_P[x];
-            const uint32_t Rb = x >= ri ? s_R[x - ri] : 0;
-            auto size_of = [&](uint32_t e) -> uint64_t {
-                const uint32_t last = x + ((e - 1 - x) / ri) * ri;  // last restart row of [x, e)
-                return 2ull + (s_P[e] - Pb) + (s_R[last] - Rb);
+            auto size_of = [&](uint32_t e) -> uint64_t {  // + the surcharges of the restart rows x, x + ri, ...
+                uint64_t sz = 2ull + (s_P[e] - Pb);
+                for (uint32_t r = x; r < e; r += ri) sz += s_R[r];
+                return sz;
             };
             // start from an estimate and step (sizes are positive, so size(b, e) grows with e)
             uint32_t lo = x + 1;  // size(b, lo) may exceed block_size: a one-entry block
@@ -495,7 +504,11 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(EncodeArgs a) {
     __shared__ uint32_t s_W;
     __shared__ unsigned long long s_err;
     __shared__ uint64_t s_stat[5][kGroupThreads / 64];
-    const uint32_t K = a.nchunks, g = blockIdx.x, G = a.group, ngroups = gridDim.x;
+    const uint32_t K = a.nchunks, g = blockIdx.x, G = a.group, ngroups = (K + G - 1) / G;
+    if (g >= ngroups) {  // bloom role: bin one tile of k_seg's (h0, d0) into the slice queues
+        bloom_bin_tile<true>(g - ngroups, nullptr, nullptr, a.hd, a.n, a.bpl, a.bq, (uint32_t *)smem);
+        return;
+    }
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     if (tid == 0) {
         s_W = 0;
@@ -750,15 +763,20 @@ SDB_DEV bool emit_fast(const BlockDesc &d) {
 // K5a: enumerate the blocks of each chunk (binary lifting over next()) -> BlockMeta offsets and the
 //      per-block descriptors the emitter streams.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_enum(EncodeArgs a) {
+__global__ __launch_bounds__(kEnumThreads) void k_enum(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint64_t s_anc[4];  // entry point, first block, first byte, blocks of this chunk
     const uint32_t k = blockIdx.x, K = a.nchunks;
+    if (k >= K) {  // bloom role: OR one slice's queued probes into LDS, write the slice
+        bloom_fill_slice(k - K, nullptr, nullptr, a.hd, a.n, a.bpl, a.bq, a.bloom_out, a.bloom_len, (uint32_t *)smem);
+        return;
+    }
     if (*a.err != ~0ull) return;
     const uint64_t cs = (uint64_t)k * kChunk;
     const uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
     const uint32_t cn = (uint32_t)(ce - cs);
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    PHASE_MARK_E(0);
     uint32_t *bl_s = (uint32_t *)smem;
     uint32_t *bl_b = bl_s + kChunk;
     uint64_t *bl_o = (uint64_t *)(bl_b + kChunk);
@@ -772,34 +790,45 @@ __global__ __launch_bounds__(256) void k_enum(EncodeArgs a) {
         uint32_t *t_ex = (uint32_t *)lv;                 // ntab x W each
         uint32_t *t_cn = (uint32_t *)((uint8_t *)lv + tb4);
         uint64_t *t_by = (uint64_t *)((uint8_t *)lv + 2 * tb4);
-        for (uint32_t idx = tid; idx < ntab * W; idx += nt) {
-            const uint32_t q = idx / W, o = idx - q * W;
-            uint32_t x, c;
-            uint64_t b;
-            if (q < g) {
-                const uint64_t t = (uint64_t)q * a.seg_look + o;
-                x = a.gtab_exit[t];
-                c = a.gtab_cnt[t];
-                b = a.gtab_bytes[t];
-            } else {
-                const uint32_t kk = k0 + (q - g);
-                const uint64_t ccs = (uint64_t)kk * kChunk, cce = ccs + kChunk < a.n ? ccs + kChunk : a.n;
-                x = 0;
-                c = 0;
-                b = 0;
-                if (ccs + o < cce) {
-                    const uint64_t t = (uint64_t)kk * a.seg_look + o;
-                    const uint32_t te = a.tab_exit[t];
-                    x = te >= cce ? te - (uint32_t)cce : 0;
-                    c = a.tab_cnt[t];
-                    b = a.tab_bytes[t];
+        constexpr uint32_t kU = 8;  // table entries per thread per batch: all loads issued first
+        for (uint32_t base = 0; base < ntab * W; base += kU * nt) {
+            uint32_t x[kU], c[kU];
+            uint64_t b[kU];
+#pragma unroll
+            for (uint32_t u = 0; u < kU; u++) {
+                const uint32_t idx = base + u * nt + tid;
+                x[u] = c[u] = 0;
+                b[u] = 0;
+                if (idx >= ntab * W) continue;
+                const uint32_t q = idx / W, o = idx - q * W;
+                if (q < g) {
+                    const uint64_t t = (uint64_t)q * a.seg_look + o;
+                    x[u] = a.gtab_exit[t];
+                    c[u] = a.gtab_cnt[t];
+                    b[u] = a.gtab_bytes[t];
+                } else {
+                    const uint32_t kk = k0 + (q - g);
+                    const uint64_t ccs = (uint64_t)kk * kChunk, cce = ccs + kChunk < a.n ? ccs + kChunk : a.n;
+                    if (ccs + o < cce) {
+                        const uint64_t t = (uint64_t)kk * a.seg_look + o;
+                        const uint32_t te = a.tab_exit[t];
+                        x[u] = te >= cce ? te - (uint32_t)cce : 0;
+                        c[u] = a.tab_cnt[t];
+                        b[u] = a.tab_bytes[t];
+                    }
                 }
             }
-            t_ex[idx] = x < W ? x : W - 1;
-            t_cn[idx] = c;
-            t_by[idx] = b;
+#pragma unroll
+            for (uint32_t u = 0; u < kU; u++) {
+                const uint32_t idx = base + u * nt + tid;
+                if (idx >= ntab * W) continue;
+                t_ex[idx] = x[u] < W ? x[u] : W - 1;
+                t_cn[idx] = c[u];
+                t_by[idx] = b[u];
+            }
         }
         __syncthreads();
+        PHASE_MARK_E(1);
         if (tid == 0) {
             uint32_t e = 0;
             uint64_t blk = 0, by = 0;
@@ -831,6 +860,7 @@ __global__ __launch_bounds__(256) void k_enum(EncodeArgs a) {
         s_anc[3] = a.anchor_blk[k + 1] - a.anchor_blk[k];
     }
     __syncthreads();
+    PHASE_MARK_E(2);
     const uint64_t e0 = s_anc[0];
     const uint32_t blk0 = (uint32_t)s_anc[1];
     const uint32_t nb = (uint32_t)s_anc[3];
@@ -846,11 +876,26 @@ __global__ __launch_bounds__(256) void k_enum(EncodeArgs a) {
     if (!nb) return;
     uint32_t levels = 1;
     while ((1u << levels) < nb) levels++;
-    for (uint32_t x = tid; x < cn; x += nt) {
-        uint64_t nx = a.next[cs + x];
-        lv[x] = (uint16_t)(nx >= ce ? cn : (uint32_t)(nx - cs));
+    {
+        constexpr uint32_t kU = kChunk / 256;  // next() of the chunk: all loads issued first
+        uint32_t nx[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t x = u * nt + tid;
+            nx[u] = x < cn ? a.next[cs + x] : 0;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t x = u * nt + tid;
+            if (x < cn) lv[x] = (uint16_t)(nx[u] >= ce ? cn : (uint32_t)(nx[u] - cs));
+        }
+        for (uint32_t x = kU * nt + tid; x < cn; x += nt) {  // (blockDim < 256 only)
+            const uint64_t v = a.next[cs + x];
+            lv[x] = (uint16_t)(v >= ce ? cn : (uint32_t)(v - cs));
+        }
     }
     __syncthreads();
+    PHASE_MARK_E(3);
     for (uint32_t j = 1; j < levels; j++) {
         uint16_t *src = lv + (uint64_t)(j - 1) * kChunk, *dst = lv + (uint64_t)j * kChunk;
         for (uint32_t x = tid; x < cn; x += nt) {
@@ -867,6 +912,7 @@ __global__ __launch_bounds__(256) void k_enum(EncodeArgs a) {
         bl_b[t] = a.bbytes[cs + x];
     }
     __syncthreads();
+    PHASE_MARK_E(4);
     if (tid < 64) {
         uint64_t carry = byte0;
         for (uint32_t g = 0; g < nb; g += 64) {
@@ -879,7 +925,7 @@ __global__ __launch_bounds__(256) void k_enum(EncodeArgs a) {
     }
     __syncthreads();
     for (uint32_t t = tid; t < nb; t += nt) {
-        uint64_t s = bl_s[t], e = a.next[s];
+        const uint64_t s = bl_s[t], e = t + 1 < nb ? bl_s[t + 1] : a.next[s];
         uint32_t blk = blk0 + t;
         a.out_block_off[blk] = bl_o[t];
         a.out_block_first[blk] = (uint32_t)s;
@@ -896,6 +942,7 @@ __global__ __launch_bounds__(256) void k_enum(EncodeArgs a) {
         a.desc[blk] = d;
         if (!emit_fast(d)) a.slow_list[atomicAdd(a.slow_count, 1u)] = blk;
     }
+    PHASE_MARK_E(5);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1692,6 +1739,9 @@ extern "C" int sdb_diag_wave_rt(uint64_t *out, int nwaves) {
     return -1;
 #endif
 }
+extern "C" int sdb_diag_enum_phase(uint64_t *out, int nblocks) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_enum), sizeof(uint64_t) * 8 * nblocks) == hipSuccess ? 0 : -1;
+}
 extern "C" int sdb_diag_phase_times(uint64_t *out, int nblocks) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(uint64_t) * 8 * nblocks) == hipSuccess ? 0 : -1;
 }
@@ -1719,7 +1769,7 @@ static void set_lds_attrs() {
     hipFuncSetAttribute((const void *)k_emit<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
     hipFuncSetAttribute((const void *)k_emit<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
     hipFuncSetAttribute((const void *)k_enum, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEnumLds);
-    hipFuncSetAttribute((const void *)k_group, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGroupLds);
+    hipFuncSetAttribute((const void *)k_group, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLds);
     hipFuncSetAttribute((const void *)k_seg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLds);
     lds_attrs_set = true;
 }
@@ -1736,10 +1786,12 @@ hipError_t launch_encode(EncodeArgs a, hipStream_t st) {
     hipLaunchKernelGGL(k_seg, dim3(a.nchunks), dim3(kSegThreads), kSegLds, st, a);
     stage_mark(st, kStSeg, false);
     stage_mark(st, kStResolve, true);
-    hipLaunchKernelGGL(k_group, dim3((a.nchunks + a.group - 1) / a.group), dim3(kGroupThreads), kGroupLds, st, a);
+    const uint32_t ngroups = (a.nchunks + a.group - 1) / a.group;
+    const size_t glds = a.bloom_fused && bloom_bin_lds(a.bpl) > kGroupLds ? bloom_bin_lds(a.bpl) : kGroupLds;
+    hipLaunchKernelGGL(k_group, dim3(ngroups + (a.bloom_fused ? a.bpl.tiles : 0)), dim3(kGroupThreads), glds, st, a);
     stage_mark(st, kStResolve, false);
     stage_mark(st, kStEnum, true);
-    hipLaunchKernelGGL(k_enum, dim3(a.nchunks), dim3(256), kEnumLds, st, a);
+    hipLaunchKernelGGL(k_enum, dim3(a.nchunks + (a.bloom_fused ? a.bpl.nslices : 0)), dim3(kEnumThreads), kEnumLds, st, a);
     stage_mark(st, kStEnum, false);
     stage_mark(st, kStEmit, true);
     if (a.version == 2) hipLaunchKernelGGL(k_emit<2>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, a);

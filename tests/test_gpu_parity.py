@@ -277,3 +277,33 @@ def test_device_round_trip_full_d1(rt):
     assert (d.val_len == 100).all()
     vals = enc.data[(d.val_off[:, None] + np.arange(100, dtype=np.uint64)).astype(np.int64)]
     assert np.array_equal(vals.reshape(-1), b.val_bytes)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [5000, 100000, datasets.D1_N])
+def test_bloom_queues_do_not_overflow(rt, n):
+    """The fused bloom's slice queues are sized for uniform probes: D1-shaped batches must take the
+    queued fill (no overflow flag), not the rebuild-from-hashes fallback."""
+    import ctypes as C
+    import torch
+    runtime = rt
+    b = datasets.d1(n=n)
+    prm = runtime.params(block_size=4096, sst_version=2, bloom_bits_per_key=10)
+    out = runtime.DeviceSstOutput(b.n, b.logical_bytes(), b.logical_bytes(), prm)
+    runtime.encode_sst_device(b.to_device("cuda"), out)
+    torch.cuda.synchronize()
+    got = out.to_host()
+    ref = O.encode_sst(b, O.params(block_size=4096, sst_version=2, bloom_bits_per_key=10))
+    assert np.array_equal(got["bloom"], ref.bloom)
+    cd = C.CDLL(runtime.LIB_PATH)
+    cd.sdb_diag_bloom_ws_offset.restype = C.c_uint64
+    cd.sdb_diag_bloom_ws_offset.argtypes = [C.c_uint64, C.c_void_p]
+    off = (cd.sdb_diag_bloom_ws_offset(b.n, C.byref(prm)) + 255) // 256 * 256
+    fb = (n * 10 + 7) // 8
+    sb = 15
+    while sb < 19 and -(-fb * 8 // (1 << sb)) > 256:
+        sb += 1
+    nslices = -(-fb * 8 // (1 << sb))
+    cur = out.workspace[off: off + 4 * (nslices * 8 + 1)].cpu().numpy().view(np.uint32)
+    assert cur[nslices * 8] == 0, "bloom queue overflow flag set"
+    assert int(cur[: nslices * 8].sum()) == n * 6
