@@ -11,7 +11,7 @@ from slatedb_amd import datasets, runtime  # noqa: E402
 
 lib = runtime.lib()
 dev = torch.device("cuda", 0)
-prm = runtime.params(block_size=4096, sst_version=2, restart_interval=16, bloom_bits_per_key=0)
+prm = runtime.params(block_size=4096, sst_version=2, restart_interval=16, bloom_bits_per_key=int(os.environ.get('BPK', '10')))
 h = datasets.d1(sst_index=1)
 db = h.to_device(dev)
 out = runtime.DeviceSstOutput(h.n, h.logical_bytes(), h.logical_bytes(), prm, device=dev)
@@ -26,7 +26,7 @@ cdll = C.CDLL(runtime.LIB_PATH)
 cdll.sdb_diag_phase_times.argtypes = [C.c_void_p, C.c_int]
 assert cdll.sdb_diag_phase_times(C.addressof(buf), 1024) == 0
 t = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 8)[:nb].astype(np.int64)
-marks = 6
+marks = 7
 d = np.diff(t[:, :marks], axis=1)
 print("phase durations (s_memtime ticks) mean/max over %d workgroups:" % nb)
 for i in range(marks - 1):

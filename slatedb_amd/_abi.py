@@ -146,7 +146,7 @@ SIGNATURES = {
 }
 
 
-STAGES = ["bloom", "seg", "resolve", "enum", "emit", "emit_slow"]
+STAGES = ["bloom", "facts", "seg", "group", "enum", "emit", "emit_slow"]
 
 
 def bind(lib):

@@ -146,6 +146,9 @@ sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const 
         a.seg_look = (uint32_t)(look < kSegLook ? look : kSegLook);
     }
     a.lcp = carve<uint32_t>(workspace, wl.lcp);
+    a.szr = carve<uint32_t>(workspace, wl.szr);
+    a.sznr = carve<uint32_t>(workspace, wl.sznr);
+    a.hd = carve<uint64_t>(workspace, wl.hd);
     a.row_scratch = carve<uint32_t>(workspace, wl.row_scratch);
     a.next = carve<uint32_t>(workspace, wl.next);
     a.bbytes = carve<uint32_t>(workspace, wl.bbytes);
@@ -186,14 +189,13 @@ sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const 
     a.filter_built = want_filter ? 1 : 0;
     hipStream_t s = S(stream);
     if (want_filter && n) {
-        // the bloom runs inside the encode kernels (k_seg hashes, k_group bins, k_enum fills) when the
-        // binned build fits; otherwise it is built on the stream before the encode
-        const BloomPlan pl = bloom_plan(n, a.num_probes, fb);
-        if (bloom_plan_fits(pl, n) && bloom_fill_lds(pl) <= 64 * 1024) {
+        // the bloom runs inside the encode kernels (k_seg hashes and bins each chunk, k_enum fills the
+        // slices) when the binned build fits; otherwise it is built on the stream before the encode
+        const BloomPlan pl = bloom_plan(n, a.num_probes, fb, kChunk);
+        if (bloom_plan_fits(pl) && bloom_bin_lds(pl) <= kSegLdsMax && bloom_fill_lds(pl) <= kEnumLds) {
             a.bloom_fused = 1;
-            a.hd = carve<uint64_t>(workspace, wl.hd);
             a.bpl = pl;
-            a.bq = bloom_queues(carve<void>(workspace, wl.bloom_rep), n, pl);
+            a.bq = bloom_slots(carve<void>(workspace, wl.bloom_rep), pl);
             a.bloom_out = out->bloom;
         } else {
             stage_mark(s, kStBloom, true);
@@ -290,7 +292,7 @@ void stage_mark(hipStream_t st, int stage, bool begin) {
     hipEventRecord(e, st);
     if (begin) {
         g_open[stage] = e;
-        if (stage == kStSeg) g_launches++;
+        if (stage == kStFacts) g_launches++;
     } else {
         g_recs.push_back({stage, g_open[stage], e});
         g_open[stage] = nullptr;
@@ -724,8 +726,16 @@ sdb_status sdb_decoder_decode_host(sdb_decoder *d, const uint8_t *blocks, const 
 
 }  // extern "C"
 
-// Diagnostics: byte offset of the bloom queue region (cursors first) inside sdb_encode_sst's workspace.
-extern "C" uint64_t sdb_diag_bloom_ws_offset(uint64_t n, const sdb_sst_params *p) {
-    uint64_t fb = p && p->bloom_bits_per_key ? filter_bytes_for(n, p->bloom_bits_per_key) : 0;
-    return sdb::encode_workspace_layout(n, fb, p ? num_probes_for(p->bloom_bits_per_key) : 0).bloom_rep;
+// Diagnostics: the fused bloom's slot plan inside sdb_encode_sst's workspace: byte offset of the run
+// counts (tiles x nslices u32), tiles, slices and slot capacity.
+extern "C" uint64_t sdb_diag_bloom_slots(uint64_t n, const sdb_sst_params *p, uint32_t *tiles, uint32_t *nslices,
+                                         uint32_t *cap) {
+    const uint64_t fb = p && p->bloom_bits_per_key ? filter_bytes_for(n, p->bloom_bits_per_key) : 0;
+    const uint32_t k = p ? num_probes_for(p->bloom_bits_per_key) : 0;
+    const BloomPlan pl = bloom_plan(n, k, fb, kChunk);
+    *tiles = pl.tiles;
+    *nslices = pl.nslices;
+    *cap = bloom_slot_cap(pl);
+    const uint64_t off = sdb::encode_workspace_layout(n, fb, k).bloom_rep;
+    return (off + 255) & ~255ull;
 }

@@ -95,21 +95,20 @@ SDB_DEV void for_each_probe(uint64_t hash, uint32_t k, uint32_t m, F f) {
 // Build by binning probes into bitmap slices, then setting bits in LDS.  Random 32-bit atomics to
 // HBM/L2 run at ~25 G/s on MI355X whatever their scope (scripts/probe.hip), i.e. ~136 us for the
 // 3.47 M probes of one 64 MiB SST; LDS atomics are two orders of magnitude faster.
-//   k_bloom_bin   one workgroup per tile of kBinKeys keys: SipHash-1-3, the k probes, an LDS
-//                 counting sort by slice; one global atomicAdd per (tile, slice) reserves a run in
-//                 that slice's queue and the sorted probes are written run by run.
-//   k_bloom_fill  one workgroup per slice of 2^sb bits: reads its queue (coalesced), ORs the probes
-//                 into an LDS copy of the slice, writes the slice with plain stores.
-// The queues hold the expected load + 8 sigma + one tile; a queue that would overflow (only for
-// adversarial key sets) sets a flag and its slice is rebuilt by re-hashing every key.  The queue
-// cursors and the flag are zeroed on the stream before the binning.  Deterministic (an OR).
+//   bin   one workgroup per tile of T keys (k_bloom_bin, or k_seg's chunk): SipHash-1-3, the k
+//         probes, an LDS counting sort by slice.  The run of slice s goes to the tile's own slot
+//         (s, tile) and its length to count[tile][s]: fixed places, so there is no global atomic
+//         and nothing to initialise between calls.
+//   fill  one workgroup per slice of 2^sb bits (k_bloom_fill, or k_enum's bloom role): every
+//         tile's slot of the slice, ORed into an LDS copy of the slice, written with plain stores.
+// A slot holds the expected run + 6 sigma + 16 probes; a longer run (adversarial key sets only) is
+// recorded as kSlotOverflow and the fill rebuilds that slice from every key.  Deterministic (an OR).
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t kBinThreads = 1024, kBinKeysPerThread = 4, kFillThreads = 1024;
 constexpr uint32_t kBinMaxK = 15;  // probes per key (larger k: atomic path)
 constexpr uint32_t kBinLds = 128 * 1024;
-constexpr uint32_t kShards = 8;    // queues per slice: the tile's XCD-ish shard (blockIdx & 7)
-constexpr uint32_t kFillUnroll = 8;  // 16-byte queue loads in flight per k_bloom_fill thread
-
+constexpr uint32_t kSlotOverflow = 0xFFFFFFFFu;
+constexpr uint32_t kNoProbe = 0xFFFFFFFFu;  // never a probe: m < 2^32
 
 // (h0, d0) of the enhanced double hashing for one key: h0 = lo % m, d0 = hi % m
 SDB_DEV uint64_t key_hash(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t i) {
@@ -142,158 +141,106 @@ SDB_DEV void probes_hd(uint32_t h, uint32_t d, uint32_t k, uint32_t m, F f) {
     }
 }
 
-// One binning tile (k_bloom_bin, or the bloom role of k_group): the (h0, d0) of each key come from
-// the keys (FROM_HD false) or from hd[] (k_seg wrote them, FROM_HD true).  lds: dynamic LDS.
-template <bool FROM_HD>
-SDB_DEV void bloom_bin_tile(uint32_t tile, const uint8_t *__restrict__ key_bytes, const uint64_t *__restrict__ key_off,
-                            const uint64_t *__restrict__ hd, uint64_t n, const BloomPlan &pl, const BloomQueues &q,
-                            uint32_t *lds) {
+// Bin one tile whose keys' (h0, d0) are held in registers: key tid + j * blockDim.x of the tile in
+// (hh[j], dd[j]), nk keys.  Each probe takes the next position of its slice's slot from an LDS
+// counter and is stored straight into the slot (the slot's lines fill in L2 before they leave); the
+// final counters are the run lengths.  The order inside a run depends on the atomics' order; the
+// bitmap (an OR) does not.  lds: >= bloom_bin_lds(pl) bytes.  Called by the whole workgroup.
+template <uint32_t KPT>
+SDB_DEV void bloom_bin_core(uint32_t tile, const uint32_t (&hh)[KPT], const uint32_t (&dd)[KPT], uint32_t nk,
+                            const BloomPlan &pl, const BloomSlots &q, uint32_t *lds) {
     const uint32_t S = pl.nslices;
-    uint32_t *hist = lds;                          // S: counts, then local run starts
-    uint32_t *cur = hist + S;                      // S: local scatter cursors
-    uint32_t *gbase = cur + S;                     // S: reserved queue positions
-    uint32_t *sorted = gbase + S;                  // T * k probes, slice order
-    __shared__ uint64_t s_w[17];
+    uint32_t *cnt = lds;  // S: next free position of each slice's slot
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    for (uint32_t x = tid; x < S; x += nt) cnt[x] = 0;
+    __syncthreads();
+    uint32_t *slots = q.slot + (uint64_t)tile * q.cap;  // slot (sl, tile) at slots + sl * tiles * cap
+    const uint64_t stride = (uint64_t)pl.tiles * q.cap;
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; j++)
+        if (tid + j * nt < nk)
+            probes_hd(hh[j], dd[j], pl.k, pl.m, [&](uint32_t p) {
+                const uint32_t sl = p >> pl.sb;
+                const uint32_t pos = atomicAdd(&cnt[sl], 1u);
+                if (pos < q.cap) slots[sl * stride + pos] = p;
+            });
+    __syncthreads();
+    for (uint32_t x = tid; x < S; x += nt) {
+        const uint32_t c = cnt[x];
+        q.count[(uint64_t)tile * S + x] = c <= q.cap ? c : kSlotOverflow;
+    }
+}
+
+// One binning tile of the standalone build: hash the tile's keys, then bin.
+SDB_DEV void bloom_bin_tile(uint32_t tile, const uint8_t *__restrict__ key_bytes, const uint64_t *__restrict__ key_off,
+                            uint64_t n, const BloomPlan &pl, const BloomSlots &q, uint32_t *lds) {
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint64_t k0 = (uint64_t)tile * pl.T;
-    const uint64_t k1 = k0 + pl.T < n ? k0 + pl.T : n;
-    const uint32_t nk = (uint32_t)(k1 - k0), np = nk * pl.k;
-    const uint32_t shard = tile & (kShards - 1);
-    for (uint32_t x = tid; x < S; x += nt) hist[x] = 0;
-    // hashes stay in registers: key tid + j * nt of the tile
+    const uint32_t nk = (uint32_t)((k0 + pl.T < n ? k0 + pl.T : n) - k0);
     uint32_t hh[kBinKeysPerThread], dd[kBinKeysPerThread];
 #pragma unroll
     for (uint32_t j = 0; j < kBinKeysPerThread; j++) {
         const uint32_t i = tid + j * nt;
         hh[j] = dd[j] = 0;
-        if (i < nk) {
-            if (FROM_HD) {
-                const uint64_t v = hd[k0 + i];
-                hh[j] = (uint32_t)v;
-                dd[j] = (uint32_t)(v >> 32);
-            } else {
-                key_hd(key_bytes, key_off, k0 + i, pl, hh[j], dd[j]);
-            }
-        }
+        if (i < nk) key_hd(key_bytes, key_off, k0 + i, pl, hh[j], dd[j]);
     }
-#if defined(SDB_EXP_BIN_STAGE) && SDB_EXP_BIN_STAGE == 1
-    if ((hh[0] ^ dd[1] ^ hh[2] ^ dd[3]) == 0x12345) q.cursor[0] = 7;  // keep the hashes live
-    return;
-#endif
-    __syncthreads();
-#pragma unroll
-    for (uint32_t j = 0; j < kBinKeysPerThread; j++)
-        if (tid + j * nt < nk) probes_hd(hh[j], dd[j], pl.k, pl.m, [&](uint32_t p) { atomicAdd(&hist[p >> pl.sb], 1u); });
-    __syncthreads();
-#if defined(SDB_EXP_BIN_STAGE) && SDB_EXP_BIN_STAGE == 2
-    return;
-#endif
-    // local run starts (exclusive scan) + one reservation per non-empty slice in this shard
-    uint64_t carry = 0;
-    for (uint32_t x0 = 0; x0 < S; x0 += nt) {
-        const uint32_t x = x0 + tid;
-        const uint32_t c = x < S ? hist[x] : 0;
-        uint64_t tot;
-        const uint64_t ex = block_excl_scan_u64(c, s_w, &tot);
-        if (x < S) {
-            gbase[x] = c ? atomicAdd(q.cursor + (uint64_t)x * kShards + shard, c) : 0;
-            hist[x] = (uint32_t)(carry + ex);
-            cur[x] = (uint32_t)(carry + ex);
-        }
-        carry += tot;
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t j = 0; j < kBinKeysPerThread; j++)
-        if (tid + j * nt < nk)
-            probes_hd(hh[j], dd[j], pl.k, pl.m, [&](uint32_t p) { sorted[atomicAdd(&cur[p >> pl.sb], 1u)] = p; });
-    __syncthreads();
-#if defined(SDB_EXP_BIN_STAGE) && SDB_EXP_BIN_STAGE == 3
-    return;
-#endif
-    // write the runs: sorted[x] belongs to slice sl = p >> sb at run position x - hist[sl]
-    bool over = false;
-    for (uint32_t x = tid; x < np; x += nt) {
-        const uint32_t p = sorted[x], sl = p >> pl.sb;
-        const uint32_t pos = gbase[sl] + (x - hist[sl]);
-        if (pos < q.cap) q.queue[(sl * kShards + shard) * q.cap + pos] = p;  // < 2^32 probes (plan_fits)
-        else over = true;
-    }
-    if (over) q.cursor[(uint64_t)S * kShards] = 1u;
+    bloom_bin_core<kBinKeysPerThread>(tile, hh, dd, nk, pl, q, lds);
 }
 
-// One bitmap slice (k_bloom_fill, or the bloom role of k_enum).  lds: dynamic LDS (2^sb bits).
+// One bitmap slice (k_bloom_fill, or the bloom role of k_enum).  lds: bloom_fill_lds(pl) bytes of
+// dynamic LDS (the slice's bits, then the run length of every tile).
 SDB_DEV void bloom_fill_slice(uint32_t s, const uint8_t *__restrict__ key_bytes, const uint64_t *__restrict__ key_off,
-                              const uint64_t *__restrict__ hd, uint64_t n, const BloomPlan &pl, const BloomQueues &q, uint8_t *bitmap, uint64_t bytes,
+                              uint64_t n, const BloomPlan &pl, const BloomSlots &q, uint8_t *bitmap, uint64_t bytes,
                               uint32_t *lds) {
-    const uint32_t words = 1u << (pl.sb - 5);
-    uint32_t *bits = lds;  // 2^sb bits
+    const uint32_t words = 1u << (pl.sb - 5), T = pl.tiles;
+    uint32_t *bits = lds;         // 2^sb bits
+    uint32_t *cnt = bits + words;  // T: run length of each tile's slot
+    __shared__ uint32_t s_over;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    if (tid == 0) s_over = 0;
     for (uint32_t x = tid; x < words; x += nt) bits[x] = 0;
     __syncthreads();
+    for (uint32_t t = tid; t < T; t += nt) {
+        const uint32_t c = q.count[(uint64_t)t * pl.nslices + s];
+        cnt[t] = c;
+        if (c == kSlotOverflow) s_over = 1;
+    }
+    __syncthreads();
     const uint32_t lo = s << pl.sb;
-#if defined(SDB_EXP_FILL_NOSET)
-    auto set = [&](uint32_t p) { if (p == 0xFFFFFFFFu) bits[0] = p; };
-#else
     auto set = [&](uint32_t p) { atomicOr(&bits[(p - lo) >> 5], 1u << (p & 31)); };
-#endif
-    if (q.cursor[(uint64_t)pl.nslices * kShards] == 0) {
-        // the slice's kShards queues as one sequence of 16-byte units (each queue's < 4 tail probes
-        // separately); every thread keeps kFillUnroll units in flight
-        __shared__ uint32_t s_u[kShards + 1], s_cnt[kShards];
-        if (tid < kShards) s_cnt[tid] = q.cursor[(uint64_t)s * kShards + tid];
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t u = 0;
-            for (uint32_t sh = 0; sh < kShards; sh++) {
-                s_u[sh] = u;
-                u += s_cnt[sh] >> 2;
-            }
-            s_u[kShards] = u;
-        }
-        __syncthreads();
-        const uint32_t nu = s_u[kShards];
-        const uint4 *q4 = (const uint4 *)(q.queue + (uint64_t)s * kShards * q.cap);
-        const uint32_t cap4 = q.cap >> 2;
-        auto unit = [&](uint32_t u) -> const uint4 * {
-            uint32_t sh = 0;
+    if (!s_over) {
+        // wave w takes tiles w, w + nw, ...; lane l reads probes l, l + 64, ... of a slot; four slots
+        // in flight per wave
+        const uint32_t w = tid >> 6, nw = nt >> 6, l = tid & 63;
+        const uint32_t *base = q.slot + (uint64_t)s * T * q.cap;
+        for (uint32_t t0 = w; t0 < T; t0 += 4 * nw) {
+            uint32_t v[4][4];
 #pragma unroll
-            for (uint32_t j = 1; j < kShards; j++) sh += u >= s_u[j];
-            return q4 + sh * cap4 + (u - s_u[sh]);
-        };
-        for (uint32_t u0 = 0; u0 < nu; u0 += kFillUnroll * nt) {
-            uint4 v[kFillUnroll];
+            for (uint32_t u = 0; u < 4; u++) {
+                const uint32_t t = t0 + u * nw;
+                const uint32_t c = t < T ? cnt[t] : 0;
 #pragma unroll
-            for (uint32_t j = 0; j < kFillUnroll; j++) {
-                const uint32_t u = u0 + j * nt + tid;
-                if (u < nu) v[j] = *unit(u);
-            }
-#pragma unroll
-            for (uint32_t j = 0; j < kFillUnroll; j++) {
-                if (u0 + j * nt + tid < nu) {
-                    set(v[j].x);
-                    set(v[j].y);
-                    set(v[j].z);
-                    set(v[j].w);
+                for (uint32_t r = 0; r < 4; r++) {
+                    const uint32_t i = l + 64 * r;
+                    v[u][r] = i < c ? base[(uint64_t)t * q.cap + i] : kNoProbe;
                 }
             }
-        }
-        if (tid < kShards * 4) {  // tails: thread 4 sh + r takes probe r of queue sh's tail
-            const uint32_t sh = tid >> 2, r = tid & 3, c = s_cnt[sh];
-            if (r < (c & 3)) set(q.queue[((uint64_t)s * kShards + sh) * q.cap + (c & ~3u) + r]);
+#pragma unroll
+            for (uint32_t u = 0; u < 4; u++) {
+#pragma unroll
+                for (uint32_t r = 0; r < 4; r++)
+                    if (v[u][r] != kNoProbe) set(v[u][r]);
+                const uint32_t t = t0 + u * nw;  // runs longer than 256 probes (q.cap > 256)
+                const uint32_t c = t < T ? cnt[t] : 0;
+                for (uint32_t i = 256 + l; i < c; i += 64) set(base[(uint64_t)t * q.cap + i]);
+            }
         }
     } else {
-        // a queue overflowed: rebuild this slice from every key (hd: k_seg's (h0, d0), else hash)
+        // a slot overflowed: rebuild this slice from every key
         const uint32_t hi = lo + (1u << pl.sb) - 1;
         for (uint64_t i = tid; i < n; i += nt) {
             uint32_t h, d;
-            if (hd) {
-                const uint64_t v = hd[i];
-                h = (uint32_t)v;
-                d = (uint32_t)(v >> 32);
-            } else {
-                key_hd(key_bytes, key_off, i, pl, h, d);
-            }
+            key_hd(key_bytes, key_off, i, pl, h, d);
             probes_hd(h, d, pl.k, pl.m, [&](uint32_t p) {
                 if (p >= lo && p <= hi) set(p);
             });
@@ -312,11 +259,11 @@ SDB_DEV void bloom_fill_slice(uint32_t s, const uint8_t *__restrict__ key_bytes,
 }
 
 // Host-side plan helpers (sdb_bloom.hip).
-uint32_t bloom_queue_cap(uint64_t n, const BloomPlan &pl);
-bool bloom_plan_fits(const BloomPlan &pl, uint64_t n);
-uint64_t bloom_cursor_bytes(const BloomPlan &pl);
+uint32_t bloom_slot_cap(const BloomPlan &pl);
+bool bloom_plan_fits(const BloomPlan &pl);
 size_t bloom_bin_lds(const BloomPlan &pl);
 size_t bloom_fill_lds(const BloomPlan &pl);
-BloomQueues bloom_queues(void *ws, uint64_t n, const BloomPlan &pl);
+uint64_t bloom_slots_bytes(const BloomPlan &pl);
+BloomSlots bloom_slots(void *ws, const BloomPlan &pl);
 
 }  // namespace sdb

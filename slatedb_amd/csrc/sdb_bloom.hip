@@ -25,17 +25,17 @@ __global__ __launch_bounds__(256) void k_bloom_atomic(const uint8_t *__restrict_
 
 __global__ __launch_bounds__(kBinThreads) void k_bloom_bin(const uint8_t *__restrict__ key_bytes,
                                                            const uint64_t *__restrict__ key_off, uint64_t n,
-                                                           BloomPlan pl, BloomQueues q) {
+                                                           BloomPlan pl, BloomSlots q) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    bloom_bin_tile<false>(blockIdx.x, key_bytes, key_off, nullptr, n, pl, q, lds);
+    bloom_bin_tile(blockIdx.x, key_bytes, key_off, n, pl, q, lds);
 }
 
 __global__ __launch_bounds__(kFillThreads) void k_bloom_fill(const uint8_t *__restrict__ key_bytes,
                                                              const uint64_t *__restrict__ key_off, uint64_t n,
-                                                             BloomPlan pl, BloomQueues q, uint8_t *bitmap,
+                                                             BloomPlan pl, BloomSlots q, uint8_t *bitmap,
                                                              uint64_t bytes) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    bloom_fill_slice(blockIdx.x, key_bytes, key_off, nullptr, n, pl, q, bitmap, bytes, lds);
+    bloom_fill_slice(blockIdx.x, key_bytes, key_off, n, pl, q, bitmap, bytes, lds);
 }
 
 __global__ __launch_bounds__(256) void k_bloom_query(const uint32_t *bitmap, uint32_t k, uint32_t m,
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void k_bloom_query(const uint32_t *bitmap, uin
     }
 }
 
-BloomPlan bloom_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes) {
+BloomPlan bloom_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes, uint32_t tile_keys) {
     BloomPlan pl{};
     pl.k = k ? k : 1;
     pl.m = (uint32_t)(bitmap_bytes * 8);
@@ -70,9 +70,8 @@ BloomPlan bloom_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes) {
     while (pl.sb < 19 && (((uint64_t)pl.m + (1ull << pl.sb) - 1) >> pl.sb) > 256) pl.sb++;
     pl.nslices = (uint32_t)(((uint64_t)pl.m + (1ull << pl.sb) - 1) >> pl.sb);
     if (pl.nslices == 0) pl.nslices = 1;
-    // keys per binning tile: kBinKeysPerThread per thread, fewer when the sorted probes outgrow LDS
-    uint32_t T = kBinThreads * kBinKeysPerThread;
-    while (T > kBinThreads && 4ull * (3 * pl.nslices + (uint64_t)T * pl.k) > kBinLds) T -= kBinThreads;
+    uint32_t T = tile_keys;
+    if (!T) T = kBinThreads * kBinKeysPerThread;  // kBinKeysPerThread keys per thread
     pl.T = T;
     pl.tiles = (uint32_t)((n + T - 1) / T);
     if (pl.tiles == 0) pl.tiles = 1;
@@ -80,40 +79,43 @@ BloomPlan bloom_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes) {
     return pl;
 }
 
-uint32_t bloom_queue_cap(uint64_t n, const BloomPlan &pl) {
-    // uniform probes: a queue (slice, shard) receives the probes of the shard's tiles (<= ceil(tiles /
-    // kShards) of T keys) that land in its slice (2^sb of the m bits); + 8 sigma + 1024
-    const double tiles_per_shard = (double)((pl.tiles + kShards - 1) / kShards);
+uint32_t bloom_slot_cap(const BloomPlan &pl) {
+    // uniform probes: a slot (slice, tile) receives the probes of the tile's T keys that land in the
+    // slice (2^sb of the m bits); + 6 sigma + 16
     const double frac = pl.m ? (double)(1ull << pl.sb) / pl.m : 1.0;
-    const double mean = tiles_per_shard * pl.T * pl.k * (frac < 1.0 ? frac : 1.0);
-    uint64_t cap = (uint64_t)(mean + 8.0 * __builtin_sqrt(mean + 1.0)) + 1024;
-    cap = (cap + 63) & ~63ull;
-    return (uint32_t)(cap < 0xFFFFFFC0ull ? cap : 0xFFFFFFC0ull);
+    const double mean = (double)pl.T * pl.k * (frac < 1.0 ? frac : 1.0);
+    uint64_t cap = (uint64_t)(mean + 6.0 * __builtin_sqrt(mean + 1.0)) + 16;
+    cap = (cap + 3) & ~3ull;
+    const uint64_t most = (uint64_t)pl.T * pl.k;  // a slot never holds more than the tile's probes
+    if (cap > most) cap = (most + 3) & ~3ull;
+    return (uint32_t)cap;
 }
 
-bool bloom_plan_fits(const BloomPlan &pl, uint64_t n) {
-    return pl.k <= kBinMaxK && pl.sb <= 19 && pl.m >= 2 && 4ull * (3 * pl.nslices + (uint64_t)pl.T * pl.k) <= kBinLds &&
-           (uint64_t)pl.nslices * kShards * bloom_queue_cap(n, pl) < (1ull << 32);
+bool bloom_plan_fits(const BloomPlan &pl) {
+    return pl.k <= kBinMaxK && pl.sb <= 19 && pl.m >= 2 && bloom_bin_lds(pl) <= kBinLds &&
+           bloom_fill_lds(pl) <= 96 * 1024;
 }
 
-uint64_t bloom_cursor_bytes(const BloomPlan &pl) { return ((uint64_t)(pl.nslices * kShards + 1) * 4 + 255) & ~255ull; }
+uint64_t bloom_slots_bytes(const BloomPlan &pl) {
+    const uint64_t counts = ((uint64_t)pl.tiles * pl.nslices * 4 + 255) & ~255ull;
+    return 256 + counts + (uint64_t)pl.nslices * pl.tiles * bloom_slot_cap(pl) * 4;
+}
 
 uint64_t bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes) {
-    BloomPlan pl = bloom_plan(n, k, bitmap_bytes);
-    return bloom_cursor_bytes(pl) + (uint64_t)pl.nslices * kShards * bloom_queue_cap(n, pl) * 4 + 512;
+    return bloom_slots_bytes(bloom_plan(n, k, bitmap_bytes));
 }
 
-BloomQueues bloom_queues(void *ws, uint64_t n, const BloomPlan &pl) {
+BloomSlots bloom_slots(void *ws, const BloomPlan &pl) {
     uint8_t *w = (uint8_t *)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
-    BloomQueues q;
-    q.cursor = (uint32_t *)w;
-    q.queue = (uint32_t *)(w + bloom_cursor_bytes(pl));
-    q.cap = bloom_queue_cap(n, pl);
+    BloomSlots q;
+    q.count = (uint32_t *)w;
+    q.slot = (uint32_t *)(w + (((uint64_t)pl.tiles * pl.nslices * 4 + 255) & ~255ull));
+    q.cap = bloom_slot_cap(pl);
     return q;
 }
 
-size_t bloom_bin_lds(const BloomPlan &pl) { return 4 * (3 * (size_t)pl.nslices + (size_t)pl.T * pl.k); }
-size_t bloom_fill_lds(const BloomPlan &pl) { return 4 * (size_t)(1u << (pl.sb - 5)); }
+size_t bloom_bin_lds(const BloomPlan &pl) { return 4 * (size_t)pl.nslices; }
+size_t bloom_fill_lds(const BloomPlan &pl) { return 4 * ((size_t)(1u << (pl.sb - 5)) + pl.tiles); }
 
 hipError_t launch_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
                               uint32_t num_probes, uint8_t *bitmap, uint64_t bitmap_bytes, void *ws,
@@ -121,7 +123,7 @@ hipError_t launch_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off,
     if (bitmap_bytes == 0) return hipSuccess;
     if (n == 0 || num_probes == 0) return hipMemsetAsync(bitmap, 0, bitmap_bytes, st);
     BloomPlan pl = bloom_plan(n, num_probes, bitmap_bytes);
-    if (!ws || !bloom_plan_fits(pl, n) || bloom_fill_lds(pl) > 64 * 1024) {
+    if (!ws || !bloom_plan_fits(pl)) {
         // no workspace (or a plan the binning cannot hold): device-scope atomics into the bitmap
         hipError_t e = hipMemsetAsync(bitmap, 0, bitmap_bytes, st);
         if (e != hipSuccess) return e;
@@ -134,13 +136,11 @@ hipError_t launch_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off,
     static bool attrs = false;
     if (!attrs) {
         hipFuncSetAttribute((const void *)k_bloom_bin, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLds);
-        hipFuncSetAttribute((const void *)k_bloom_fill, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+        hipFuncSetAttribute((const void *)k_bloom_fill, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
         (void)hipGetLastError();  // an unsupported attribute value must not poison the launch status
         attrs = true;
     }
-    const BloomQueues q = bloom_queues(ws, n, pl);
-    hipError_t e = hipMemsetAsync(q.cursor, 0, (size_t)(pl.nslices * kShards + 1) * 4, st);
-    if (e != hipSuccess) return e;
+    const BloomSlots q = bloom_slots(ws, pl);
     hipLaunchKernelGGL(k_bloom_bin, dim3(pl.tiles), dim3(kBinThreads), bloom_bin_lds(pl), st, key_bytes, key_off, n, pl, q);
     hipLaunchKernelGGL(k_bloom_fill, dim3(pl.nslices), dim3(kFillThreads), bloom_fill_lds(pl), st, key_bytes, key_off, n, pl,
                        q, bitmap, bitmap_bytes);
@@ -159,4 +159,14 @@ hipError_t launch_bloom_query(const uint8_t *bitmap, uint64_t bitmap_bytes, uint
     return hipGetLastError();
 }
 
+}  // namespace sdb
+
+namespace sdb {
+// The encode workspace serves either build: the fused one (tiles = k_seg's chunks) or the standalone
+// kernels (sdb_encode_sst falls back to them when the fused plan does not fit).
+uint64_t encode_bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes) {
+    const uint64_t a = bloom_workspace_bytes(n, k, bitmap_bytes);
+    const uint64_t b = bloom_slots_bytes(bloom_plan(n, k, bitmap_bytes, kChunk));
+    return a > b ? a : b;
+}
 }  // namespace sdb

@@ -17,11 +17,14 @@ constexpr uint32_t kKeyStageCap = 1024;      // key staging per wave
 constexpr uint32_t kSegLook = 1024;           // k_seg: max lookahead entries staged past the chunk
 constexpr uint32_t kSegSpan = kChunk + kSegLook;
 constexpr uint32_t kSegThreads = 1024;
+constexpr uint32_t kFactsThreads = 256;       // k_facts: one entry per thread
 constexpr uint32_t kSegLds = (3 * kSegSpan + 4) * 4 + kChunk * 6;
+constexpr uint32_t kSegLdsMax = 64 * 1024;          // k_seg's LDS with the fused bloom binning
+constexpr uint32_t kHashPerT = kChunk / kSegThreads;  // chunk entries (hashes) per k_seg thread
 constexpr uint32_t kEmitThreads = 1024;      // 16 waves per workgroup (two blocks in flight each), 1 per CU
 constexpr uint32_t kEmitWgPerCu = 1;
 constexpr uint32_t kEmitWaveLds = kStageGuard + kImgCap + 16 + kKeyStageCap + 64 * 16;  // guard, image, key stage, spans
-constexpr uint32_t kEmitLds = kCrcLds + (kEmitThreads / 64) * kEmitWaveLds;
+constexpr uint32_t kEmitLds = kCrcLds + 16 + (kEmitThreads / 64) * kEmitWaveLds;  // tables, ticket, waves
 constexpr uint32_t kEnumLds = kChunk * 16 + 12 * kChunk * 2;  // block list + 12 lifting levels
 constexpr uint32_t kEnumTabLds = 12 * kChunk * 2;  // k_enum's table walk (aliases the lifting levels)
 constexpr uint32_t kGroupThreads = 1024;
@@ -35,9 +38,9 @@ struct BloomPlan {
     uint32_t nslices, T, tiles;
     uint64_t mmod;        // Lemire fastmod constant: floor((2^64 - 1) / m) + 1
 };
-struct BloomQueues {
-    uint32_t *cursor;  // nslices * kShards (+1: the overflow flag)
-    uint32_t *queue;   // (nslices * kShards) x cap probes
+struct BloomSlots {
+    uint32_t *count;  // tiles x nslices: run length of each (tile, slice) slot (kSlotOverflow: too long)
+    uint32_t *slot;   // (nslices x tiles) x cap probes, slice-major
     uint32_t cap;
 };
 
@@ -68,6 +71,9 @@ struct EncodeArgs {
     uint32_t seg_look;      // lookahead entries staged by k_seg (covers the longest possible block)
     // workspace
     uint32_t *lcp;
+    uint32_t *szr, *sznr;   // per entry (k_facts): restart-row size, non-restart size (V1: both the row size)
+    uint64_t *hd;           // per entry (k_facts, fused bloom): h0 | d0 << 32, first probe and step
+    uint32_t nfacts;        // k_facts workgroups (partials: stat_part / err_part are per facts workgroup)
     uint32_t *row_scratch;  // per entry: row offsets of slow-path blocks
     uint32_t *next;
     uint32_t *bbytes;
@@ -82,22 +88,22 @@ struct EncodeArgs {
     uint32_t *slow_count;
     uint32_t *slow_list;
     BlockDesc *desc;
-    uint64_t *stat_part;    // per chunk: raw key, raw val, puts, deletes, merges
+    uint64_t *stat_part;    // per k_facts workgroup: raw key, raw val, puts, deletes, merges
     uint32_t *wmax_part;    // per chunk: longest candidate block (entries)
-    unsigned long long *err_part;  // per chunk: min (entry << 8 | code) of k_seg's checks (~0: none)
+    unsigned long long *err_part;  // per k_facts workgroup: min (entry << 8 | code) of the checks (~0: none)
     uint32_t *gtab_exit;    // per group of kGroup chunks, seg_look candidates: composed transfer table
     uint32_t *gtab_cnt;
     uint64_t *gtab_bytes;
     uint32_t *mode;         // k_group -> k_enum: 1 = compose the tables, 0 = anchors were walked
     uint32_t group;         // chunks per group (host: ~sqrt(nchunks))
-    // bloom fused into the encode: k_seg hashes (-> hd), k_group bins, k_enum fills
+    // bloom fused into the encode: k_seg hashes and bins each chunk (tile = chunk), k_enum fills
     uint32_t bloom_fused;
-    uint64_t *hd;           // per entry: h0 | d0 << 32 (first probe, first step)
     BloomPlan bpl;
-    BloomQueues bq;
+    BloomSlots bq;
     uint8_t *bloom_out;
     uint32_t *done;         // k_emit workgroups finished (the last one writes the summary)
     uint32_t nprep_wg;
+    uint32_t seg_lds;       // k_seg's dynamic LDS bytes
     // outputs (device)
     uint8_t *out_data;
     uint64_t *out_block_off;
@@ -112,12 +118,13 @@ struct EncodeArgs {
 
 // Workspace layout for n entries (all offsets 256-byte aligned).
 struct EncodeWorkspace {
-    uint64_t lcp, row_scratch, next, bbytes, tab_exit, tab_cnt, tab_bytes;
+    uint64_t lcp, szr, sznr, hd, row_scratch, next, bbytes, tab_exit, tab_cnt, tab_bytes;
     uint64_t anchor_e, anchor_blk, anchor_byte, err, wmax, slow_count, slow_list, desc, stat_part, wmax_part, bloom_rep;
-    uint64_t err_part, done, gtab_exit, gtab_cnt, gtab_bytes, mode, hd;
+    uint64_t err_part, done, gtab_exit, gtab_cnt, gtab_bytes, mode;
     uint64_t total;
 };
 uint64_t bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
+uint64_t encode_bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
 inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes, uint32_t num_probes) {
     EncodeWorkspace w{};
     uint64_t off = 0;
@@ -128,6 +135,9 @@ inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes
     };
     uint64_t nc = (n + kChunk - 1) / kChunk;
     w.lcp = take(4 * (n + 1));
+    w.szr = take(4 * (n + 1));
+    w.sznr = take(4 * (n + 1));
+    w.hd = take(filter_bytes ? 8 * (n + 1) : 0);
     w.row_scratch = take(4 * (n + 1));
     w.next = take(4 * (n + 1));
     w.bbytes = take(4 * (n + 1));
@@ -142,16 +152,16 @@ inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes
     w.slow_count = take(4);
     w.slow_list = take(4 * (n + 1));
     w.desc = take(sizeof(BlockDesc) * (n + 1));
-    w.stat_part = take(8 * 5 * (nc + 1));
+    const uint64_t nf = (n + kFactsThreads - 1) / kFactsThreads;
+    w.stat_part = take(8 * 5 * (nf + 1));
     w.wmax_part = take(4 * (nc + 1));
-    w.err_part = take(8 * (nc + 1));
+    w.err_part = take(8 * (nf + 1));
     w.done = take(4);
     w.gtab_exit = take(4 * (nc * kSegLook + 1));  // one table per group (<= one per chunk)
     w.gtab_cnt = take(4 * (nc * kSegLook + 1));
     w.gtab_bytes = take(8 * (nc * kSegLook + 1));
     w.mode = take(4);
-    w.hd = take(filter_bytes ? 8 * (n + 1) : 0);
-    w.bloom_rep = take(filter_bytes ? bloom_workspace_bytes(n, num_probes, filter_bytes) : 0);  // bloom buckets
+    w.bloom_rep = take(filter_bytes ? encode_bloom_workspace_bytes(n, num_probes, filter_bytes) : 0);  // bloom slots
     w.total = off;
     return w;
 }
@@ -159,13 +169,14 @@ inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes
 hipError_t launch_encode(EncodeArgs a, hipStream_t st);
 
 // stage timing (diagnostics)
-enum Stage { kStBloom = 0, kStSeg, kStResolve, kStEnum, kStEmit, kStEmitSlow, kNumStages };
+enum Stage { kStBloom = 0, kStFacts, kStSeg, kStGroup, kStEnum, kStEmit, kStEmitSlow, kNumStages };
 void stage_mark(hipStream_t st, int stage, bool begin);
 bool stage_timing_on();
 
 // bloom (sdb_bloom.hip)
 
-BloomPlan bloom_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
+// tile_keys: keys per binning tile (0: the standalone build's choice; the fused encode bins per chunk)
+BloomPlan bloom_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes, uint32_t tile_keys = 0);
 uint64_t bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
 // ws: bloom_workspace_bytes(...) of scratch, or NULL (device-scope atomics; slow)
 hipError_t launch_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,

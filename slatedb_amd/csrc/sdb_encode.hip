@@ -33,6 +33,9 @@ namespace sdb {
 // Phase timestamps (diagnostic builds with -DSDB_PHASE_TIMING): per workgroup of the instrumented
 // kernel, s_memtime at each phase mark of thread 0 -> g_phase[blockIdx][mark].  A mark adds its own
 // barrier in timing builds only: it never stands in for a barrier the algorithm needs.
+#ifndef SDB_SEG_WAVES
+#define SDB_SEG_WAVES 8
+#endif
 #ifdef SDB_PHASE_TIMING
 __device__ uint64_t g_phase[1024][8];
 #define PHASE_MARK(i)                                                              \
@@ -173,6 +176,111 @@ SDB_DEV EntryFacts entry_facts(const EncodeArgs &a, uint64_t i) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// K0 facts: one thread per entry (a lean, high-occupancy pass, so the loads of many entries are in
+// flight per CU): LCP vs the previous key, restart / non-restart row sizes, reference errors, SstStats
+// partials per workgroup and, for the fused bloom, filter_hash (filter.rs:196-204) reduced to the
+// first probe and step.  Lanes hold consecutive entries: the next entry's offsets and the previous
+// key's first 16 bytes come from the neighbour lane by DPP (lane 63 / lane 0 load their own).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kFactsThreads) void k_facts(EncodeArgs a) {
+    __shared__ uint64_t s_part[kFactsThreads / 64][5];
+    __shared__ unsigned long long s_err[kFactsThreads / 64];
+    const uint32_t tid = threadIdx.x, lane = (uint32_t)lane_id();
+    const uint64_t e = (uint64_t)blockIdx.x * kFactsThreads + tid;
+    const uint64_t n = a.n;
+    FactsIn in;
+    in.ko0 = in.ko1 = in.vo0 = in.vo1 = in.pko = 0;
+    in.kd = in.m = 0;
+    if (e <= n) {
+        in.ko0 = a.key_off[e];
+        in.vo0 = a.val_off[e];
+        if (e < n) {
+            in.kd = a.kind ? a.kind[e] : 0;
+            in.m = a.ts_mask ? a.ts_mask[e] : 0;
+            if (lane == 63) {
+                in.ko1 = a.key_off[e + 1];
+                in.vo1 = a.val_off[e + 1];
+            }
+            if (lane == 0 && e > 0) in.pko = a.key_off[e - 1];
+        }
+    }
+    {
+        const uint64_t nk = wave_next_lane(in.ko0), nv = wave_next_lane(in.vo0);
+        if (lane != 63) {
+            in.ko1 = nk;
+            in.vo1 = nv;
+        }
+    }
+    in.ck0 = in.ck1 = in.pk0 = in.pk1 = 0;
+    if (e < n) {
+        const uint64_t kl = in.ko1 - in.ko0;
+        const uint32_t kn = (uint32_t)(kl < 16 ? kl : 16);
+        if (kn) in.ck0 = load8(a.key_bytes + in.ko0, kn < 8 ? kn : 8);
+        if (kn > 8) in.ck1 = load8(a.key_bytes + in.ko0 + 8, kn - 8);
+        if (lane == 0 && e > 0) {
+            const uint64_t pl = in.ko0 - in.pko;
+            const uint32_t pn = (uint32_t)(pl < 16 ? pl : 16);
+            if (pn) in.pk0 = load8(a.key_bytes + in.pko, pn < 8 ? pn : 8);
+            if (pn > 8) in.pk1 = load8(a.key_bytes + in.pko + 8, pn - 8);
+        }
+    }
+    {
+        const uint64_t pko = wave_prev_lane(in.ko0), pk0 = wave_prev_lane(in.ck0), pk1 = wave_prev_lane(in.ck1);
+        if (lane != 0) {
+            in.pko = pko;
+            in.pk0 = pk0;
+            in.pk1 = pk1;
+        } else if (e == 0) {
+            in.pko = in.ko0;
+        }
+    }
+    uint64_t rk = 0, rv = 0, c = 0;
+    uint64_t err = ~0ull;
+    if (e < n) {
+        const EntryFacts f = facts_finish(a, e, in);
+        a.lcp[e] = f.lcp;
+        a.szr[e] = f.s_r;
+        a.sznr[e] = f.s_nr;
+        if (a.bloom_fused) {
+            const uint64_t kl = in.ko1 - in.ko0;
+            const uint64_t h = kl == 16 ? siphash13_16(in.ck0, in.ck1) : siphash13(a.key_bytes + in.ko0, kl);
+            a.hd[e] = (uint64_t)fastmod_u32((uint32_t)h, a.bpl.mmod, a.bpl.m) |
+                      ((uint64_t)fastmod_u32((uint32_t)(h >> 32), a.bpl.mmod, a.bpl.m) << 32);
+        }
+        if (f.err) err = (e << 8) | (uint64_t)f.err;
+        rk = f.klen;
+        rv = f.vlen;
+        c = (uint64_t)(f.kind == SDB_KIND_VALUE) | ((uint64_t)(f.kind == SDB_KIND_TOMBSTONE) << 20) |
+            ((uint64_t)(f.kind == SDB_KIND_MERGE) << 40);
+    }
+    // SstStats (sst_builder.rs:225-226, 315-317) and the first error: per-workgroup partials
+    rk = wave_sum(rk);
+    rv = wave_sum(rv);
+    c = wave_sum(c);
+    err = wave_readlane(wave_incl_scan_op(err, [](uint64_t x, uint64_t y) { return x < y ? x : y; }), 63);
+    const uint32_t w = tid >> 6;
+    if (lane == 0) {
+        s_part[w][0] = rk;
+        s_part[w][1] = rv;
+        s_part[w][2] = c & 0xFFFFF;
+        s_part[w][3] = (c >> 20) & 0xFFFFF;
+        s_part[w][4] = (c >> 40) & 0xFFFFF;
+        s_err[w] = err;
+    }
+    __syncthreads();
+    if (tid < 5) {
+        uint64_t t = 0;
+        for (uint32_t q = 0; q < kFactsThreads / 64; q++) t += s_part[q][tid];
+        a.stat_part[5 * (uint64_t)blockIdx.x + tid] = t;
+    }
+    if (tid == 0) {
+        unsigned long long m = ~0ull;
+        for (uint32_t q = 0; q < kFactsThreads / 64; q++) m = s_err[q] < m ? s_err[q] : m;
+        a.err_part[blockIdx.x] = m;  // every workgroup writes its slot: no initialisation needed
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // K1 seg: one workgroup per chunk of kChunk entries, plus a lookahead of seg_look entries (the
 // longest block a chunk entry can start) staged in LDS.
 //   a. entry facts for the staged span: LCP, errors and stats of the chunk's own entries; row sizes
@@ -193,21 +301,15 @@ SDB_DEV uint32_t walk_size_v2(const EncodeArgs &a, uint64_t j, bool rs) {
     return rs ? f.s_r : f.s_nr;
 }
 
-__global__ __launch_bounds__(kSegThreads, 8) void k_seg(EncodeArgs a) {
+__global__ __launch_bounds__(kSegThreads, SDB_SEG_WAVES) void k_seg(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t *s_r = (uint32_t *)smem;          // kSegSpan: true restart-row sizes (V1: row sizes)
     uint32_t *s_P = s_r + kSegSpan;            // kSegSpan + 4: prefix of clamped non-restart sizes
     uint32_t *s_R = s_P + kSegSpan + 4;        // kSegSpan: restart surcharge of each entry
     uint32_t *s_bb = s_R + kSegSpan;           // kChunk: encoded block bytes for blocks starting here
     uint16_t *s_nx = (uint16_t *)(s_bb + kChunk);  // kChunk: next(b) - cs (0xFFFF: out of range)
-    __shared__ uint64_t s_part[kSegThreads / 64][5];
     __shared__ uint32_t s_len[kSegThreads / 64];
-    __shared__ unsigned long long s_err;
     const uint32_t k = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-    if (tid == 0) s_err = ~0ull;
-    __syncthreads();
-    if (a.bloom_fused && k == 0)  // the bloom queue cursors for k_group's binning
-        for (uint32_t i = tid; i <= a.bpl.nslices * kShards; i += nt) a.bq.cursor[i] = 0;
     const uint64_t cs = (uint64_t)k * kChunk;
     const uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
     const uint64_t se = ce + a.seg_look < a.n ? ce + a.seg_look : a.n;
@@ -219,109 +321,37 @@ __global__ __launch_bounds__(kSegThreads, 8) void k_seg(EncodeArgs a) {
     const bool v2 = a.version == 2 && bs <= (1u << 20);
     const uint32_t ri = a.restart_interval;
     PHASE_MARK(0);
-    // a. facts
-    uint64_t rk = 0, rv = 0;
-    uint32_t puts = 0, dels = 0, merges = 0;
-    // lanes hold consecutive entries.  Two rounds of loads: (1) the entry's and the next entry's
-    // offsets (lane 0 also the previous key's offset), kind, ts mask; (2) the first 16 bytes of the
-    // key (lane 0 also of the previous key).  The previous key's prefix of lanes 1..63 comes from the
-    // neighbour lane (DPP).
+    // a. row sizes of the staged span (k_facts) and, for the fused bloom, the chunk's (h0, d0)
     constexpr uint32_t kPerT = kSegSpan / kSegThreads;
-    FactsIn fin[kPerT];
     const uint32_t lane = (uint32_t)lane_id();
+    uint32_t zr[kPerT], znr[kPerT];
+    uint64_t hdv[kHashPerT];
 #pragma unroll
     for (uint32_t u = 0; u < kPerT; u++) {
         const uint32_t x = tid + u * nt;
-        FactsIn &in = fin[u];
-        in.ko0 = in.ko1 = in.vo0 = in.vo1 = in.pko = 0;
-        in.kd = in.m = 0;
+        zr[u] = znr[u] = 0;
         if (x < sn) {
-            const uint64_t e = cs + x;
-            in.ko0 = a.key_off[e];
-            in.ko1 = a.key_off[e + 1];
-            in.vo0 = a.val_off[e];
-            in.vo1 = a.val_off[e + 1];
-            in.kd = a.kind ? a.kind[e] : 0;
-            in.m = a.ts_mask ? a.ts_mask[e] : 0;
-            if (lane == 0 && e > 0) in.pko = a.key_off[e - 1];
+            zr[u] = a.szr[cs + x];
+            znr[u] = a.sznr[cs + x];
         }
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kHashPerT; r++) {
+        const uint32_t x = tid + r * nt;
+        hdv[r] = (a.bloom_fused && x < cn) ? a.hd[cs + x] : 0;
     }
 #pragma unroll
     for (uint32_t u = 0; u < kPerT; u++) {
         const uint32_t x = tid + u * nt;
-        FactsIn &in = fin[u];
-        in.ck0 = in.ck1 = in.pk0 = in.pk1 = 0;
-        if (x < sn) {
-            const uint64_t kl = in.ko1 - in.ko0;
-            const uint32_t n = (uint32_t)(kl < 16 ? kl : 16);
-            if (n) in.ck0 = load8(a.key_bytes + in.ko0, n < 8 ? n : 8);
-            if (n > 8) in.ck1 = load8(a.key_bytes + in.ko0 + 8, n - 8);
-            if (lane == 0 && cs + x > 0) {
-                const uint64_t pl = in.ko0 - in.pko;
-                const uint32_t pn = (uint32_t)(pl < 16 ? pl : 16);
-                if (pn) in.pk0 = load8(a.key_bytes + in.pko, pn < 8 ? pn : 8);
-                if (pn > 8) in.pk1 = load8(a.key_bytes + in.pko + 8, pn - 8);
-            }
-        }
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < kPerT; u++) {
-        const uint32_t x = tid + u * nt;
-        const uint64_t e = cs + x;
-        FactsIn &in = fin[u];
-        const uint64_t pko = wave_prev_lane(in.ko0), pk0 = wave_prev_lane(in.ck0), pk1 = wave_prev_lane(in.ck1);
-        if (lane != 0) {
-            in.pko = pko;
-            in.pk0 = pk0;
-            in.pk1 = pk1;
-        } else if (e == 0) {
-            in.pko = in.ko0;
-        }
         if (x >= sn) continue;
-        EntryFacts f = facts_finish(a, e, in);
-        s_r[x] = f.s_r;
+        s_r[x] = zr[u];
         if (v2) {
-            const uint32_t cr = f.s_r < clampv ? f.s_r : clampv, cnr = f.s_nr < clampv ? f.s_nr : clampv;
+            const uint32_t cr = zr[u] < clampv ? zr[u] : clampv, cnr = znr[u] < clampv ? znr[u] : clampv;
             s_P[x] = cnr;
             s_R[x] = cr + 2 - cnr;  // restart row: restart size + its 2-byte offset, instead of cnr
         }
-        if (a.bloom_fused && e < ce) {  // filter_hash (filter.rs:196-204) -> first probe / step
-            const uint64_t kl = in.ko1 - in.ko0;
-            const uint64_t h = kl == 16 ? siphash13_16(in.ck0, in.ck1) : siphash13(a.key_bytes + in.ko0, kl);
-            a.hd[e] = (uint64_t)fastmod_u32((uint32_t)h, a.bpl.mmod, a.bpl.m) |
-                      ((uint64_t)fastmod_u32((uint32_t)(h >> 32), a.bpl.mmod, a.bpl.m) << 32);
-        }
-        if (e < ce) {
-            a.lcp[e] = f.lcp;
-            if (f.err) atomicMin(&s_err, (unsigned long long)((e << 8) | (uint64_t)f.err));
-            rk += f.klen;
-            rv += f.vlen;
-            puts += f.kind == SDB_KIND_VALUE;
-            merges += f.kind == SDB_KIND_MERGE;
-            dels += f.kind == SDB_KIND_TOMBSTONE;
-        }
-    }
-    // SstStats (sst_builder.rs:225-226, 315-317): per-chunk partials, summed in k_resolve
-    {
-        rk = wave_sum(rk);
-        rv = wave_sum(rv);
-        uint64_t c = wave_sum((uint64_t)puts | ((uint64_t)dels << 20) | ((uint64_t)merges << 40));
-        if (lane_id() == 0) {
-            uint32_t w = tid >> 6;
-            s_part[w][0] = rk;
-            s_part[w][1] = rv;
-            s_part[w][2] = c & 0xFFFFF;
-            s_part[w][3] = (c >> 20) & 0xFFFFF;
-            s_part[w][4] = (c >> 40) & 0xFFFFF;
-        }
     }
     __syncthreads();
-    if (tid < 5) {
-        uint64_t t = 0;
-        for (uint32_t q = 0; q < nt / 64; q++) t += s_part[q][tid];
-        a.stat_part[5 * (uint64_t)k + tid] = t;
-    }
-    if (tid == 0) a.err_part[k] = s_err;  // every chunk writes its slot: no initialisation needed
     PHASE_MARK(1);
     // b. P = exclusive prefix of the clamped non-restart sizes (V2): one block scan of the three
     //    strided rows (entry x = tid + u * nt); the restart surcharges stay per entry (s_R)
@@ -487,6 +517,18 @@ __global__ __launch_bounds__(kSegThreads, 8) void k_seg(EncodeArgs a) {
         a.tab_bytes[t] = by;
     }
     PHASE_MARK(5);
+    // e. bloom: the chunk's probes -> its slots (tile = chunk); the staged sizes above are dead
+    if (a.bloom_fused) {
+        uint32_t hh[kHashPerT], dd[kHashPerT];
+#pragma unroll
+        for (uint32_t r = 0; r < kHashPerT; r++) {
+            hh[r] = (uint32_t)hdv[r];
+            dd[r] = (uint32_t)(hdv[r] >> 32);
+        }
+        __syncthreads();
+        bloom_bin_core<kHashPerT>(k, hh, dd, cn, a.bpl, a.bq, (uint32_t *)smem);
+    }
+    PHASE_MARK(6);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -505,10 +547,6 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(EncodeArgs a) {
     __shared__ unsigned long long s_err;
     __shared__ uint64_t s_stat[5][kGroupThreads / 64];
     const uint32_t K = a.nchunks, g = blockIdx.x, G = a.group, ngroups = (K + G - 1) / G;
-    if (g >= ngroups) {  // bloom role: bin one tile of k_seg's (h0, d0) into the slice queues
-        bloom_bin_tile<true>(g - ngroups, nullptr, nullptr, a.hd, a.n, a.bpl, a.bq, (uint32_t *)smem);
-        return;
-    }
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     if (tid == 0) {
         s_W = 0;
@@ -522,7 +560,9 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(EncodeArgs a) {
         for (uint32_t q = tid; q < K; q += nt) {
             const uint32_t w = a.wmax_part[q];
             m = w > m ? w : m;
-            if (g == 0) {
+        }
+        if (g == 0) {
+            for (uint32_t q = tid; q < a.nfacts; q += nt) {
                 const unsigned long long ep = a.err_part[q];
                 em = ep < em ? ep : em;
 #pragma unroll
@@ -768,7 +808,7 @@ __global__ __launch_bounds__(kEnumThreads) void k_enum(EncodeArgs a) {
     __shared__ uint64_t s_anc[4];  // entry point, first block, first byte, blocks of this chunk
     const uint32_t k = blockIdx.x, K = a.nchunks;
     if (k >= K) {  // bloom role: OR one slice's queued probes into LDS, write the slice
-        bloom_fill_slice(k - K, nullptr, nullptr, a.hd, a.n, a.bpl, a.bq, a.bloom_out, a.bloom_len, (uint32_t *)smem);
+        bloom_fill_slice(k - K, a.key_bytes, a.key_off, a.n, a.bpl, a.bq, a.bloom_out, a.bloom_len, (uint32_t *)smem);
         return;
     }
     if (*a.err != ~0ull) return;
@@ -1467,6 +1507,8 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(EncodeArgs a) {
 #endif
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), wpb = blockDim.x >> 6;
     const uint32_t gw = blockIdx.x * wpb + wave, G = gridDim.x * wpb;
+    (void)gw;
+    (void)G;
     const uint32_t l = (uint32_t)lane_id();
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     bool run = *a.err == ~0ull;  // any earlier error (incl. capacity): write nothing
@@ -1480,33 +1522,50 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(EncodeArgs a) {
         for (uint32_t q = threadIdx.x; q < 4 * 256; q += blockDim.x) crc[8 * 256 + q] = (&c_mul256.t[0][0])[q];
         for (uint32_t q = threadIdx.x; q < kTreeSteps * 4 * 256; q += blockDim.x) crc[12 * 256 + q] = (&g_tree.t[0][0][0])[q];
         __syncthreads();
-        emit_slow_blocks<V>(a, (uint8_t *)smem + kCrcLds, (const uint32_t(*)[256])smem);
+        emit_slow_blocks<V>(a, (uint8_t *)smem + kCrcLds + 16, (const uint32_t(*)[256])smem);
+        __syncthreads();
+        if (threadIdx.x == 0) *(lu32 *)(smem + kCrcLds) = blockDim.x >> 6;  // block ticket (first blocks: r0 + wave)
         __syncthreads();
         const uint32_t nb = a.anchor_blk[a.nchunks];
-        lu8 *wbase = (lu8 *)smem + kCrcLds + wave * kEmitWaveLds;
+        lu8 *wbase = (lu8 *)smem + kCrcLds + 16 + wave * kEmitWaveLds;
         lu8 *img = wbase + kStageGuard;
         lu8 *kst = img + kImgCap + 16;
         lSpanCopy *rtab = (lSpanCopy *)(kst + kKeyStageCap);
         const uint32_t *dw = (const uint32_t *)a.desc;
-        uint32_t blk = gw;
-        if (blk < nb) {
-            // prologue: block gw's descriptor, its prefetch, and block gw + G's descriptor
+        // schedule: workgroup b owns an equal share [r0, r1) of the blocks; its waves start on blocks
+        // r0 + wave and then take the rest in order from an LDS ticket, so a wave that runs fast takes
+        // more (per-block times vary with the memory traffic around them)
+        const uint32_t r0 = (uint32_t)((uint64_t)nb * blockIdx.x / gridDim.x);
+        const uint32_t r1 = (uint32_t)((uint64_t)nb * (blockIdx.x + 1) / gridDim.x);
+        lu32 *ticket = (lu32 *)(smem + kCrcLds);
+        auto take = [&]() -> uint32_t {
+            uint32_t t = 0;
+            if (l == 0) t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return r0 + (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+        };
+        uint32_t blk = r0 + wave;
+        if (blk < r1) {
+            // prologue: the first block's descriptor and prefetch, and the next block's descriptor
             BlockDesc dn = desc_from_lanes(l < 14 ? dw[14 * (uint64_t)blk + l] : 0);
             EmitPre pn;
             bool fn = emit_fast(dn);
             if (fn) emit_prefetch(a, dn, pn);
-            uint32_t dv = (blk + G < nb && l < 14) ? dw[14 * (uint64_t)(blk + G) + l] : 0;
-            for (; blk < nb; blk += G) {
+            uint32_t nblk = take();
+            uint32_t dv = (nblk < r1 && l < 14) ? dw[14 * (uint64_t)nblk + l] : 0;
+            while (blk < r1) {
                 const BlockDesc d = dn;
                 const EmitPre p = pn;
                 const bool fast = fn;
-                if (blk + G < nb) {  // issue block blk + G (and blk + 2G's descriptor)
+                const uint32_t cur = blk;
+                blk = nblk;
+                if (blk < r1) {  // issue the next block (and the descriptor of the one after it)
                     dn = desc_from_lanes(dv);
                     fn = emit_fast(dn);
                     if (fn) emit_prefetch(a, dn, pn);
-                    dv = (blk + 2 * G < nb && l < 14) ? dw[14 * (uint64_t)(blk + 2 * G) + l] : 0;
+                    nblk = take();
+                    dv = (nblk < r1 && l < 14) ? dw[14 * (uint64_t)nblk + l] : 0;
                 }
-                if (fast) emit_block<V>(a, blk, d, p, img, kst, rtab, crc, ph);  // slow blocks: done above
+                if (fast) emit_block<V>(a, cur, d, p, img, kst, rtab, crc, ph);  // slow blocks: done above
             }
         }
     }
@@ -1751,7 +1810,7 @@ static bool lds_attrs_set = false;
 static int g_cus = 0;
 static uint32_t g_emit_threads = kEmitThreads, g_emit_wg_per_cu = kEmitWgPerCu;
 static uint32_t emit_grid() { return (uint32_t)(g_cus > 0 ? g_emit_wg_per_cu * g_cus : 512); }
-static uint32_t emit_lds() { return kCrcLds + (g_emit_threads / 64) * kEmitWaveLds; }
+static uint32_t emit_lds() { return kCrcLds + 16 + (g_emit_threads / 64) * kEmitWaveLds; }
 static void set_lds_attrs() {
     if (lds_attrs_set) return;
     int dev = 0;
@@ -1769,8 +1828,8 @@ static void set_lds_attrs() {
     hipFuncSetAttribute((const void *)k_emit<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
     hipFuncSetAttribute((const void *)k_emit<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
     hipFuncSetAttribute((const void *)k_enum, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEnumLds);
-    hipFuncSetAttribute((const void *)k_group, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLds);
-    hipFuncSetAttribute((const void *)k_seg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLds);
+    hipFuncSetAttribute((const void *)k_group, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGroupLds);
+    hipFuncSetAttribute((const void *)k_seg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLdsMax);
     lds_attrs_set = true;
 }
 
@@ -1782,14 +1841,19 @@ hipError_t launch_encode(EncodeArgs a, hipStream_t st) {
         return hipGetLastError();
     }
     a.nprep_wg = a.nchunks;
+    a.nfacts = (uint32_t)((a.n + kFactsThreads - 1) / kFactsThreads);
+    a.seg_lds = kSegLds;
+    if (a.bloom_fused && bloom_bin_lds(a.bpl) > a.seg_lds) a.seg_lds = (uint32_t)bloom_bin_lds(a.bpl);
+    stage_mark(st, kStFacts, true);
+    hipLaunchKernelGGL(k_facts, dim3(a.nfacts), dim3(kFactsThreads), 0, st, a);
+    stage_mark(st, kStFacts, false);
     stage_mark(st, kStSeg, true);
-    hipLaunchKernelGGL(k_seg, dim3(a.nchunks), dim3(kSegThreads), kSegLds, st, a);
+    hipLaunchKernelGGL(k_seg, dim3(a.nchunks), dim3(kSegThreads), a.seg_lds, st, a);
     stage_mark(st, kStSeg, false);
-    stage_mark(st, kStResolve, true);
+    stage_mark(st, kStGroup, true);
     const uint32_t ngroups = (a.nchunks + a.group - 1) / a.group;
-    const size_t glds = a.bloom_fused && bloom_bin_lds(a.bpl) > kGroupLds ? bloom_bin_lds(a.bpl) : kGroupLds;
-    hipLaunchKernelGGL(k_group, dim3(ngroups + (a.bloom_fused ? a.bpl.tiles : 0)), dim3(kGroupThreads), glds, st, a);
-    stage_mark(st, kStResolve, false);
+    hipLaunchKernelGGL(k_group, dim3(ngroups), dim3(kGroupThreads), kGroupLds, st, a);
+    stage_mark(st, kStGroup, false);
     stage_mark(st, kStEnum, true);
     hipLaunchKernelGGL(k_enum, dim3(a.nchunks + (a.bloom_fused ? a.bpl.nslices : 0)), dim3(kEnumThreads), kEnumLds, st, a);
     stage_mark(st, kStEnum, false);

@@ -281,9 +281,9 @@ def test_device_round_trip_full_d1(rt):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [5000, 100000, datasets.D1_N])
-def test_bloom_queues_do_not_overflow(rt, n):
-    """The fused bloom's slice queues are sized for uniform probes: D1-shaped batches must take the
-    queued fill (no overflow flag), not the rebuild-from-hashes fallback."""
+def test_bloom_slots_do_not_overflow(rt, n):
+    """The fused bloom's (tile, slice) slots are sized for uniform probes: D1-shaped batches must take
+    the slotted fill (no overflowing run), not the rebuild-from-keys fallback."""
     import ctypes as C
     import torch
     runtime = rt
@@ -296,14 +296,10 @@ def test_bloom_queues_do_not_overflow(rt, n):
     ref = O.encode_sst(b, O.params(block_size=4096, sst_version=2, bloom_bits_per_key=10))
     assert np.array_equal(got["bloom"], ref.bloom)
     cd = C.CDLL(runtime.LIB_PATH)
-    cd.sdb_diag_bloom_ws_offset.restype = C.c_uint64
-    cd.sdb_diag_bloom_ws_offset.argtypes = [C.c_uint64, C.c_void_p]
-    off = (cd.sdb_diag_bloom_ws_offset(b.n, C.byref(prm)) + 255) // 256 * 256
-    fb = (n * 10 + 7) // 8
-    sb = 15
-    while sb < 19 and -(-fb * 8 // (1 << sb)) > 256:
-        sb += 1
-    nslices = -(-fb * 8 // (1 << sb))
-    cur = out.workspace[off: off + 4 * (nslices * 8 + 1)].cpu().numpy().view(np.uint32)
-    assert cur[nslices * 8] == 0, "bloom queue overflow flag set"
-    assert int(cur[: nslices * 8].sum()) == n * 6
+    cd.sdb_diag_bloom_slots.restype = C.c_uint64
+    cd.sdb_diag_bloom_slots.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    tiles, nsl, cap = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    off = cd.sdb_diag_bloom_slots(b.n, C.byref(prm), C.byref(tiles), C.byref(nsl), C.byref(cap))
+    cnt = out.workspace[off: off + 4 * tiles.value * nsl.value].cpu().numpy().view(np.uint32)
+    assert (cnt <= cap.value).all(), "a bloom slot overflowed"
+    assert int(cnt.sum()) == n * 6
