@@ -65,3 +65,12 @@ assert cdll.sdb_diag_enum_phase(C.addressof(eb), 1024) == 0
 t = np.frombuffer(eb, dtype=np.uint64).reshape(1024, 8)[:nb].astype(np.int64)
 d = np.diff(t[:, :6], axis=1)
 print("k_enum phases (ticks) mean/max: " + "  ".join("%d->%d %.0f/%.0f" % (i, i + 1, d[:, i].mean(), d[:, i].max()) for i in range(5)))
+
+# per-workgroup end time of k_emit (max over its waves), grouped by workgroup % 8 (XCD round-robin)
+wpb = 16
+nwg = len(r) // wpb
+wend = en[: nwg * wpb].reshape(nwg, wpb).max(axis=1)
+print("k_emit workgroup end (us) by wg%%8: " + "  ".join("%d:%.1f/%.1f" % (x, np.median(wend[x::8]), wend[x::8].max()) for x in range(8)))
+print("k_emit workgroup end (us) percentiles p0 %.1f p10 %.1f p50 %.1f p90 %.1f p100 %.1f" % tuple(np.percentile(wend, [0, 10, 50, 90, 100])))
+slow = np.argsort(wend)[-8:]
+print("slowest workgroups:", list(slow), [round(float(wend[i]), 1) for i in slow])

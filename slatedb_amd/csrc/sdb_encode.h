@@ -101,7 +101,7 @@ struct EncodeArgs {
     BloomPlan bpl;
     BloomSlots bq;
     uint8_t *bloom_out;
-    uint32_t *done;         // k_emit workgroups finished (the last one writes the summary)
+    uint32_t *done;         // [0] k_emit workgroups finished (the last one writes the summary); [1] block ticket
     uint32_t nprep_wg;
     uint32_t seg_lds;       // k_seg's dynamic LDS bytes
     // outputs (device)
@@ -156,7 +156,7 @@ inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes
     w.stat_part = take(8 * 5 * (nf + 1));
     w.wmax_part = take(4 * (nc + 1));
     w.err_part = take(8 * (nf + 1));
-    w.done = take(4);
+    w.done = take(8);
     w.gtab_exit = take(4 * (nc * kSegLook + 1));  // one table per group (<= one per chunk)
     w.gtab_cnt = take(4 * (nc * kSegLook + 1));
     w.gtab_bytes = take(8 * (nc * kSegLook + 1));

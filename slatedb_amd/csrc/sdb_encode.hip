@@ -588,7 +588,8 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(EncodeArgs a) {
         *a.wmax = W;
         *a.err = s_err;
         *a.slow_count = 0;
-        *a.done = 0;
+        a.done[0] = 0;
+        a.done[1] = 0;
         *a.mode = fast ? 1u : 0u;
         sdb_sst_summary *sm = a.summary;
         uint64_t t[5];
@@ -1418,12 +1419,22 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     }
     // partner = lane + 2^s: DPP row_shl inside a row, then permlane16 / permlane32 swaps (only the
     // lanes with bit s clear use the result)
-    c = crc_tree_mul<0>(c) ^ dpp32<0x101>(c);
-    c = crc_tree_mul<1>(c) ^ dpp32<0x102>(c);
-    c = crc_tree_mul<2>(c) ^ dpp32<0x104>(c);
-    c = crc_tree_mul<3>(c) ^ dpp32<0x108>(c);
-    c = crc_tree_mul<4>(c) ^ (uint32_t)__builtin_amdgcn_permlane16_swap(c, c, false, false)[1];
-    c = crc_tree_mul<5>(c) ^ (uint32_t)__builtin_amdgcn_permlane32_swap(c, c, false, false)[1];
+    // lanes l with l % 2^(s+1) != 0 hold nothing the tree still needs: their table lookups are masked
+    // off (inactive lanes take no part in the LDS banking), 63 lanes' lookups in all instead of 384
+    {
+        uint32_t p = dpp32<0x101>(c);
+        if ((l & 1) == 0) c = crc_tree_mul<0>(c) ^ p;
+        p = dpp32<0x102>(c);
+        if ((l & 3) == 0) c = crc_tree_mul<1>(c) ^ p;
+        p = dpp32<0x104>(c);
+        if ((l & 7) == 0) c = crc_tree_mul<2>(c) ^ p;
+        p = dpp32<0x108>(c);
+        if ((l & 15) == 0) c = crc_tree_mul<3>(c) ^ p;
+        p = (uint32_t)__builtin_amdgcn_permlane16_swap(c, c, false, false)[1];
+        if ((l & 31) == 0) c = crc_tree_mul<4>(c) ^ p;
+        p = (uint32_t)__builtin_amdgcn_permlane32_swap(c, c, false, false)[1];
+        if (l == 0) c = crc_tree_mul<5>(c) ^ p;
+    }
     const uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
     const uint32_t pad = (uint32_t)__builtin_amdgcn_readfirstlane((int)((nseg << 6) - Lc));
     const uint32_t crc32 = gf_mul(c_seg.unpad[pad], u) ^ 0xFFFFFFFFu;
@@ -1518,38 +1529,40 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(EncodeArgs a) {
     }
     if (run) {
         lu32 *crc = (lu32 *)smem;
+        // schedule: workgroup b owns an equal share [r0, r1) of the blocks; its waves start on blocks
+        // r0 + wave and then take the rest in order from an LDS ticket, so a wave that runs fast takes
+        // more.  (One global ticket for all waves measured 3x slower: the atomics serialise.)
+        const uint32_t nb = a.anchor_blk[a.nchunks];
+        const uint32_t r0 = (uint32_t)((uint64_t)nb * blockIdx.x / gridDim.x);
+        const uint32_t r1 = (uint32_t)((uint64_t)nb * (blockIdx.x + 1) / gridDim.x);
+        const uint32_t *dw = (const uint32_t *)a.desc;
+        uint32_t blk = r0 + wave;
+        // the first block's descriptor is in flight while the CRC tables are copied, its values and
+        // metadata while the workgroup does the slow blocks and sets up the ticket
+        const uint32_t dv0 = (blk < r1 && l < 14) ? dw[14 * (uint64_t)blk + l] : 0;
         for (uint32_t q = threadIdx.x; q < 8 * 256; q += blockDim.x) crc[q] = (&c_crc.t[0][0])[q];
         for (uint32_t q = threadIdx.x; q < 4 * 256; q += blockDim.x) crc[8 * 256 + q] = (&c_mul256.t[0][0])[q];
         for (uint32_t q = threadIdx.x; q < kTreeSteps * 4 * 256; q += blockDim.x) crc[12 * 256 + q] = (&g_tree.t[0][0][0])[q];
+        BlockDesc dn = desc_from_lanes(dv0);
+        EmitPre pn;
+        bool fn = blk < r1 && emit_fast(dn);
+        if (fn) emit_prefetch(a, dn, pn);
         __syncthreads();
         emit_slow_blocks<V>(a, (uint8_t *)smem + kCrcLds + 16, (const uint32_t(*)[256])smem);
         __syncthreads();
         if (threadIdx.x == 0) *(lu32 *)(smem + kCrcLds) = blockDim.x >> 6;  // block ticket (first blocks: r0 + wave)
         __syncthreads();
-        const uint32_t nb = a.anchor_blk[a.nchunks];
         lu8 *wbase = (lu8 *)smem + kCrcLds + 16 + wave * kEmitWaveLds;
         lu8 *img = wbase + kStageGuard;
         lu8 *kst = img + kImgCap + 16;
         lSpanCopy *rtab = (lSpanCopy *)(kst + kKeyStageCap);
-        const uint32_t *dw = (const uint32_t *)a.desc;
-        // schedule: workgroup b owns an equal share [r0, r1) of the blocks; its waves start on blocks
-        // r0 + wave and then take the rest in order from an LDS ticket, so a wave that runs fast takes
-        // more (per-block times vary with the memory traffic around them)
-        const uint32_t r0 = (uint32_t)((uint64_t)nb * blockIdx.x / gridDim.x);
-        const uint32_t r1 = (uint32_t)((uint64_t)nb * (blockIdx.x + 1) / gridDim.x);
         lu32 *ticket = (lu32 *)(smem + kCrcLds);
         auto take = [&]() -> uint32_t {
             uint32_t t = 0;
             if (l == 0) t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             return r0 + (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
         };
-        uint32_t blk = r0 + wave;
         if (blk < r1) {
-            // prologue: the first block's descriptor and prefetch, and the next block's descriptor
-            BlockDesc dn = desc_from_lanes(l < 14 ? dw[14 * (uint64_t)blk + l] : 0);
-            EmitPre pn;
-            bool fn = emit_fast(dn);
-            if (fn) emit_prefetch(a, dn, pn);
             uint32_t nblk = take();
             uint32_t dv = (nblk < r1 && l < 14) ? dw[14 * (uint64_t)nblk + l] : 0;
             while (blk < r1) {
@@ -1583,7 +1596,7 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(EncodeArgs a) {
     __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence();
-        if (atomicAdd(a.done, 1u) == gridDim.x - 1) {
+        if (atomicAdd(&a.done[0], 1u) == gridDim.x - 1) {
             __threadfence();
             finish_summary(a);
         }
