@@ -12,20 +12,28 @@
 // D3 emit    one wave per block: parse again and write keys (restored against the previous key),
 //            value references into `blocks`, seq, flags and timestamps.
 #include "sdb_decode.h"
+#include "sdb_crc.h"
 #include "sdb_device.h"
 
 namespace sdb {
 
-constexpr uint32_t kDecCap = 8192;  // LDS staging per wave (bytes); larger blocks parse from HBM
+constexpr uint32_t kDecThreads = 1024;                   // 16 waves: one workgroup (and CRC table copy) per CU
+constexpr uint32_t kDecImg = 4096 + 32;                  // fast path: staged block image per wave
+constexpr uint32_t kDecKeys = 2048;                      // fast path: restored keys of one block
+constexpr uint32_t kDecWaveLds = kDecImg + kDecKeys;
+constexpr uint32_t kDecLds = kCrcTablesLds + (kDecThreads / 64) * kDecWaveLds;
+constexpr uint32_t kDecCap = kDecWaveLds;  // other blocks: generic staging per wave; larger ones parse from HBM
 
-SDB_DEV uint64_t rd_be(const uint8_t *p, int nb) {
+template <typename P>
+SDB_DEV uint64_t rd_be(P p, int nb) {
     uint64_t v = 0;
     for (int i = 0; i < nb; i++) v = (v << 8) | p[i];
     return v;
 }
 
 // Parse one varint (decode_varint, utils.rs:622-634) from d[*pos] (bounded by end).
-SDB_DEV bool rd_varint(const uint8_t *d, uint32_t end, uint32_t *pos, uint32_t *v) {
+template <typename P>
+SDB_DEV bool rd_varint(P d, uint32_t end, uint32_t *pos, uint32_t *v) {
     uint32_t r = 0;
     int sh = 0;
     for (;;) {
@@ -51,7 +59,8 @@ struct RowV2 {
 };
 
 // SstRowCodecV2::decode (row_codec_v2.rs:172-220).  Returns 0 or an sdb_status.
-SDB_DEV int parse_v2(const uint8_t *d, uint32_t end, uint32_t pos, RowV2 *r) {
+template <typename P>
+SDB_DEV int parse_v2(P d, uint32_t end, uint32_t pos, RowV2 *r) {
     if (!rd_varint(d, end, &pos, &r->shared) || !rd_varint(d, end, &pos, &r->unshared) ||
         !rd_varint(d, end, &pos, &r->vlen))
         return SDB_CORRUPT_BLOCK;
@@ -81,6 +90,66 @@ SDB_DEV int parse_v2(const uint8_t *d, uint32_t end, uint32_t pos, RowV2 *r) {
     return 0;
 }
 
+// The same decode for rows staged in LDS: the header and the trailer are each read as one unaligned
+// 16-byte window (five aligned dwords + v_alignbyte, all in flight together) instead of byte by byte,
+// and single-byte varints (every length < 128) decode from the window in registers.
+SDB_DEV void lds_read16(const lu8 *p, uint32_t (&w)[4]) {
+    const uint32_t addr = lds_addr((const void *)p), sh = addr & 3;
+    const lu32 *d = (const lu32 *)(uintptr_t)(addr & ~3u);
+    const uint32_t x0 = d[0], x1 = d[1], x2 = d[2], x3 = d[3], x4 = d[4];
+    w[0] = __builtin_amdgcn_alignbyte(x1, x0, sh);
+    w[1] = __builtin_amdgcn_alignbyte(x2, x1, sh);
+    w[2] = __builtin_amdgcn_alignbyte(x3, x2, sh);
+    w[3] = __builtin_amdgcn_alignbyte(x4, x3, sh);
+}
+SDB_DEV uint64_t be64_at(uint32_t lo, uint32_t hi) { return __builtin_bswap64((uint64_t)lo | ((uint64_t)hi << 32)); }
+
+SDB_DEV int parse_v2(const lu8 *d, uint32_t end, uint32_t pos, RowV2 *r) {
+    uint32_t w[4];
+    lds_read16(d + pos, w);
+    if ((w[0] & 0x808080u) == 0 && pos + 3 <= end) {
+        r->shared = w[0] & 0x7F;
+        r->unshared = (w[0] >> 8) & 0x7F;
+        r->vlen = (w[0] >> 16) & 0x7F;
+        pos += 3;
+    } else if (!rd_varint(d, end, &pos, &r->shared) || !rd_varint(d, end, &pos, &r->unshared) ||
+               !rd_varint(d, end, &pos, &r->vlen)) {
+        return SDB_CORRUPT_BLOCK;
+    }
+    if ((uint64_t)pos + r->unshared + r->vlen + 9 > end) return SDB_CORRUPT_BLOCK;
+    r->suf_pos = pos;
+    pos += r->unshared;
+    r->val_pos = pos;
+    pos += r->vlen;
+    uint32_t x[4];
+    lds_read16(d + pos, x);  // seq (8), flags (1), the first 7 bytes of the timestamps
+    r->seq = be64_at(x[0], x[1]);
+    const uint8_t f = (uint8_t)x[2];
+    pos += 9;
+    if (!flags_ok(f)) return SDB_INVALID_ROW_FLAGS;
+    const uint32_t need = ((f & SDB_FLAG_HAS_EXPIRE_TS) ? 8 : 0) + ((f & SDB_FLAG_HAS_CREATE_TS) ? 8 : 0);
+    if ((uint64_t)pos + need > end) return SDB_CORRUPT_BLOCK;
+    r->ets = 0;
+    r->cts = 0;
+    if (need) {
+        uint32_t y[4];
+        lds_read16(d + pos + 7, y);  // bytes 16.. of the trailer window
+        // trailer bytes 9..16 and 17..24 as little-endian dword pairs
+        const uint32_t t0 = __builtin_amdgcn_alignbyte(x[3], x[2], 1), t1 = __builtin_amdgcn_alignbyte(y[0], x[3], 1);
+        const uint32_t t2 = __builtin_amdgcn_alignbyte(y[1], y[0], 1), t3 = __builtin_amdgcn_alignbyte(y[2], y[1], 1);
+        const int64_t first = (int64_t)be64_at(t0, t1), second = (int64_t)be64_at(t2, t3);
+        if (f & SDB_FLAG_HAS_EXPIRE_TS) {
+            r->ets = first;
+            if (f & SDB_FLAG_HAS_CREATE_TS) r->cts = second;
+        } else {
+            r->cts = first;
+        }
+    }
+    r->flags = f;
+    r->next = pos + need;
+    return 0;
+}
+
 struct RowV0 {
     uint32_t prefix, suf, suf_pos, vlen, val_pos;
     uint64_t seq;
@@ -89,7 +158,8 @@ struct RowV0 {
 };
 
 // SstRowCodecV0::decode (row.rs:200-249).
-SDB_DEV int parse_v0(const uint8_t *d, uint32_t end, uint32_t pos, RowV0 *r) {
+template <typename P>
+SDB_DEV int parse_v0(P d, uint32_t end, uint32_t pos, RowV0 *r) {
     if ((uint64_t)pos + 4 > end) return SDB_CORRUPT_BLOCK;
     r->prefix = (uint32_t)rd_be(d + pos, 2);
     r->suf = (uint32_t)rd_be(d + pos + 2, 2);
@@ -135,13 +205,16 @@ SDB_DEV void wave_sync_d() {
 }
 
 // Block parse plan shared by count and emit: where the data lives and how rows are split on lanes.
-struct BlockView {
-    const uint8_t *d;      // block bytes (LDS or global), CRC stripped
+template <typename P>
+struct BlockViewT {
+    P d;                   // block bytes (LDS or global), CRC stripped
     uint32_t data_end;     // end of rows
     uint32_t count;        // trailer count (restarts for V2, entries for V1)
-    const uint8_t *offs;   // trailer offsets (big-endian u16)
+    P offs;                // trailer offsets (big-endian u16)
     int status;
 };
+typedef BlockViewT<const uint8_t *> BlockView;
+typedef BlockViewT<const lu8 *> LdsBlockView;
 
 // Stage + CRC-check block k; fills the view.  Called by a whole wave.
 SDB_DEV BlockView load_block(const DecodeArgs &a, uint64_t k, uint8_t *stage, const uint32_t (*crc)[256]) {
@@ -209,6 +282,102 @@ SDB_DEV BlockView load_block(const DecodeArgs &a, uint64_t k, uint8_t *stage, co
     return v;
 }
 
+// Fast path: a block whose CRC input fits one 4 KiB wave image.  The block's 16-byte granules are
+// staged so that image byte p0 = s & 15 is block byte 0; the bytes before it and past the CRC input
+// (to the end of the last 64-byte segment) are zeroed, crc32fast's init is folded into the first four
+// message bytes in place, and the shared wave CRC (sdb_crc.h) runs once; the four bytes are restored
+// for the parse.  check = false (the emit pass) only stages.
+SDB_DEV bool dec_fast(uint64_t s, uint64_t e) {
+    const uint64_t len = e - s;
+    return e >= s && len >= 8 && (s & 15) + len <= kDecImg && (s & 15) + len - 4 <= 4096;
+}
+
+SDB_DEV LdsBlockView stage_lds(const DecodeArgs &a, uint64_t s, uint64_t e, lu8 *img, bool check) {
+    LdsBlockView v{};
+    const uint32_t l = (uint32_t)lane_id();
+    const uint32_t p0 = (uint32_t)(s & 15), len = (uint32_t)(e - s), blen = len - 4, Lc = p0 + blen;
+    const uint64_t a0 = s & ~15ull;
+    const uint32_t ng = (uint32_t)((((e + 15) & ~15ull) - a0) >> 4);
+    const uint4 *src = (const uint4 *)(a.blocks + a0);  // aligned granules that hold block bytes
+    for (uint32_t q = l; q < ng; q += 64) {
+        const uint4 g = src[q];
+        u32x4 w;
+        w.x = g.x;
+        w.y = g.y;
+        w.z = g.z;
+        w.w = g.w;
+        ((lu128 *)img)[q] = w;
+    }
+    wave_sync_d();
+    const lu8 *d = img + p0;
+    if (check) {
+        const uint32_t stored = ((uint32_t)d[blen] << 24) | ((uint32_t)d[blen + 1] << 16) | ((uint32_t)d[blen + 2] << 8) |
+                                (uint32_t)d[blen + 3];
+        wave_sync_d();
+        if (l < p0) img[l] = 0;
+        for (uint32_t x = Lc + l; x < ((Lc + 63) & ~63u); x += 64) img[x] = 0;
+        if (l < 4) img[p0 + l] ^= 0xFF;
+        wave_sync_d();
+        const uint32_t c = wave_crc_image(img, Lc, false);
+        wave_sync_d();
+        if (l < 4) img[p0 + l] ^= 0xFF;
+        wave_sync_d();
+        if (c != stored) {
+            v.status = SDB_CHECKSUM_MISMATCH;  // validate_checksum (format/sst.rs:1029-1038)
+            return v;
+        }
+    }
+    const uint32_t cnt = (uint32_t)rd_be(d + blen - 2, 2);  // Block::decode (format/block.rs:28-46)
+    if (2 + 2 * (uint64_t)cnt > blen) {
+        v.status = SDB_CORRUPT_BLOCK;
+        return v;
+    }
+    v.d = d;
+    v.count = cnt;
+    v.data_end = blen - 2 - 2 * cnt;
+    v.offs = d + v.data_end;
+    v.status = 0;
+    return v;
+}
+
+// LDS -> LDS byte copy, eight bytes in flight per step (one wait per step, not per byte).
+SDB_DEV void lds_copy_small(lu8 *dst, const lu8 *src, uint32_t n) {
+    uint32_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint8_t t[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) t[q] = src[i + q];
+#pragma unroll
+        for (int q = 0; q < 8; q++) dst[i + q] = t[q];
+    }
+    for (; i < n; i++) dst[i] = src[i];
+}
+
+// Store LDS bytes kbuf[o .. o + n) to global [g, g + n), o = g & 15: 16-byte stores for the granules
+// inside the range, byte stores at its two edges (neighbouring blocks' keys share those granules).
+SDB_DEV void wave_store_bytes(uint8_t *g, const lu8 *kbuf, uint64_t n) {
+    if (!n) return;
+    const uintptr_t d0 = (uintptr_t)g, d1 = d0 + n;
+    const uintptr_t a0 = d0 & ~(uintptr_t)15, a1 = (d1 + 15) & ~(uintptr_t)15;
+    const uint32_t nch = (uint32_t)((a1 - a0) >> 4);
+    for (uint32_t c = lane_id(); c < nch; c += 64) {
+        const uintptr_t ga = a0 + 16 * (uintptr_t)c;
+        const lu8 *li = kbuf + 16 * c;
+        if (ga >= d0 && ga + 16 <= d1) {
+            const u32x4 w = *(const lu128 *)li;
+            uint4 o;
+            o.x = w.x;
+            o.y = w.y;
+            o.z = w.z;
+            o.w = w.w;
+            *(uint4 *)ga = o;
+        } else {
+            for (int q = 0; q < 16; q++)
+                if (ga + q >= d0 && ga + q < d1) ((uint8_t *)ga)[q] = li[q];
+        }
+    }
+}
+
 // V2 plan: lane q parses restart region q when the block is "regular" (restart 0 at offset 0,
 // strictly increasing restarts, regions ending exactly on the next restart, shared == 0 at every
 // region start); otherwise lane 0 walks the whole block like BlockIteratorV2::next does.
@@ -219,7 +388,8 @@ struct Tally {
     bool sequential;
 };
 
-SDB_DEV Tally tally_v2(const BlockView &v) {
+template <typename P>
+SDB_DEV Tally tally_v2(const BlockViewT<P> &v) {
     Tally t{0, 0, 0, false};
     const int l = lane_id();
     const uint32_t R = v.count;
@@ -306,7 +476,8 @@ SDB_DEV Tally tally_v2(const BlockView &v) {
     return t;
 }
 
-SDB_DEV Tally tally_v1(const BlockView &v) {
+template <typename P>
+SDB_DEV Tally tally_v1(const BlockViewT<P> &v) {
     Tally t{0, 0, 0, false};
     const int l = lane_id();
     const uint32_t R = v.count;
@@ -350,18 +521,33 @@ SDB_DEV Tally tally_v1(const BlockView &v) {
     return t;
 }
 
-__global__ __launch_bounds__(256) void k_dec_count(DecodeArgs a) {
+// D1 count.  LDS: the CRC tables at address 0 (sdb_crc.h: this kernel has no static LDS), then one
+// region of kDecWaveLds per wave.
+__global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint32_t(*crc)[256] = (uint32_t(*)[256])smem;
-    for (uint32_t q = threadIdx.x; q < 8 * 256; q += blockDim.x) ((uint32_t *)crc)[q] = (&c_crc.t[0][0])[q];
+    if (lds_addr((const void *)smem) != 0) {  // sdb_crc.h's lookups assume the tables at LDS address 0
+        if (threadIdx.x == 0) atomicMin(a.err, (unsigned long long)SDB_DEVICE_ERROR);
+        return;
+    }
+    crc_tables_to_lds((lu32 *)smem);
     __syncthreads();
+    const uint32_t(*crc)[256] = (const uint32_t(*)[256])smem;
     const uint32_t wave = threadIdx.x >> 6;
-    uint8_t *stage = smem + 8192 + wave * (kDecCap + 64);
+    lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kDecWaveLds;
+    uint8_t *stage = (uint8_t *)img;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave; k < a.nblocks; k += nwaves) {
-        BlockView v = load_block(a, k, stage, crc);
-        Tally t{0, 0, v.status, false};
-        if (!v.status) t = (a.version == 2) ? tally_v2(v) : tally_v1(v);
+        const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
+        Tally t{0, 0, 0, false};
+        if (dec_fast(s, e)) {
+            const LdsBlockView v = stage_lds(a, s, e, img, true);
+            t.status = v.status;
+            if (!v.status) t = (a.version == 2) ? tally_v2(v) : tally_v1(v);
+        } else {
+            const BlockView v = load_block(a, k, stage, crc);
+            t.status = v.status;
+            if (!v.status) t = (a.version == 2) ? tally_v2(v) : tally_v1(v);
+        }
         if (lane_id() == 0) {
             if (t.status) {
                 a.cnt[k] = 0;
@@ -381,26 +567,151 @@ __global__ __launch_bounds__(256) void k_dec_count(DecodeArgs a) {
 }
 
 // --- emit -----------------------------------------------------------------------------------------
-SDB_DEV void put_entry(const DecodeArgs &a, uint64_t idx, uint64_t kpos, uint32_t klen, uint64_t vref,
-                       uint32_t vlen, uint64_t seq, uint8_t flags, int64_t cts, int64_t ets) {
+// Columns of one entry.  Timestamps are written only when the row carries them (the contract:
+// create_ts / expire_ts are valid iff the flag is set).
+SDB_DEV void put_entry(const DecodeArgs &a, uint64_t idx, uint64_t kpos, uint64_t vref, uint32_t vlen, uint64_t seq,
+                       uint8_t flags, int64_t cts, int64_t ets) {
     a.out.key_off[idx] = kpos;
     a.out.val_off[idx] = vlen ? vref : 0;
     a.out.val_len[idx] = vlen;
     a.out.seq[idx] = seq;
     a.out.flags[idx] = flags;
-    a.out.create_ts[idx] = (flags & SDB_FLAG_HAS_CREATE_TS) ? cts : 0;
-    a.out.expire_ts[idx] = (flags & SDB_FLAG_HAS_EXPIRE_TS) ? ets : 0;
-    (void)klen;
+    if (flags & SDB_FLAG_HAS_CREATE_TS) a.out.create_ts[idx] = cts;
+    if (flags & SDB_FLAG_HAS_EXPIRE_TS) a.out.expire_ts[idx] = ets;
 }
 
-__global__ __launch_bounds__(256) void k_dec_emit(DecodeArgs a) {
+// V2 emit of one block (BlockIteratorV2 ascending, block_iterator_v2.rs:235-267; restore_full_key,
+// row_codec_v2.rs:83-89).  Keys are restored into `kb` (LDS, the block's keys at kb + (kb0 & 15) + rel)
+// when kbuf is set, else straight into the arena.  Regular blocks: lane q walks restart region q (a
+// wave scan over the regions gives each lane its first entry and key position); otherwise lane 0 walks
+// the block.
+template <typename P>
+SDB_DEV void emit_v2(const DecodeArgs &a, const BlockViewT<P> &v, bool sequential, uint64_t ent0, uint64_t kb0,
+                     uint64_t gbase, lu8 *kbuf) {
+    const uint32_t l = (uint32_t)lane_id();
+    const uint32_t ko = (uint32_t)(kb0 & 15);
+    auto key_at = [&](uint64_t kp) -> uint8_t * { return a.out.key_arena + kp; };
+    if (!sequential) {
+        const uint32_t R = v.count;
+        uint64_t ecarry = ent0, kcarry = kb0;
+        for (uint32_t q0 = 0; q0 < R; q0 += 64) {
+            const uint32_t q = q0 + l;
+            uint32_t pos = 0, end = 0, ne = 0, nk = 0;
+            if (q < R) {
+                pos = (uint32_t)rd_be(v.offs + 2 * q, 2);
+                end = (q + 1 < R) ? (uint32_t)rd_be(v.offs + 2 * q + 2, 2) : v.data_end;
+                uint32_t p = pos;
+                while (p < end) {
+                    RowV2 r;
+                    parse_v2(v.d, v.data_end, p, &r);
+                    ne++;
+                    nk += r.shared + r.unshared;
+                    p = r.next;
+                }
+            }
+            const uint64_t ie = wave_incl_scan((uint64_t)ne), ik = wave_incl_scan((uint64_t)nk);
+            uint64_t idx = ecarry + ie - ne, kp = kcarry + ik - nk;
+            if (q < R) {
+                uint64_t prev_kp = 0;
+                uint32_t p = pos;
+                while (p < end) {
+                    RowV2 r;
+                    parse_v2(v.d, v.data_end, p, &r);
+                    if (kbuf) {
+                        lu8 *dst = kbuf + ko + (uint32_t)(kp - kb0);
+                        lds_copy_small(dst, kbuf + ko + (uint32_t)(prev_kp - kb0), r.shared);
+                        for (uint32_t x = 0; x < r.unshared; x++) dst[r.shared + x] = v.d[r.suf_pos + x];
+                    } else {
+                        uint8_t *dst = key_at(kp);
+                        const uint8_t *pk = key_at(prev_kp);
+                        for (uint32_t x = 0; x < r.shared; x++) dst[x] = pk[x];
+                        for (uint32_t x = 0; x < r.unshared; x++) dst[r.shared + x] = v.d[r.suf_pos + x];
+                    }
+                    const uint32_t vl = (r.flags & SDB_FLAG_TOMBSTONE) ? 0 : r.vlen;
+                    put_entry(a, idx, kp, gbase + r.val_pos, vl, r.seq, r.flags, r.cts, r.ets);
+                    prev_kp = kp;
+                    kp += r.shared + r.unshared;
+                    idx++;
+                    p = r.next;
+                }
+            }
+            ecarry += wave_readlane(ie, 63);
+            kcarry += wave_readlane(ik, 63);
+        }
+    } else if (l == 0) {
+        // sequential walk (BlockIteratorV2 ascending); the initial current_key is the key at restart 0
+        uint64_t idx = ent0, kp = kb0, prev_kp = 0;
+        uint32_t pos = 0;
+        uint32_t p0 = (uint32_t)rd_be(v.offs, 2), sh = 0, un = 0, vl0 = 0;
+        rd_varint(v.d, v.data_end, &p0, &sh);
+        rd_varint(v.d, v.data_end, &p0, &un);
+        rd_varint(v.d, v.data_end, &p0, &vl0);
+        const uint32_t init_key = p0;  // position of restart 0's key suffix (= its whole key)
+        bool first = true;
+        while (pos < v.data_end) {
+            RowV2 r;
+            parse_v2(v.d, v.data_end, pos, &r);
+            if (kbuf) {
+                lu8 *dst = kbuf + ko + (uint32_t)(kp - kb0);
+                for (uint32_t x = 0; x < r.shared; x++) dst[x] = first ? v.d[init_key + x] : kbuf[ko + (uint32_t)(prev_kp - kb0) + x];
+                for (uint32_t x = 0; x < r.unshared; x++) dst[r.shared + x] = v.d[r.suf_pos + x];
+            } else {
+                uint8_t *dst = key_at(kp);
+                for (uint32_t x = 0; x < r.shared; x++) dst[x] = first ? v.d[init_key + x] : a.out.key_arena[prev_kp + x];
+                for (uint32_t x = 0; x < r.unshared; x++) dst[r.shared + x] = v.d[r.suf_pos + x];
+            }
+            const uint32_t vl = (r.flags & SDB_FLAG_TOMBSTONE) ? 0 : r.vlen;
+            put_entry(a, idx, kp, gbase + r.val_pos, vl, r.seq, r.flags, r.cts, r.ets);
+            prev_kp = kp;
+            kp += r.shared + r.unshared;
+            idx++;
+            first = false;
+            pos = r.next;
+        }
+    }
+}
+
+// V1 emit (BlockIterator, block_iterator.rs:54-267): lane = entry, key = first key's prefix + suffix.
+template <typename P>
+SDB_DEV void emit_v1(const DecodeArgs &a, const BlockViewT<P> &v, uint64_t ent0, uint64_t kb0, uint64_t gbase) {
+    const uint32_t l = (uint32_t)lane_id();
+    const uint32_t R = v.count;
+    uint64_t carry = kb0;
+    for (uint32_t g0 = 0; g0 < R; g0 += 64) {
+        const uint32_t i = g0 + l;
+        RowV0 r;
+        uint32_t kl = 0;
+        if (i < R) {
+            parse_v0(v.d, v.data_end, (uint32_t)rd_be(v.offs + 2 * i, 2), &r);
+            kl = r.prefix + r.suf;
+        }
+        const uint64_t inc = wave_incl_scan((uint64_t)kl);
+        if (i < R) {
+            const uint64_t kp = carry + inc - kl;
+            uint8_t *dst = a.out.key_arena + kp;
+            for (uint32_t q = 0; q < r.prefix; q++) dst[q] = v.d[4 + q];
+            for (uint32_t q = 0; q < r.suf; q++) dst[r.prefix + q] = v.d[r.suf_pos + q];
+            put_entry(a, ent0 + i, kp, gbase + r.val_pos, r.vlen, r.seq, r.flags, r.cts, r.ets);
+        }
+        carry += wave_readlane(inc, 63);
+    }
+}
+
+// D3 emit: one wave per block, stage again (no CRC: the count pass checked it), write the columns.
+__global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint32_t(*crc)[256] = (uint32_t(*)[256])smem;
-    for (uint32_t q = threadIdx.x; q < 8 * 256; q += blockDim.x) ((uint32_t *)crc)[q] = (&c_crc.t[0][0])[q];
+    if (lds_addr((const void *)smem) != 0) {  // sdb_crc.h's lookups assume the tables at LDS address 0
+        if (threadIdx.x == 0) atomicMin(a.err, (unsigned long long)SDB_DEVICE_ERROR);
+        return;
+    }
+    crc_tables_to_lds((lu32 *)smem);  // the generic path of oversized blocks still checks windows
     __syncthreads();
+    const uint32_t(*crc)[256] = (const uint32_t(*)[256])smem;
     const uint32_t wave = threadIdx.x >> 6;
     const int l = lane_id();
-    uint8_t *stage = smem + 8192 + wave * (kDecCap + 64);
+    lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kDecWaveLds;
+    lu8 *kbuf = img + kDecImg;
+    uint8_t *stage = (uint8_t *)img;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     // capacity guard: if the counted output does not fit the caller's arrays, write nothing
     if (a.ent_start[a.nblocks] > a.out.cap_entries || a.key_start[a.nblocks] > a.out.key_arena_cap) return;
@@ -409,105 +720,27 @@ __global__ __launch_bounds__(256) void k_dec_emit(DecodeArgs a) {
         const uint64_t n_ent = a.ent_start[k + 1] - ent0;
         if (l == 0) a.out.block_entry_start[k] = ent0;
         if (n_ent == 0) continue;
-        BlockView v = load_block(a, k, stage, crc);
-        if (v.status) continue;  // cannot happen: count pass accepted it
-        const uint64_t kb0 = a.key_start[k];
-        const uint64_t gbase = a.block_off[k];
-        // value references are offsets into `blocks`; d may be LDS (staged) or HBM
-        const uint8_t *g = a.blocks + gbase;
-        if (a.version == 1) {
-            const uint32_t R = v.count;
-            const uint32_t fk = (uint32_t)rd_be(v.d + 2, 2);
-            // key positions: exclusive scan of restored key lengths over the entries
-            uint64_t carry = kb0;
-            for (uint32_t g0 = 0; g0 < R; g0 += 64) {
-                uint32_t i = g0 + l;
-                RowV0 r;
-                uint32_t kl = 0;
-                if (i < R) {
-                    parse_v0(v.d, v.data_end, (uint32_t)rd_be(v.offs + 2 * i, 2), &r);
-                    kl = r.prefix + r.suf;
+        const uint64_t kb0 = a.key_start[k], kbn = a.key_start[k + 1] - kb0;
+        const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
+        const bool seq = a.flag[k] != 0;
+        if (dec_fast(s, e)) {
+            const LdsBlockView v = stage_lds(a, s, e, img, false);
+            if (v.status) continue;  // cannot happen: the count pass accepted it
+            if (a.version == 1) {
+                emit_v1(a, v, ent0, kb0, s);
+            } else {
+                const bool lds_keys = kbn + 16 <= kDecKeys;
+                emit_v2(a, v, seq, ent0, kb0, s, lds_keys ? kbuf : nullptr);
+                if (lds_keys) {
+                    wave_sync_d();
+                    wave_store_bytes(a.out.key_arena + kb0, kbuf, kbn);
                 }
-                uint64_t inc = wave_incl_scan((uint64_t)kl);
-                if (i < R) {
-                    uint64_t kp = carry + inc - kl;
-                    uint8_t *dst = a.out.key_arena + kp;
-                    for (uint32_t q = 0; q < r.prefix; q++) dst[q] = v.d[4 + q];
-                    for (uint32_t q = 0; q < r.suf; q++) dst[r.prefix + q] = v.d[r.suf_pos + q];
-                    put_entry(a, ent0 + i, kp, kl, gbase + r.val_pos, r.vlen, r.seq, r.flags, r.cts, r.ets);
-                }
-                carry += __shfl(inc, 63, 64);
             }
-            (void)fk;
-            (void)g;
-        } else if (!a.flag[k]) {
-            // regular: lane q owns restart region q; entry/key bases by wave scans over regions
-            const uint32_t R = v.count;
-            uint64_t ecarry = ent0, kcarry = kb0;
-            for (uint32_t q0 = 0; q0 < R; q0 += 64) {
-                uint32_t q = q0 + l;
-                uint32_t pos = 0, end = 0, ne = 0, nk = 0;
-                if (q < R) {
-                    pos = (uint32_t)rd_be(v.offs + 2 * q, 2);
-                    end = (q + 1 < R) ? (uint32_t)rd_be(v.offs + 2 * q + 2, 2) : v.data_end;
-                    uint32_t p = pos;
-                    while (p < end) {
-                        RowV2 r;
-                        parse_v2(v.d, v.data_end, p, &r);
-                        ne++;
-                        nk += r.shared + r.unshared;
-                        p = r.next;
-                    }
-                }
-                uint64_t ie = wave_incl_scan((uint64_t)ne), ik = wave_incl_scan((uint64_t)nk);
-                uint64_t idx = ecarry + ie - ne, kp = kcarry + ik - nk;
-                if (q < R) {
-                    uint64_t prev_kp = 0;
-                    uint32_t p = pos;
-                    while (p < end) {
-                        RowV2 r;
-                        parse_v2(v.d, v.data_end, p, &r);
-                        uint8_t *dst = a.out.key_arena + kp;
-                        const uint8_t *pk = a.out.key_arena + prev_kp;
-                        for (uint32_t x = 0; x < r.shared; x++) dst[x] = pk[x];
-                        for (uint32_t x = 0; x < r.unshared; x++) dst[r.shared + x] = v.d[r.suf_pos + x];
-                        uint32_t vl = (r.flags & SDB_FLAG_TOMBSTONE) ? 0 : r.vlen;
-                        put_entry(a, idx, kp, r.shared + r.unshared, gbase + r.val_pos, vl, r.seq, r.flags, r.cts,
-                                  r.ets);
-                        prev_kp = kp;
-                        kp += r.shared + r.unshared;
-                        idx++;
-                        p = r.next;
-                    }
-                }
-                ecarry += __shfl(ie, 63, 64);
-                kcarry += __shfl(ik, 63, 64);
-            }
-        } else if (l == 0) {
-            // sequential walk (BlockIteratorV2 ascending)
-            uint64_t idx = ent0, kp = kb0, prev_kp = 0;
-            uint32_t pos = 0;
-            // initial current_key = key at restart 0
-            uint32_t p0 = (uint32_t)rd_be(v.offs, 2), sh = 0, un = 0, vl0 = 0;
-            rd_varint(v.d, v.data_end, &p0, &sh);
-            rd_varint(v.d, v.data_end, &p0, &un);
-            rd_varint(v.d, v.data_end, &p0, &vl0);
-            const uint8_t *init_key = v.d + p0;
-            bool first = true;
-            while (pos < v.data_end) {
-                RowV2 r;
-                parse_v2(v.d, v.data_end, pos, &r);
-                uint8_t *dst = a.out.key_arena + kp;
-                for (uint32_t x = 0; x < r.shared; x++) dst[x] = first ? init_key[x] : a.out.key_arena[prev_kp + x];
-                for (uint32_t x = 0; x < r.unshared; x++) dst[r.shared + x] = v.d[r.suf_pos + x];
-                uint32_t vl = (r.flags & SDB_FLAG_TOMBSTONE) ? 0 : r.vlen;
-                put_entry(a, idx, kp, r.shared + r.unshared, gbase + r.val_pos, vl, r.seq, r.flags, r.cts, r.ets);
-                prev_kp = kp;
-                kp += r.shared + r.unshared;
-                idx++;
-                first = false;
-                pos = r.next;
-            }
+        } else {
+            const BlockView v = load_block(a, k, stage, crc);
+            if (v.status) continue;
+            if (a.version == 1) emit_v1(a, v, ent0, kb0, s);
+            else emit_v2(a, v, seq, ent0, kb0, s, nullptr);
         }
         wave_sync_d();
     }
@@ -596,12 +829,21 @@ __global__ void k_dec_finish(DecodeArgs a) {
 
 hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
     hipLaunchKernelGGL(k_dec_init, dim3(1), dim3(64), 0, st, a);
-    const size_t lds = 8192 + 4 * (kDecCap + 64);
-    uint64_t waves = a.nblocks;
-    uint64_t wgs = (waves + 3) / 4;
-    if (wgs > 4096) wgs = 4096;
+    static bool attrs = false;
+    if (!attrs) {
+        hipFuncSetAttribute((const void *)k_dec_count, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDecLds);
+        hipFuncSetAttribute((const void *)k_dec_emit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDecLds);
+        (void)hipGetLastError();
+        attrs = true;
+    }
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    uint64_t wgs = (a.nblocks + 15) / 16;  // one wave per block, one workgroup per CU at most
+    if (cus > 0 && wgs > (uint64_t)cus) wgs = (uint64_t)cus;
     if (wgs == 0) wgs = 1;
-    if (a.nblocks) hipLaunchKernelGGL(k_dec_count, dim3((uint32_t)wgs), dim3(256), lds, st, a);
+    const size_t lds = kDecLds;
+    if (a.nblocks) hipLaunchKernelGGL(k_dec_count, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
     // scans: ent_start = excl(cnt), key_start = excl(kbytes)
     uint64_t nt = (a.nblocks + kScanTile - 1) / kScanTile;
     if (a.nblocks) {
@@ -614,7 +856,7 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
         hipMemsetAsync(a.ent_start, 0, 8, st);
         hipMemsetAsync(a.key_start, 0, 8, st);
     }
-    if (a.nblocks) hipLaunchKernelGGL(k_dec_emit, dim3((uint32_t)wgs), dim3(256), lds, st, a);
+    if (a.nblocks) hipLaunchKernelGGL(k_dec_emit, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
     hipLaunchKernelGGL(k_dec_finish, dim3(1), dim3(64), 0, st, a);
     return hipGetLastError();
 }

@@ -27,6 +27,7 @@
 #include <stdlib.h>
 
 #include "sdb_bloom.h"
+#include "sdb_crc.h"
 
 namespace sdb {
 
@@ -998,11 +999,6 @@ __global__ __launch_bounds__(kEnumThreads) void k_enum(EncodeArgs a) {
 //      lookups), wave XOR, the zero padding of the last segment removed by x^(-8 t);
 //   4. 16-byte stores at the block's (unaligned) HBM offset; the < 16-byte tail by one lane.
 // ------------------------------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) uint8_t lu8;
-typedef __attribute__((address_space(3))) uint32_t lu32;
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) u32x4 lu128;
-
 SDB_DEV void lds_put_bytes(lu8 *p, uint64_t w, uint32_t n) {  // w little-endian, n <= 8
     for (uint32_t i = 0; i < n; i++) p[i] = (uint8_t)(w >> (8 * i));
 }
@@ -1161,45 +1157,6 @@ SDB_DEV uint32_t write_row_hdr_trailer(lu8 *dst, const RowInfo &r, uint64_t seq,
     return h;
 }
 
-// 4 * byte SEL of w in one VALU op (SDWA operand select): the LDS byte offset of a table entry.
-template <int SEL>
-SDB_DEV uint32_t bytex4(uint32_t w) {
-    uint32_t r;
-    if constexpr (SEL == 0)
-        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
-            : "=v"(r) : "v"(w));
-    else if constexpr (SEL == 1)
-        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
-            : "=v"(r) : "v"(w));
-    else if constexpr (SEL == 2)
-        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
-            : "=v"(r) : "v"(w));
-    else
-        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
-            : "=v"(r) : "v"(w));
-    return r;
-}
-// k_emit keeps the tables at LDS address 0 (its only LDS is the dynamic region, checked at entry),
-// so a lookup is ds_read_b32 <byte offset>, offset:<table * 1024> with no address add.
-template <int T>
-SDB_DEV uint32_t crc_tab(const lu32 *, uint32_t off4) {
-    return *(const lu32 *)(uintptr_t)(T * 1024 + off4);
-}
-// slicing-by-8 step over the 8 message bytes (lo, hi), tables at LDS `tab` (8 x 256 u32)
-SDB_DEV uint32_t crc_slice8_lds(uint32_t c, uint32_t lo, uint32_t hi, const lu32 *tab) {
-    lo ^= c;
-    const uint32_t x = crc_tab<7>(tab, bytex4<0>(lo)) ^ crc_tab<6>(tab, bytex4<1>(lo)) ^ crc_tab<5>(tab, bytex4<2>(lo));
-    const uint32_t y = crc_tab<4>(tab, bytex4<3>(lo)) ^ crc_tab<3>(tab, bytex4<0>(hi)) ^ crc_tab<2>(tab, bytex4<1>(hi));
-    const uint32_t z = crc_tab<1>(tab, bytex4<2>(hi)) ^ crc_tab<0>(tab, bytex4<3>(hi));
-    return x ^ y ^ z;
-}
-
-// x^256 * c (the x^(8*32) shift of a CRC) from the 4 byte tables at LDS 8 KiB (k_emit layout)
-SDB_DEV uint32_t crc_mul256_lds(uint32_t c) {
-    return crc_tab<8>(nullptr, bytex4<0>(c)) ^ crc_tab<9>(nullptr, bytex4<1>(c)) ^ crc_tab<10>(nullptr, bytex4<2>(c)) ^
-           crc_tab<11>(nullptr, bytex4<3>(c));
-}
-
 // Everything one block needs from HBM, loaded into registers one block ahead (software pipeline):
 // the block's value / key granules (lane l holds granules l, 64 + l, ...) and the row metadata
 // (lane = row).  Plain loads only: the compute phase of the current block issues no global load,
@@ -1261,13 +1218,6 @@ SDB_DEV void emit_prefetch(const EncodeArgs &a, const BlockDesc &d, EmitPre &p) 
     p.cts = a.create_ts ? a.create_ts[j] : 0;
     p.ets = a.expire_ts ? a.expire_ts[j] : 0;
     p.pko = (l == 0 && d.s > 0) ? a.key_off[d.s - 1] : 0;
-}
-
-// x^(8*64*2^s) * c from the 4 byte tables of tree step s (LDS 12 KiB + s * 4 KiB, k_emit layout)
-template <int S>
-SDB_DEV uint32_t crc_tree_mul(uint32_t c) {
-    return crc_tab<12 + 4 * S>(nullptr, bytex4<0>(c)) ^ crc_tab<13 + 4 * S>(nullptr, bytex4<1>(c)) ^
-           crc_tab<14 + 4 * S>(nullptr, bytex4<2>(c)) ^ crc_tab<15 + 4 * S>(nullptr, bytex4<3>(c));
 }
 
 template <int V>
@@ -1395,49 +1345,8 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     }
     wave_sync();
     WAVE_T(t4);
-    // 4. CRC32 (format/sst.rs:541-552).  Segments are right-aligned on the lanes: lane l holds
-    //    64-byte segment l - (64 - nseg), two 32-byte slicing-by-8 chains each; lanes before the
-    //    first segment hold 0 (leading zero bytes leave a raw CRC unchanged).  Six pairwise tree
-    //    steps combine them (lane 0 ends with the whole image), then the zero padding of the last
-    //    segment is removed by x^(-8 t).
-    uint32_t c = 0;
-    {
-        const int sg = (int)l - (64 - (int)nseg);
-        if (sg >= 0) {
-            const lu128 *src = (const lu128 *)(img + 64 * sg);
-            u32x4 v0 = src[0], v1 = src[1], v2 = src[2], v3 = src[3];
-            if (sg == 0) v0.x = ~v0.x;  // crc32fast init 0xFFFFFFFF folded into bytes [0, 4)
-            uint32_t ca = crc_slice8_lds(0, v0.x, v0.y, crc), cb = crc_slice8_lds(0, v2.x, v2.y, crc);
-            ca = crc_slice8_lds(ca, v0.z, v0.w, crc);
-            cb = crc_slice8_lds(cb, v2.z, v2.w, crc);
-            ca = crc_slice8_lds(ca, v1.x, v1.y, crc);
-            cb = crc_slice8_lds(cb, v3.x, v3.y, crc);
-            ca = crc_slice8_lds(ca, v1.z, v1.w, crc);
-            cb = crc_slice8_lds(cb, v3.z, v3.w, crc);
-            c = crc_mul256_lds(ca) ^ cb;  // raw(seg) = raw(first 32) * x^256 + raw(last 32)
-        }
-    }
-    // partner = lane + 2^s: DPP row_shl inside a row, then permlane16 / permlane32 swaps (only the
-    // lanes with bit s clear use the result)
-    // lanes l with l % 2^(s+1) != 0 hold nothing the tree still needs: their table lookups are masked
-    // off (inactive lanes take no part in the LDS banking), 63 lanes' lookups in all instead of 384
-    {
-        uint32_t p = dpp32<0x101>(c);
-        if ((l & 1) == 0) c = crc_tree_mul<0>(c) ^ p;
-        p = dpp32<0x102>(c);
-        if ((l & 3) == 0) c = crc_tree_mul<1>(c) ^ p;
-        p = dpp32<0x104>(c);
-        if ((l & 7) == 0) c = crc_tree_mul<2>(c) ^ p;
-        p = dpp32<0x108>(c);
-        if ((l & 15) == 0) c = crc_tree_mul<3>(c) ^ p;
-        p = (uint32_t)__builtin_amdgcn_permlane16_swap(c, c, false, false)[1];
-        if ((l & 31) == 0) c = crc_tree_mul<4>(c) ^ p;
-        p = (uint32_t)__builtin_amdgcn_permlane32_swap(c, c, false, false)[1];
-        if (l == 0) c = crc_tree_mul<5>(c) ^ p;
-    }
-    const uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
-    const uint32_t pad = (uint32_t)__builtin_amdgcn_readfirstlane((int)((nseg << 6) - Lc));
-    const uint32_t crc32 = gf_mul(c_seg.unpad[pad], u) ^ 0xFFFFFFFFu;
+    // 4. CRC32 (format/sst.rs:541-552) of the image [0, Lc), zero padded to whole 64-byte segments
+    const uint32_t crc32 = wave_crc_image(img, Lc, true);
     if (l == 0) {
         img[Lc] = (uint8_t)(crc32 >> 24);
         img[Lc + 1] = (uint8_t)(crc32 >> 16);
@@ -1529,6 +1438,7 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(EncodeArgs a) {
     }
     if (run) {
         lu32 *crc = (lu32 *)smem;
+        (void)crc;
         // schedule: workgroup b owns an equal share [r0, r1) of the blocks; its waves start on blocks
         // r0 + wave and then take the rest in order from an LDS ticket, so a wave that runs fast takes
         // more.  (One global ticket for all waves measured 3x slower: the atomics serialise.)
@@ -1540,9 +1450,7 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(EncodeArgs a) {
         // the first block's descriptor is in flight while the CRC tables are copied, its values and
         // metadata while the workgroup does the slow blocks and sets up the ticket
         const uint32_t dv0 = (blk < r1 && l < 14) ? dw[14 * (uint64_t)blk + l] : 0;
-        for (uint32_t q = threadIdx.x; q < 8 * 256; q += blockDim.x) crc[q] = (&c_crc.t[0][0])[q];
-        for (uint32_t q = threadIdx.x; q < 4 * 256; q += blockDim.x) crc[8 * 256 + q] = (&c_mul256.t[0][0])[q];
-        for (uint32_t q = threadIdx.x; q < kTreeSteps * 4 * 256; q += blockDim.x) crc[12 * 256 + q] = (&g_tree.t[0][0][0])[q];
+        crc_tables_to_lds(crc);
         BlockDesc dn = desc_from_lanes(dv0);
         EmitPre pn;
         bool fn = blk < r1 && emit_fast(dn);

@@ -217,8 +217,12 @@ def assert_decode_same(ref, got, what=""):
     assert got.status == ref.status, (what, got.status, ref.status)
     assert got.n == ref.n, what
     assert np.array_equal(got.block_entry_start, ref.block_entry_start), what
-    for f in ("key_off", "val_off", "val_len", "seq", "flags", "create_ts", "expire_ts"):
+    for f in ("key_off", "val_off", "val_len", "seq", "flags"):
         assert np.array_equal(getattr(got, f), getattr(ref, f)), (what, f)
+    # timestamps are valid iff the row's flag says so (include/slatedb_amd.h, sdb_decoded_out)
+    for f, bit in (("create_ts", _abi.FLAG_HAS_CREATE_TS), ("expire_ts", _abi.FLAG_HAS_EXPIRE_TS)):
+        m = (ref.flags & bit) != 0
+        assert np.array_equal(getattr(got, f)[m], getattr(ref, f)[m]), (what, f)
     assert np.array_equal(got.key_arena, ref.key_arena), what
     assert sorted(got.bad_block.tolist()) == sorted(ref.bad_block.tolist()), what
 
