@@ -189,10 +189,10 @@ sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const 
     a.filter_built = want_filter ? 1 : 0;
     hipStream_t s = S(stream);
     if (want_filter && n) {
-        // the bloom runs inside the encode kernels (k_seg hashes and bins each chunk, k_enum fills the
-        // slices) when the binned build fits; otherwise it is built on the stream before the encode
+        // the bloom is fused with the encode (k_facts hashes; the binning and fill run on a side stream
+        // beside k_seg .. k_emit) when the binned build fits; otherwise it is built before the encode
         const BloomPlan pl = bloom_plan(n, a.num_probes, fb, kChunk);
-        if (bloom_plan_fits(pl) && bloom_bin_lds(pl) <= kSegLdsMax && bloom_fill_lds(pl) <= kEnumLds) {
+        if (bloom_plan_fits(pl)) {
             a.bloom_fused = 1;
             a.bpl = pl;
             a.bq = bloom_slots(carve<void>(workspace, wl.bloom_rep), pl);

@@ -142,32 +142,52 @@ SDB_DEV void probes_hd(uint32_t h, uint32_t d, uint32_t k, uint32_t m, F f) {
 }
 
 // Bin one tile whose keys' (h0, d0) are held in registers: key tid + j * blockDim.x of the tile in
-// (hh[j], dd[j]), nk keys.  Each probe takes the next position of its slice's slot from an LDS
-// counter and is stored straight into the slot (the slot's lines fill in L2 before they leave); the
-// final counters are the run lengths.  The order inside a run depends on the atomics' order; the
-// bitmap (an OR) does not.  lds: >= bloom_bin_lds(pl) bytes.  Called by the whole workgroup.
+// (hh[j], dd[j]), nk keys.  An LDS counting sort by slice (histogram, scan, scatter), then every
+// slice's run is written to the tile's slot with consecutive lanes on consecutive words (coalesced;
+// storing each probe straight to its slot measured 3x slower: one cache line per lane).  lds: >=
+// bloom_bin_lds(pl) bytes.  Called by the whole workgroup (barriers inside).
 template <uint32_t KPT>
 SDB_DEV void bloom_bin_core(uint32_t tile, const uint32_t (&hh)[KPT], const uint32_t (&dd)[KPT], uint32_t nk,
                             const BloomPlan &pl, const BloomSlots &q, uint32_t *lds) {
     const uint32_t S = pl.nslices;
-    uint32_t *cnt = lds;  // S: next free position of each slice's slot
-    const uint32_t tid = threadIdx.x, nt = blockDim.x;
-    for (uint32_t x = tid; x < S; x += nt) cnt[x] = 0;
+    uint32_t *hist = lds;        // S: counts, then local run starts
+    uint32_t *cur = hist + S;    // S: local scatter cursors
+    uint32_t *sorted = cur + S;  // nk * k probes, slice order
+    __shared__ uint64_t s_w[17];
+    const uint32_t tid = threadIdx.x, nt = blockDim.x, np = nk * pl.k;
+    for (uint32_t x = tid; x < S; x += nt) hist[x] = 0;
     __syncthreads();
-    uint32_t *slots = q.slot + (uint64_t)tile * q.cap;  // slot (sl, tile) at slots + sl * tiles * cap
-    const uint64_t stride = (uint64_t)pl.tiles * q.cap;
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; j++)
+        if (tid + j * nt < nk) probes_hd(hh[j], dd[j], pl.k, pl.m, [&](uint32_t p) { atomicAdd(&hist[p >> pl.sb], 1u); });
+    __syncthreads();
+    // local run starts (exclusive scan); run lengths -> count[tile][s]
+    uint64_t carry = 0;
+    for (uint32_t x0 = 0; x0 < S; x0 += nt) {
+        const uint32_t x = x0 + tid;
+        const uint32_t c = x < S ? hist[x] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_excl_scan_u64(c, s_w, &tot);
+        if (x < S) {
+            q.count[(uint64_t)tile * S + x] = c <= q.cap ? c : kSlotOverflow;
+            hist[x] = (uint32_t)(carry + ex);
+            cur[x] = (uint32_t)(carry + ex);
+        }
+        carry += tot;
+    }
+    __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < KPT; j++)
         if (tid + j * nt < nk)
-            probes_hd(hh[j], dd[j], pl.k, pl.m, [&](uint32_t p) {
-                const uint32_t sl = p >> pl.sb;
-                const uint32_t pos = atomicAdd(&cnt[sl], 1u);
-                if (pos < q.cap) slots[sl * stride + pos] = p;
-            });
+            probes_hd(hh[j], dd[j], pl.k, pl.m, [&](uint32_t p) { sorted[atomicAdd(&cur[p >> pl.sb], 1u)] = p; });
     __syncthreads();
-    for (uint32_t x = tid; x < S; x += nt) {
-        const uint32_t c = cnt[x];
-        q.count[(uint64_t)tile * S + x] = c <= q.cap ? c : kSlotOverflow;
+    // write the runs: sorted[x] belongs to slice sl = p >> sb at run position x - hist[sl]
+    const uint64_t stride = (uint64_t)pl.tiles * q.cap;
+    uint32_t *slots = q.slot + (uint64_t)tile * q.cap;
+    for (uint32_t x = tid; x < np; x += nt) {
+        const uint32_t p = sorted[x], sl = p >> pl.sb;
+        const uint32_t pos = x - hist[sl];
+        if (pos < q.cap) slots[sl * stride + pos] = p;
     }
 }
 

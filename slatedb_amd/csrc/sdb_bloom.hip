@@ -71,7 +71,10 @@ BloomPlan bloom_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes, uint32_t til
     pl.nslices = (uint32_t)(((uint64_t)pl.m + (1ull << pl.sb) - 1) >> pl.sb);
     if (pl.nslices == 0) pl.nslices = 1;
     uint32_t T = tile_keys;
-    if (!T) T = kBinThreads * kBinKeysPerThread;  // kBinKeysPerThread keys per thread
+    if (!T) {  // kBinKeysPerThread keys per thread, fewer when the sorted probes outgrow LDS
+        T = kBinThreads * kBinKeysPerThread;
+        while (T > kBinThreads && 4ull * (2 * pl.nslices + (uint64_t)T * pl.k) > kBinLds) T -= kBinThreads;
+    }
     pl.T = T;
     pl.tiles = (uint32_t)((n + T - 1) / T);
     if (pl.tiles == 0) pl.tiles = 1;
@@ -114,7 +117,7 @@ BloomSlots bloom_slots(void *ws, const BloomPlan &pl) {
     return q;
 }
 
-size_t bloom_bin_lds(const BloomPlan &pl) { return 4 * (size_t)pl.nslices; }
+size_t bloom_bin_lds(const BloomPlan &pl) { return 4 * (2 * (size_t)pl.nslices + (size_t)pl.T * pl.k); }
 size_t bloom_fill_lds(const BloomPlan &pl) { return 4 * ((size_t)(1u << (pl.sb - 5)) + pl.tiles); }
 
 hipError_t launch_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,

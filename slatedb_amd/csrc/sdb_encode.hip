@@ -26,6 +26,8 @@
 //               assembled directly in HBM by one workgroup each.
 #include <stdlib.h>
 
+#include <mutex>
+
 #include "sdb_bloom.h"
 #include "sdb_crc.h"
 
@@ -322,11 +324,10 @@ __global__ __launch_bounds__(kSegThreads, SDB_SEG_WAVES) void k_seg(EncodeArgs a
     const bool v2 = a.version == 2 && bs <= (1u << 20);
     const uint32_t ri = a.restart_interval;
     PHASE_MARK(0);
-    // a. row sizes of the staged span (k_facts) and, for the fused bloom, the chunk's (h0, d0)
+    // a. row sizes of the staged span (k_facts)
     constexpr uint32_t kPerT = kSegSpan / kSegThreads;
     const uint32_t lane = (uint32_t)lane_id();
     uint32_t zr[kPerT], znr[kPerT];
-    uint64_t hdv[kHashPerT];
 #pragma unroll
     for (uint32_t u = 0; u < kPerT; u++) {
         const uint32_t x = tid + u * nt;
@@ -335,11 +336,6 @@ __global__ __launch_bounds__(kSegThreads, SDB_SEG_WAVES) void k_seg(EncodeArgs a
             zr[u] = a.szr[cs + x];
             znr[u] = a.sznr[cs + x];
         }
-    }
-#pragma unroll
-    for (uint32_t r = 0; r < kHashPerT; r++) {
-        const uint32_t x = tid + r * nt;
-        hdv[r] = (a.bloom_fused && x < cn) ? a.hd[cs + x] : 0;
     }
 #pragma unroll
     for (uint32_t u = 0; u < kPerT; u++) {
@@ -518,17 +514,6 @@ __global__ __launch_bounds__(kSegThreads, SDB_SEG_WAVES) void k_seg(EncodeArgs a
         a.tab_bytes[t] = by;
     }
     PHASE_MARK(5);
-    // e. bloom: the chunk's probes -> its slots (tile = chunk); the staged sizes above are dead
-    if (a.bloom_fused) {
-        uint32_t hh[kHashPerT], dd[kHashPerT];
-#pragma unroll
-        for (uint32_t r = 0; r < kHashPerT; r++) {
-            hh[r] = (uint32_t)hdv[r];
-            dd[r] = (uint32_t)(hdv[r] >> 32);
-        }
-        __syncthreads();
-        bloom_bin_core<kHashPerT>(k, hh, dd, cn, a.bpl, a.bq, (uint32_t *)smem);
-    }
     PHASE_MARK(6);
 }
 
@@ -809,10 +794,6 @@ __global__ __launch_bounds__(kEnumThreads) void k_enum(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint64_t s_anc[4];  // entry point, first block, first byte, blocks of this chunk
     const uint32_t k = blockIdx.x, K = a.nchunks;
-    if (k >= K) {  // bloom role: OR one slice's queued probes into LDS, write the slice
-        bloom_fill_slice(k - K, a.key_bytes, a.key_off, a.n, a.bpl, a.bq, a.bloom_out, a.bloom_len, (uint32_t *)smem);
-        return;
-    }
     if (*a.err != ~0ull) return;
     const uint64_t cs = (uint64_t)k * kChunk;
     const uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
@@ -1751,8 +1732,57 @@ static void set_lds_attrs() {
     hipFuncSetAttribute((const void *)k_enum, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEnumLds);
     hipFuncSetAttribute((const void *)k_group, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGroupLds);
     hipFuncSetAttribute((const void *)k_seg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLdsMax);
+
     lds_attrs_set = true;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Bloom (fused with the encode's k_facts hashes): bin tiles of kChunk keys' probes into (tile, slice)
+// slots, then one workgroup per slice ORs them into LDS and writes the bitmap slice (sdb_bloom.h).
+// They run on a per-device side stream forked after k_facts and joined after k_emit, so they fill
+// the CUs the latency-bound k_seg / k_group / k_enum leave idle.
+// ------------------------------------------------------------------------------------------------
+static_assert(kChunk == kBinThreads * kHashPerT, "bloom tiles are k_facts hash tiles of kChunk keys");
+__global__ __launch_bounds__(kBinThreads) void k_bloom_bin_hd(EncodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t blds[];
+    const uint32_t tile = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    const uint64_t k0 = (uint64_t)tile * a.bpl.T;
+    const uint32_t nk = (uint32_t)((k0 + a.bpl.T < a.n ? k0 + a.bpl.T : a.n) - k0);
+    uint32_t hh[kHashPerT], dd[kHashPerT];
+#pragma unroll
+    for (uint32_t r = 0; r < kHashPerT; r++) {
+        const uint32_t x = tid + r * nt;
+        const uint64_t v = x < nk ? a.hd[k0 + x] : 0;
+        hh[r] = (uint32_t)v;
+        dd[r] = (uint32_t)(v >> 32);
+    }
+    bloom_bin_core<kHashPerT>(tile, hh, dd, nk, a.bpl, a.bq, blds);
+}
+__global__ __launch_bounds__(kFillThreads) void k_bloom_fill_hd(EncodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t blds[];
+    bloom_fill_slice(blockIdx.x, a.key_bytes, a.key_off, a.n, a.bpl, a.bq, a.bloom_out, a.bloom_len, blds);
+}
+
+namespace {
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+std::mutex g_side_mu;
+SideStream g_side[64];
+SideStream *side_for_current_device() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    SideStream &ss = g_side[dev];
+    if (!ss.s) {
+        if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess)
+            return nullptr;
+    }
+    return &ss;
+}
+}  // namespace
 
 hipError_t launch_encode(EncodeArgs a, hipStream_t st) {
     set_lds_attrs();
@@ -1764,10 +1794,34 @@ hipError_t launch_encode(EncodeArgs a, hipStream_t st) {
     a.nprep_wg = a.nchunks;
     a.nfacts = (uint32_t)((a.n + kFactsThreads - 1) / kFactsThreads);
     a.seg_lds = kSegLds;
-    if (a.bloom_fused && bloom_bin_lds(a.bpl) > a.seg_lds) a.seg_lds = (uint32_t)bloom_bin_lds(a.bpl);
     stage_mark(st, kStFacts, true);
     hipLaunchKernelGGL(k_facts, dim3(a.nfacts), dim3(kFactsThreads), 0, st, a);
     stage_mark(st, kStFacts, false);
+    // the bloom: fork a side stream after k_facts (it needs only the hashes), join it at the end
+    std::unique_lock<std::mutex> lk(g_side_mu, std::defer_lock);
+    SideStream *side = nullptr;
+    if (a.bloom_fused) {
+        lk.lock();
+        static bool fill_attr = false;
+        if (!fill_attr) {
+            (void)hipFuncSetAttribute((const void *)k_bloom_fill_hd, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+            (void)hipFuncSetAttribute((const void *)k_bloom_bin_hd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLds);
+            (void)hipGetLastError();
+            fill_attr = true;
+        }
+        side = side_for_current_device();
+        hipStream_t bs = st;
+        if (side) {
+            (void)hipEventRecord(side->fork, st);
+            (void)hipStreamWaitEvent(side->s, side->fork, 0);
+            bs = side->s;
+        }
+        stage_mark(bs, kStBloom, true);
+        hipLaunchKernelGGL(k_bloom_bin_hd, dim3(a.bpl.tiles), dim3(kBinThreads), bloom_bin_lds(a.bpl), bs, a);
+        hipLaunchKernelGGL(k_bloom_fill_hd, dim3(a.bpl.nslices), dim3(kFillThreads), bloom_fill_lds(a.bpl), bs, a);
+        stage_mark(bs, kStBloom, false);
+        if (side) (void)hipEventRecord(side->join, side->s);
+    }
     stage_mark(st, kStSeg, true);
     hipLaunchKernelGGL(k_seg, dim3(a.nchunks), dim3(kSegThreads), a.seg_lds, st, a);
     stage_mark(st, kStSeg, false);
@@ -1776,12 +1830,13 @@ hipError_t launch_encode(EncodeArgs a, hipStream_t st) {
     hipLaunchKernelGGL(k_group, dim3(ngroups), dim3(kGroupThreads), kGroupLds, st, a);
     stage_mark(st, kStGroup, false);
     stage_mark(st, kStEnum, true);
-    hipLaunchKernelGGL(k_enum, dim3(a.nchunks + (a.bloom_fused ? a.bpl.nslices : 0)), dim3(kEnumThreads), kEnumLds, st, a);
+    hipLaunchKernelGGL(k_enum, dim3(a.nchunks), dim3(kEnumThreads), kEnumLds, st, a);
     stage_mark(st, kStEnum, false);
     stage_mark(st, kStEmit, true);
     if (a.version == 2) hipLaunchKernelGGL(k_emit<2>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, a);
     else hipLaunchKernelGGL(k_emit<1>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, a);
     stage_mark(st, kStEmit, false);
+    if (side) (void)hipStreamWaitEvent(st, side->join, 0);  // join: the caller's stream ends after the bloom
     return hipGetLastError();
 }
 
