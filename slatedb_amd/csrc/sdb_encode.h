@@ -188,3 +188,4 @@ hipError_t launch_bloom_query(const uint8_t *bitmap, uint64_t bitmap_bytes, uint
 
 }  // namespace sdb
 static_assert(sdb::kSegSpan % sdb::kSegThreads == 0 && sdb::kChunk % 64 == 0, "k_seg geometry");
+static_assert(sdb::kEmitLds <= 160 * 1024, "k_emit LDS");
