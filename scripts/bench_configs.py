@@ -86,6 +86,21 @@ def decode_bench(reps):
     with torch.cuda.stream(s):
         ms = timed(run, reps, s)
     torch.cuda.synchronize()
+    if os.environ.get("SDB_DEC_PHASE"):  # phase ticks of one full decode (timing build only)
+        cd = C.CDLL(runtime.LIB_PATH)
+        cd.sdb_diag_dec_phase.argtypes = [C.c_void_p]
+        b0 = np.zeros((2, 8192, 4), np.uint64)
+        b1 = np.zeros((2, 8192, 4), np.uint64)
+        cd.sdb_diag_dec_phase(b0.ctypes.data)
+        with torch.cuda.stream(s):
+            run()
+        torch.cuda.synchronize()
+        cd.sdb_diag_dec_phase(b1.ctypes.data)
+        d = (b1 - b0).astype(np.int64)
+        for pas, name, labels in ((0, "count", ["stage+crc", "tally", "-"]), (1, "emit", ["stage", "walk+cols", "keystore"])):
+            nbk = max(int(d[pas, :, 3].sum()), 1)
+            per = d[pas, :, :3].sum(axis=0) / nbk
+            print("%s: %d blocks; ticks per block: %s" % (name, nbk, "  ".join("%s %.0f" % (l, v) for l, v in zip(labels, per))), flush=True)
     sm = _abi.DecodeSummary.from_buffer_copy(smy.cpu().numpy().tobytes()[:C.sizeof(_abi.DecodeSummary)])
     ok = sm.status == 0 and sm.num_entries == nent and sm.num_bad_blocks == 0
     ok = ok and np.array_equal(ka[:kbytes].cpu().numpy(), np.concatenate(keys))

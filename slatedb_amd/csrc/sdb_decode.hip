@@ -11,12 +11,23 @@
 // D2 scan    exclusive scans over blocks (tile sums -> tile scan -> apply).
 // D3 emit    one wave per block: parse again and write keys (restored against the previous key),
 //            value references into `blocks`, seq, flags and timestamps.
+#include <type_traits>
+
 #include "sdb_decode.h"
 #include "sdb_crc.h"
 #include "sdb_device.h"
 
 namespace sdb {
 
+#ifdef SDB_PHASE_TIMING
+__device__ uint64_t g_dec_phase[2][8192][4];  // [count / emit][wave][phase] s_memtime ticks
+#define DEC_T(var) const uint64_t var = __builtin_amdgcn_s_memtime()
+#define DEC_ACC(pass, ph, dt) \
+    do { if (lane_id() == 0 && gwave < 8192) g_dec_phase[pass][gwave][ph] += (dt); } while (0)
+#else
+#define DEC_T(var) do { } while (0)
+#define DEC_ACC(pass, ph, dt) do { } while (0)
+#endif
 constexpr uint32_t kDecThreads = 1024;                   // 16 waves: one workgroup (and CRC table copy) per CU
 constexpr uint32_t kDecImg = 4096 + 32;                  // fast path: staged block image per wave
 constexpr uint32_t kDecKeys = 2048;                      // fast path: restored keys of one block
@@ -476,6 +487,59 @@ SDB_DEV Tally tally_v2(const BlockViewT<P> &v) {
     return t;
 }
 
+// Regular V2 blocks staged in LDS, fast path: each region lane walks its rows reading only the header
+// (one 4-byte window: single-byte varints) and stepping by hdr + unshared + vlen + 9, i.e. assuming no
+// timestamps; every row's flags byte is read off the critical path and checked after the walk.  Any
+// multi-byte varint, timestamp or bad flag sends the block to the exact walk (tally_v2).
+SDB_DEV uint32_t lds_read4(const lu8 *p) {
+    const uint32_t addr = lds_addr((const void *)p), sh = addr & 3;
+    const lu32 *d = (const lu32 *)(uintptr_t)(addr & ~3u);
+    return __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+}
+
+SDB_DEV bool tally_v2_fast(const LdsBlockView &v, Tally &t) {
+    const int l = lane_id();
+    const uint32_t R = v.count;
+    if (R == 0 || rd_be(v.offs, 2) != 0) return false;
+    uint32_t my_entries = 0, my_kb = 0;
+    bool ok = true;
+    for (uint32_t q = l; q < R && ok; q += 64) {
+        const uint32_t pos = (uint32_t)rd_be(v.offs + 2 * q, 2);
+        const uint32_t end = (q + 1 < R) ? (uint32_t)rd_be(v.offs + 2 * q + 2, 2) : v.data_end;
+        if (end <= pos || end > v.data_end) {
+            ok = false;
+            break;
+        }
+        uint32_t p = pos, prevlen = 0, fl = 0, bad = 0;
+        bool first = true;
+        while (p < end) {
+            const uint32_t h = lds_read4(v.d + p);
+            // the previous row's flags (read one step earlier, off the chain): value, tombstone or merge
+            // only (no timestamps, not both kinds, no unknown bits)
+            bad |= (fl != 0 && fl != SDB_FLAG_TOMBSTONE && fl != SDB_FLAG_MERGE_OPERAND) ? 1u : 0u;
+            const uint32_t sh = h & 0xFF, un = (h >> 8) & 0xFF, vl = (h >> 16) & 0xFF;
+            if ((h & 0x808080u) || (first && sh) || (!first && sh > prevlen) || p + 12 + un + vl > end) {
+                ok = false;
+                break;
+            }
+            fl = v.d[p + 11 + un + vl];
+            first = false;
+            prevlen = sh + un;
+            my_entries++;
+            my_kb += prevlen;
+            p += 12 + un + vl;
+        }
+        bad |= (fl != 0 && fl != SDB_FLAG_TOMBSTONE && fl != SDB_FLAG_MERGE_OPERAND) ? 1u : 0u;
+        if (p != end || bad) ok = false;
+    }
+    if (__ballot(!ok) != 0) return false;
+    t.entries = wave_sum((uint64_t)my_entries);
+    t.key_bytes = wave_sum((uint64_t)my_kb);
+    t.status = 0;
+    t.sequential = false;
+    return true;
+}
+
 template <typename P>
 SDB_DEV Tally tally_v1(const BlockViewT<P> &v) {
     Tally t{0, 0, 0, false};
@@ -536,13 +600,24 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
     lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kDecWaveLds;
     uint8_t *stage = (uint8_t *)img;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    (void)gwave;
     for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave; k < a.nblocks; k += nwaves) {
+        DEC_T(t0);
         const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
         Tally t{0, 0, 0, false};
         if (dec_fast(s, e)) {
             const LdsBlockView v = stage_lds(a, s, e, img, true);
+            DEC_T(t1);
             t.status = v.status;
-            if (!v.status) t = (a.version == 2) ? tally_v2(v) : tally_v1(v);
+            if (!v.status) {
+                if (a.version == 1) t = tally_v1(v);
+                else if (!tally_v2_fast(v, t)) t = tally_v2(v);
+            }
+            DEC_T(t2);
+            DEC_ACC(0, 0, t1 - t0);
+            DEC_ACC(0, 1, t2 - t1);
+            DEC_ACC(0, 3, 1);
         } else {
             const BlockView v = load_block(a, k, stage, crc);
             t.status = v.status;
@@ -597,7 +672,35 @@ SDB_DEV void emit_v2(const DecodeArgs &a, const BlockViewT<P> &v, bool sequentia
         for (uint32_t q0 = 0; q0 < R; q0 += 64) {
             const uint32_t q = q0 + l;
             uint32_t pos = 0, end = 0, ne = 0, nk = 0;
-            if (q < R) {
+            bool exact = true;
+            if constexpr (std::is_same<P, const lu8 *>::value) {
+                // header-only steps (single-byte varints, no timestamps), flags checked off the chain;
+                // any other shape in the batch: the exact walk below
+                bool ok = true;
+                if (q < R) {
+                    pos = (uint32_t)rd_be(v.offs + 2 * q, 2);
+                    end = (q + 1 < R) ? (uint32_t)rd_be(v.offs + 2 * q + 2, 2) : v.data_end;
+                    uint32_t p = pos, fl = 0, bad = 0;
+                    while (p < end) {
+                        const uint32_t h = lds_read4(v.d + p);
+                        bad |= (fl & (SDB_FLAG_HAS_EXPIRE_TS | SDB_FLAG_HAS_CREATE_TS)) ? 1u : 0u;
+                        const uint32_t un = (h >> 8) & 0xFF, vl = (h >> 16) & 0xFF;
+                        if ((h & 0x808080u) || p + 12 + un + vl > end) {
+                            ok = false;
+                            break;
+                        }
+                        fl = v.d[p + 11 + un + vl];
+                        ne++;
+                        nk += (h & 0xFF) + un;
+                        p += 12 + un + vl;
+                    }
+                    bad |= (fl & (SDB_FLAG_HAS_EXPIRE_TS | SDB_FLAG_HAS_CREATE_TS)) ? 1u : 0u;
+                    if (p != end || bad) ok = false;
+                }
+                exact = __ballot(!ok) != 0;
+                if (exact) ne = nk = 0;
+            }
+            if (exact && q < R) {
                 pos = (uint32_t)rd_be(v.offs + 2 * q, 2);
                 end = (q + 1 < R) ? (uint32_t)rd_be(v.offs + 2 * q + 2, 2) : v.data_end;
                 uint32_t p = pos;
@@ -713,6 +816,8 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
     lu8 *kbuf = img + kDecImg;
     uint8_t *stage = (uint8_t *)img;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    (void)gwave;
     // capacity guard: if the counted output does not fit the caller's arrays, write nothing
     if (a.ent_start[a.nblocks] > a.out.cap_entries || a.key_start[a.nblocks] > a.out.key_arena_cap) return;
     for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave; k < a.nblocks; k += nwaves) {
@@ -724,18 +829,26 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
         const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
         const bool seq = a.flag[k] != 0;
         if (dec_fast(s, e)) {
+            DEC_T(t0);
             const LdsBlockView v = stage_lds(a, s, e, img, false);
             if (v.status) continue;  // cannot happen: the count pass accepted it
+            DEC_T(t1);
             if (a.version == 1) {
                 emit_v1(a, v, ent0, kb0, s);
             } else {
                 const bool lds_keys = kbn + 16 <= kDecKeys;
                 emit_v2(a, v, seq, ent0, kb0, s, lds_keys ? kbuf : nullptr);
+                DEC_T(t2);
                 if (lds_keys) {
                     wave_sync_d();
                     wave_store_bytes(a.out.key_arena + kb0, kbuf, kbn);
                 }
+                DEC_T(t3);
+                DEC_ACC(1, 1, t2 - t1);
+                DEC_ACC(1, 2, t3 - t2);
             }
+            DEC_ACC(1, 0, t1 - t0);
+            DEC_ACC(1, 3, 1);
         } else {
             const BlockView v = load_block(a, k, stage, crc);
             if (v.status) continue;
@@ -862,3 +975,9 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
 }
 
 }  // namespace sdb
+
+#ifdef SDB_PHASE_TIMING
+extern "C" int sdb_diag_dec_phase(uint64_t *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(sdb::g_dec_phase), sizeof(uint64_t) * 2 * 8192 * 4) == hipSuccess ? 0 : -1;
+}
+#endif
