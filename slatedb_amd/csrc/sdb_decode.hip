@@ -33,7 +33,9 @@ constexpr uint32_t kDecImg = 4096 + 32;                  // fast path: staged bl
 constexpr uint32_t kDecKeys = 2048;                      // fast path: restored keys of one block
 constexpr uint32_t kDecWaveLds = kDecImg + kDecKeys;
 constexpr uint32_t kDecLds = kCrcTablesLds + (kDecThreads / 64) * kDecWaveLds;
-constexpr uint32_t kDecCap = kDecWaveLds;  // other blocks: generic staging per wave; larger ones parse from HBM
+constexpr uint32_t kDecCap = kDecWaveLds;
+constexpr uint32_t kRowTmp = kDecKeys - 256;  // emit: row positions of the lane-per-row path (4 x 32 u16) in kbuf
+typedef __attribute__((address_space(3))) uint16_t lu16;  // other blocks: generic staging per wave; larger ones parse from HBM
 
 template <typename P>
 SDB_DEV uint64_t rd_be(P p, int nb) {
@@ -646,6 +648,10 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
 // create_ts / expire_ts are valid iff the flag is set).
 SDB_DEV void put_entry(const DecodeArgs &a, uint64_t idx, uint64_t kpos, uint64_t vref, uint32_t vlen, uint64_t seq,
                        uint8_t flags, int64_t cts, int64_t ets) {
+#ifdef SDB_EXP_NO_PUT
+    if (seq == 0x123456789ull) a.out.key_off[idx] = kpos;  // experiment: no column stores
+    return;
+#endif
     a.out.key_off[idx] = kpos;
     a.out.val_off[idx] = vlen ? vref : 0;
     a.out.val_len[idx] = vlen;
@@ -653,6 +659,32 @@ SDB_DEV void put_entry(const DecodeArgs &a, uint64_t idx, uint64_t kpos, uint64_
     a.out.flags[idx] = flags;
     if (flags & SDB_FLAG_HAS_CREATE_TS) a.out.create_ts[idx] = cts;
     if (flags & SDB_FLAG_HAS_EXPIRE_TS) a.out.expire_ts[idx] = ets;
+}
+
+// Keys of <= 16 bytes as two little-endian u64 (byte x at bits 8x): key = cur[:shared] ++ suffix, the
+// suffix a 16-byte window (restore_full_key, row_codec_v2.rs:83-89, on the VALU).  Bytes past the key
+// are garbage.
+SDB_DEV void key16_merge(uint64_t &lo, uint64_t &hi, uint32_t shared, const uint32_t (&w)[4]) {
+    const uint64_t slo = (uint64_t)w[0] | ((uint64_t)w[1] << 32), shi = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+    const uint32_t b = 8 * shared;  // 0 .. 128
+    uint64_t tlo, thi, mlo, mhi;    // suffix << b; mask of the kept prefix bytes
+    if (b == 0) {
+        tlo = slo;
+        thi = shi;
+        mlo = mhi = 0;
+    } else if (b < 64) {
+        tlo = slo << b;
+        thi = (shi << b) | (slo >> (64 - b));
+        mlo = ~0ull >> (64 - b);
+        mhi = 0;
+    } else {
+        tlo = 0;
+        thi = b < 128 ? slo << (b - 64) : 0;
+        mlo = ~0ull;
+        mhi = b == 64 ? 0 : (b >= 128 ? ~0ull : ~0ull >> (128 - b));
+    }
+    lo = (lo & mlo) | (tlo & ~mlo);
+    hi = (hi & mhi) | (thi & ~mhi);
 }
 
 // V2 emit of one block (BlockIteratorV2 ascending, block_iterator_v2.rs:235-267; restore_full_key,
@@ -690,6 +722,7 @@ SDB_DEV void emit_v2(const DecodeArgs &a, const BlockViewT<P> &v, bool sequentia
                             break;
                         }
                         fl = v.d[p + 11 + un + vl];
+                        if (kbuf && q < 4 && ne < 32) ((lu16 *)(kbuf + kRowTmp))[q * 32 + ne] = (uint16_t)p;
                         ne++;
                         nk += (h & 0xFF) + un;
                         p += 12 + un + vl;
@@ -714,7 +747,91 @@ SDB_DEV void emit_v2(const DecodeArgs &a, const BlockViewT<P> &v, bool sequentia
             }
             const uint64_t ie = wave_incl_scan((uint64_t)ne), ik = wave_incl_scan((uint64_t)nk);
             uint64_t idx = ecarry + ie - ne, kp = kcarry + ik - nk;
-            if (q < R) {
+            bool done_fast = false;
+            if constexpr (std::is_same<P, const lu8 *>::value) {
+                // lane = row: the block has the fast shape, <= 4 regions of <= 32 rows, <= 64 rows, keys of
+                // <= 16 bytes, and walk 1 recorded every row's position; the rows are parsed in parallel
+                // and key byte b of row j is suffix byte b of the last row r <= j with shared_r <= b (a
+                // max-scan over the lanes per byte position)
+                const uint32_t NE = (uint32_t)wave_readlane(ie, 63);
+                const uint32_t maxne = wave_max(q < R ? ne : 0u);
+                const uint64_t kbn_blk = wave_readlane(ik, 63);
+                if (!exact && kbuf && q0 == 0 && R <= 4 && NE <= 64 && maxne <= 32 && kbn_blk + 16 <= kRowTmp) {
+                    const uint32_t j = l;
+                    const bool live = j < NE;
+                    const uint32_t exn = (uint32_t)(ie - ne);  // region lane: its first row
+                    uint32_t qj = 0;
+#pragma unroll
+                    for (uint32_t qq = 1; qq < 4; qq++)
+                        if (qq < R && j >= (uint32_t)__builtin_amdgcn_readlane((int)exn, (int)qq)) qj = qq;
+                    const uint32_t b0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(qj << 2), (int)exn);
+                    const uint32_t pj = live ? (uint32_t)((const lu16 *)(kbuf + kRowTmp))[qj * 32 + (j - b0)] : 0;
+                    const uint32_t h = lds_read4(v.d + pj);
+                    const uint32_t sh = live ? (h & 0xFF) : 0, un = live ? (h >> 8) & 0xFF : 0, vl = (h >> 16) & 0xFF;
+                    uint32_t x[4];
+                    lds_read16(v.d + pj + 3 + un + vl, x);
+                    const uint32_t klen = sh + un;
+                    if (wave_max(klen) <= 16) {
+                        const uint32_t kinc = wave_incl_scan(klen);
+                        const uint32_t krel = kinc - klen;  // key position of row j in the block's keys
+                        const uint32_t baddr = pj + 3 - sh;  // key byte b of row j (b >= sh) is v.d[baddr + b]
+                        lu8 *dst = kbuf + ko + krel;
+#pragma unroll
+                        for (uint32_t b = 0; b < 16; b++) {
+                            const uint32_t m = (live && sh <= b) ? j : 0;
+                            const uint32_t src = wave_incl_scan_op(m, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
+                            const uint32_t sa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)baddr);
+                            if (b < klen) dst[b] = v.d[sa + b];
+                        }
+                        if (live) {
+                            const uint8_t f = (uint8_t)x[2];
+                            put_entry(a, ecarry + j, kb0 + krel, gbase + (pj + 3 + un), (f & SDB_FLAG_TOMBSTONE) ? 0 : vl,
+                                      be64_at(x[0], x[1]), f, 0, 0);
+                        }
+                        done_fast = true;
+                    }
+                }
+                if (!done_fast && !exact && kbuf) {
+                    // the batch has the fast shape (checked by the counting walk): header-only steps; the
+                    // trailer, the previous key and the suffix are 16-byte windows off the chain, and
+                    // keys of <= 16 bytes are merged in registers and written byte by byte (no waits)
+                    done_fast = true;
+                    if (q < R) {
+                        uint64_t prev_kp = 0;
+                        uint32_t p = pos;
+                        while (p < end) {
+                            const uint32_t h = lds_read4(v.d + p);
+                            const uint32_t sh = h & 0xFF, un = (h >> 8) & 0xFF, vl = (h >> 16) & 0xFF;
+                            const uint32_t t = p + 3 + un + vl;
+                            uint32_t x[4];
+                            lds_read16(v.d + t, x);
+                            const uint32_t klen = sh + un;
+                            lu8 *dst = kbuf + ko + (uint32_t)(kp - kb0);
+                            if (klen <= 16) {
+                                uint32_t pw[4] = {0, 0, 0, 0}, sw[4];
+                                if (sh) lds_read16(kbuf + ko + (uint32_t)(prev_kp - kb0), pw);
+                                lds_read16(v.d + p + 3, sw);
+                                uint64_t lo = (uint64_t)pw[0] | ((uint64_t)pw[1] << 32), hi = (uint64_t)pw[2] | ((uint64_t)pw[3] << 32);
+                                key16_merge(lo, hi, sh, sw);
+#pragma unroll
+                                for (uint32_t b = 0; b < 16; b++)
+                                    if (b < klen) dst[b] = (uint8_t)(b < 8 ? lo >> (8 * b) : hi >> (8 * (b - 8)));
+                            } else {
+                                lds_copy_small(dst, kbuf + ko + (uint32_t)(prev_kp - kb0), sh);
+                                for (uint32_t b = 0; b < un; b++) dst[sh + b] = v.d[p + 3 + b];
+                            }
+                            const uint8_t f = (uint8_t)x[2];
+                            put_entry(a, idx, kp, gbase + (p + 3 + un), (f & SDB_FLAG_TOMBSTONE) ? 0 : vl, be64_at(x[0], x[1]), f,
+                                      0, 0);
+                            prev_kp = kp;
+                            kp += klen;
+                            idx++;
+                            p = t + 9;
+                        }
+                    }
+                }
+            }
+            if (!done_fast && q < R) {
                 uint64_t prev_kp = 0;
                 uint32_t p = pos;
                 while (p < end) {
