@@ -253,6 +253,8 @@ sdb_status sdb_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, u
     a.cnt = carve<uint64_t>(workspace, wl.cnt);
     a.kbytes = carve<uint64_t>(workspace, wl.kbytes);
     a.flag = carve<uint8_t>(workspace, wl.flag);
+    a.rcnt = carve<uint64_t>(workspace, wl.rcnt);
+    a.rowpos = carve<uint16_t>(workspace, wl.rowpos);
     a.ent_start = carve<uint64_t>(workspace, wl.ent_start);
     a.key_start = carve<uint64_t>(workspace, wl.key_start);
     a.tile_x = carve<uint64_t>(workspace, wl.tile_x);

@@ -16,6 +16,8 @@ struct DecodeArgs {
     // workspace
     uint64_t *cnt, *kbytes;            // per block
     uint8_t *flag;                     // per block: 1 = sequential V2 walk
+    uint64_t *rcnt;                    // per block: rows of restart regions 0..3 (16 bits each; ~0: not recorded)
+    uint16_t *rowpos;                  // per block: 4 x 32 row positions (region q, row i at q * 32 + i)
     uint64_t *ent_start, *key_start;   // nblocks+1
     uint64_t *tile_x, *tile_y;         // per 1024-block tile (+1)
     unsigned long long *err, *nbad;
@@ -24,7 +26,7 @@ struct DecodeArgs {
 };
 
 struct DecodeWorkspace {
-    uint64_t cnt, kbytes, flag, ent_start, key_start, tile_x, tile_y, err, nbad, total;
+    uint64_t cnt, kbytes, flag, rcnt, rowpos, ent_start, key_start, tile_x, tile_y, err, nbad, total;
 };
 inline DecodeWorkspace decode_workspace_layout(uint64_t nblocks) {
     DecodeWorkspace w{};
@@ -38,6 +40,8 @@ inline DecodeWorkspace decode_workspace_layout(uint64_t nblocks) {
     w.cnt = take(8 * (nblocks + 1));
     w.kbytes = take(8 * (nblocks + 1));
     w.flag = take(nblocks + 1);
+    w.rcnt = take(8 * (nblocks + 1));
+    w.rowpos = take(256 * (nblocks + 1));
     w.ent_start = take(8 * (nblocks + 1));
     w.key_start = take(8 * (nblocks + 1));
     w.tile_x = take(8 * (nt + 1));

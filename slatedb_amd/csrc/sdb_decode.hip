@@ -499,11 +499,11 @@ SDB_DEV uint32_t lds_read4(const lu8 *p) {
     return __builtin_amdgcn_alignbyte(d[1], d[0], sh);
 }
 
-SDB_DEV bool tally_v2_fast(const LdsBlockView &v, Tally &t) {
+SDB_DEV bool tally_v2_fast(const LdsBlockView &v, Tally &t, uint16_t *rowpos, uint64_t *rcnt) {
     const int l = lane_id();
     const uint32_t R = v.count;
     if (R == 0 || rd_be(v.offs, 2) != 0) return false;
-    uint32_t my_entries = 0, my_kb = 0;
+    uint32_t my_entries = 0, my_kb = 0, my_kmax = 0;
     bool ok = true;
     for (uint32_t q = l; q < R && ok; q += 64) {
         const uint32_t pos = (uint32_t)rd_be(v.offs + 2 * q, 2);
@@ -527,6 +527,8 @@ SDB_DEV bool tally_v2_fast(const LdsBlockView &v, Tally &t) {
             fl = v.d[p + 11 + un + vl];
             first = false;
             prevlen = sh + un;
+            if (q < 4 && my_entries < 32) rowpos[q * 32 + my_entries] = (uint16_t)p;
+            my_kmax = prevlen > my_kmax ? prevlen : my_kmax;
             my_entries++;
             my_kb += prevlen;
             p += 12 + un + vl;
@@ -539,6 +541,15 @@ SDB_DEV bool tally_v2_fast(const LdsBlockView &v, Tally &t) {
     t.key_bytes = wave_sum((uint64_t)my_kb);
     t.status = 0;
     t.sequential = false;
+    // the emit pass parses lane = row straight from the recorded positions when the block has <= 4
+    // regions of <= 32 rows, <= 64 rows and keys of <= 16 bytes
+    const uint32_t mx = wave_max((uint32_t)l < R ? my_entries : 0u), kmx = wave_max(my_kmax);
+    uint64_t c = ~0ull;
+    if (R <= 4 && mx <= 32 && t.entries <= 64 && kmx <= 16) {
+        c = 0;
+        for (uint32_t q = 0; q < R; q++) c |= (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)my_entries, (int)q) << (16 * q);
+    }
+    if (l == 0) *rcnt = c;
     return true;
 }
 
@@ -608,13 +619,14 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
         DEC_T(t0);
         const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
         Tally t{0, 0, 0, false};
+        if (lane_id() == 0) a.rcnt[k] = ~0ull;  // row positions not recorded (tally_v2_fast overwrites)
         if (dec_fast(s, e)) {
             const LdsBlockView v = stage_lds(a, s, e, img, true);
             DEC_T(t1);
             t.status = v.status;
             if (!v.status) {
                 if (a.version == 1) t = tally_v1(v);
-                else if (!tally_v2_fast(v, t)) t = tally_v2(v);
+                else if (!tally_v2_fast(v, t, a.rowpos + 128 * k, a.rcnt + k)) t = tally_v2(v);
             }
             DEC_T(t2);
             DEC_ACC(0, 0, t1 - t0);
@@ -891,6 +903,43 @@ SDB_DEV void emit_v2(const DecodeArgs &a, const BlockViewT<P> &v, bool sequentia
     }
 }
 
+// V2 emit, lane = row, for blocks whose row positions the count pass recorded (rc: rows of restart
+// regions 0..3, 16 bits each; pos: 4 x 32 positions): no walk at all.  Key byte b of row j is suffix byte
+// b of the last row r <= j with shared_r <= b (a max-scan over the lanes per byte position).
+SDB_DEV void emit_v2_rows(const DecodeArgs &a, const LdsBlockView &v, uint64_t rc, const uint16_t *pos, uint64_t ent0,
+                          uint64_t kb0, uint64_t gbase, lu8 *kbuf) {
+    const uint32_t j = (uint32_t)lane_id();
+    const uint32_t c0 = rc & 0xFFFF, c1 = (rc >> 16) & 0xFFFF, c2 = (rc >> 32) & 0xFFFF, c3 = (rc >> 48) & 0xFFFF;
+    const uint32_t NE = c0 + c1 + c2 + c3;
+    const bool live = j < NE;
+    uint32_t q = 0, i = j;
+    if (i >= c0) { i -= c0; q = 1; }
+    if (q == 1 && i >= c1) { i -= c1; q = 2; }
+    if (q == 2 && i >= c2) { i -= c2; q = 3; }
+    const uint32_t pj = live ? pos[q * 32 + i] : 0;
+    const uint32_t h = lds_read4(v.d + pj);
+    const uint32_t sh = live ? (h & 0xFF) : 0, un = live ? (h >> 8) & 0xFF : 0, vl = (h >> 16) & 0xFF;
+    uint32_t x[4];
+    lds_read16(v.d + pj + 3 + un + vl, x);
+    const uint32_t klen = sh + un;
+    const uint32_t kinc = wave_incl_scan(klen);
+    const uint32_t krel = kinc - klen;   // key position of row j among the block's keys
+    const uint32_t baddr = pj + 3 - sh;  // key byte b of row j (b >= sh) is v.d[baddr + b]
+    lu8 *dst = kbuf + (uint32_t)(kb0 & 15) + krel;
+#pragma unroll
+    for (uint32_t b = 0; b < 16; b++) {
+        const uint32_t m = (live && sh <= b) ? j : 0;
+        const uint32_t src = wave_incl_scan_op(m, [](uint32_t u, uint32_t w) { return u > w ? u : w; });
+        const uint32_t sa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)baddr);
+        if (b < klen) dst[b] = v.d[sa + b];
+    }
+    if (live) {
+        const uint8_t f = (uint8_t)x[2];
+        put_entry(a, ent0 + j, kb0 + krel, gbase + (pj + 3 + un), (f & SDB_FLAG_TOMBSTONE) ? 0 : vl, be64_at(x[0], x[1]), f, 0,
+                  0);
+    }
+}
+
 // V1 emit (BlockIterator, block_iterator.rs:54-267): lane = entry, key = first key's prefix + suffix.
 template <typename P>
 SDB_DEV void emit_v1(const DecodeArgs &a, const BlockViewT<P> &v, uint64_t ent0, uint64_t kb0, uint64_t gbase) {
@@ -954,7 +1003,9 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
                 emit_v1(a, v, ent0, kb0, s);
             } else {
                 const bool lds_keys = kbn + 16 <= kDecKeys;
-                emit_v2(a, v, seq, ent0, kb0, s, lds_keys ? kbuf : nullptr);
+                const uint64_t rc = seq ? ~0ull : a.rcnt[k];
+                if (rc != ~0ull && kbn + 16 <= kRowTmp) emit_v2_rows(a, v, rc, a.rowpos + 128 * k, ent0, kb0, s, kbuf);
+                else emit_v2(a, v, seq, ent0, kb0, s, lds_keys ? kbuf : nullptr);
                 DEC_T(t2);
                 if (lds_keys) {
                     wave_sync_d();
