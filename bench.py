@@ -95,6 +95,17 @@ def cpu_baseline(budget_s, threads):
                                                           sum(o[0] for o in outs), model)}
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC passes over this same bench command
+    (profiles/r1_pmc_traffic.json, written by scripts/collect_profiles.py; FETCH_SIZE/WRITE_SIZE
+    corrected per MI355X_MICROARCH.md).  PMC counters cannot be read from inside the timed run."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")))
+        return d["per_dispatch"][kernel]["traffic_bytes"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -205,7 +216,7 @@ def main():
                    "parallelism": "independent SSTs per GPU (no collective)"},
         "roofline": {"bound": "hbm", "kernel": "k_emit", "achieved": round(emit_gbs, 1),
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(emit_gbs / PEAK_HBM_GBS, 4),
-                     "traffic": None, "algorithmic_bytes_per_launch": emit_bytes,
+                     "traffic": pmc_traffic("k_emit"), "algorithmic_bytes_per_launch": emit_bytes,
                      "avg_launch_ms": round(emit_ms, 5),
                      "pipeline": {"algorithmic_bytes_per_sst": alg_bytes, "device_ms_per_sst": round(dev_ms / args.steps, 5),
                                   "achieved_GBps": round(pipe_gbs, 1), "frac": round(pipe_gbs / PEAK_HBM_GBS, 4),
