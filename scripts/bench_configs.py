@@ -41,7 +41,7 @@ def timed(fn, reps, stream):
     return e0.elapsed_time(e1) / reps
 
 
-def decode_bench(reps):
+def decode_bench(reps, granular=True):
     lib = runtime.lib()
     dev = torch.device("cuda", 0)
     s = torch.cuda.Stream(device=dev)
@@ -111,6 +111,8 @@ def decode_bench(reps):
                       "ms": round(ms, 4), "GiB_per_s_encoded": round(enc / (ms * 1e-3) / 2**30, 2),
                       "algorithmic_bytes": alg, "achieved_GBps": round(gbs, 1), "frac": round(gbs / PEAK, 4),
                       "verified_keys": bool(ok)}), flush=True)
+    if not granular:
+        return
     # 2 MiB ranged-GET granularity (≈ 520 blocks per call), launched back to back
     per = 520
     ranges = [(b, min(nb, b + per)) for b in range(0, nb, per)]
@@ -183,6 +185,7 @@ def main():
     p.add_argument("--bloom", action="store_true")
     p.add_argument("--e2e", action="store_true")
     p.add_argument("--reps", type=int, default=20)
+    p.add_argument("--no-granular", action="store_true", help="decode: skip the 2 MiB granularity run")
     a = p.parse_args()
     allp = not (a.decode or a.bloom or a.e2e)
     torch.cuda.set_device(0)
@@ -190,7 +193,7 @@ def main():
     if a.bloom or allp:
         bloom_bench(a.reps)
     if a.decode or allp:
-        decode_bench(a.reps)
+        decode_bench(a.reps, not a.no_granular)
     if a.e2e or allp:
         e2e_bench(a.reps)
 
