@@ -206,6 +206,39 @@ sdb_status sdb_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, u
                              uint64_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * SST footer (host): everything after the data section, so data ++ footer is the whole SST object
+ * EncodedSsTableBuilder::build / EncodedWalSsTableBuilder::build hand to write_sst.
+ * Replaces EncodedSsTableFooterBuilder::build (format/sst.rs:383-487) plus the index the builders
+ * accumulate per block (sst_builder.rs:228-237, 307-313; wal/slatedb/sst_builder.rs:129-205),
+ * SstStats::encode (sst_stats.rs:52-86) and SsTableInfo::encode (format/sst.rs:195-199).
+ * Layout: [filter block + crc]? [index + crc] [stats + crc]? [SsTableInfo + crc] [u64 BE meta
+ * offset] [u16 BE version]; flatbuffer bytes identical to the `flatbuffers` 25.12.19 crate.
+ * ------------------------------------------------------------------------------------------- */
+enum { SDB_SST_COMPACTED = 0, SDB_SST_WAL = 1 };   /* SstType (schemas/sst.fbs) */
+typedef struct sdb_footer_in {
+    uint16_t sst_version;             /* trailing u16 (SST_FORMAT_VERSION: 1 or 2) */
+    uint8_t sst_type;                 /* SDB_SST_COMPACTED | SDB_SST_WAL */
+    uint8_t has_filter;               /* write the composite "_bf" filter block */
+    uint32_t num_probes;              /* Filter::encode header (filter.rs:177-180) */
+    uint64_t data_len;                /* blocks_size: bytes of the data section before the footer */
+    uint64_t num_blocks;
+    const uint64_t *block_off;        /* num_blocks: BlockMeta.offset */
+    const uint8_t *first_key_bytes;   /* BlockMeta.first_key of block k = */
+    const uint64_t *first_key_off;    /*   first_key_bytes[first_key_off[k] .. first_key_off[k+1]) */
+    const uint8_t *first_entry;       /* SsTableInfo.first_entry; NULL = None */
+    uint64_t first_entry_len;
+    const uint8_t *last_entry;        /* SsTableInfo.last_entry; NULL = None (WAL) */
+    uint64_t last_entry_len;
+    const sdb_sst_summary *stats;     /* SstStats totals; NULL = no stats block (WAL) */
+    const uint16_t *block_stats;      /* 3 per block (puts, deletes, merges) */
+    const uint8_t *bloom;             /* bitmap (has_filter) */
+    uint64_t bloom_len;
+} sdb_footer_in;
+/* Writes the footer into out[0..cap) and its length into *len.  out == NULL: size query only.
+ * cap too small: SDB_LIMIT_EXCEEDED (with *len set). */
+sdb_status sdb_sst_footer(const sdb_footer_in *in, uint8_t *out, uint64_t cap, uint64_t *len);
+
+/* ---------------------------------------------------------------------------------------------
  * Host entry points: device arena + pinned staging per handle (E2E path: H2D -> kernels -> D2H)
  * ------------------------------------------------------------------------------------------- */
 typedef struct sdb_encoder sdb_encoder;

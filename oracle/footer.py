@@ -1,0 +1,343 @@
+"""Oracle for the SST footer: filter block, index block, stats block, SsTableInfo, meta offset, version.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in slatedb_amd/ imports this; tests/ use it as the checker for
+`sdb_sst_footer` (slatedb_amd/csrc/sdb_footer.cpp).  Pure-Python loops: sized for the test cases.
+
+Restates (paths relative to /root/reference/slatedb/src):
+  - EncodedSsTableFooterBuilder::build            format/sst.rs:383-487
+  - compress_and_transform (no codec/transformer)  format/sst.rs:525-554  (data ++ crc32 BE)
+  - SsTableInfo::encode                           format/sst.rs:195-199
+  - index built by EncodedSsTableBuilder          sst_builder.rs:228-237, 307-313 (interleaved:
+    first_key vector of block k, then BlockMeta(k) at finish_block)
+  - WAL variant                                   wal/slatedb/sst_builder.rs:129-205 (first_key = seq BE)
+  - SstStats::encode                              sst_stats.rs:52-86
+  - DbFlatBufferBuilder::add_sst_info             flatbuffer_types.rs:775-800
+  - generated table builders (field add order)    generated/root_generated.rs:1238-1255 (SsTableInfo),
+    1497-1506 (BlockStats), 1631-1643 (SstStats), 1809-1817 (BlockMeta), 1923-1930 (SsTableIndex)
+and the third-party `flatbuffers` crate 25.12.19 (Cargo.lock), absent from /root/reference, whose
+published Rust FlatBufferBuilder algorithm is restated in `FBB` below: back-to-front building,
+`align` padding to the running min_align, scalars equal to their default omitted, vtables written
+after the table's soffset and deduplicated by exact byte equality, u8 vectors without a NUL, and
+`finish` aligning the root uoffset to min_align.
+
+Pins: the reference's own size assertions (index = 88 B, sst_builder.rs:1087-1139; whole 500-entry
+SST = 23,794 B compacted / 22,928 B WAL, sst_builder.rs:484-584 via SURVEY.md §4).  No reference test
+holds footer bytes, so beyond those sizes byte layout is pinned by the restated crate algorithm and
+by `parse_*` below (a schema-driven reader, schemas/sst.fbs) reading every field back.
+"""
+import struct
+import zlib
+
+
+class FBB:
+    """flatbuffers::FlatBufferBuilder (Rust, 25.12.19) — the subset the SST footer uses."""
+
+    def __init__(self, cap=1024):
+        self.buf = bytearray(cap)
+        self.head = cap
+        self.min_align = 1
+        self.field_locs = []
+        self.vtables = {}  # vtable bytes -> revpos (written_vtable_revpos; binary search = exact match)
+
+    def used(self):
+        return len(self.buf) - self.head
+
+    def _ensure(self, n):
+        while self.head < n:
+            old = len(self.buf)
+            new = max(2 * old, 1)
+            nb = bytearray(new)
+            nb[new - old + self.head:] = self.buf[self.head:]
+            self.head += new - old
+            self.buf = nb
+
+    def make_space(self, n):
+        self._ensure(n)
+        self.head -= n
+        return self.used()
+
+    def align(self, length, alignment):
+        self.min_align = max(self.min_align, alignment)
+        pad = (-(self.used() + length)) & (alignment - 1)
+        self.make_space(pad)
+
+    def push(self, fmt, v):
+        sz = struct.calcsize(fmt)
+        self.align(sz, sz)
+        self.make_space(sz)
+        struct.pack_into("<" + fmt, self.buf, self.head, v)
+        return self.used()
+
+    def push_uoffset(self, target):
+        self.align(4, 4)
+        self.make_space(4)
+        struct.pack_into("<I", self.buf, self.head, self.used() - target)
+        return self.used()
+
+    def create_vector_u8(self, data):
+        n = len(data)
+        self.align(n, 4)
+        self._ensure(n + 4)
+        self.head -= n
+        self.buf[self.head:self.head + n] = data
+        return self.push("I", n)
+
+    def create_vector_offsets(self, offs):
+        n = len(offs)
+        self.align(4 * n, 4)
+        self._ensure(4 * n + 4)
+        self.head -= 4 * n
+        top = self.used()
+        for i, t in enumerate(offs):
+            struct.pack_into("<I", self.buf, self.head + 4 * i, top - 4 * i - t)
+        return self.push("I", n)
+
+    def start_table(self):
+        self.field_locs = []
+        return self.used()
+
+    def slot(self, vt, fmt, v, default=0):
+        if v != default:
+            self.field_locs.append((vt, self.push(fmt, v)))
+
+    def slot_offset(self, vt, target):
+        self.field_locs.append((vt, self.push_uoffset(target)))
+
+    def end_table(self, tail):
+        obj = self.push("I", 0xF0F0F0F0)
+        vtlen = (max(fid for fid, _ in self.field_locs) + 2) if self.field_locs else 4
+        self.make_space(vtlen)
+        vt = bytearray(vtlen)
+        struct.pack_into("<HH", vt, 0, vtlen, obj - tail)
+        for fid, off in self.field_locs:
+            struct.pack_into("<H", vt, fid, obj - off)
+        vt = bytes(vt)
+        if vt in self.vtables:
+            self.buf[self.head:self.head + vtlen] = bytes(vtlen)
+            self.head += vtlen
+            final = self.vtables[vt]
+        else:
+            self.buf[self.head:self.head + vtlen] = vt
+            final = self.used()
+            self.vtables[vt] = final
+        struct.pack_into("<i", self.buf, len(self.buf) - obj, final - obj)
+        self.field_locs = []
+        return obj
+
+    def finish(self, root):
+        self.vtables = {}
+        self.align(4, self.min_align)
+        self.push_uoffset(root)
+        return bytes(self.buf[self.head:])
+
+
+def _checksummed(b):
+    return b + struct.pack(">I", zlib.crc32(b))
+
+
+def index_block(first_keys, block_off):
+    """SsTableIndex of one SST, in the reference's creation order (vector k, BlockMeta k, ...)."""
+    f = FBB()
+    metas = []
+    for fk, off in zip(first_keys, block_off):
+        v = f.create_vector_u8(fk)
+        t = f.start_table()
+        f.slot(4, "Q", int(off))          # BlockMeta.offset (default 0 omitted)
+        f.slot_offset(6, v)               # BlockMeta.first_key (required)
+        metas.append(f.end_table(t))
+    vec = f.create_vector_offsets(metas)
+    t = f.start_table()
+    f.slot_offset(4, vec)                 # SsTableIndex.block_meta
+    return f.finish(f.end_table(t))
+
+
+def stats_block(num_puts, num_deletes, num_merges, raw_key_size, raw_val_size, block_stats):
+    f = FBB()
+    tabs = []
+    for p, d, m in block_stats:
+        t = f.start_table()
+        f.slot(8, "H", int(m))
+        f.slot(6, "H", int(d))
+        f.slot(4, "H", int(p))
+        tabs.append(f.end_table(t))
+    vec = f.create_vector_offsets(tabs) if tabs else None
+    t = f.start_table()
+    f.slot(12, "Q", int(raw_val_size))
+    f.slot(10, "Q", int(raw_key_size))
+    f.slot(8, "Q", int(num_merges))
+    f.slot(6, "Q", int(num_deletes))
+    f.slot(4, "Q", int(num_puts))
+    if vec is not None:
+        f.slot_offset(14, vec)
+    return f.finish(f.end_table(t))
+
+
+def info_block(first_entry, last_entry, index_offset, index_len, filter_offset, filter_len,
+               sst_type, stats_offset, stats_len, compression=0, filter_format=1):
+    f = FBB()
+    fe = f.create_vector_u8(first_entry) if first_entry is not None else None
+    le = f.create_vector_u8(last_entry) if last_entry is not None else None
+    t = f.start_table()
+    f.slot(22, "Q", stats_len)
+    f.slot(20, "Q", stats_offset)
+    f.slot(12, "Q", filter_len)
+    f.slot(10, "Q", filter_offset)
+    f.slot(8, "Q", index_len)
+    f.slot(6, "Q", index_offset)
+    if le is not None:
+        f.slot_offset(18, le)
+    if fe is not None:
+        f.slot_offset(4, fe)
+    f.slot(24, "B", filter_format)
+    f.slot(16, "B", sst_type)
+    f.slot(14, "B", compression)
+    return f.finish(f.end_table(t))
+
+
+def sst_footer(data_len, first_keys, block_off, sst_version=2, sst_type=0, first_entry=None,
+               last_entry=None, stats=None, bloom=None, num_probes=0):
+    """EncodedSsTableFooterBuilder::build.  stats = (puts, deletes, merges, raw_key, raw_val,
+    block_stats) or None; bloom = bitmap bytes (a `_bf` filter is written) or None."""
+    buf = b""
+    filter_offset = data_len
+    filter_len = 0
+    if bloom is not None:
+        enc = struct.pack(">H", num_probes) + bytes(bloom)                       # filter.rs:177-180
+        comp = struct.pack(">HH", 1, 3) + b"_bf" + struct.pack(">Q", len(enc)) + enc
+        buf += _checksummed(comp)
+        filter_len = len(comp) + 4
+    idx = index_block(first_keys, block_off)
+    index_offset = data_len + len(buf)
+    buf += _checksummed(idx)
+    index_len = len(idx) + 4
+    stats_offset = stats_len = 0
+    if stats is not None:
+        sb = stats_block(*stats)
+        stats_offset = data_len + len(buf)
+        buf += _checksummed(sb)
+        stats_len = len(sb) + 4
+    meta_offset = data_len + len(buf)
+    info = info_block(first_entry, last_entry, index_offset, index_len, filter_offset, filter_len,
+                      sst_type, stats_offset, stats_len)
+    buf += _checksummed(info)
+    buf += struct.pack(">QH", meta_offset, sst_version)
+    return buf, len(idx)
+
+
+# ------------------------------------------------------------------------------------------------
+# Schema-driven reader (schemas/sst.fbs) — reads a footer back field by field.
+# ------------------------------------------------------------------------------------------------
+class _Table:
+    def __init__(self, buf, pos):
+        self.buf, self.pos = buf, pos
+        vt = pos - struct.unpack_from("<i", buf, pos)[0]
+        self.vt = vt
+        self.vtlen = struct.unpack_from("<H", buf, vt)[0]
+
+    def _fo(self, slot):
+        if slot >= self.vtlen:
+            return 0
+        return struct.unpack_from("<H", self.buf, self.vt + slot)[0]
+
+    def scalar(self, slot, fmt, default=0):
+        o = self._fo(slot)
+        return struct.unpack_from("<" + fmt, self.buf, self.pos + o)[0] if o else default
+
+    def _deref(self, slot):
+        o = self._fo(slot)
+        if not o:
+            return None
+        p = self.pos + o
+        return p + struct.unpack_from("<I", self.buf, p)[0]
+
+    def bytes_(self, slot):
+        p = self._deref(slot)
+        if p is None:
+            return None
+        n = struct.unpack_from("<I", self.buf, p)[0]
+        return bytes(self.buf[p + 4:p + 4 + n])
+
+    def tables(self, slot):
+        p = self._deref(slot)
+        if p is None:
+            return None
+        n = struct.unpack_from("<I", self.buf, p)[0]
+        out = []
+        for i in range(n):
+            e = p + 4 + 4 * i
+            out.append(_Table(self.buf, e + struct.unpack_from("<I", self.buf, e)[0]))
+        return out
+
+
+def _root(b):
+    return _Table(b, struct.unpack_from("<I", b, 0)[0])
+
+
+def parse_index(b):
+    return [(m.scalar(4, "Q"), m.bytes_(6)) for m in _root(b).tables(4)]
+
+
+def parse_stats(b):
+    r = _root(b)
+    bs = r.tables(14) or []
+    return (r.scalar(4, "Q"), r.scalar(6, "Q"), r.scalar(8, "Q"), r.scalar(10, "Q"), r.scalar(12, "Q"),
+            [(t.scalar(4, "H"), t.scalar(6, "H"), t.scalar(8, "H")) for t in bs])
+
+
+def parse_info(b):
+    r = _root(b)
+    return dict(first_entry=r.bytes_(4), index_offset=r.scalar(6, "Q"), index_len=r.scalar(8, "Q"),
+                filter_offset=r.scalar(10, "Q"), filter_len=r.scalar(12, "Q"),
+                compression=r.scalar(14, "B"), sst_type=r.scalar(16, "B"), last_entry=r.bytes_(18),
+                stats_offset=r.scalar(20, "Q"), stats_len=r.scalar(22, "Q"),
+                filter_format=r.scalar(24, "B"))
+
+
+def parse_sst(obj):
+    """SsTableFormat::read_info + read_index/read_filter/read_stats over a whole SST object
+    (format/sst.rs:600-760): returns (version, info, index, stats or None, filter payload or None),
+    checking every block's CRC."""
+    obj = bytes(obj)
+    version = struct.unpack(">H", obj[-2:])[0]
+    meta_off = struct.unpack(">Q", obj[-10:-2])[0]
+    raw = obj[meta_off:-10]
+
+    def unck(b):
+        assert struct.unpack(">I", b[-4:])[0] == zlib.crc32(b[:-4]), "checksum mismatch"
+        return b[:-4]
+
+    info = parse_info(unck(raw))
+    index = parse_index(unck(obj[info["index_offset"]:info["index_offset"] + info["index_len"]]))
+    stats = None
+    if info["stats_len"]:
+        stats = parse_stats(unck(obj[info["stats_offset"]:info["stats_offset"] + info["stats_len"]]))
+    filt = None
+    if info["filter_len"]:
+        filt = unck(obj[info["filter_offset"]:info["filter_offset"] + info["filter_len"]])
+    return version, info, index, stats, filt
+
+
+def sst_object(batch, res, sst_version=2, sst_type=0, bloom_bits_per_key=10):
+    """Whole SST object (data section ++ footer) from an encode result (oracle.SstResult or the
+    device result as host arrays): what EncodedSsTableBuilder::build + write_sst store.
+    sst_type 1 = WAL (wal/slatedb/sst_builder.rs): first_key = first seq BE, no last entry,
+    no stats, no filter."""
+    nb = len(res.block_off) - 1
+    starts = [int(x) for x in res.block_first_entry[:nb]]
+    if sst_type == 1:
+        fks = [struct.pack(">Q", int(batch.seq[s])) for s in starts]
+        first = fks[0] if nb else None
+        last = None
+        stats = None
+        bloom = None
+    else:
+        fks = [batch.key(s)[:int(res.index_key_len[k])] for k, s in enumerate(starts)]
+        first = batch.key(0) if batch.n else None
+        last = batch.key(batch.n - 1) if batch.n else None
+        sm = res.summary
+        stats = (sm.num_puts, sm.num_deletes, sm.num_merges, sm.raw_key_size, sm.raw_val_size,
+                 [tuple(int(v) for v in row) for row in res.block_stats])
+        bloom = bytes(res.bloom) if sm.filter_built else None
+    foot, _ = sst_footer(int(res.summary.data_len), fks, [int(x) for x in res.block_off[:nb]],
+                         sst_version, sst_type, first, last, stats, bloom, int(res.summary.num_probes))
+    return bytes(res.data) + foot

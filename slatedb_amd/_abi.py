@@ -108,6 +108,21 @@ class DecodeHostResult(C.Structure):
     ]
 
 
+class FooterIn(C.Structure):
+    _fields_ = [
+        ("sst_version", C.c_uint16), ("sst_type", C.c_uint8), ("has_filter", C.c_uint8),
+        ("num_probes", C.c_uint32), ("data_len", C.c_uint64), ("num_blocks", C.c_uint64),
+        ("block_off", C.c_void_p), ("first_key_bytes", C.c_void_p), ("first_key_off", C.c_void_p),
+        ("first_entry", C.c_char_p), ("first_entry_len", C.c_uint64),
+        ("last_entry", C.c_char_p), ("last_entry_len", C.c_uint64),
+        ("stats", C.c_void_p), ("block_stats", C.c_void_p), ("bloom", C.c_void_p),
+        ("bloom_len", C.c_uint64),
+    ]
+
+
+SST_COMPACTED, SST_WAL = 0, 1
+
+
 # Every symbol include/slatedb_amd.h declares, with its ctypes signature.
 SIGNATURES = {
     "sdb_abi_version": (C.c_uint32, []),
@@ -126,6 +141,7 @@ SIGNATURES = {
     "sdb_decode_workspace_bytes": (C.c_uint64, [C.c_uint64]),
     "sdb_decode_blocks": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint16,
                                     C.POINTER(DecodedOut), C.c_void_p, C.c_uint64, C.c_void_p]),
+    "sdb_sst_footer": (C.c_int, [C.POINTER(FooterIn), C.c_void_p, C.c_uint64, u64p]),
     "sdb_encoder_create": (C.c_void_p, [C.c_int, C.POINTER(SstParams)]),
     "sdb_encoder_destroy": (None, [C.c_void_p]),
     "sdb_encoder_encode_host": (C.c_int, [C.c_void_p, C.POINTER(KvBatch), C.POINTER(SstHostResult)]),

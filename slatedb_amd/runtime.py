@@ -128,6 +128,57 @@ class EncodedSst:
         return comp + struct.pack(">I", zlib.crc32(comp))
 
 
+def sst_footer(batch, enc, sst_version=2, sst_type=_abi.SST_COMPACTED):
+    """Footer bytes after the data section (sdb_sst_footer; EncodedSsTableFooterBuilder::build,
+    format/sst.rs:383-487).  `enc` is an encode result with host arrays (EncodedSst, the
+    DeviceSstOutput.to_host() dict wrapped by `_FooterView`, or anything with data/block_off/
+    block_first_entry/index_key_len/block_stats/bloom/summary).  For SST_WAL the block first keys
+    are the first entries' seq numbers, big-endian (wal/slatedb/sst_builder.rs:137-155), and there
+    is no last entry, stats or filter.  Host code: no device needed."""
+    sm = enc.summary if isinstance(enc.summary, _abi.SstSummary) else _abi.SstSummary(**enc.summary)
+    nb = len(enc.block_off) - 1 if len(enc.block_off) else 0
+    starts = np.asarray(enc.block_first_entry[:nb], np.int64)
+    if sst_type == _abi.SST_WAL:
+        seqs = (np.zeros(batch.n, np.uint64) if batch.seq is None else batch.seq)[starts]
+        fk = seqs.astype(">u8").view(np.uint8).copy()
+        fko = np.arange(nb + 1, dtype=np.uint64) * 8
+        first = fk[:8].tobytes() if nb else None
+        last = None
+    else:
+        ikl = np.asarray(enc.index_key_len[:nb], np.uint64)
+        fko = np.zeros(nb + 1, np.uint64)
+        fko[1:] = np.cumsum(ikl)
+        ks = batch.key_off[starts] if nb else np.zeros(0, np.uint64)
+        idx = np.repeat(ks - fko[:-1], ikl.astype(np.int64)) + np.arange(int(fko[-1]), dtype=np.uint64)
+        fk = batch.key_bytes[idx.astype(np.int64)].copy() if len(idx) else np.zeros(1, np.uint8)
+        first = batch.key(0) if batch.n else None
+        last = batch.key(batch.n - 1) if batch.n else None
+    boff = np.ascontiguousarray(enc.block_off[:nb], np.uint64)
+    bst = np.ascontiguousarray(np.asarray(enc.block_stats, np.uint16).reshape(-1))
+    bloom = np.ascontiguousarray(np.asarray(enc.bloom, np.uint8))
+    fk = np.ascontiguousarray(fk if len(fk) else np.zeros(1, np.uint8))
+    wal = sst_type == _abi.SST_WAL
+    fi = _abi.FooterIn(sst_version, sst_type, 0 if wal else int(bool(sm.filter_built)), sm.num_probes,
+                       int(sm.data_len), nb, boff.ctypes.data, fk.ctypes.data, fko.ctypes.data,
+                       first, len(first or b""), last, len(last or b""),
+                       None if wal else C.addressof(sm), bst.ctypes.data if len(bst) else None,
+                       bloom.ctypes.data if len(bloom) else None, 0 if wal else int(sm.bloom_len))
+    n = C.c_uint64(0)
+    st = lib().sdb_sst_footer(C.byref(fi), None, 0, C.byref(n))
+    if st:
+        raise SdbError(st, "sdb_sst_footer")
+    out = np.zeros(max(n.value, 1), np.uint8)
+    st = lib().sdb_sst_footer(C.byref(fi), out.ctypes.data, n.value, C.byref(n))
+    if st:
+        raise SdbError(st, "sdb_sst_footer")
+    return out[:n.value].tobytes()
+
+
+def sst_object(batch, enc, sst_version=2, sst_type=_abi.SST_COMPACTED):
+    """The whole SST object (data section ++ footer) that write_sst stores."""
+    return np.asarray(enc.data, np.uint8).tobytes() + sst_footer(batch, enc, sst_version, sst_type)
+
+
 class Encoder:
     """Host-buffer encoder (device arena + pinned staging + its own stream)."""
 

@@ -1,0 +1,145 @@
+"""SST footer (§8 f1): index block, stats block, composite filter block, SsTableInfo, meta offset,
+version — i.e. the whole SST object = data section ++ footer.
+
+CPU tests: the product's host builder `sdb_sst_footer` (slatedb_amd/csrc/sdb_footer.cpp, through the
+C ABI) against the oracle restatement (oracle/footer.py) on oracle-encoded data sections, plus the
+reference's own size KATs:
+  - index block = 88 B              sst_builder.rs:1087-1139 (test_sstable_index_size)
+  - 500-entry SST = 23,794 B        sst_builder.rs:484-584 (estimate 26,859 - 3065)
+  - same entries as WAL = 22,928 B  sst_builder.rs:573-583 (estimate - 2993)
+The device path (data section from the GPU, footer from its outputs) is covered in
+tests/test_gpu_parity.py::test_whole_sst_object.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+from oracle import footer as F
+from oracle import oracle as O
+from slatedb_amd import _abi, datasets, runtime
+from slatedb_amd.batch import Batch
+
+from .test_oracle_kats import ent, sst500_batch
+
+
+def _both(batch, sst_type=0, **kw):
+    prm = O.params(**kw)
+    r = O.encode_sst(batch, prm)
+    assert r.status == 0
+    want = F.sst_object(batch, r, sst_version=prm.sst_version, sst_type=sst_type)
+    got = runtime.sst_object(batch, r, sst_version=prm.sst_version, sst_type=sst_type)
+    return r, want, got
+
+
+def test_index_size_kat():
+    # two entries with create_ts, block_size 32: one block each (sst_builder.rs:1087-1139)
+    b = Batch.from_entries([ent("key1", "value1", 0, create=1), ent("key2", "value2", 0, create=2)])
+    r = O.encode_sst(b, O.params(block_size=32))
+    assert r.summary.num_blocks == 2
+    fks = [b.key(int(s))[:int(r.index_key_len[k])] for k, s in enumerate(r.block_first_entry[:-1])]
+    idx = F.index_block(fks, r.block_off[:-1])
+    assert len(idx) == 88
+    assert F.parse_index(idx) == [(0, b""), (int(r.block_off[1]), b"key2")]
+    obj = runtime.sst_object(b, r)
+    _, info, index, _, _ = F.parse_sst(obj)
+    assert info["index_len"] == 88 + 4 and info["first_entry"] == b"key1"
+    assert obj == F.sst_object(b, r)
+
+
+def test_sst500_compacted_and_wal_size_kats():
+    b = sst500_batch()
+    r, want, got = _both(b, block_size=1024, bloom_bits_per_key=10, min_filter_keys=0)
+    assert len(want) == 23794 and got == want
+    r, want, got = _both(b, sst_type=_abi.SST_WAL, block_size=1024, bloom_bits_per_key=10)
+    assert len(want) == 22928 and got == want
+
+
+def test_parse_back_every_field():
+    b = datasets.d3(n=3000)
+    r, want, got = _both(b, block_size=1024)
+    assert got == want
+    version, info, index, stats, filt = F.parse_sst(got)
+    nb = r.summary.num_blocks
+    assert version == 2
+    assert info["filter_offset"] == r.summary.data_len and info["filter_format"] == 1
+    assert info["sst_type"] == 0 and info["compression"] == 0
+    assert info["first_entry"] == b.key(0) and info["last_entry"] == b.key(b.n - 1)
+    assert [o for o, _ in index] == [int(x) for x in r.block_off[:nb]]
+    for k, (_, fk) in enumerate(index):
+        full = b.key(int(r.block_first_entry[k]))
+        assert full.startswith(fk) and len(fk) == int(r.index_key_len[k])
+        if k:  # compute_index_key: prev_last < fk <= first; full key on duplicates (utils.rs:198-226)
+            assert b.key(int(r.block_first_entry[k]) - 1) <= fk <= full
+    sm = r.summary
+    assert stats[:5] == (sm.num_puts, sm.num_deletes, sm.num_merges, sm.raw_key_size, sm.raw_val_size)
+    assert stats[5] == [tuple(int(v) for v in row) for row in r.block_stats]
+    assert sm.num_deletes > 0 and sm.num_merges > 0  # d3 mixes kinds: non-default BlockStats slots
+    assert filt[:7] == struct.pack(">HH", 1, 3) + b"_bf"
+    assert struct.unpack(">Q", filt[7:15])[0] == 2 + sm.bloom_len
+    assert filt[15:17] == struct.pack(">H", sm.num_probes) and filt[17:] == r.bloom.tobytes()
+
+
+@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("block_size", [64, 256, 4096])
+def test_d3_versions_and_block_sizes(version, block_size):
+    b = datasets.d3(n=1500)
+    _, want, got = _both(b, sst_version=version, block_size=block_size)
+    assert got == want
+    assert struct.unpack(">H", got[-2:])[0] == version
+
+
+def test_no_filter_cases():
+    b = datasets.d1(n=500)
+    r, want, got = _both(b, min_filter_keys=1000)   # num_rows < min_filter_keys
+    assert not r.summary.filter_built and got == want
+    assert F.parse_sst(got)[1]["filter_len"] == 0
+    r, want, got = _both(b, bloom_bits_per_key=0)   # no filter policy
+    assert got == want and F.parse_sst(got)[4] is None
+
+
+def test_empty_sst():
+    b = Batch.from_entries([])
+    r, want, got = _both(b)
+    assert got == want
+    version, info, index, stats, _ = F.parse_sst(got)
+    assert index == [] and info["first_entry"] is None and stats[:5] == (0, 0, 0, 0, 0)
+
+
+def test_wal_first_keys_are_seq_be():
+    es = [ent("k%05d" % i, "v" * (i % 37), seq=1000 + i) for i in range(2000)]
+    b = Batch.from_entries(es)
+    r, want, got = _both(b, sst_type=_abi.SST_WAL, block_size=512)
+    assert got == want
+    _, info, index, stats, filt = F.parse_sst(got)
+    assert info["sst_type"] == 1 and info["last_entry"] is None and stats is None and filt is None
+    assert info["first_entry"] == struct.pack(">Q", 1000)
+    assert [fk for _, fk in index] == [struct.pack(">Q", 1000 + int(s)) for s in r.block_first_entry[:-1]]
+
+
+def test_vtable_dedup_and_alignment_variety():
+    # key lengths 1..40 make first_key vectors of every padding class, offsets >= 2^32 are not
+    # reachable here but offsets with zero low bytes are (block 0's offset is the omitted default)
+    es = [ent(bytes([65 + (i % 26)]) * (1 + i % 40) + struct.pack(">I", i), "x" * (i % 300), i)
+          for i in range(3000)]
+    es.sort(key=lambda e: e[0])
+    b = Batch.from_entries(es)
+    _, want, got = _both(b, block_size=256)
+    assert got == want
+
+
+def test_footer_d1_full():
+    b = datasets.d1()
+    r, want, got = _both(b)
+    assert got == want and len(got) - r.summary.data_len == 1540206
+
+
+def test_footer_errors():
+    fi = _abi.FooterIn()
+    fi.num_blocks = 1  # NULL arrays
+    n = np.zeros(1, np.uint64)
+    assert runtime.lib().sdb_sst_footer(fi, None, 0, n.ctypes.data_as(_abi.u64p)) == _abi.SDB_INVALID_ARGUMENT
+    b = sst500_batch()
+    r = O.encode_sst(b, O.params(block_size=1024))
+    foot = runtime.sst_footer(b, r)
+    assert len(foot) == 23794 - 21998

@@ -307,3 +307,33 @@ def test_bloom_slots_do_not_overflow(rt, n):
     cnt = out.workspace[off: off + 4 * tiles.value * nsl.value].cpu().numpy().view(np.uint32)
     assert (cnt <= cap.value).all(), "a bloom slot overflowed"
     assert int(cnt.sum()) == n * 6
+
+
+# ------------------------------------------------------------------------------------------------
+# whole SST object (§8 f1): GPU data section + host footer from the device's per-block outputs
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("case", ["d1", "d3v1", "d3v2", "sst500", "sst500_wal"])
+def test_whole_sst_object(rt, case):
+    from oracle import footer as F
+    from .test_oracle_kats import sst500_batch
+    kw, sst_type = {}, _abi.SST_COMPACTED
+    if case == "d1":
+        b = datasets.d1()
+    elif case.startswith("d3"):
+        b = datasets.d3(n=3000)
+        kw = dict(sst_version=int(case[-1]), block_size=512)
+    else:
+        b = sst500_batch()
+        kw = dict(block_size=1024)
+        if case.endswith("wal"):
+            sst_type = _abi.SST_WAL
+    ref, got = encode_both(rt, b, **kw)
+    assert_same(ref, got, case)
+    v = kw.get("sst_version", 2)
+    want = F.sst_object(b, ref, sst_version=v, sst_type=sst_type)
+    obj = rt.sst_object(b, got, sst_version=v, sst_type=sst_type)
+    assert obj == want, case
+    if case == "sst500":
+        assert len(obj) == 23794
+    if case == "sst500_wal":
+        assert len(obj) == 22928
