@@ -261,6 +261,7 @@ sdb_status sdb_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, u
     a.tile_y = carve<uint64_t>(workspace, wl.tile_y);
     a.err = carve<unsigned long long>(workspace, wl.err);
     a.nbad = carve<unsigned long long>(workspace, wl.nbad);
+    a.done = carve<uint32_t>(workspace, wl.done);
     a.bad_block = out->bad_block;
     a.bad_cap = out->bad_cap;
     if (launch_decode(a, S(stream)) != hipSuccess) return SDB_DEVICE_ERROR;

@@ -21,12 +21,14 @@ struct DecodeArgs {
     uint64_t *ent_start, *key_start;   // nblocks+1
     uint64_t *tile_x, *tile_y;         // per 1024-block tile (+1)
     unsigned long long *err, *nbad;
+    uint32_t *done;                    // k_dec_emit workgroups finished (small batches: the last one finishes)
+    uint32_t small;                    // 1: nblocks <= 1024 and one block per wave: k_dec_emit scans the counts itself
     uint32_t *bad_block;
     uint64_t bad_cap;
 };
 
 struct DecodeWorkspace {
-    uint64_t cnt, kbytes, flag, rcnt, rowpos, ent_start, key_start, tile_x, tile_y, err, nbad, total;
+    uint64_t cnt, kbytes, flag, rcnt, rowpos, ent_start, key_start, tile_x, tile_y, err, nbad, done, total;
 };
 inline DecodeWorkspace decode_workspace_layout(uint64_t nblocks) {
     DecodeWorkspace w{};
@@ -48,6 +50,7 @@ inline DecodeWorkspace decode_workspace_layout(uint64_t nblocks) {
     w.tile_y = take(8 * (nt + 1));
     w.err = take(8);
     w.nbad = take(8);
+    w.done = take(8);
     w.total = off;
     return w;
 }

@@ -966,14 +966,67 @@ SDB_DEV void emit_v1(const DecodeArgs &a, const BlockViewT<P> &v, uint64_t ent0,
     }
 }
 
+SDB_DEV void dec_finish(const DecodeArgs &a) {
+    sdb_decode_summary *s = a.out.summary;
+    const uint64_t ne = a.ent_start[a.nblocks], kb = a.key_start[a.nblocks];
+    s->num_entries = ne;
+    s->key_bytes = kb;
+    s->num_bad_blocks = atomicAdd(a.nbad, 0ull);
+    const unsigned long long e = atomicOr(a.err, 0ull);
+    s->status = e == ~0ull ? 0 : (int32_t)(e & 0xFF);
+    s->pad = 0;
+    a.out.block_entry_start[a.nblocks] = ne;
+    if (ne > a.out.cap_entries || kb > a.out.key_arena_cap) s->status = SDB_INVALID_ARGUMENT;
+    else a.out.key_off[ne] = kb;
+}
+
 // D3 emit: one wave per block, stage again (no CRC: the count pass checked it), write the columns.
+// Small batches (a.small: <= 1024 blocks, one per wave — a 2 MiB read_blocks range is ~520) skip the
+// three scan kernels: every workgroup scans the per-block counts itself (one 1024-thread scan), and
+// the last workgroup to finish writes the summary (no k_dec_finish launch).
 __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    bool run = true;
     if (lds_addr((const void *)smem) != 0) {  // sdb_crc.h's lookups assume the tables at LDS address 0
         if (threadIdx.x == 0) atomicMin(a.err, (unsigned long long)SDB_DEVICE_ERROR);
-        return;
+        run = false;
     }
-    crc_tables_to_lds((lu32 *)smem);  // the generic path of oversized blocks still checks windows
+    uint64_t s_ent0 = 0, s_ent1 = 0, s_kb0 = 0, s_kb1 = 0, tot_ent = 0, tot_kb = 0;
+    if (a.small) {
+        // exclusive scans of cnt / kbytes over all blocks; scratch in wave 0's (still unused) region
+        uint64_t *sw = (uint64_t *)(smem + kCrcTablesLds);
+        uint64_t *sres = sw + 32;
+        const uint32_t t = threadIdx.x, b0 = blockIdx.x * (kDecThreads / 64);
+        const uint64_t vx = t < a.nblocks ? a.cnt[t] : 0, vy = t < a.nblocks ? a.kbytes[t] : 0;
+        const uint64_t ex = block_excl_scan_u64(vx, sw, &tot_ent);
+        const uint64_t ey = block_excl_scan_u64(vy, sw, &tot_kb);
+        if (t >= b0 && t < b0 + kDecThreads / 64) {
+            uint64_t *r = sres + 4 * (t - b0);
+            r[0] = ex;
+            r[1] = ex + vx;
+            r[2] = ey;
+            r[3] = ey + vy;
+        }
+        if (blockIdx.x == 0 && t < a.nblocks) {
+            a.ent_start[t] = ex;
+            a.key_start[t] = ey;
+        }
+        if (blockIdx.x == 0 && t == 0) {  // nblocks may be 1024 = blockDim.x
+            a.ent_start[a.nblocks] = tot_ent;
+            a.key_start[a.nblocks] = tot_kb;
+        }
+        __syncthreads();
+        const uint64_t *r = sres + 4 * (threadIdx.x >> 6);
+        s_ent0 = r[0];
+        s_ent1 = r[1];
+        s_kb0 = r[2];
+        s_kb1 = r[3];
+        __syncthreads();
+    } else {
+        tot_ent = a.ent_start[a.nblocks];
+        tot_kb = a.key_start[a.nblocks];
+    }
+    if (run) crc_tables_to_lds((lu32 *)smem);  // the generic path of oversized blocks still checks windows
     __syncthreads();
     const uint32_t(*crc)[256] = (const uint32_t(*)[256])smem;
     const uint32_t wave = threadIdx.x >> 6;
@@ -985,13 +1038,14 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
     const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
     (void)gwave;
     // capacity guard: if the counted output does not fit the caller's arrays, write nothing
-    if (a.ent_start[a.nblocks] > a.out.cap_entries || a.key_start[a.nblocks] > a.out.key_arena_cap) return;
-    for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave; k < a.nblocks; k += nwaves) {
-        const uint64_t ent0 = a.ent_start[k];
-        const uint64_t n_ent = a.ent_start[k + 1] - ent0;
+    if (tot_ent > a.out.cap_entries || tot_kb > a.out.key_arena_cap) run = false;
+    for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave; run && k < a.nblocks; k += nwaves) {
+        const uint64_t ent0 = a.small ? s_ent0 : a.ent_start[k];
+        const uint64_t n_ent = (a.small ? s_ent1 : a.ent_start[k + 1]) - ent0;
         if (l == 0) a.out.block_entry_start[k] = ent0;
         if (n_ent == 0) continue;
-        const uint64_t kb0 = a.key_start[k], kbn = a.key_start[k + 1] - kb0;
+        const uint64_t kb0 = a.small ? s_kb0 : a.key_start[k];
+        const uint64_t kbn = (a.small ? s_kb1 : a.key_start[k + 1]) - kb0;
         const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
         const bool seq = a.flag[k] != 0;
         if (dec_fast(s, e)) {
@@ -1024,6 +1078,16 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
             else emit_v2(a, v, seq, ent0, kb0, s, nullptr);
         }
         wave_sync_d();
+    }
+    if (a.small) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            if (atomicAdd(a.done, 1u) == gridDim.x - 1) {
+                __threadfence();
+                dec_finish(a);
+            }
+        }
     }
 }
 
@@ -1089,23 +1153,12 @@ __global__ void k_dec_init(DecodeArgs a) {
     if (threadIdx.x == 0) {
         *a.err = ~0ull;
         *a.nbad = 0;
+        *a.done = 0;
     }
 }
 
 __global__ void k_dec_finish(DecodeArgs a) {
-    if (threadIdx.x == 0) {
-        sdb_decode_summary *s = a.out.summary;
-        uint64_t ne = a.ent_start[a.nblocks], kb = a.key_start[a.nblocks];
-        s->num_entries = ne;
-        s->key_bytes = kb;
-        s->num_bad_blocks = *a.nbad;
-        unsigned long long e = *a.err;
-        s->status = e == ~0ull ? 0 : (int32_t)(e & 0xFF);
-        s->pad = 0;
-        a.out.block_entry_start[a.nblocks] = ne;
-        if (ne > a.out.cap_entries || kb > a.out.key_arena_cap) s->status = SDB_INVALID_ARGUMENT;
-        else a.out.key_off[ne] = kb;
-    }
+    if (threadIdx.x == 0) dec_finish(a);
 }
 
 hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
@@ -1125,9 +1178,11 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
     if (wgs == 0) wgs = 1;
     const size_t lds = kDecLds;
     if (a.nblocks) hipLaunchKernelGGL(k_dec_count, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
-    // scans: ent_start = excl(cnt), key_start = excl(kbytes)
+    // scans: ent_start = excl(cnt), key_start = excl(kbytes); small batches scan inside k_dec_emit
+    a.small = a.nblocks > 0 && a.nblocks <= kScanTile && wgs * (kDecThreads / 64) >= a.nblocks ? 1u : 0u;
     uint64_t nt = (a.nblocks + kScanTile - 1) / kScanTile;
-    if (a.nblocks) {
+    if (a.small) {
+    } else if (a.nblocks) {
         hipLaunchKernelGGL(k_scan_tiles, dim3((uint32_t)nt), dim3(kScanTile), 0, st, a.cnt, a.kbytes, a.nblocks,
                            a.tile_x, a.tile_y);
         hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanTile), 0, st, a.tile_x, a.tile_y, nt);
@@ -1138,7 +1193,7 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
         hipMemsetAsync(a.key_start, 0, 8, st);
     }
     if (a.nblocks) hipLaunchKernelGGL(k_dec_emit, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
-    hipLaunchKernelGGL(k_dec_finish, dim3(1), dim3(64), 0, st, a);
+    if (!a.small) hipLaunchKernelGGL(k_dec_finish, dim3(1), dim3(64), 0, st, a);
     return hipGetLastError();
 }
 

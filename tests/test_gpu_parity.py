@@ -337,3 +337,21 @@ def test_whole_sst_object(rt, case):
         assert len(obj) == 23794
     if case == "sst500_wal":
         assert len(obj) == 22928
+
+
+def test_decode_small_batches(rt):
+    """<= 1024 blocks take the fused path (scan inside k_dec_emit, last workgroup finishes): the
+    2 MiB read_blocks granularity (~520 blocks, format/sst.rs:919-978); 1025 takes the scan kernels."""
+    b = datasets.d1(n=40000)
+    enc = O.encode_sst(b, O.params())
+    dec = rt.Decoder()
+    for b0, b1 in [(0, 1), (0, 520), (520, 1040), (0, 1024), (0, 1025), (100, 1124), (1170, enc.summary.num_blocks)]:
+        off = enc.block_off[b0:b1 + 1]
+        got = dec.decode(enc.data, off, 2)
+        assert_decode_same(O.decode_blocks(enc.data, off, 2), got, "range %d-%d" % (b0, b1))
+    data = enc.data.copy()
+    data[int(enc.block_off[600]) + 5] ^= 1
+    off = enc.block_off[520:1040 + 1]
+    ref = O.decode_blocks(data, off, 2)
+    assert ref.status == _abi.SDB_CHECKSUM_MISMATCH
+    assert_decode_same(ref, dec.decode(data, off, 2), "small corrupt")
