@@ -89,6 +89,8 @@ typedef struct sdb_kv_batch {
     const uint8_t *ts_mask;     /* n; NULL = no timestamps */
 } sdb_kv_batch;
 
+enum { SDB_SST_COMPACTED = 0, SDB_SST_WAL = 1 };   /* SstType (schemas/sst.fbs) */
+
 /* SsTableFormat knobs on this path (format/sst.rs:620-643, db/builder.rs:439-531). */
 typedef struct sdb_sst_params {
     uint32_t block_size;         /* SstBlockSize, default 4096 (config.rs:231-267) */
@@ -96,6 +98,9 @@ typedef struct sdb_sst_params {
     uint16_t restart_interval;   /* V2 only; reference constant 16 (block_v2.rs:8) */
     uint32_t bloom_bits_per_key; /* BloomFilterPolicy::new(bpk) (filter_policy.rs:201); 0 = none */
     uint32_t min_filter_keys;    /* filter built iff num_rows >= min_filter_keys (sst_builder.rs:390) */
+    uint32_t sst_type;           /* SDB_SST_COMPACTED, or SDB_SST_WAL: EncodedWalSsTableBuilder
+                                    (wal/slatedb/sst_builder.rs:68-205): entries in insertion order,
+                                    no compute_index_key (so no prefix panic), no filter; V2 only */
 } sdb_sst_params;
 
 /* Scalar results of one SST encode, written by the device. */
@@ -214,7 +219,6 @@ sdb_status sdb_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, u
  * Layout: [filter block + crc]? [index + crc] [stats + crc]? [SsTableInfo + crc] [u64 BE meta
  * offset] [u16 BE version]; flatbuffer bytes identical to the `flatbuffers` 25.12.19 crate.
  * ------------------------------------------------------------------------------------------- */
-enum { SDB_SST_COMPACTED = 0, SDB_SST_WAL = 1 };   /* SstType (schemas/sst.fbs) */
 typedef struct sdb_footer_in {
     uint16_t sst_version;             /* trailing u16 (SST_FORMAT_VERSION: 1 or 2) */
     uint8_t sst_type;                 /* SDB_SST_COMPACTED | SDB_SST_WAL */

@@ -168,9 +168,9 @@ def bounds(batch, params):
 
 
 def params(block_size=4096, sst_version=2, restart_interval=16, bloom_bits_per_key=10,
-           min_filter_keys=0):
+           min_filter_keys=0, sst_type=0):
     return _abi.SstParams(block_size, sst_version, restart_interval, bloom_bits_per_key,
-                          min_filter_keys)
+                          min_filter_keys, sst_type)
 
 
 def encode_sst(batch, prm):

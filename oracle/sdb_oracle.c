@@ -483,6 +483,9 @@ sdb_status orc_encode_sst(const sdb_kv_batch *batch, const sdb_sst_params *param
     sm->first_error_entry = UINT64_MAX;
     if (params->sst_version != 1 && params->sst_version != 2) return (sdb_status)(sm->status = SDB_INVALID_ARGUMENT);
     if (params->sst_version == 2 && params->restart_interval == 0) return (sdb_status)(sm->status = SDB_INVALID_ARGUMENT);
+    /* EncodedWalSsTableBuilder uses BlockBuilder::new_latest (V2) only */
+    if (params->sst_type > SDB_SST_WAL || (params->sst_type == SDB_SST_WAL && params->sst_version != 2))
+        return (sdb_status)(sm->status = SDB_INVALID_ARGUMENT);
     uint64_t n = batch->n;
     blk_t b;
     memset(&b, 0, sizeof b);
@@ -530,7 +533,10 @@ sdb_status orc_encode_sst(const sdb_kv_batch *batch, const sdb_sst_params *param
         sm->raw_val_size += e.vlen;
         /* compute_index_key runs on every entry (sst_builder.rs:228) and panics on an empty or
          * non-sorted-prefix key (utils.rs:210-216). */
-        int64_t ik = orc_index_key_len(prev_key, prev_klen, has_prev, e.key, e.klen);
+        /* WAL SSTs (wal/slatedb/sst_builder.rs:123-150) never call compute_index_key: their block
+         * first key is the first entry's seq, built with the footer. */
+        const int wal = params->sst_type == SDB_SST_WAL;
+        int64_t ik = wal ? 0 : orc_index_key_len(prev_key, prev_klen, has_prev, e.key, e.klen);
         if (ik < 0) { st = e.klen == 0 ? SDB_EMPTY_KEY : SDB_INVALID_ARGUMENT; err_entry = i; goto done; }
         if (!blk_would_fit(&b, &e)) {
             FINISH_BLOCK();
@@ -554,7 +560,7 @@ sdb_status orc_encode_sst(const sdb_kv_batch *batch, const sdb_sst_params *param
     sm->num_entries = n;
 
     /* Filters (sst_builder.rs:388-403): one bloom per SST when num_rows >= min_filter_keys. */
-    if (params->bloom_bits_per_key > 0 && n >= params->min_filter_keys) {
+    if (params->sst_type != SDB_SST_WAL && params->bloom_bits_per_key > 0 && n >= params->min_filter_keys) {
         uint64_t fb = orc_filter_size_bytes(n, params->bloom_bits_per_key);
         if (fb > out->bloom_cap) { st = SDB_INVALID_ARGUMENT; goto done; }
         orc_bloom_build(batch->key_bytes, batch->key_off, n, params->bloom_bits_per_key, out->bloom, fb);

@@ -47,7 +47,7 @@ class KvBatch(C.Structure):
 class SstParams(C.Structure):
     _fields_ = [
         ("block_size", C.c_uint32), ("sst_version", C.c_uint16), ("restart_interval", C.c_uint16),
-        ("bloom_bits_per_key", C.c_uint32), ("min_filter_keys", C.c_uint32),
+        ("bloom_bits_per_key", C.c_uint32), ("min_filter_keys", C.c_uint32), ("sst_type", C.c_uint32),
     ]
 
 

@@ -40,6 +40,7 @@ sdb_status check_params(const sdb_sst_params *p) {
     if (p->sst_version != 1 && p->sst_version != 2) return SDB_INVALID_ARGUMENT;
     if (p->block_size == 0) return SDB_INVALID_ARGUMENT;
     if (p->sst_version == 2 && p->restart_interval == 0) return SDB_INVALID_ARGUMENT;
+    if (p->sst_type > SDB_SST_WAL || (p->sst_type == SDB_SST_WAL && p->sst_version != 2)) return SDB_INVALID_ARGUMENT;
     return SDB_OK;
 }
 
@@ -115,7 +116,7 @@ sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const 
     const uint64_t n = b->n;
     if (n >= (1ull << 31)) return SDB_LIMIT_EXCEEDED;
     if (n && (!b->key_bytes || !b->key_off || !b->val_off)) return SDB_INVALID_ARGUMENT;
-    const bool want_filter = p->bloom_bits_per_key > 0 && n >= p->min_filter_keys;
+    const bool want_filter = p->sst_type != SDB_SST_WAL && p->bloom_bits_per_key > 0 && n >= p->min_filter_keys;
     const uint64_t fb = want_filter ? filter_bytes_for(n, p->bloom_bits_per_key) : 0;
     EncodeWorkspace wl = encode_workspace_layout(n, p->bloom_bits_per_key ? filter_bytes_for(n, p->bloom_bits_per_key) : 0,
                                                  num_probes_for(p->bloom_bits_per_key));
@@ -139,6 +140,7 @@ sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const 
     a.block_size = p->block_size;
     a.restart_interval = p->sst_version == 2 ? p->restart_interval : 1;
     a.version = p->sst_version;
+    a.wal = p->sst_type == SDB_SST_WAL;
     a.nchunks = (uint32_t)((n + kChunk - 1) / kChunk);
     {   // a block holds at most (block_size - 2) / 12 + 1 entries (smallest row: 12 bytes in V2, 13 in V1);
         // blocks longer than the lookahead continue from HBM inside k_seg

@@ -67,6 +67,7 @@ struct EncodeArgs {
     uint32_t block_size;
     uint32_t restart_interval;
     uint32_t version;
+    uint32_t wal;           // WAL SST: no compute_index_key (no prefix panic), index_key_len 0
     uint32_t nchunks;
     uint32_t seg_look;      // lookahead entries staged by k_seg (covers the longest possible block)
     // workspace

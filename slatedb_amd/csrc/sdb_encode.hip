@@ -146,7 +146,7 @@ SDB_DEV EntryFacts facts_finish(const EncodeArgs &a, uint64_t i, const FactsIn &
         // compute_index_key runs on every entry (sst_builder.rs:228): assert on empty keys and
         // out-of-bounds panic when this key is a proper prefix of the previous one (utils.rs:210-216)
         if (klen == 0) err = SDB_EMPTY_KEY;
-        else if (plen > 0 && lcp == klen && klen < plen) err = SDB_INVALID_ARGUMENT;
+        else if (!a.wal && plen > 0 && lcp == klen && klen < plen) err = SDB_INVALID_ARGUMENT;
     }
     if (!err && klen == 0) err = SDB_EMPTY_KEY;  // BlockBuilder*::add (block_v2.rs:168-170)
     const uint32_t ts8 = 8u * (((m & SDB_TS_CREATE) != 0) + ((m & SDB_TS_EXPIRE) != 0));
@@ -1369,7 +1369,7 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
         a.out_block_stats[3 * (uint64_t)blk + 1] = (uint16_t)__popcll(de);
         a.out_block_stats[3 * (uint64_t)blk + 2] = (uint16_t)__popcll(me);
         uint32_t ik = 0;
-        if (d.s > 0) ik = (lcp == prev_klen && prev_klen == klen) ? klen : lcp + 1;
+        if (d.s > 0 && !a.wal) ik = (lcp == prev_klen && prev_klen == klen) ? klen : lcp + 1;
         a.out_index_key_len[blk] = ik;
     }
     wave_sync();
@@ -1595,7 +1595,7 @@ SDB_DEV void emit_slow_blocks(const EncodeArgs &a, uint8_t *scratch, const uint3
             a.out_block_stats[3 * (uint64_t)blk + 1] = (uint16_t)de;
             a.out_block_stats[3 * (uint64_t)blk + 2] = (uint16_t)me;
             uint32_t ik = 0;
-            if (b > 0) {
+            if (b > 0 && !a.wal) {
                 uint64_t fl = a.key_off[b + 1] - a.key_off[b];
                 uint64_t pl = a.key_off[b] - a.key_off[b - 1];
                 uint32_t lc = a.lcp[b];

@@ -24,7 +24,7 @@ from .test_oracle_kats import ent, sst500_batch
 
 
 def _both(batch, sst_type=0, **kw):
-    prm = O.params(**kw)
+    prm = O.params(sst_type=sst_type, **kw)
     r = O.encode_sst(batch, prm)
     assert r.status == 0
     want = F.sst_object(batch, r, sst_version=prm.sst_version, sst_type=sst_type)
@@ -143,3 +143,33 @@ def test_footer_errors():
     r = O.encode_sst(b, O.params(block_size=1024))
     foot = runtime.sst_footer(b, r)
     assert len(foot) == 23794 - 21998
+
+
+def _wal_batch(n=3000, seed=5):
+    rng = np.random.default_rng(seed)
+    es = []
+    for i in range(n):
+        k = b"user:%06d" % int(rng.integers(0, 10 ** 6))
+        if i % 97 == 5:
+            k = es[-1][0][:4]          # a proper prefix of the previous key: compute_index_key panics
+        kind = [_abi.KIND_VALUE, _abi.KIND_VALUE, _abi.KIND_TOMBSTONE, _abi.KIND_MERGE][i % 4]
+        es.append(ent(k, b"v" * int(rng.integers(0, 200)), seq=10 ** 6 + i, kind=kind,
+                      expire=(i if i % 7 == 0 else None)))
+    return Batch.from_entries(es)
+
+
+def test_wal_insertion_order():
+    """EncodedWalSsTableBuilder (wal/slatedb/sst_builder.rs:68-205): insertion order, no
+    compute_index_key, no filter; the same V2 blocks decode back in insertion order."""
+    b = _wal_batch()
+    bad = O.encode_sst(b, O.params(block_size=1024))
+    assert bad.status == _abi.SDB_INVALID_ARGUMENT  # compacted builder panics on the prefix key
+    r, want, got = _both(b, sst_type=_abi.SST_WAL, block_size=1024)
+    assert got == want and not r.summary.filter_built
+    _, info, index, stats, filt = F.parse_sst(got)
+    assert info["sst_type"] == 1 and stats is None and filt is None
+    assert [fk for _, fk in index] == [struct.pack(">Q", int(b.seq[int(s)])) for s in r.block_first_entry[:-1]]
+    d = O.decode_blocks(r.data, r.block_off, 2)
+    assert d.status == 0 and d.n == b.n and np.array_equal(d.key_arena, b.key_bytes)
+    assert np.array_equal(d.seq, b.seq)
+    assert O.encode_sst(b, O.params(sst_version=1, sst_type=_abi.SST_WAL)).status == _abi.SDB_INVALID_ARGUMENT

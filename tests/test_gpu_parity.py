@@ -312,7 +312,7 @@ def test_bloom_slots_do_not_overflow(rt, n):
 # ------------------------------------------------------------------------------------------------
 # whole SST object (§8 f1): GPU data section + host footer from the device's per-block outputs
 # ------------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("case", ["d1", "d3v1", "d3v2", "sst500", "sst500_wal"])
+@pytest.mark.parametrize("case", ["d1", "d3v1", "d3v2", "sst500", "sst500_wal", "wal_insertion_order"])
 def test_whole_sst_object(rt, case):
     from oracle import footer as F
     from .test_oracle_kats import sst500_batch
@@ -322,12 +322,15 @@ def test_whole_sst_object(rt, case):
     elif case.startswith("d3"):
         b = datasets.d3(n=3000)
         kw = dict(sst_version=int(case[-1]), block_size=512)
+    elif case == "wal_insertion_order":
+        from .test_footer import _wal_batch
+        b, kw, sst_type = _wal_batch(), dict(block_size=1024), _abi.SST_WAL
     else:
         b = sst500_batch()
         kw = dict(block_size=1024)
         if case.endswith("wal"):
             sst_type = _abi.SST_WAL
-    ref, got = encode_both(rt, b, **kw)
+    ref, got = encode_both(rt, b, sst_type=sst_type, **kw)
     assert_same(ref, got, case)
     v = kw.get("sst_version", 2)
     want = F.sst_object(b, ref, sst_version=v, sst_type=sst_type)
