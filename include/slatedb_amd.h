@@ -241,6 +241,8 @@ typedef struct sdb_footer_in {
 /* Writes the footer into out[0..cap) and its length into *len.  out == NULL: size query only.
  * cap too small: SDB_LIMIT_EXCEEDED (with *len set). */
 sdb_status sdb_sst_footer(const sdb_footer_in *in, uint8_t *out, uint64_t cap, uint64_t *len);
+/* Upper bound on the footer length (arithmetic only), to size `out` for a single sdb_sst_footer call. */
+uint64_t sdb_sst_footer_bound(const sdb_footer_in *in);
 
 /* ---------------------------------------------------------------------------------------------
  * Host entry points: device arena + pinned staging per handle (E2E path: H2D -> kernels -> D2H)

@@ -142,6 +142,7 @@ SIGNATURES = {
     "sdb_decode_blocks": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint16,
                                     C.POINTER(DecodedOut), C.c_void_p, C.c_uint64, C.c_void_p]),
     "sdb_sst_footer": (C.c_int, [C.POINTER(FooterIn), C.c_void_p, C.c_uint64, u64p]),
+    "sdb_sst_footer_bound": (C.c_uint64, [C.POINTER(FooterIn)]),
     "sdb_encoder_create": (C.c_void_p, [C.c_int, C.POINTER(SstParams)]),
     "sdb_encoder_destroy": (None, [C.c_void_p]),
     "sdb_encoder_encode_host": (C.c_int, [C.c_void_p, C.POINTER(KvBatch), C.POINTER(SstHostResult)]),

@@ -16,8 +16,7 @@
 // 64 MiB SST), produced after the device encode from its per-block outputs.
 #include <cstdint>
 #include <cstring>
-#include <string>
-#include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "../../include/slatedb_amd.h"
@@ -114,22 +113,30 @@ class BackWriter {
         const uint32_t obj = scalar<uint32_t>(0);  // soffset to the vtable, patched below
         uint16_t vlen = 4;
         for (const auto &f : fields_) vlen = f.slot + 2 > vlen ? (uint16_t)(f.slot + 2) : vlen;
-        std::string vt(vlen, '\0');
+        VTable vt{};
+        vt.len = vlen;
         const uint16_t hdr[2] = {vlen, (uint16_t)(obj - tail)};
-        memcpy(&vt[0], hdr, 4);
+        memcpy(vt.b, hdr, 4);
         for (const auto &f : fields_) {
             const uint16_t d = (uint16_t)(obj - f.rev);
-            memcpy(&vt[f.slot], &d, 2);
+            memcpy(vt.b + f.slot, &d, 2);
         }
-        uint32_t vt_rev;
-        auto it = vtables_.find(vt);
-        if (it != vtables_.end()) {
-            vt_rev = it->second;
-        } else {
+        // a footer has a handful of distinct vtables (one per padding pattern): linear search,
+        // most recent first
+        uint32_t vt_rev = 0;
+        bool found = false;
+        for (size_t i = vtables_.size(); i-- > 0;)
+            if (vtables_[i].len == vlen && !memcmp(vtables_[i].b, vt.b, vlen)) {
+                vt_rev = vtables_[i].rev;
+                found = true;
+                if (i + 1 != vtables_.size()) std::swap(vtables_[i], vtables_.back());
+                break;
+            }
+        if (!found) {
             reserve(vlen);
-            memcpy(&buf_[head_], vt.data(), vlen);
-            vt_rev = rev();
-            vtables_.emplace(std::move(vt), vt_rev);
+            memcpy(&buf_[head_], vt.b, vlen);
+            vt_rev = vt.rev = rev();
+            vtables_.push_back(vt);
         }
         const int32_t so = (int32_t)vt_rev - (int32_t)obj;
         memcpy(&buf_[buf_.size() - obj], &so, 4);
@@ -149,6 +156,11 @@ class BackWriter {
         uint16_t slot;
         uint32_t rev;
     };
+    struct VTable {
+        uint8_t b[32];  // widest vtable here: SsTableInfo, 26 bytes
+        uint16_t len;
+        uint32_t rev;
+    };
     void reserve(size_t n) {
         if (head_ < n) {
             size_t cap = buf_.size();
@@ -165,7 +177,7 @@ class BackWriter {
     size_t head_;
     size_t max_align_ = 1;
     std::vector<Field> fields_;
-    std::unordered_map<std::string, uint32_t> vtables_;
+    std::vector<VTable> vtables_;
 };
 
 void put_be(std::vector<uint8_t> &o, uint64_t v, int nbytes) {
@@ -180,6 +192,17 @@ uint64_t append_checked(std::vector<uint8_t> &o, const uint8_t *p, size_t n) {
 
 }  // namespace
 
+extern "C" uint64_t sdb_sst_footer_bound(const sdb_footer_in *in) {
+    if (!in) return 0;
+    const uint64_t nb = in->num_blocks;
+    const uint64_t keys = nb && in->first_key_off ? in->first_key_off[nb] - in->first_key_off[0] : 0;
+    uint64_t b = 256 + in->first_entry_len + in->last_entry_len;  // SsTableInfo, crcs, trailer
+    if (in->has_filter) b += 32 + in->bloom_len;                  // composite filter block
+    b += 64 + keys + 48 * nb;                                      // index: key, len, pads, BlockMeta, vtable, slot
+    if (in->stats) b += 128 + 32 * nb;                             // stats: BlockStats tables + vector
+    return b;
+}
+
 extern "C" sdb_status sdb_sst_footer(const sdb_footer_in *in, uint8_t *out, uint64_t cap,
                                      uint64_t *len) {
     if (!in || !len) return SDB_INVALID_ARGUMENT;
@@ -190,6 +213,7 @@ extern "C" sdb_status sdb_sst_footer(const sdb_footer_in *in, uint8_t *out, uint
     if (in->sst_type > 1) return SDB_INVALID_ARGUMENT;
     const uint64_t base = in->data_len;
     std::vector<uint8_t> o;
+    o.reserve(sdb_sst_footer_bound(in));
 
     // 1. composite filter block [u16 count][u16 name_len]["_bf"][u64 len][Filter::encode]
     //    (format/sst.rs:394-421; Filter::encode = u16 BE num_probes ++ bitmap, filter.rs:177-180)

@@ -164,11 +164,9 @@ def sst_footer(batch, enc, sst_version=2, sst_type=_abi.SST_COMPACTED):
                        None if wal else C.addressof(sm), bst.ctypes.data if len(bst) else None,
                        bloom.ctypes.data if len(bloom) else None, 0 if wal else int(sm.bloom_len))
     n = C.c_uint64(0)
-    st = lib().sdb_sst_footer(C.byref(fi), None, 0, C.byref(n))
-    if st:
-        raise SdbError(st, "sdb_sst_footer")
-    out = np.zeros(max(n.value, 1), np.uint8)
-    st = lib().sdb_sst_footer(C.byref(fi), out.ctypes.data, n.value, C.byref(n))
+    cap = lib().sdb_sst_footer_bound(C.byref(fi))
+    out = np.empty(max(cap, 1), np.uint8)
+    st = lib().sdb_sst_footer(C.byref(fi), out.ctypes.data, cap, C.byref(n))
     if st:
         raise SdbError(st, "sdb_sst_footer")
     return out[:n.value].tobytes()
