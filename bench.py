@@ -1,20 +1,24 @@
 """bench.py — device-resident SST block encode + bloom build, 64 MiB sorted KV per SST.
 
 Metric (BASELINE.json): GiB/s of logical KV bytes Σ(|key|+|value|) encoded per second, whole job,
-inputs resident in HBM when the timed region starts.  One step = every rank encodes one complete
-64 MiB D1 SST (configs[1]: 578,524 entries of 16 B keys / 100 B values -> 17,016 V2 blocks with
-CRC32 + a 10 bits/key bloom) through the C ABI (sdb_encode_sst).  Ranks encode independent SSTs
-(the compaction sharding of configs[4]); no collective is on the data path — the only RCCL calls
-are the timing barrier and the max-over-ranks of the elapsed time.
+inputs resident in HBM when the timed region starts.  A 64 MiB D1 SST is 578,524 entries of 16 B keys
+/ 100 B values -> 17,016 V2 4 KiB blocks with CRC32 + a 10 bits/key bloom (configs[1]).
 
-  python bench.py [--gpus N --steps K --warmup W]
+One step = every rank encodes `--batch` distinct 64 MiB SSTs (default 8: the per-GPU share of the
+configs[4] compaction job, 64 SSTs on 8 GPUs) through ONE sdb_encode_ssts launch sequence — the
+several concurrent SST builders of a compaction / flush (config.rs:1081, 1383-1390).  SST j of the
+job goes to rank j mod N (slatedb_amd/job.py); ranks share nothing, the only RCCL calls are the
+timing barrier and the max / sum of scalars.  `--job-ssts 64` runs configs[4] as a fixed job (strong
+scaling); `--batch 1` is the single-SST configs[1] shape.  The single-SST latency (sdb_encode_sst,
+one SST per launch sequence) is reported beside the headline as `single_sst`.
+
+  python bench.py [--gpus N --steps K --warmup W --batch B]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
 import ctypes as C
 import json
 import os
-import subprocess
 import sys
 import time
 
@@ -24,23 +28,40 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from slatedb_amd import _abi, datasets, runtime  # noqa: E402
+from slatedb_amd import _abi, datasets, job, runtime  # noqa: E402
 
-PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s); the box's STREAM copy: DESIGN.md §5
+PMC_FILE = "r2_pmc_traffic.json"
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--ssts", type=int, default=4, help="distinct resident input SSTs per rank (rotated)")
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
-    p.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cpus))")
+    p.add_argument("--steps", type=int, default=1500)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--batch", type=int, default=8, help="SSTs per GPU per step (one sdb_encode_ssts call)")
+    p.add_argument("--job-ssts", type=int, default=0,
+                   help="configs[4] fixed job: J distinct SSTs over all ranks (SST j -> rank j mod N), one pass per step")
+    p.add_argument("--ssts", type=int, default=0, help="distinct resident input SSTs per rank (0: 2 x batch)")
+    p.add_argument("--stage-steps", type=int, default=40, help="steps of the per-kernel HIP-event pass")
+    p.add_argument("--single-steps", type=int, default=200, help="single-SST (configs[1]) latency steps")
+    p.add_argument("--cpu-seconds", type=float, default=16.0, help="budget of the CPU baseline sample")
+    p.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: the box's CPU share)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--bpk", type=int, default=10, help="bloom bits per key (0 = no filter; diagnostics)")
     return p.parse_args()
+
+
+def cpu_share():
+    """Threads this process may use: OMP_NUM_THREADS (the GPU box sets it to its CPU share), else the
+    affinity mask (os.cpu_count() shows the whole machine there)."""
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        return max(1, int(os.environ["OMP_NUM_THREADS"]))
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
 def cpu_baseline(budget_s, threads):
@@ -51,7 +72,6 @@ def cpu_baseline(budget_s, threads):
     import threading
     from oracle import oracle as O
     prm = O.params(block_size=4096, sst_version=2, bloom_bits_per_key=10)
-    logical = None
 
     def run(batch, deadline, out, i):
         done, t_used = 0, 0.0
@@ -65,17 +85,15 @@ def cpu_baseline(budget_s, threads):
                 break
         out[i] = (done, t_used)
 
-    # 1 thread
     b0 = datasets.d1(sst_index=9000)
     logical = b0.logical_bytes()
     out1 = [None]
-    run(b0, time.perf_counter() + budget_s / 2, out1, 0)
+    run(b0, time.perf_counter() + budget_s / 4, out1, 0)
     single = out1[0][0] * logical / out1[0][1] / 2**30
-    # T threads, one SST each
     batches = [b0] + [datasets.d1(sst_index=9001 + i) for i in range(threads - 1)]
     outs = [None] * threads
     t0 = time.perf_counter()
-    deadline = t0 + budget_s / 2
+    deadline = t0 + budget_s * 3 / 4
     ths = [threading.Thread(target=run, args=(batches[i], deadline, outs, i)) for i in range(threads)]
     for t in ths:
         t.start()
@@ -88,22 +106,25 @@ def cpu_baseline(budget_s, threads):
     except Exception:
         model = "unknown"
     return {"value": round(multi, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "single_thread_value": round(single, 4),
-            "sample": "whole D1 SSTs (64 MiB logical KV each, encode + 10 bits/key bloom) by "
+            "single_thread_value": round(single, 4), "nproc": os.cpu_count(),
+            "sample": "whole D1 SSTs (64 MiB logical KV each, encode + CRC + 10 bits/key bloom) by "
                       "oracle/sdb_oracle.c: %d SSTs on 1 thread (%.1f s), then %d threads x 1 SST each "
-                      "for %.1f s wall (%d SSTs), on %s" % (out1[0][0], out1[0][1], threads, wall,
-                                                          sum(o[0] for o in outs), model)}
+                      "for %.1f s wall (%d SSTs) on %s; %d threads = this process's CPU share "
+                      "(OMP_NUM_THREADS / affinity), nproc = %d" % (
+                          out1[0][0], out1[0][1], threads, wall, sum(o[0] for o in outs), model, threads,
+                          os.cpu_count() or 0)}
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC passes over this same bench command
-    (profiles/r1_pmc_traffic.json, written by scripts/collect_profiles.py; FETCH_SIZE/WRITE_SIZE
-    corrected per MI355X_MICROARCH.md).  PMC counters cannot be read from inside the timed run."""
+def pmc_traffic():
+    """HBM bytes per SST of the encode from the committed PMC passes over this same bench command
+    (profiles/r2_pmc_traffic.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes, corrected per
+    MI355X_MICROARCH.md, written by scripts/collect_profiles.py).  PMC counters are collected in
+    their own rocprofv3 runs, never inside the timed region."""
     try:
-        d = json.load(open(os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")))
-        return d["per_dispatch"][kernel]["traffic_bytes"]
+        d = json.load(open(os.path.join(ROOT, "profiles", PMC_FILE)))
+        return d.get("per_sst_bytes"), d.get("per_kernel", {})
     except (OSError, KeyError, ValueError):
-        return None
+        return None, {}
 
 
 def main():
@@ -112,6 +133,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    tdist = None
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
@@ -123,37 +145,54 @@ def main():
     lib = runtime.lib()
     prm = runtime.params(block_size=4096, sst_version=2, restart_interval=16, bloom_bits_per_key=args.bpk)
 
-    # resident inputs: distinct D1 SSTs per rank
-    hosts = [datasets.d1(sst_index=rank * 64 + j) for j in range(args.ssts)]
+    # this rank's SSTs: the fixed job's share (configs[4]) or `batch` per step (weak scaling)
+    if args.job_ssts:
+        mine = job.share(args.job_ssts, world, rank)
+        batch = len(mine)
+        ids = mine
+        scaling = "strong"
+    else:
+        batch = args.batch
+        nres = args.ssts or 2 * batch
+        ids = [rank + world * q for q in range(nres)]  # SST j of the job -> rank j mod N
+        scaling = "weak"
+    hosts = [datasets.d1(sst_index=j) for j in ids]
     dbs = [h.to_device(dev) for h in hosts]
     logical = hosts[0].logical_bytes()
-    outs = [runtime.DeviceSstOutput(hosts[0].n, logical, logical, prm, device=dev) for _ in range(2)]
+    nsets = max(1, len(dbs) // batch)
+    sets = [dbs[q * batch:(q + 1) * batch] for q in range(nsets)]
+    outs = [[runtime.DeviceSstOutput(hosts[0].n, logical, logical, prm, device=dev, workspace=False) for _ in range(batch)]
+            for _ in range(2)]
+    wss = [runtime.ssts_workspace(sets[0], prm, device=dev) for _ in range(2)]
     stream = torch.cuda.Stream(device=dev)
 
     def step(i):
-        runtime.encode_sst_device(dbs[i % len(dbs)], outs[i % 2], stream)
+        runtime.encode_ssts_device(sets[i % nsets], outs[i % 2], prm, wss[i % 2], stream)
 
     with torch.cuda.stream(stream):
         for i in range(args.warmup):
             step(i)
     torch.cuda.synchronize()
 
-    # verify one SST against the oracle (bit-exact) before timing
+    # verify against the oracle (bit-exact) before timing: the first and the last SST of a set
     verified = None
     if not args.no_verify:
         step(0)
         torch.cuda.synchronize()
-        got = outs[0].to_host()
-        sm = got["summary"]
-        assert sm.status == 0, "encode failed: %s" % _abi.STATUS_NAMES.get(sm.status)
-        if rank == 0:
-            from oracle import oracle as O
-            ref = O.encode_sst(hosts[0], O.params(block_size=4096, sst_version=2, bloom_bits_per_key=args.bpk))
-            verified = bool(np.array_equal(got["data"], ref.data) and np.array_equal(got["bloom"], ref.bloom)
-                            and np.array_equal(got["block_off"], ref.block_off))
-            assert verified, "GPU output differs from the oracle"
-    sm = outs[0].summary_host()
-    alg_bytes = hosts[0].algorithmic_input_bytes() + sm.data_len + sm.bloom_len
+        from oracle import oracle as O
+        oprm = O.params(block_size=4096, sst_version=2, bloom_bits_per_key=args.bpk)
+        verified = True
+        for q in sorted({0, batch - 1}):
+            got = outs[0][q].to_host()
+            assert got["summary"].status == 0, "encode failed: %s" % _abi.STATUS_NAMES.get(got["summary"].status)
+            if rank == 0:
+                ref = O.encode_sst(hosts[q], oprm)
+                ok = (np.array_equal(got["data"], ref.data) and np.array_equal(got["bloom"], ref.bloom)
+                      and np.array_equal(got["block_off"], ref.block_off)
+                      and np.array_equal(got["index_key_len"], ref.index_key_len))
+                assert ok, "GPU output of SST %d differs from the oracle" % q
+    sm = outs[0][0].summary_host()
+    alg_sst = hosts[0].algorithmic_input_bytes() + sm.data_len + sm.bloom_len
 
     # timed region
     if dist:
@@ -168,34 +207,48 @@ def main():
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+    elapsed = time.perf_counter() - t0
     dev_ms = ev0.elapsed_time(ev1)
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    total_bytes, max_elapsed = job.aggregate(tdist if dist else None, args.steps * batch * logical, elapsed, dev)
 
-    # stage timing pass (HIP events around each kernel on the encode stream)
+    # per-kernel pass: HIP events recorded around each kernel on the encode stream (sdb_diag_*)
     lib.sdb_diag_enable_stage_timing(1)
-    for i in range(args.steps):
+    for i in range(args.stage_steps):
         step(i)
     torch.cuda.synchronize()
     lib.sdb_diag_enable_stage_timing(0)
     ms = (C.c_double * 16)()
     launches = C.c_uint64(0)
     ns = lib.sdb_diag_stage_times(ms, 16, C.byref(launches))
-    nl = max(launches.value, 1)
-    stage_ms = {_abi.STAGES[i]: ms[i] / nl for i in range(ns)}
-    emit_ms = stage_ms["emit"]
-    # algorithmic bytes of the emit kernel: read keys+values(+seq/flags), write the data section
-    emit_bytes = hosts[0].algorithmic_input_bytes() + sm.data_len
-    emit_gbs = emit_bytes / (emit_ms * 1e-3) / 1e9
+    nl = max(args.stage_steps, 1)
+    stage_ms = {_abi.STAGES[i]: ms[i] / nl for i in range(ns) if ms[i] > 0}
+    emit_ms = stage_ms.get("emit", 0.0)
+    emit_bytes = batch * (hosts[0].algorithmic_input_bytes() + sm.data_len)  # read keys+values(+seq/flags), write data
+    emit_gbs = emit_bytes / (emit_ms * 1e-3) / 1e9 if emit_ms else 0.0
 
-    total_logical = world * args.steps * logical
-    value = total_logical / elapsed / 2**30
-    ms_per_step = elapsed / args.steps * 1e3
-    pipe_gbs = alg_bytes / (dev_ms / args.steps * 1e-3) / 1e9
+    # single-SST latency (configs[1] shape: sdb_encode_sst, one SST per launch sequence)
+    single = None
+    if args.single_steps and rank == 0:
+        one = runtime.DeviceSstOutput(hosts[0].n, logical, logical, prm, device=dev)
+        for i in range(10):
+            runtime.encode_sst_device(dbs[i % len(dbs)], one, stream)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(args.single_steps):
+            runtime.encode_sst_device(dbs[i % len(dbs)], one, stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        sms = e0.elapsed_time(e1) / args.single_steps
+        sg = alg_sst / (sms * 1e-3) / 1e9
+        single = {"device_ms_per_sst": round(sms, 5), "GiB_per_s": round(logical / (sms * 1e-3) / 2**30, 2),
+                  "achieved_GBps": round(sg, 1), "frac": round(sg / PEAK_HBM_GBS, 4)}
+
+    value = job.job_rate_gibs(total_bytes, max_elapsed)
+    ms_per_step = max_elapsed / args.steps * 1e3
+    set_ms = dev_ms / args.steps
+    pipe_gbs = batch * alg_sst / (set_ms * 1e-3) / 1e9
+    traffic_sst, traffic_kernels = pmc_traffic()
     line = {
         "metric": "GiB/s device-resident SST block encode+bloom, 64 MiB sorted KV, 1/2/4/8 GPU",
         "value": round(value, 3),
@@ -205,27 +258,37 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (D1: seeded 12-byte BE counter keys + 4-byte SST index, 100 random value bytes)",
-        "config": {"workload": "configs[1]: encode one 64 MiB L0 SST (578,524 x 16 B key / 100 B value) "
-                               "-> 17,016 V2 4 KiB blocks + CRC32 + bloom 10 bits/key, per GPU per step",
-                   "entries_per_sst": hosts[0].n, "block_size": 4096, "sst_version": 2,
-                   "bloom_bits_per_key": 10, "resident_ssts_per_gpu": args.ssts,
+        "data": "synthetic (D1: seeded 12-byte BE counter keys + 4-byte BE SST index, 100 random value bytes)",
+        "config": {"workload": ("configs[4] job: %d distinct 64 MiB SSTs, SST j -> GPU j mod N, one pass per step"
+                                % args.job_ssts) if args.job_ssts else
+                               ("%d distinct 64 MiB L0/compaction SSTs per GPU per step (the per-GPU share of "
+                                "configs[4]; each SST = configs[1]: 578,524 x 16 B key / 100 B value -> 17,016 "
+                                "V2 4 KiB blocks + CRC32 + bloom 10 bits/key), one sdb_encode_ssts launch "
+                                "sequence" % batch),
+                   "ssts_per_gpu_per_step": batch, "entries_per_sst": hosts[0].n, "block_size": 4096,
+                   "sst_version": 2, "bloom_bits_per_key": args.bpk, "resident_input_ssts_per_gpu": len(dbs),
                    "parallelism": "independent SSTs per GPU (no collective)"},
-        "roofline": {"bound": "hbm", "kernel": "k_emit", "achieved": round(emit_gbs, 1),
-                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(emit_gbs / PEAK_HBM_GBS, 4),
-                     "traffic": pmc_traffic("k_emit"), "algorithmic_bytes_per_launch": emit_bytes,
-                     "avg_launch_ms": round(emit_ms, 5),
-                     "pipeline": {"algorithmic_bytes_per_sst": alg_bytes, "device_ms_per_sst": round(dev_ms / args.steps, 5),
-                                  "achieved_GBps": round(pipe_gbs, 1), "frac": round(pipe_gbs / PEAK_HBM_GBS, 4),
-                                  "stage_ms": {k: round(v, 5) for k, v in stage_ms.items()}}},
+        "roofline": {"bound": "hbm", "kernel": "whole encode pipeline (k_facts, k_bloom_bin_hd, k_seg, k_group, "
+                                               "k_enum, k_bloom_fill_hd, k_emit: one launch sequence per step)",
+                     "achieved": round(pipe_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(pipe_gbs / PEAK_HBM_GBS, 4),
+                     "traffic": traffic_sst * batch if traffic_sst else None,
+                     "traffic_source": ("committed PMC passes profiles/%s (same command, per SST x batch)" % PMC_FILE)
+                     if traffic_sst else None,
+                     "algorithmic_bytes_per_step": batch * alg_sst, "algorithmic_bytes_per_sst": alg_sst,
+                     "device_ms_per_step": round(set_ms, 5), "device_ms_per_sst": round(set_ms / batch, 5),
+                     "k_emit": {"achieved": round(emit_gbs, 1), "frac": round(emit_gbs / PEAK_HBM_GBS, 4),
+                                "avg_launch_ms": round(emit_ms, 5), "algorithmic_bytes_per_launch": emit_bytes,
+                                "traffic_per_sst": traffic_kernels.get("k_emit")},
+                     "stage_ms_per_step": {k: round(v, 5) for k, v in stage_ms.items()}},
+        "single_sst": single,
         "verified_vs_oracle": verified,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, threads)
+        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_threads or cpu_share())
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:

@@ -28,8 +28,10 @@
  *
  * Conventions
  *   - "device" entry points take device pointers and enqueue on `stream` (a hipStream_t passed as
- *     void*; NULL = the legacy default stream).  They never allocate, never synchronise, and are
- *     safe to capture into a HIP graph.  Results that the host needs (lengths, status) are written
+ *     void*; NULL = the legacy default stream).  They never allocate, never synchronise, launch only
+ *     on `stream` (no side streams, no cross-stream events; concurrent calls on different streams
+ *     share nothing), and are safe to capture into a HIP graph.  Results that the host needs
+ *     (lengths, status) are written
  *     to a device-resident summary struct the caller copies back.
  *   - "host" entry points take host pointers, manage a per-handle device arena + pinned staging and
  *     return synchronously.
@@ -48,7 +50,7 @@
 extern "C" {
 #endif
 
-#define SDB_ABI_VERSION 1u
+#define SDB_ABI_VERSION 2u
 
 /* Status codes.  Mirrors the hot-path variants of SlateDBError (slatedb/src/error.rs:23-38,
  * 142-152, 197); the reference *panics* where SDB_LIMIT_EXCEEDED is returned. */
@@ -160,17 +162,32 @@ sdb_status sdb_encode_sst(const sdb_kv_batch *batch, const sdb_sst_params *param
                           const sdb_sst_out *out, void *workspace, uint64_t workspace_bytes,
                           void *stream);
 
+/* Encode `count` independent SSTs that share `params` in ONE launch sequence on `stream` (the SSTs of
+ * one compaction job or of concurrent L0 flushes: l0_flush_parallelism / subcompactions,
+ * config.rs:1081, 1383-1390).  Same per-SST contract as sdb_encode_sst (outs[i] for batches[i]; the
+ * device checks land in outs[i].summary).  The kernels of up to 8 SSTs share each launch, so the
+ * latency-bound segmentation of small grids fills the chip; larger counts run as consecutive sets.
+ * workspace: sdb_encode_ssts_workspace_bytes(count, batches, params) bytes (only batches[i].n is read
+ * on the host). */
+uint64_t sdb_encode_ssts_workspace_bytes(uint32_t count, const sdb_kv_batch *batches,
+                                         const sdb_sst_params *params);
+sdb_status sdb_encode_ssts(uint32_t count, const sdb_kv_batch *batches, const sdb_sst_params *params,
+                           const sdb_sst_out *outs, void *workspace, uint64_t workspace_bytes,
+                           void *stream);
+
 /* Bloom bitmap over n keys (BloomFilterBuilder with whole-key filtering, filter.rs:40-90).
- * bitmap must hold sdb_bloom_filter_bytes(n, bpk) bytes; it is zeroed and filled on `stream`.
- * workspace (sdb_bloom_workspace_bytes) holds the per-XCD replicas; NULL selects the slower
- * device-scope-atomic build. */
+ * bitmap must hold sdb_bloom_filter_bytes(n, bpk) bytes and be 4-byte aligned (the build stores
+ * 32-bit words); it is zeroed and filled on `stream`.  workspace (sdb_bloom_workspace_bytes) holds
+ * the binned probes; NULL selects the slower device-scope-atomic build, which also needs
+ * bitmap_bytes >= the filter size rounded up to 4.  Otherwise SDB_INVALID_ARGUMENT. */
 uint64_t sdb_bloom_workspace_bytes(uint64_t num_keys, uint32_t bits_per_key);
 sdb_status sdb_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
                            uint32_t bits_per_key, uint8_t *bitmap, uint64_t bitmap_bytes,
                            void *workspace, uint64_t workspace_bytes, void *stream);
 
 /* Batched BloomFilter::might_contain(filter_hash(key)) (filter.rs:124-136, 150-175): result[i]=1
- * iff every probe bit is set.  An empty bitmap answers 0. */
+ * iff every probe bit is set.  An empty bitmap answers 0.  The bitmap may start at any byte address
+ * (e.g. inside an SST's filter block); only bytes [0, bitmap_bytes) are read. */
 sdb_status sdb_bloom_might_contain(const uint8_t *bitmap, uint64_t bitmap_bytes,
                                    uint32_t num_probes, const uint8_t *key_bytes,
                                    const uint64_t *key_off, uint64_t n, uint8_t *result,

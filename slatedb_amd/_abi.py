@@ -133,6 +133,9 @@ SIGNATURES = {
     "sdb_bloom_num_probes": (C.c_uint32, [C.c_uint32]),
     "sdb_encode_sst": (C.c_int, [C.POINTER(KvBatch), C.POINTER(SstParams), C.POINTER(SstOut),
                                  C.c_void_p, C.c_uint64, C.c_void_p]),
+    "sdb_encode_ssts_workspace_bytes": (C.c_uint64, [C.c_uint32, C.POINTER(KvBatch), C.POINTER(SstParams)]),
+    "sdb_encode_ssts": (C.c_int, [C.c_uint32, C.POINTER(KvBatch), C.POINTER(SstParams), C.POINTER(SstOut),
+                                  C.c_void_p, C.c_uint64, C.c_void_p]),
     "sdb_bloom_workspace_bytes": (C.c_uint64, [C.c_uint64, C.c_uint32]),
     "sdb_bloom_build": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p,
                                   C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]),
@@ -163,7 +166,7 @@ SIGNATURES = {
 }
 
 
-STAGES = ["bloom", "facts", "seg", "group", "enum", "emit", "emit_slow"]
+STAGES = ["bloom", "facts", "seg", "group", "enum", "emit", "emit_slow", "bloom_fill"]
 
 
 def bind(lib):

@@ -98,9 +98,166 @@ sdb_status sdb_encode_bounds(uint64_t n, uint64_t total_key_bytes, uint64_t tota
     return SDB_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// One SST's workspace region (256-byte multiple) inside a set's workspace.
+uint64_t sst_ws_bytes(uint64_t n, const sdb_sst_params *p) {
+    const uint64_t fb = p->bloom_bits_per_key ? filter_bytes_for(n, p->bloom_bits_per_key) : 0;
+    return (encode_workspace_layout(n, fb, num_probes_for(p->bloom_bits_per_key)).total + 255) & ~255ull;
+}
+
+sdb_status check_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const sdb_sst_out *out) {
+    if (!b || !out || !out->summary) return SDB_INVALID_ARGUMENT;
+    const uint64_t n = b->n;
+    if (n >= (1ull << 31)) return SDB_LIMIT_EXCEEDED;
+    if (n && (!b->key_bytes || !b->key_off || !b->val_off)) return SDB_INVALID_ARGUMENT;
+    const bool want_filter = p->sst_type != SDB_SST_WAL && p->bloom_bits_per_key > 0 && n >= p->min_filter_keys;
+    const uint64_t fb = want_filter ? filter_bytes_for(n, p->bloom_bits_per_key) : 0;
+    if (want_filter && fb && (!out->bloom || out->bloom_cap < fb)) return SDB_INVALID_ARGUMENT;
+    if (n && (!out->data || !out->block_off || !out->block_first_entry || !out->index_key_len || !out->block_stats))
+        return SDB_INVALID_ARGUMENT;
+    return SDB_OK;
+}
+
+// The slot of one SST (no launches); *standalone_bloom: the filter needs the standalone build first.
+SstSlot plan_slot(const sdb_kv_batch *b, const sdb_sst_params *p, const sdb_sst_out *out, uint8_t *ws,
+                  bool *standalone_bloom) {
+    const uint64_t n = b->n;
+    const bool want_filter = p->sst_type != SDB_SST_WAL && p->bloom_bits_per_key > 0 && n >= p->min_filter_keys;
+    const uint64_t fb = want_filter ? filter_bytes_for(n, p->bloom_bits_per_key) : 0;
+    SstSlot s{};
+    s.key_bytes = b->key_bytes;
+    s.key_off = b->key_off;
+    s.val_bytes = b->val_bytes;
+    s.val_off = b->val_off;
+    s.kind = b->kind;
+    s.seq = b->seq;
+    s.create_ts = b->create_ts;
+    s.expire_ts = b->expire_ts;
+    s.ts_mask = b->ts_mask;
+    s.n = n;
+    s.out_data = out->data;
+    s.out_block_off = out->block_off;
+    s.out_block_first = out->block_first_entry;
+    s.out_index_key_len = out->index_key_len;
+    s.out_block_stats = out->block_stats;
+    s.data_cap = out->data_cap;
+    s.block_cap = out->block_cap;
+    s.summary = out->summary;
+    s.bloom_out = out->bloom;
+    s.bloom_len = fb;
+    s.ws = ws;
+    s.num_probes = want_filter ? num_probes_for(p->bloom_bits_per_key) : 0;
+    s.filter_built = want_filter ? 1 : 0;
+    s.has_filter_ws = (p->bloom_bits_per_key && filter_bytes_for(n, p->bloom_bits_per_key)) ? 1 : 0;
+    s.nchunks = (uint32_t)((n + kChunk - 1) / kChunk);
+    s.nfacts = (uint32_t)((n + kFactsThreads - 1) / kFactsThreads);
+    {   // chunks per group: about sqrt(nchunks), so k_enum walks <= ~2 sqrt(nchunks) tables
+        uint32_t g = 16;
+        while ((uint64_t)g * g < s.nchunks) g++;
+        s.group = g;
+    }
+    *standalone_bloom = false;
+    if (want_filter && n) {
+        // the bloom is fused with the encode (k_facts hashes, binned per chunk) when the binned build
+        // fits; otherwise the standalone build runs before the set
+        const BloomPlan pl = bloom_plan(n, s.num_probes, fb, kChunk);
+        if (bloom_plan_fits(pl)) {
+            s.bloom_fused = 1;
+            s.bpl = pl;
+            s.slot_cap = bloom_slot_cap(pl);
+        } else {
+            *standalone_bloom = true;
+        }
+    }
+    return s;
+}
+
+SstSet set_header(const sdb_sst_params *p) {
+    SstSet P{};
+    P.block_size = p->block_size;
+    P.restart_interval = p->sst_version == 2 ? p->restart_interval : 1;
+    P.version = p->sst_version;
+    P.wal = p->sst_type == SDB_SST_WAL;
+    // a block holds at most (block_size - 2) / 12 + 1 entries (smallest row: 12 bytes in V2, 13 in V1);
+    // blocks longer than the lookahead continue from HBM inside k_seg
+    const uint64_t look = (uint64_t)p->block_size / 12 + 2;
+    P.seg_look = (uint32_t)(look < kSegLook ? look : kSegLook);
+    return P;
+}
+}  // namespace
+
+extern "C" {
+
 uint64_t sdb_encode_workspace_bytes(uint64_t n, const sdb_sst_params *params) {
-    uint64_t fb = params && params->bloom_bits_per_key ? filter_bytes_for(n, params->bloom_bits_per_key) : 0;
-    return encode_workspace_layout(n, fb, params ? num_probes_for(params->bloom_bits_per_key) : 0).total;
+    if (!params) return 0;
+    return sst_ws_bytes(n, params) + 256;
+}
+
+uint64_t sdb_encode_ssts_workspace_bytes(uint32_t count, const sdb_kv_batch *batches, const sdb_sst_params *params) {
+    if (!params || (count && !batches)) return 0;
+    uint64_t t = 256;
+    for (uint32_t i = 0; i < count; i++) t += sst_ws_bytes(batches[i].n, params);
+    return t;
+}
+
+sdb_status sdb_encode_ssts(uint32_t count, const sdb_kv_batch *batches, const sdb_sst_params *p,
+                           const sdb_sst_out *outs, void *workspace, uint64_t workspace_bytes, void *stream) {
+    sdb_status st = check_params(p);
+    if (st) return st;
+    if (count && (!batches || !outs)) return SDB_INVALID_ARGUMENT;
+    for (uint32_t i = 0; i < count; i++)
+        if ((st = check_sst(&batches[i], p, &outs[i]))) return st;
+    if (!device_ok()) return SDB_DEVICE_ERROR;
+    if (!workspace || workspace_bytes < sdb_encode_ssts_workspace_bytes(count, batches, p)) return SDB_INVALID_ARGUMENT;
+    hipStream_t s = S(stream);
+    uint8_t *ws = (uint8_t *)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+    SstSet P = set_header(p);
+    size_t bin_lds = 0, fill_lds = 0;
+    auto flush = [&]() -> bool {
+        const bool ok = launch_encode_set(P, bin_lds, fill_lds, s) == hipSuccess;
+        SstSet q = set_header(p);
+        P = q;
+        bin_lds = fill_lds = 0;
+        return ok;
+    };
+    for (uint32_t i = 0; i < count; i++) {
+        bool standalone = false;
+        const SstSlot slot = plan_slot(&batches[i], p, &outs[i], ws, &standalone);
+        ws += sst_ws_bytes(batches[i].n, p);
+        if (standalone) {
+            SstSet one = set_header(p);
+            one.count = 1;
+            one.s[0] = slot;
+            const EncodeArgs a = make_args(one, 0);
+            stage_mark(s, kStBloom, true);
+            if (launch_bloom_build(slot.key_bytes, slot.key_off, slot.n, slot.num_probes, slot.bloom_out, slot.bloom_len,
+                                   (void *)a.bq.count, s) != hipSuccess)
+                return SDB_DEVICE_ERROR;
+            stage_mark(s, kStBloom, false);
+        }
+        if (!slot.n) {  // empty SST: summary only (a filter of an empty SST has no bytes)
+            SstSet one = set_header(p);
+            one.count = 1;
+            one.s[0] = slot;
+            if (launch_encode_empty(make_args(one, 0), s) != hipSuccess) return SDB_DEVICE_ERROR;
+            continue;
+        }
+        P.s[P.count++] = slot;
+        P.max_facts = std::max(P.max_facts, slot.nfacts);
+        P.max_chunks = std::max(P.max_chunks, slot.nchunks);
+        P.max_groups = std::max(P.max_groups, (slot.nchunks + slot.group - 1) / slot.group);
+        if (slot.bloom_fused) {
+            P.max_tiles = std::max(P.max_tiles, slot.bpl.tiles);
+            P.max_slices = std::max(P.max_slices, slot.bpl.nslices);
+            bin_lds = std::max(bin_lds, bloom_bin_lds(slot.bpl));
+            fill_lds = std::max(fill_lds, bloom_fill_lds(slot.bpl));
+        }
+        if (P.count == kMaxSsts && !flush()) return SDB_DEVICE_ERROR;
+    }
+    if (P.count && !flush()) return SDB_DEVICE_ERROR;
+    return SDB_OK;
 }
 
 uint64_t sdb_bloom_workspace_bytes(uint64_t n, uint32_t bits_per_key) {
@@ -109,109 +266,8 @@ uint64_t sdb_bloom_workspace_bytes(uint64_t n, uint32_t bits_per_key) {
 
 sdb_status sdb_encode_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const sdb_sst_out *out,
                           void *workspace, uint64_t workspace_bytes, void *stream) {
-    if (!b || !out || !out->summary) return SDB_INVALID_ARGUMENT;
-    sdb_status st = check_params(p);
-    if (st) return st;
-    if (!device_ok()) return SDB_DEVICE_ERROR;
-    const uint64_t n = b->n;
-    if (n >= (1ull << 31)) return SDB_LIMIT_EXCEEDED;
-    if (n && (!b->key_bytes || !b->key_off || !b->val_off)) return SDB_INVALID_ARGUMENT;
-    const bool want_filter = p->sst_type != SDB_SST_WAL && p->bloom_bits_per_key > 0 && n >= p->min_filter_keys;
-    const uint64_t fb = want_filter ? filter_bytes_for(n, p->bloom_bits_per_key) : 0;
-    EncodeWorkspace wl = encode_workspace_layout(n, p->bloom_bits_per_key ? filter_bytes_for(n, p->bloom_bits_per_key) : 0,
-                                                 num_probes_for(p->bloom_bits_per_key));
-    if (!workspace || workspace_bytes < wl.total) return SDB_INVALID_ARGUMENT;
-    if (want_filter && fb && (!out->bloom || out->bloom_cap < fb)) return SDB_INVALID_ARGUMENT;
-    if (n && (!out->data || !out->block_off || !out->block_first_entry || !out->index_key_len ||
-              !out->block_stats))
-        return SDB_INVALID_ARGUMENT;
-
-    EncodeArgs a{};
-    a.key_bytes = b->key_bytes;
-    a.key_off = b->key_off;
-    a.val_bytes = b->val_bytes;
-    a.val_off = b->val_off;
-    a.kind = b->kind;
-    a.seq = b->seq;
-    a.create_ts = b->create_ts;
-    a.expire_ts = b->expire_ts;
-    a.ts_mask = b->ts_mask;
-    a.n = n;
-    a.block_size = p->block_size;
-    a.restart_interval = p->sst_version == 2 ? p->restart_interval : 1;
-    a.version = p->sst_version;
-    a.wal = p->sst_type == SDB_SST_WAL;
-    a.nchunks = (uint32_t)((n + kChunk - 1) / kChunk);
-    {   // a block holds at most (block_size - 2) / 12 + 1 entries (smallest row: 12 bytes in V2, 13 in V1);
-        // blocks longer than the lookahead continue from HBM inside k_seg
-        uint64_t look = (uint64_t)p->block_size / 12 + 2;
-        a.seg_look = (uint32_t)(look < kSegLook ? look : kSegLook);
-    }
-    a.lcp = carve<uint32_t>(workspace, wl.lcp);
-    a.szr = carve<uint32_t>(workspace, wl.szr);
-    a.sznr = carve<uint32_t>(workspace, wl.sznr);
-    a.hd = carve<uint64_t>(workspace, wl.hd);
-    a.row_scratch = carve<uint32_t>(workspace, wl.row_scratch);
-    a.next = carve<uint32_t>(workspace, wl.next);
-    a.bbytes = carve<uint32_t>(workspace, wl.bbytes);
-    a.tab_exit = carve<uint32_t>(workspace, wl.tab_exit);
-    a.tab_cnt = carve<uint32_t>(workspace, wl.tab_cnt);
-    a.tab_bytes = carve<uint64_t>(workspace, wl.tab_bytes);
-    a.anchor_e = carve<uint32_t>(workspace, wl.anchor_e);
-    a.anchor_blk = carve<uint32_t>(workspace, wl.anchor_blk);
-    a.anchor_byte = carve<uint64_t>(workspace, wl.anchor_byte);
-    a.err = carve<unsigned long long>(workspace, wl.err);
-    a.wmax = carve<uint32_t>(workspace, wl.wmax);
-    a.slow_count = carve<uint32_t>(workspace, wl.slow_count);
-    a.slow_list = carve<uint32_t>(workspace, wl.slow_list);
-    a.desc = carve<BlockDesc>(workspace, wl.desc);
-    a.stat_part = carve<uint64_t>(workspace, wl.stat_part);
-    a.wmax_part = carve<uint32_t>(workspace, wl.wmax_part);
-    a.err_part = carve<unsigned long long>(workspace, wl.err_part);
-    a.done = carve<uint32_t>(workspace, wl.done);
-    a.gtab_exit = carve<uint32_t>(workspace, wl.gtab_exit);
-    a.gtab_cnt = carve<uint32_t>(workspace, wl.gtab_cnt);
-    a.gtab_bytes = carve<uint64_t>(workspace, wl.gtab_bytes);
-    a.mode = carve<uint32_t>(workspace, wl.mode);
-    {   // chunks per group: about sqrt(nchunks), so k_enum walks <= ~2 sqrt(nchunks) tables
-        uint32_t g = 16;
-        while ((uint64_t)g * g < a.nchunks) g++;
-        a.group = g;
-    }
-    a.out_data = out->data;
-    a.out_block_off = out->block_off;
-    a.out_block_first = out->block_first_entry;
-    a.out_index_key_len = out->index_key_len;
-    a.out_block_stats = out->block_stats;
-    a.data_cap = out->data_cap;
-    a.block_cap = out->block_cap;
-    a.summary = out->summary;
-    a.bloom_len = fb;
-    a.num_probes = want_filter ? num_probes_for(p->bloom_bits_per_key) : 0;
-    a.filter_built = want_filter ? 1 : 0;
-    hipStream_t s = S(stream);
-    if (want_filter && n) {
-        // the bloom is fused with the encode (k_facts hashes; the binning and fill run on a side stream
-        // beside k_seg .. k_emit) when the binned build fits; otherwise it is built before the encode
-        const BloomPlan pl = bloom_plan(n, a.num_probes, fb, kChunk);
-        if (bloom_plan_fits(pl)) {
-            a.bloom_fused = 1;
-            a.bpl = pl;
-            a.bq = bloom_slots(carve<void>(workspace, wl.bloom_rep), pl);
-            a.bloom_out = out->bloom;
-        } else {
-            stage_mark(s, kStBloom, true);
-            if (launch_bloom_build(b->key_bytes, b->key_off, n, a.num_probes, out->bloom, fb,
-                                   carve<void>(workspace, wl.bloom_rep), s) != hipSuccess)
-                return SDB_DEVICE_ERROR;
-            stage_mark(s, kStBloom, false);
-        }
-    } else if (want_filter) {
-        if (launch_bloom_build(b->key_bytes, b->key_off, n, a.num_probes, out->bloom, fb, nullptr, s) != hipSuccess)
-            return SDB_DEVICE_ERROR;
-    }
-    if (launch_encode(a, s) != hipSuccess) return SDB_DEVICE_ERROR;
-    return SDB_OK;
+    if (!b || !out) return SDB_INVALID_ARGUMENT;
+    return sdb_encode_ssts(1, b, p, out, workspace, workspace_bytes, stream);
 }
 
 sdb_status sdb_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
@@ -220,6 +276,9 @@ sdb_status sdb_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, ui
     if (!device_ok()) return SDB_DEVICE_ERROR;
     uint64_t fb = filter_bytes_for(n, bits_per_key);
     if (bitmap_bytes < fb || (fb && !bitmap) || (n && (!key_bytes || !key_off))) return SDB_INVALID_ARGUMENT;
+    // the build writes 32-bit words: a 4-byte aligned bitmap, and (atomic path, no workspace) room for
+    // the word that holds the last byte
+    if (((uintptr_t)bitmap & 3) || (!workspace && fb && bitmap_bytes < ((fb + 3) & ~3ull))) return SDB_INVALID_ARGUMENT;
     if (workspace && workspace_bytes < sdb_bloom_workspace_bytes(n, bits_per_key)) return SDB_INVALID_ARGUMENT;
     if (launch_bloom_build(key_bytes, key_off, n, num_probes_for(bits_per_key), bitmap, fb, workspace, S(stream)) != hipSuccess)
         return SDB_DEVICE_ERROR;

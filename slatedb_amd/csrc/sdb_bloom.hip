@@ -5,6 +5,8 @@
 // (siphasher 1.0.3, filter.rs:196-204); probes by enhanced double hashing (filter.rs:206-221);
 // LSB-first bit order (filter.rs:223-233).  Bit p of the byte-addressed bitmap is bit (p & 31) of the
 // little-endian 32-bit word p >> 5, so setting it is one 32-bit atomicOr.
+#include <mutex>
+
 #include "sdb_bloom.h"
 
 namespace sdb {
@@ -38,7 +40,9 @@ __global__ __launch_bounds__(kFillThreads) void k_bloom_fill(const uint8_t *__re
     bloom_fill_slice(blockIdx.x, key_bytes, key_off, n, pl, q, bitmap, bytes, lds);
 }
 
-__global__ __launch_bounds__(256) void k_bloom_query(const uint32_t *bitmap, uint32_t k, uint32_t m,
+// Byte-granular probe reads: the bitmap may sit at any address (e.g. 17 bytes into an SST's filter
+// block, format/sst.rs:394-421) and is read only inside [0, ceil(m / 8)).
+__global__ __launch_bounds__(256) void k_bloom_query(const uint8_t *bitmap, uint32_t k, uint32_t m,
                                                      const uint8_t *__restrict__ key_bytes,
                                                      const uint64_t *__restrict__ key_off, uint64_t n,
                                                      uint8_t *result) {
@@ -50,7 +54,7 @@ __global__ __launch_bounds__(256) void k_bloom_query(const uint32_t *bitmap, uin
             uint64_t h = siphash13(key_bytes + ko, key_off[i + 1] - ko);
             r = 1;
             for_each_probe(h, k, m, [&](uint32_t p) {
-                if (!((bitmap[p >> 5] >> (p & 31)) & 1u)) {
+                if (!((bitmap[p >> 3] >> (p & 7)) & 1u)) {
                     r = 0;
                     return false;
                 }
@@ -136,13 +140,12 @@ hipError_t launch_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off,
                            num_probes, pl.m, (uint32_t *)bitmap);
         return hipGetLastError();
     }
-    static bool attrs = false;
-    if (!attrs) {
-        hipFuncSetAttribute((const void *)k_bloom_bin, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLds);
-        hipFuncSetAttribute((const void *)k_bloom_fill, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    static std::once_flag attrs;
+    std::call_once(attrs, [] {
+        (void)hipFuncSetAttribute((const void *)k_bloom_bin, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLds);
+        (void)hipFuncSetAttribute((const void *)k_bloom_fill, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
         (void)hipGetLastError();  // an unsupported attribute value must not poison the launch status
-        attrs = true;
-    }
+    });
     const BloomSlots q = bloom_slots(ws, pl);
     hipLaunchKernelGGL(k_bloom_bin, dim3(pl.tiles), dim3(kBinThreads), bloom_bin_lds(pl), st, key_bytes, key_off, n, pl, q);
     hipLaunchKernelGGL(k_bloom_fill, dim3(pl.nslices), dim3(kFillThreads), bloom_fill_lds(pl), st, key_bytes, key_off, n, pl,
@@ -157,7 +160,7 @@ hipError_t launch_bloom_query(const uint8_t *bitmap, uint64_t bitmap_bytes, uint
     uint32_t m = (uint32_t)(bitmap_bytes * 8);
     uint64_t blocks = (n + 255) / 256;
     if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(k_bloom_query, dim3((uint32_t)blocks), dim3(256), 0, st, (const uint32_t *)bitmap,
+    hipLaunchKernelGGL(k_bloom_query, dim3((uint32_t)blocks), dim3(256), 0, st, bitmap,
                        num_probes, m, key_bytes, key_off, n, result);
     return hipGetLastError();
 }

@@ -234,7 +234,7 @@ SDB_DEV BlockView load_block(const DecodeArgs &a, uint64_t k, uint8_t *stage, co
     BlockView v{};
     const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
     const uint64_t len = e - s;
-    if (len < 4) {
+    if (e < s || len < 4) {  // a non-monotone block_off is a corrupt range, never a huge read
         v.status = SDB_CORRUPT_BLOCK;
         return v;
     }

@@ -117,7 +117,9 @@ struct EncodeArgs {
     uint32_t num_probes, filter_built;
 };
 
-// Workspace layout for n entries (all offsets 256-byte aligned).
+// Workspace layout for n entries (all offsets 256-byte aligned).  Everything up to `bloom_rep` depends
+// only on n (and whether a filter is built), so the kernels recompute the layout on the device from
+// the SST's workspace base; the bloom slots come last and are sized on the host.
 struct EncodeWorkspace {
     uint64_t lcp, szr, sznr, hd, row_scratch, next, bbytes, tab_exit, tab_cnt, tab_bytes;
     uint64_t anchor_e, anchor_blk, anchor_byte, err, wmax, slow_count, slow_list, desc, stat_part, wmax_part, bloom_rep;
@@ -126,7 +128,7 @@ struct EncodeWorkspace {
 };
 uint64_t bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
 uint64_t encode_bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
-inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes, uint32_t num_probes) {
+__host__ __device__ inline EncodeWorkspace encode_workspace_offsets(uint64_t n, bool has_filter) {
     EncodeWorkspace w{};
     uint64_t off = 0;
     auto take = [&](uint64_t bytes) {
@@ -138,7 +140,7 @@ inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes
     w.lcp = take(4 * (n + 1));
     w.szr = take(4 * (n + 1));
     w.sznr = take(4 * (n + 1));
-    w.hd = take(filter_bytes ? 8 * (n + 1) : 0);
+    w.hd = take(has_filter ? 8 * (n + 1) : 0);
     w.row_scratch = take(4 * (n + 1));
     w.next = take(4 * (n + 1));
     w.bbytes = take(4 * (n + 1));
@@ -162,15 +164,137 @@ inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes
     w.gtab_cnt = take(4 * (nc * kSegLook + 1));
     w.gtab_bytes = take(8 * (nc * kSegLook + 1));
     w.mode = take(4);
-    w.bloom_rep = take(filter_bytes ? encode_bloom_workspace_bytes(n, num_probes, filter_bytes) : 0);  // bloom slots
+    w.bloom_rep = off;  // bloom slots (host-sized) last
     w.total = off;
     return w;
 }
+inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes, uint32_t num_probes) {
+    EncodeWorkspace w = encode_workspace_offsets(n, filter_bytes != 0);
+    w.total = w.bloom_rep + ((filter_bytes ? encode_bloom_workspace_bytes(n, num_probes, filter_bytes) : 0) + 255) / 256 * 256;
+    return w;
+}
 
-hipError_t launch_encode(EncodeArgs a, hipStream_t st);
+// ------------------------------------------------------------------------------------------------
+// A launch set: up to kMaxSsts independent SSTs with the same SsTableFormat knobs encoded by ONE
+// launch sequence (blockIdx.y = SST for the per-SST grids; k_emit spreads every SST's blocks over one
+// persistent grid).  The compaction / flush callers run several builders at once (l0_flush_parallelism,
+// subcompactions: config.rs:1081, 1383-1390); batching them fills the GPU with the latency-bound
+// segmentation kernels of all of them at once.  Passed by value (kernel arguments).
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kMaxSsts = 8;
+struct SstSlot {
+    const uint8_t *key_bytes;
+    const uint64_t *key_off;
+    const uint8_t *val_bytes;
+    const uint64_t *val_off;
+    const uint8_t *kind;
+    const uint64_t *seq;
+    const int64_t *create_ts;
+    const int64_t *expire_ts;
+    const uint8_t *ts_mask;
+    uint64_t n;
+    uint8_t *out_data;
+    uint64_t *out_block_off;
+    uint32_t *out_block_first;
+    uint32_t *out_index_key_len;
+    uint16_t *out_block_stats;
+    uint64_t data_cap, block_cap;
+    sdb_sst_summary *summary;
+    uint8_t *bloom_out;
+    uint64_t bloom_len;
+    uint8_t *ws;              // this SST's workspace (256-byte aligned)
+    uint32_t num_probes, filter_built, bloom_fused, has_filter_ws;  // has_filter_ws: hd in the layout
+    uint32_t nchunks, nfacts, group, slot_cap;
+    BloomPlan bpl;            // fused bloom plan (bloom_fused)
+};
+struct SstSet {
+    uint32_t count;
+    uint32_t block_size, restart_interval, version, wal, seg_look;
+    uint32_t max_facts, max_chunks, max_groups, max_tiles, max_slices, pad;
+    SstSlot s[kMaxSsts];
+};
+
+// EncodeArgs of SST i of a set (workspace carved from the slot's base; host and device).
+__host__ __device__ inline EncodeArgs make_args(const SstSet &P, uint32_t i) {
+    const SstSlot &s = P.s[i];
+    EncodeArgs a{};
+    a.key_bytes = s.key_bytes;
+    a.key_off = s.key_off;
+    a.val_bytes = s.val_bytes;
+    a.val_off = s.val_off;
+    a.kind = s.kind;
+    a.seq = s.seq;
+    a.create_ts = s.create_ts;
+    a.expire_ts = s.expire_ts;
+    a.ts_mask = s.ts_mask;
+    a.n = s.n;
+    a.block_size = P.block_size;
+    a.restart_interval = P.restart_interval;
+    a.version = P.version;
+    a.wal = P.wal;
+    a.nchunks = s.nchunks;
+    a.seg_look = P.seg_look;
+    const EncodeWorkspace w = encode_workspace_offsets(s.n, s.has_filter_ws != 0);
+    uint8_t *b = s.ws;
+    a.lcp = (uint32_t *)(b + w.lcp);
+    a.szr = (uint32_t *)(b + w.szr);
+    a.sznr = (uint32_t *)(b + w.sznr);
+    a.hd = (uint64_t *)(b + w.hd);
+    a.nfacts = s.nfacts;
+    a.row_scratch = (uint32_t *)(b + w.row_scratch);
+    a.next = (uint32_t *)(b + w.next);
+    a.bbytes = (uint32_t *)(b + w.bbytes);
+    a.tab_exit = (uint32_t *)(b + w.tab_exit);
+    a.tab_cnt = (uint32_t *)(b + w.tab_cnt);
+    a.tab_bytes = (uint64_t *)(b + w.tab_bytes);
+    a.anchor_e = (uint32_t *)(b + w.anchor_e);
+    a.anchor_blk = (uint32_t *)(b + w.anchor_blk);
+    a.anchor_byte = (uint64_t *)(b + w.anchor_byte);
+    a.err = (unsigned long long *)(b + w.err);
+    a.wmax = (uint32_t *)(b + w.wmax);
+    a.slow_count = (uint32_t *)(b + w.slow_count);
+    a.slow_list = (uint32_t *)(b + w.slow_list);
+    a.desc = (BlockDesc *)(b + w.desc);
+    a.stat_part = (uint64_t *)(b + w.stat_part);
+    a.wmax_part = (uint32_t *)(b + w.wmax_part);
+    a.err_part = (unsigned long long *)(b + w.err_part);
+    a.gtab_exit = (uint32_t *)(b + w.gtab_exit);
+    a.gtab_cnt = (uint32_t *)(b + w.gtab_cnt);
+    a.gtab_bytes = (uint64_t *)(b + w.gtab_bytes);
+    a.mode = (uint32_t *)(b + w.mode);
+    a.group = s.group;
+    a.bloom_fused = s.bloom_fused;
+    a.bpl = s.bpl;
+    {  // bloom slots (BloomSlots, sdb_bloom.hip): counts then slots, 256-byte aligned
+        uint8_t *q = b + w.bloom_rep;
+        a.bq.count = (uint32_t *)q;
+        a.bq.slot = (uint32_t *)(q + (((uint64_t)s.bpl.tiles * s.bpl.nslices * 4 + 255) & ~255ull));
+        a.bq.cap = s.slot_cap;
+    }
+    a.bloom_out = s.bloom_out;
+    a.done = (uint32_t *)(b + w.done);
+    a.nprep_wg = s.nchunks;
+    a.seg_lds = kSegLds;
+    a.out_data = s.out_data;
+    a.out_block_off = s.out_block_off;
+    a.out_block_first = s.out_block_first;
+    a.out_index_key_len = s.out_index_key_len;
+    a.out_block_stats = s.out_block_stats;
+    a.data_cap = s.data_cap;
+    a.block_cap = s.block_cap;
+    a.summary = s.summary;
+    a.bloom_len = s.bloom_len;
+    a.num_probes = s.num_probes;
+    a.filter_built = s.filter_built;
+    return a;
+}
+
+// Enqueue the encode of every SST of the set on `st` (one launch sequence).
+hipError_t launch_encode_set(const SstSet &P, size_t bin_lds, size_t fill_lds, hipStream_t st);
+hipError_t launch_encode_empty(EncodeArgs a, hipStream_t st);
 
 // stage timing (diagnostics)
-enum Stage { kStBloom = 0, kStFacts, kStSeg, kStGroup, kStEnum, kStEmit, kStEmitSlow, kNumStages };
+enum Stage { kStBloom = 0, kStFacts, kStSeg, kStGroup, kStEnum, kStEmit, kStEmitSlow, kStBloomFill, kNumStages };
 void stage_mark(hipStream_t st, int stage, bool begin);
 bool stage_timing_on();
 

@@ -185,7 +185,9 @@ SDB_DEV EntryFacts entry_facts(const EncodeArgs &a, uint64_t i) {
 // first probe and step.  Lanes hold consecutive entries: the next entry's offsets and the previous
 // key's first 16 bytes come from the neighbour lane by DPP (lane 63 / lane 0 load their own).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kFactsThreads) void k_facts(EncodeArgs a) {
+__global__ __launch_bounds__(kFactsThreads) void k_facts(SstSet P) {
+    const EncodeArgs a = make_args(P, blockIdx.y);
+    if (blockIdx.x >= a.nfacts) return;
     __shared__ uint64_t s_part[kFactsThreads / 64][5];
     __shared__ unsigned long long s_err[kFactsThreads / 64];
     const uint32_t tid = threadIdx.x, lane = (uint32_t)lane_id();
@@ -304,7 +306,9 @@ SDB_DEV uint32_t walk_size_v2(const EncodeArgs &a, uint64_t j, bool rs) {
     return rs ? f.s_r : f.s_nr;
 }
 
-__global__ __launch_bounds__(kSegThreads, SDB_SEG_WAVES) void k_seg(EncodeArgs a) {
+__global__ __launch_bounds__(kSegThreads, SDB_SEG_WAVES) void k_seg(SstSet P) {
+    const EncodeArgs a = make_args(P, blockIdx.y);
+    if (blockIdx.x >= a.nchunks) return;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t *s_r = (uint32_t *)smem;          // kSegSpan: true restart-row sizes (V1: row sizes)
     uint32_t *s_P = s_r + kSegSpan;            // kSegSpan + 4: prefix of clamped non-restart sizes
@@ -527,12 +531,14 @@ __global__ __launch_bounds__(kSegThreads, SDB_SEG_WAVES) void k_seg(EncodeArgs a
 // the staged lookahead) or do not fit k_enum's LDS, workgroup 0 walks next() serially instead and
 // writes every chunk's anchors (mode 0).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kGroupThreads) void k_group(EncodeArgs a) {
+__global__ __launch_bounds__(kGroupThreads) void k_group(SstSet P) {
+    const EncodeArgs a = make_args(P, blockIdx.y);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint32_t s_W;
     __shared__ unsigned long long s_err;
     __shared__ uint64_t s_stat[5][kGroupThreads / 64];
     const uint32_t K = a.nchunks, g = blockIdx.x, G = a.group, ngroups = (K + G - 1) / G;
+    if (g >= ngroups) return;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
     if (tid == 0) {
         s_W = 0;
@@ -790,10 +796,12 @@ SDB_DEV bool emit_fast(const BlockDesc &d) {
 // K5a: enumerate the blocks of each chunk (binary lifting over next()) -> BlockMeta offsets and the
 //      per-block descriptors the emitter streams.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kEnumThreads) void k_enum(EncodeArgs a) {
+__global__ __launch_bounds__(kEnumThreads) void k_enum(SstSet P) {
+    const EncodeArgs a = make_args(P, blockIdx.y);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint64_t s_anc[4];  // entry point, first block, first byte, blocks of this chunk
     const uint32_t k = blockIdx.x, K = a.nchunks;
+    if (k >= K) return;
     if (*a.err != ~0ull) return;
     const uint64_t cs = (uint64_t)k * kChunk;
     const uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
@@ -1401,43 +1409,73 @@ SDB_DEV void finish_summary(const EncodeArgs &a) {
 // not fit the LDS image (k_enum's slow list) are done first, one workgroup each.  The last
 // workgroup to finish writes the summary.
 template <int V>
-__global__ __launch_bounds__(kEmitThreads, 1) void k_emit(EncodeArgs a) {
+__global__ __launch_bounds__(kEmitThreads, 1) void k_emit(SstSet P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 #ifdef SDB_PHASE_TIMING
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime(), mt0 = __builtin_amdgcn_s_memtime();
 #endif
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), wpb = blockDim.x >> 6;
-    const uint32_t gw = blockIdx.x * wpb + wave, G = gridDim.x * wpb;
+    const uint32_t gw = blockIdx.x * wpb + wave;
     (void)gw;
-    (void)G;
     const uint32_t l = (uint32_t)lane_id();
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    bool run = *a.err == ~0ull;  // any earlier error (incl. capacity): write nothing
-    if (run && lds_addr((const void *)smem) != 0) {  // crc_tab / crc_mul256_lds / crc_tree_mul assume LDS address 0
-        if (threadIdx.x == 0) report_error(a.err, 0, SDB_DEVICE_ERROR);
+    // the set's blocks, SST after SST: pre[i] = blocks of SSTs < i (an SST with an earlier error,
+    // incl. capacity, emits nothing)
+    uint32_t pre[kMaxSsts + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kMaxSsts; i++) {
+        uint32_t nb = 0;
+        if (i < P.count) {
+            const EncodeArgs ai = make_args(P, i);
+            if (*ai.err == ~0ull) nb = ai.anchor_blk[ai.nchunks];
+        }
+        pre[i + 1] = pre[i] + nb;
+    }
+    bool run = pre[kMaxSsts] > 0;
+    if (lds_addr((const void *)smem) != 0) {  // crc_tab / crc_mul256_lds / crc_tree_mul assume LDS address 0
+        if (threadIdx.x == 0)
+            for (uint32_t i = 0; i < P.count; i++) report_error(make_args(P, i).err, 0, SDB_DEVICE_ERROR);
         run = false;
     }
+    // global block g -> (SST, block of that SST); g is wave-uniform
+    auto locate = [&](uint32_t g, uint32_t &si, uint32_t &lb) {
+        uint32_t i = 0, base = 0;
+#pragma unroll
+        for (uint32_t j = 1; j < kMaxSsts; j++)
+            if (g >= pre[j] && pre[j] < pre[kMaxSsts]) {
+                i = j;
+                base = pre[j];
+            }
+        si = i;
+        lb = g - base;
+    };
+    auto desc_dw = [&](uint32_t si) { return (const uint32_t *)make_args(P, si).desc; };
     if (run) {
         lu32 *crc = (lu32 *)smem;
         (void)crc;
-        // schedule: workgroup b owns an equal share [r0, r1) of the blocks; its waves start on blocks
-        // r0 + wave and then take the rest in order from an LDS ticket, so a wave that runs fast takes
-        // more.  (One global ticket for all waves measured 3x slower: the atomics serialise.)
-        const uint32_t nb = a.anchor_blk[a.nchunks];
+        // schedule: workgroup b owns an equal share [r0, r1) of the set's blocks; its waves start on
+        // blocks r0 + wave and then take the rest in order from an LDS ticket, so a wave that runs fast
+        // takes more.  (One global ticket for all waves measured 3x slower: the atomics serialise.)
+        const uint32_t nb = pre[kMaxSsts];
         const uint32_t r0 = (uint32_t)((uint64_t)nb * blockIdx.x / gridDim.x);
         const uint32_t r1 = (uint32_t)((uint64_t)nb * (blockIdx.x + 1) / gridDim.x);
-        const uint32_t *dw = (const uint32_t *)a.desc;
-        uint32_t blk = r0 + wave;
+        uint32_t blk = r0 + wave, si = 0, lb = 0;
+        locate(blk, si, lb);
         // the first block's descriptor is in flight while the CRC tables are copied, its values and
         // metadata while the workgroup does the slow blocks and sets up the ticket
-        const uint32_t dv0 = (blk < r1 && l < 14) ? dw[14 * (uint64_t)blk + l] : 0;
+        const uint32_t dv0 = (blk < r1 && l < 14) ? desc_dw(si)[14 * (uint64_t)lb + l] : 0;
         crc_tables_to_lds(crc);
         BlockDesc dn = desc_from_lanes(dv0);
         EmitPre pn;
         bool fn = blk < r1 && emit_fast(dn);
-        if (fn) emit_prefetch(a, dn, pn);
+        if (fn) emit_prefetch(make_args(P, si), dn, pn);
         __syncthreads();
-        emit_slow_blocks<V>(a, (uint8_t *)smem + kCrcLds + 16, (const uint32_t(*)[256])smem);
+        for (uint32_t i = 0; i < P.count; i++) {
+            const EncodeArgs ai = make_args(P, i);
+            if (*ai.err == ~0ull && *ai.slow_count)
+                emit_slow_blocks<V>(ai, (uint8_t *)smem + kCrcLds + 16, (const uint32_t(*)[256])smem);
+        }
         __syncthreads();
         if (threadIdx.x == 0) *(lu32 *)(smem + kCrcLds) = blockDim.x >> 6;  // block ticket (first blocks: r0 + wave)
         __syncthreads();
@@ -1452,22 +1490,26 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(EncodeArgs a) {
             return r0 + (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
         };
         if (blk < r1) {
-            uint32_t nblk = take();
-            uint32_t dv = (nblk < r1 && l < 14) ? dw[14 * (uint64_t)nblk + l] : 0;
+            uint32_t nblk = take(), nsi = 0, nlb = 0;
+            locate(nblk, nsi, nlb);
+            uint32_t dv = (nblk < r1 && l < 14) ? desc_dw(nsi)[14 * (uint64_t)nlb + l] : 0;
             while (blk < r1) {
                 const BlockDesc d = dn;
                 const EmitPre p = pn;
                 const bool fast = fn;
-                const uint32_t cur = blk;
+                const uint32_t csi = si, clb = lb;
                 blk = nblk;
+                si = nsi;
+                lb = nlb;
                 if (blk < r1) {  // issue the next block (and the descriptor of the one after it)
                     dn = desc_from_lanes(dv);
                     fn = emit_fast(dn);
-                    if (fn) emit_prefetch(a, dn, pn);
+                    if (fn) emit_prefetch(make_args(P, si), dn, pn);
                     nblk = take();
-                    dv = (nblk < r1 && l < 14) ? dw[14 * (uint64_t)nblk + l] : 0;
+                    locate(nblk, nsi, nlb);
+                    dv = (nblk < r1 && l < 14) ? desc_dw(nsi)[14 * (uint64_t)nlb + l] : 0;
                 }
-                if (fast) emit_block<V>(a, cur, d, p, img, kst, rtab, crc, ph);  // slow blocks: done above
+                if (fast) emit_block<V>(make_args(P, csi), clb, d, p, img, kst, rtab, crc, ph);  // slow blocks: done above
             }
         }
     }
@@ -1485,9 +1527,9 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(EncodeArgs a) {
     __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence();
-        if (atomicAdd(&a.done[0], 1u) == gridDim.x - 1) {
+        if (atomicAdd(&make_args(P, 0).done[0], 1u) == gridDim.x - 1) {
             __threadfence();
-            finish_summary(a);
+            for (uint32_t i = 0; i < P.count; i++) finish_summary(make_args(P, i));
         }
     }
 }
@@ -1643,8 +1685,8 @@ SDB_DEV void emit_slow_blocks(const EncodeArgs &a, uint8_t *scratch, const uint3
     }
 }
 
-template __global__ void k_emit<1>(EncodeArgs);
-template __global__ void k_emit<2>(EncodeArgs);
+template __global__ void k_emit<1>(SstSet);
+template __global__ void k_emit<2>(SstSet);
 
 // ------------------------------------------------------------------------------------------------
 // Launcher
@@ -1708,32 +1750,36 @@ extern "C" int sdb_diag_phase_times(uint64_t *out, int nblocks) {
 }
 #endif
 
-static bool lds_attrs_set = false;
+__global__ void k_bloom_bin_hd(SstSet P);
+__global__ void k_bloom_fill_hd(SstSet P);
 static int g_cus = 0;
 static uint32_t g_emit_threads = kEmitThreads, g_emit_wg_per_cu = kEmitWgPerCu;
+static std::once_flag g_attrs_once;
 static uint32_t emit_grid() { return (uint32_t)(g_cus > 0 ? g_emit_wg_per_cu * g_cus : 512); }
 static uint32_t emit_lds() { return kCrcLds + 16 + (g_emit_threads / 64) * kEmitWaveLds; }
 static void set_lds_attrs() {
-    if (lds_attrs_set) return;
-    int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
-    // tuning knobs (diagnostics): emit workgroup size and workgroups per CU
-    if (const char *e = getenv("SDB_EMIT_THREADS")) {
-        uint32_t t = (uint32_t)atoi(e);
-        if (t >= 64 && t <= kEmitThreads && t % 64 == 0) g_emit_threads = t;
-    }
-    if (const char *e = getenv("SDB_EMIT_WG_PER_CU")) {
-        uint32_t t = (uint32_t)atoi(e);
-        if (t >= 1 && t <= 32) g_emit_wg_per_cu = t;
-    }
-    hipFuncSetAttribute((const void *)k_emit<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
-    hipFuncSetAttribute((const void *)k_emit<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
-    hipFuncSetAttribute((const void *)k_enum, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEnumLds);
-    hipFuncSetAttribute((const void *)k_group, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGroupLds);
-    hipFuncSetAttribute((const void *)k_seg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLdsMax);
-
-    lds_attrs_set = true;
+    std::call_once(g_attrs_once, [] {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
+        // tuning knobs (diagnostics): emit workgroup size and workgroups per CU
+        if (const char *e = getenv("SDB_EMIT_THREADS")) {
+            uint32_t t = (uint32_t)atoi(e);
+            if (t >= 64 && t <= kEmitThreads && t % 64 == 0) g_emit_threads = t;
+        }
+        if (const char *e = getenv("SDB_EMIT_WG_PER_CU")) {
+            uint32_t t = (uint32_t)atoi(e);
+            if (t >= 1 && t <= 32) g_emit_wg_per_cu = t;
+        }
+        (void)hipFuncSetAttribute((const void *)k_emit<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
+        (void)hipFuncSetAttribute((const void *)k_emit<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
+        (void)hipFuncSetAttribute((const void *)k_enum, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEnumLds);
+        (void)hipFuncSetAttribute((const void *)k_group, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGroupLds);
+        (void)hipFuncSetAttribute((const void *)k_seg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLdsMax);
+        (void)hipFuncSetAttribute((const void *)k_bloom_fill_hd, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        (void)hipFuncSetAttribute((const void *)k_bloom_bin_hd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLds);
+        (void)hipGetLastError();  // an unsupported attribute value must not poison the next launch status
+    });
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1743,7 +1789,9 @@ static void set_lds_attrs() {
 // the CUs the latency-bound k_seg / k_group / k_enum leave idle.
 // ------------------------------------------------------------------------------------------------
 static_assert(kChunk == kBinThreads * kHashPerT, "bloom tiles are k_facts hash tiles of kChunk keys");
-__global__ __launch_bounds__(kBinThreads) void k_bloom_bin_hd(EncodeArgs a) {
+__global__ __launch_bounds__(kBinThreads) void k_bloom_bin_hd(SstSet P) {
+    const EncodeArgs a = make_args(P, blockIdx.y);
+    if (!a.bloom_fused || blockIdx.x >= a.bpl.tiles) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t blds[];
     const uint32_t tile = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
     const uint64_t k0 = (uint64_t)tile * a.bpl.T;
@@ -1758,85 +1806,51 @@ __global__ __launch_bounds__(kBinThreads) void k_bloom_bin_hd(EncodeArgs a) {
     }
     bloom_bin_core<kHashPerT>(tile, hh, dd, nk, a.bpl, a.bq, blds);
 }
-__global__ __launch_bounds__(kFillThreads) void k_bloom_fill_hd(EncodeArgs a) {
+__global__ __launch_bounds__(kFillThreads) void k_bloom_fill_hd(SstSet P) {
+    const EncodeArgs a = make_args(P, blockIdx.y);
+    if (!a.bloom_fused || blockIdx.x >= a.bpl.nslices) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t blds[];
     bloom_fill_slice(blockIdx.x, a.key_bytes, a.key_off, a.n, a.bpl, a.bq, a.bloom_out, a.bloom_len, blds);
 }
 
-namespace {
-struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-std::mutex g_side_mu;
-SideStream g_side[64];
-SideStream *side_for_current_device() {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    SideStream &ss = g_side[dev];
-    if (!ss.s) {
-        if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-        if (hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess)
-            return nullptr;
-    }
-    return &ss;
-}
-}  // namespace
-
-hipError_t launch_encode(EncodeArgs a, hipStream_t st) {
+hipError_t launch_encode_set(const SstSet &P, size_t bin_lds, size_t fill_lds, hipStream_t st) {
     set_lds_attrs();
-    if (a.n == 0) {
-        hipLaunchKernelGGL(k_init_summary, dim3(1), dim3(64), 0, st, a);
-        hipLaunchKernelGGL(k_finish_summary, dim3(1), dim3(64), 0, st, a, a.bloom_len, a.num_probes, a.filter_built);
-        return hipGetLastError();
-    }
-    a.nprep_wg = a.nchunks;
-    a.nfacts = (uint32_t)((a.n + kFactsThreads - 1) / kFactsThreads);
-    a.seg_lds = kSegLds;
+    if (!P.count) return hipSuccess;
+    // every kernel on the caller's stream, in dependency order: the set is large enough to fill the
+    // chip at each step, and one stream keeps the sequence capturable into a HIP graph
     stage_mark(st, kStFacts, true);
-    hipLaunchKernelGGL(k_facts, dim3(a.nfacts), dim3(kFactsThreads), 0, st, a);
+    hipLaunchKernelGGL(k_facts, dim3(P.max_facts, P.count), dim3(kFactsThreads), 0, st, P);
     stage_mark(st, kStFacts, false);
-    // the bloom: fork a side stream after k_facts (it needs only the hashes), join it at the end
-    std::unique_lock<std::mutex> lk(g_side_mu, std::defer_lock);
-    SideStream *side = nullptr;
-    if (a.bloom_fused) {
-        lk.lock();
-        static bool fill_attr = false;
-        if (!fill_attr) {
-            (void)hipFuncSetAttribute((const void *)k_bloom_fill_hd, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-            (void)hipFuncSetAttribute((const void *)k_bloom_bin_hd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLds);
-            (void)hipGetLastError();
-            fill_attr = true;
-        }
-        side = side_for_current_device();
-        hipStream_t bs = st;
-        if (side) {
-            (void)hipEventRecord(side->fork, st);
-            (void)hipStreamWaitEvent(side->s, side->fork, 0);
-            bs = side->s;
-        }
-        stage_mark(bs, kStBloom, true);
-        hipLaunchKernelGGL(k_bloom_bin_hd, dim3(a.bpl.tiles), dim3(kBinThreads), bloom_bin_lds(a.bpl), bs, a);
-        hipLaunchKernelGGL(k_bloom_fill_hd, dim3(a.bpl.nslices), dim3(kFillThreads), bloom_fill_lds(a.bpl), bs, a);
-        stage_mark(bs, kStBloom, false);
-        if (side) (void)hipEventRecord(side->join, side->s);
+    if (P.max_tiles) {
+        stage_mark(st, kStBloom, true);
+        hipLaunchKernelGGL(k_bloom_bin_hd, dim3(P.max_tiles, P.count), dim3(kBinThreads), bin_lds, st, P);
+        stage_mark(st, kStBloom, false);
     }
     stage_mark(st, kStSeg, true);
-    hipLaunchKernelGGL(k_seg, dim3(a.nchunks), dim3(kSegThreads), a.seg_lds, st, a);
+    hipLaunchKernelGGL(k_seg, dim3(P.max_chunks, P.count), dim3(kSegThreads), kSegLds, st, P);
     stage_mark(st, kStSeg, false);
     stage_mark(st, kStGroup, true);
-    const uint32_t ngroups = (a.nchunks + a.group - 1) / a.group;
-    hipLaunchKernelGGL(k_group, dim3(ngroups), dim3(kGroupThreads), kGroupLds, st, a);
+    hipLaunchKernelGGL(k_group, dim3(P.max_groups, P.count), dim3(kGroupThreads), kGroupLds, st, P);
     stage_mark(st, kStGroup, false);
     stage_mark(st, kStEnum, true);
-    hipLaunchKernelGGL(k_enum, dim3(a.nchunks), dim3(kEnumThreads), kEnumLds, st, a);
+    hipLaunchKernelGGL(k_enum, dim3(P.max_chunks, P.count), dim3(kEnumThreads), kEnumLds, st, P);
     stage_mark(st, kStEnum, false);
+    if (P.max_slices) {
+        stage_mark(st, kStBloomFill, true);
+        hipLaunchKernelGGL(k_bloom_fill_hd, dim3(P.max_slices, P.count), dim3(kFillThreads), fill_lds, st, P);
+        stage_mark(st, kStBloomFill, false);
+    }
     stage_mark(st, kStEmit, true);
-    if (a.version == 2) hipLaunchKernelGGL(k_emit<2>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, a);
-    else hipLaunchKernelGGL(k_emit<1>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, a);
+    if (P.version == 2) hipLaunchKernelGGL(k_emit<2>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, P);
+    else hipLaunchKernelGGL(k_emit<1>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, P);
     stage_mark(st, kStEmit, false);
-    if (side) (void)hipStreamWaitEvent(st, side->join, 0);  // join: the caller's stream ends after the bloom
+    return hipGetLastError();
+}
+
+// An empty SST (no entries): summary only, BlockMeta offsets = [0].
+hipError_t launch_encode_empty(EncodeArgs a, hipStream_t st) {
+    hipLaunchKernelGGL(k_init_summary, dim3(1), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(k_finish_summary, dim3(1), dim3(64), 0, st, a, a.bloom_len, a.num_probes, a.filter_built);
     return hipGetLastError();
 }
 

@@ -374,7 +374,7 @@ class Decoder:
 class DeviceSstOutput:
     """Caller-owned device outputs + workspace for sdb_encode_sst (allocated once, reused)."""
 
-    def __init__(self, n, total_key_bytes, total_val_bytes, prm, device="cuda"):
+    def __init__(self, n, total_key_bytes, total_val_bytes, prm, device="cuda", workspace=True):
         import torch
         dc, bc, fc = C.c_uint64(), C.c_uint64(), C.c_uint64()
         st = lib().sdb_encode_bounds(n, total_key_bytes, total_val_bytes, C.byref(prm), C.byref(dc),
@@ -389,8 +389,10 @@ class DeviceSstOutput:
         self.block_stats = torch.empty(3 * (bc.value + 1), dtype=torch.int16, device=device)
         self.bloom = torch.empty(fc.value, dtype=torch.uint8, device=device)
         self.summary = torch.zeros(C.sizeof(_abi.SstSummary), dtype=torch.uint8, device=device)
-        ws = lib().sdb_encode_workspace_bytes(n, C.byref(prm))
-        self.workspace = torch.empty(max(ws, 256), dtype=torch.uint8, device=device)
+        self.workspace = None
+        if workspace:  # own scratch for sdb_encode_sst (a set shares one, see encode_ssts_device)
+            ws = lib().sdb_encode_workspace_bytes(n, C.byref(prm))
+            self.workspace = torch.empty(max(ws, 256), dtype=torch.uint8, device=device)
         self.out = _abi.SstOut(self.data.data_ptr(), dc.value, self.block_off.data_ptr(),
                                self.block_first.data_ptr(), self.index_key_len.data_ptr(),
                                self.block_stats.data_ptr(), bc.value, self.bloom.data_ptr(), fc.value,
@@ -425,3 +427,25 @@ def encode_sst_device(dbatch, out, stream=None):
                               out.workspace.numel(), sp)
     if st:
         raise SdbError(st, "sdb_encode_sst")
+
+
+def ssts_workspace(dbatches, prm, device="cuda"):
+    """Scratch for sdb_encode_ssts over these device batches (sdb_encode_ssts_workspace_bytes)."""
+    import torch
+    kbs = (_abi.KvBatch * max(len(dbatches), 1))(*[b.to_ctypes() for b in dbatches])
+    n = lib().sdb_encode_ssts_workspace_bytes(len(dbatches), kbs, C.byref(prm))
+    return torch.empty(max(n, 256), dtype=torch.uint8, device=device)
+
+
+def encode_ssts_device(dbatches, outs, prm, workspace, stream=None):
+    """Enqueue the encode of several independent SSTs (same params) as ONE launch sequence
+    (sdb_encode_ssts): outs[i] receives batches[i]."""
+    assert len(dbatches) == len(outs)
+    sp = None
+    if stream is not None:
+        sp = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    kbs = (_abi.KvBatch * max(len(dbatches), 1))(*[b.to_ctypes() for b in dbatches])
+    os_ = (_abi.SstOut * max(len(outs), 1))(*[o.out for o in outs])
+    st = lib().sdb_encode_ssts(len(dbatches), kbs, C.byref(prm), os_, workspace.data_ptr(), workspace.numel(), sp)
+    if st:
+        raise SdbError(st, "sdb_encode_ssts")

@@ -76,7 +76,7 @@ def test_host_sizing_matches_oracle(lib):
             assert lib.sdb_bloom_filter_bytes(n, bpk) == O.filter_size_bytes(n, bpk), (n, bpk)
     for bpk in range(0, 40):
         assert lib.sdb_bloom_num_probes(bpk) == O.optimal_num_probes(bpk)
-    assert lib.sdb_abi_version() == 1
+    assert lib.sdb_abi_version() == 2
     assert lib.sdb_status_name(3) == b"CHECKSUM_MISMATCH"
 
 
