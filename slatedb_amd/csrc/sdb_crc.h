@@ -122,4 +122,77 @@ SDB_DEV uint32_t wave_crc_image(const lu8 *img, uint32_t Lc, bool fold_init) {
     return gf_mul(c_seg.unpad[pad], u) ^ 0xFFFFFFFFu;
 }
 
+// Raw CRC of one 64-byte segment held in 16 little-endian dwords: two 32-byte slicing-by-8 chains
+// combined by x^256 (the LDS tables of the k_emit layout).
+SDB_DEV uint32_t crc_seg64_lds(const uint32_t (&m)[16]) {
+    const lu32 *crc = (const lu32 *)(uintptr_t)0;
+    uint32_t ca = crc_slice8_lds(0, m[0], m[1], crc), cb = crc_slice8_lds(0, m[8], m[9], crc);
+    ca = crc_slice8_lds(ca, m[2], m[3], crc);
+    cb = crc_slice8_lds(cb, m[10], m[11], crc);
+    ca = crc_slice8_lds(ca, m[4], m[5], crc);
+    cb = crc_slice8_lds(cb, m[12], m[13], crc);
+    ca = crc_slice8_lds(ca, m[6], m[7], crc);
+    cb = crc_slice8_lds(cb, m[14], m[15], crc);
+    return crc_mul256_lds(ca) ^ cb;
+}
+
+// Combine the 64 lanes' segment CRCs (lane l's segment followed by those of lanes l+1 .. 63) into
+// lane 0 by six pairwise tree steps; returns the wave-uniform result.
+SDB_DEV uint32_t crc_tree_combine(uint32_t c) {
+    const uint32_t l = (uint32_t)lane_id();
+    // partner = lane + 2^s: DPP row_shl inside a row, then permlane16 / permlane32 swaps.  Lanes l with
+    // l % 2^(s+1) != 0 hold nothing the tree still needs: their table lookups are masked off.
+    uint32_t p = dpp32<0x101>(c);
+    if ((l & 1) == 0) c = crc_tree_mul<0>(c) ^ p;
+    p = dpp32<0x102>(c);
+    if ((l & 3) == 0) c = crc_tree_mul<1>(c) ^ p;
+    p = dpp32<0x104>(c);
+    if ((l & 7) == 0) c = crc_tree_mul<2>(c) ^ p;
+    p = dpp32<0x108>(c);
+    if ((l & 15) == 0) c = crc_tree_mul<3>(c) ^ p;
+    p = (uint32_t)__builtin_amdgcn_permlane16_swap(c, c, false, false)[1];
+    if ((l & 31) == 0) c = crc_tree_mul<4>(c) ^ p;
+    p = (uint32_t)__builtin_amdgcn_permlane32_swap(c, c, false, false)[1];
+    if (l == 0) c = crc_tree_mul<5>(c) ^ p;
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+}
+
+// crc32fast::hash of the message img[0, Lc), 4 <= Lc <= 4096, in every lane, with the 64-byte
+// segments RIGHT-aligned to the message end: lane l holds [Lc - 64 (64 - l), +64).  The segment that
+// straddles byte 0 reads the 64 bytes before img, which the caller keeps zero (leading zeros leave a
+// raw CRC unchanged), so no trailing padding has to be divided out afterwards.  The caller has
+// inverted message bytes [0, 4) in LDS (crc32fast's 0xFFFFFFFF init).  img: 4-byte aligned LDS.
+// Reads are five 16-byte-aligned ds_read_b128 per lane (the same bank pattern as aligned segments),
+// realigned by the wave-uniform byte shift Lc mod 16: a uniform branch on its dword part, one
+// v_alignbyte per dword for the rest.  Lc must be wave-uniform.
+template <int Q>
+SDB_DEV void realign16(const uint32_t (&x)[20], uint32_t r, uint32_t (&m)[16]) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_alignbyte(x[i + Q + 1], x[i + Q], r);
+}
+SDB_DEV uint32_t wave_crc_image_ra(const lu8 *img, uint32_t Lc) {
+    const uint32_t l = (uint32_t)lane_id();
+    const int s = (int)Lc - 64 * (64 - (int)l);  // segment start (message coordinates)
+    uint32_t c = 0;
+    if (s > -64) {
+        const lu128 *w = (const lu128 *)(uintptr_t)(lds_addr((const void *)img) + (uint32_t)(s - (int)(Lc & 15)));
+        uint32_t x[20], m[16];
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            const u32x4 v = w[i];
+            x[4 * i] = v.x;
+            x[4 * i + 1] = v.y;
+            x[4 * i + 2] = v.z;
+            x[4 * i + 3] = v.w;
+        }
+        const uint32_t q = (Lc >> 2) & 3, r = Lc & 3;
+        if (q == 0) realign16<0>(x, r, m);
+        else if (q == 1) realign16<1>(x, r, m);
+        else if (q == 2) realign16<2>(x, r, m);
+        else realign16<3>(x, r, m);
+        c = crc_seg64_lds(m);
+    }
+    return crc_tree_combine(c) ^ 0xFFFFFFFFu;
+}
+
 }  // namespace sdb

@@ -31,9 +31,10 @@ __device__ uint64_t g_dec_phase[2][8192][4];  // [count / emit][wave][phase] s_m
 constexpr uint32_t kDecThreads = 1024;                   // 16 waves: one workgroup (and CRC table copy) per CU
 constexpr uint32_t kDecImg = 4096 + 32;                  // fast path: staged block image per wave
 constexpr uint32_t kDecKeys = 2048;                      // fast path: restored keys of one block
-constexpr uint32_t kDecWaveLds = kDecImg + kDecKeys;
+constexpr uint32_t kDecGuard = 64;                       // zero lead-in of the right-aligned CRC segments
+constexpr uint32_t kDecWaveLds = kDecGuard + kDecImg + kDecKeys;
 constexpr uint32_t kDecLds = kCrcTablesLds + (kDecThreads / 64) * kDecWaveLds;
-constexpr uint32_t kDecCap = kDecWaveLds;
+constexpr uint32_t kDecCap = kDecWaveLds - kDecGuard;
 constexpr uint32_t kRowTmp = kDecKeys - 256;  // emit: row positions of the lane-per-row path (4 x 32 u16) in kbuf
 typedef __attribute__((address_space(3))) uint16_t lu16;  // other blocks: generic staging per wave; larger ones parse from HBM
 
@@ -328,10 +329,9 @@ SDB_DEV LdsBlockView stage_lds(const DecodeArgs &a, uint64_t s, uint64_t e, lu8 
                                 (uint32_t)d[blen + 3];
         wave_sync_d();
         if (l < p0) img[l] = 0;
-        for (uint32_t x = Lc + l; x < ((Lc + 63) & ~63u); x += 64) img[x] = 0;
         if (l < 4) img[p0 + l] ^= 0xFF;
         wave_sync_d();
-        const uint32_t c = wave_crc_image(img, Lc, false);
+        const uint32_t c = wave_crc_image_ra(img, Lc);  // zeros before img (the guard) and before p0
         wave_sync_d();
         if (l < 4) img[p0 + l] ^= 0xFF;
         wave_sync_d();
@@ -610,7 +610,8 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
     __syncthreads();
     const uint32_t(*crc)[256] = (const uint32_t(*)[256])smem;
     const uint32_t wave = threadIdx.x >> 6;
-    lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kDecWaveLds;
+    lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kDecWaveLds + kDecGuard;
+    if (lane_id() < kDecGuard / 4) ((lu32 *)(img - kDecGuard))[lane_id()] = 0;  // never written again
     uint8_t *stage = (uint8_t *)img;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
@@ -1031,7 +1032,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
     const uint32_t(*crc)[256] = (const uint32_t(*)[256])smem;
     const uint32_t wave = threadIdx.x >> 6;
     const int l = lane_id();
-    lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kDecWaveLds;
+    lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kDecWaveLds + kDecGuard;
     lu8 *kbuf = img + kDecImg;
     uint8_t *stage = (uint8_t *)img;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);

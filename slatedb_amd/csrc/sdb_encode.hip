@@ -1107,15 +1107,22 @@ template <int V>
 SDB_DEV uint32_t write_row_hdr_trailer(lu8 *dst, const RowInfo &r, uint64_t seq, int64_t ets, int64_t cts) {
     uint32_t p = 0;
     if (V == 2) {  // SstRowCodecV2::encode (row_codec_v2.rs:127-169)
-        uint32_t vals[3] = {r.shared, r.suf, r.vlen};
+        if ((r.shared | r.suf | r.vlen) < 0x80) {  // three one-byte varints (the common row)
+            dst[0] = (uint8_t)r.shared;
+            dst[1] = (uint8_t)r.suf;
+            dst[2] = (uint8_t)r.vlen;
+            p = 3;
+        } else {
+            uint32_t vals[3] = {r.shared, r.suf, r.vlen};
 #pragma unroll
-        for (int f = 0; f < 3; f++) {
-            uint32_t x = vals[f];
-            while (x >= 0x80) {
-                dst[p++] = (uint8_t)(x | 0x80);
-                x >>= 7;
+            for (int f = 0; f < 3; f++) {
+                uint32_t x = vals[f];
+                while (x >= 0x80) {
+                    dst[p++] = (uint8_t)(x | 0x80);
+                    x >>= 7;
+                }
+                dst[p++] = (uint8_t)x;
             }
-            dst[p++] = (uint8_t)x;
         }
     } else {  // SstRowCodecV0::encode (row.rs:159-198)
         dst[0] = (uint8_t)(r.shared >> 8);
@@ -1281,7 +1288,6 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     const uint32_t D = wave_readlane(inc, 63);
     const uint32_t noffs = (V == 2) ? (ne + ri - 1) / ri : ne;
     const uint32_t Lc = D + 2 * noffs + 2;  // CRC input length
-    const uint32_t nseg = (Lc + 63) >> 6;
     // copy span of the row: key suffix .. value end
     const uint32_t kstart = row_off + h, kend = kstart + r.suf;
     const uint32_t vstart = (V == 2) ? kend : row_off + size - vlen;
@@ -1308,9 +1314,12 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     //    restart table, count and the zero padding of the last CRC segment
     if (row) {
         write_row_hdr_trailer<V>(img + row_off, r, seq, ets, cts);
-        const uint32_t kj = (kend & ~3u) > kstart ? (kend & ~3u) : kstart;  // first key byte not
-        for (uint32_t x = kj; x < kend; x++)                                 // in a key dword
-            img[x] = kst[(uint32_t)(ko + shared - ka) + (x - kstart)];
+        // the <= 3 key bytes that share a dword with value / trailer bytes (predicated, no loop)
+        const uint32_t kj = (kend & ~3u) > kstart ? (kend & ~3u) : kstart;
+        const lu8 *ksrc = kst + (uint32_t)(ko + shared - ka) - kstart;
+#pragma unroll
+        for (uint32_t q = 0; q < 3; q++)
+            if (kj + q < kend) img[kj + q] = ksrc[kj + q];
     }
     if (V == 2) {
         if (row && l % ri == 0) {
@@ -1323,19 +1332,20 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
         img[D + 2 * l] = (uint8_t)(row_off >> 8);  // `as u16` (block.rs:163)
         img[D + 2 * l + 1] = (uint8_t)row_off;
     }
-    {
-        const uint32_t z0 = (Lc + 3) & ~3u, nz = ((nseg << 6) - z0) >> 2;
-        if (l < nz) ((lu32 *)(img + z0))[l] = 0;
-        if (l == 0) {
-            img[D + 2 * noffs] = (uint8_t)(noffs >> 8);
-            img[D + 2 * noffs + 1] = (uint8_t)noffs;
-            for (uint32_t x = Lc; x < z0; x++) img[x] = 0;
-        }
+    if (l == 0) {
+        img[D + 2 * noffs] = (uint8_t)(noffs >> 8);
+        img[D + 2 * noffs + 1] = (uint8_t)noffs;
     }
     wave_sync();
+    // the value stage below the image is consumed: its 64 bytes become the zero lead-in of the
+    // right-aligned CRC segments; crc32fast's init is folded in by inverting image bytes [0, 4)
+    // (undone by the store)
+    if (l < 16) ((lu32 *)(img - kStageGuard))[l] = 0;
+    if (l == 0) ((lu32 *)img)[0] = ~((const lu32 *)img)[0];
+    wave_sync();
     WAVE_T(t4);
-    // 4. CRC32 (format/sst.rs:541-552) of the image [0, Lc), zero padded to whole 64-byte segments
-    const uint32_t crc32 = wave_crc_image(img, Lc, true);
+    // 4. CRC32 (format/sst.rs:541-552) of the image [0, Lc)
+    const uint32_t crc32 = wave_crc_image_ra(img, Lc);
     if (l == 0) {
         img[Lc] = (uint8_t)(crc32 >> 24);
         img[Lc + 1] = (uint8_t)(crc32 >> 16);
@@ -1354,9 +1364,10 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
 #if !defined(SDB_EXP_NO_STORE)
     for (uint32_t cc = l; cc < nfull; cc += 64) {
         u32x4 v = ((const lu128 *)img)[cc];
+        if (cc == 0) v.x = ~v.x;  // the CRC's init fold
         __builtin_memcpy(gdst + 16 * cc, &v, 16);
     }
-    if (l < (L & 15)) gdst[(nfull << 4) + l] = img[(nfull << 4) + l];
+    if (l < (L & 15)) gdst[(nfull << 4) + l] = img[(nfull << 4) + l];  // L >= 16: never image bytes [0, 4)
 #endif
     WAVE_T(t6);
 #ifdef SDB_PHASE_TIMING
