@@ -183,11 +183,21 @@ SDB_DEV void bloom_bin_core(uint32_t tile, const uint32_t (&hh)[KPT], const uint
     __syncthreads();
     // write the runs: sorted[x] belongs to slice sl = p >> sb at run position x - hist[sl]
     const uint64_t stride = (uint64_t)pl.tiles * q.cap;
-    uint32_t *slots = q.slot + (uint64_t)tile * q.cap;
-    for (uint32_t x = tid; x < np; x += nt) {
-        const uint32_t p = sorted[x], sl = p >> pl.sb;
-        const uint32_t pos = x - hist[sl];
-        if (pos < q.cap) slots[sl * stride + pos] = p;
+    if (pl.sb <= 16) {  // u16 offsets inside the slice
+        uint16_t *slots = (uint16_t *)q.slot + (uint64_t)tile * q.cap;
+        const uint32_t mask = (1u << pl.sb) - 1;
+        for (uint32_t x = tid; x < np; x += nt) {
+            const uint32_t p = sorted[x], sl = p >> pl.sb;
+            const uint32_t pos = x - hist[sl];
+            if (pos < q.cap) slots[sl * stride + pos] = (uint16_t)(p & mask);
+        }
+    } else {
+        uint32_t *slots = q.slot + (uint64_t)tile * q.cap;
+        for (uint32_t x = tid; x < np; x += nt) {
+            const uint32_t p = sorted[x], sl = p >> pl.sb;
+            const uint32_t pos = x - hist[sl];
+            if (pos < q.cap) slots[sl * stride + pos] = p;
+        }
     }
 }
 
@@ -228,7 +238,35 @@ SDB_DEV void bloom_fill_slice(uint32_t s, const uint8_t *__restrict__ key_bytes,
     __syncthreads();
     const uint32_t lo = s << pl.sb;
     auto set = [&](uint32_t p) { atomicOr(&bits[(p - lo) >> 5], 1u << (p & 31)); };
-    if (!s_over) {
+    if (!s_over && pl.sb <= 16) {
+        // u16 offsets: wave w takes tiles w, w + nw, ...; lane l reads offsets l, l + 64, ...; four
+        // slots in flight per wave
+        const uint32_t w = tid >> 6, nw = nt >> 6, l = tid & 63;
+        const uint16_t *base = (const uint16_t *)q.slot + (uint64_t)s * T * q.cap;
+        auto set16 = [&](uint32_t o) { atomicOr(&bits[o >> 5], 1u << (o & 31)); };
+        for (uint32_t t0 = w; t0 < T; t0 += 4 * nw) {
+            uint32_t v[4][4];
+#pragma unroll
+            for (uint32_t u = 0; u < 4; u++) {
+                const uint32_t t = t0 + u * nw;
+                const uint32_t c = t < T ? cnt[t] : 0;
+#pragma unroll
+                for (uint32_t r = 0; r < 4; r++) {
+                    const uint32_t i = l + 64 * r;
+                    v[u][r] = i < c ? base[(uint64_t)t * q.cap + i] : kNoProbe;
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 4; u++) {
+#pragma unroll
+                for (uint32_t r = 0; r < 4; r++)
+                    if (v[u][r] != kNoProbe) set16(v[u][r]);
+                const uint32_t t = t0 + u * nw;  // runs longer than 256 probes (q.cap > 256)
+                const uint32_t c = t < T ? cnt[t] : 0;
+                for (uint32_t i = 256 + l; i < c; i += 64) set16(base[(uint64_t)t * q.cap + i]);
+            }
+        }
+    } else if (!s_over) {
         // wave w takes tiles w, w + nw, ...; lane l reads probes l, l + 64, ... of a slot; four slots
         // in flight per wave
         const uint32_t w = tid >> 6, nw = nt >> 6, l = tid & 63;

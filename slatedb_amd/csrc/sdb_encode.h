@@ -17,7 +17,9 @@ constexpr uint32_t kKeyStageCap = 1024;      // key staging per wave
 constexpr uint32_t kSegLook = 1024;           // k_seg: max lookahead entries staged past the chunk
 constexpr uint32_t kSegSpan = kChunk + kSegLook;
 constexpr uint32_t kSegThreads = 1024;
-constexpr uint32_t kFactsThreads = 256;       // k_facts: one entry per thread
+constexpr uint32_t kFactsThreads = 1024;      // k_facts: a chunk (= a fused bloom tile) per workgroup
+constexpr uint32_t kFactsPerT = 2;            //   entries per thread
+constexpr uint32_t kFactsEntries = kFactsThreads * kFactsPerT;
 constexpr uint32_t kSegLds = (3 * kSegSpan + 4) * 4 + kChunk * 6;
 constexpr uint32_t kSegLdsMax = 64 * 1024;          // k_seg's LDS with the fused bloom binning
 constexpr uint32_t kHashPerT = kChunk / kSegThreads;  // chunk entries (hashes) per k_seg thread
@@ -40,7 +42,8 @@ struct BloomPlan {
 };
 struct BloomSlots {
     uint32_t *count;  // tiles x nslices: run length of each (tile, slice) slot (kSlotOverflow: too long)
-    uint32_t *slot;   // (nslices x tiles) x cap probes, slice-major
+    uint32_t *slot;   // (nslices x tiles) x cap probes, slice-major: u16 offsets in the slice when
+                      // sb <= 16 (half the traffic), else u32 bit positions
     uint32_t cap;
 };
 
@@ -140,7 +143,8 @@ __host__ __device__ inline EncodeWorkspace encode_workspace_offsets(uint64_t n, 
     w.lcp = take(4 * (n + 1));
     w.szr = take(4 * (n + 1));
     w.sznr = take(4 * (n + 1));
-    w.hd = take(has_filter ? 8 * (n + 1) : 0);
+    w.hd = take(0);  // (the fused bloom bins inside k_facts: no per-entry hash array)
+    (void)has_filter;
     w.row_scratch = take(4 * (n + 1));
     w.next = take(4 * (n + 1));
     w.bbytes = take(4 * (n + 1));
@@ -155,7 +159,7 @@ __host__ __device__ inline EncodeWorkspace encode_workspace_offsets(uint64_t n, 
     w.slow_count = take(4);
     w.slow_list = take(4 * (n + 1));
     w.desc = take(sizeof(BlockDesc) * (n + 1));
-    const uint64_t nf = (n + kFactsThreads - 1) / kFactsThreads;
+    const uint64_t nf = (n + kFactsEntries - 1) / kFactsEntries;
     w.stat_part = take(8 * 5 * (nf + 1));
     w.wmax_part = take(4 * (nc + 1));
     w.err_part = take(8 * (nf + 1));

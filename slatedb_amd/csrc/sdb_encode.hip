@@ -188,75 +188,95 @@ SDB_DEV EntryFacts entry_facts(const EncodeArgs &a, uint64_t i) {
 __global__ __launch_bounds__(kFactsThreads) void k_facts(SstSet P) {
     const EncodeArgs a = make_args(P, blockIdx.y);
     if (blockIdx.x >= a.nfacts) return;
+    extern __shared__ __attribute__((aligned(16))) uint32_t blds[];  // fused bloom binning
     __shared__ uint64_t s_part[kFactsThreads / 64][5];
     __shared__ unsigned long long s_err[kFactsThreads / 64];
     const uint32_t tid = threadIdx.x, lane = (uint32_t)lane_id();
-    const uint64_t e = (uint64_t)blockIdx.x * kFactsThreads + tid;
+    const uint64_t e0 = (uint64_t)blockIdx.x * kFactsEntries + tid;  // entries e0 + r * kFactsThreads
     const uint64_t n = a.n;
-    FactsIn in;
-    in.ko0 = in.ko1 = in.vo0 = in.vo1 = in.pko = 0;
-    in.kd = in.m = 0;
-    if (e <= n) {
-        in.ko0 = a.key_off[e];
-        in.vo0 = a.val_off[e];
-        if (e < n) {
-            in.kd = a.kind ? a.kind[e] : 0;
-            in.m = a.ts_mask ? a.ts_mask[e] : 0;
-            if (lane == 63) {
-                in.ko1 = a.key_off[e + 1];
-                in.vo1 = a.val_off[e + 1];
+    // all loads of both rounds first (offsets, then the first 16 key bytes), so they overlap
+    FactsIn in[kFactsPerT];
+#pragma unroll
+    for (uint32_t r = 0; r < kFactsPerT; r++) {
+        const uint64_t e = e0 + r * kFactsThreads;
+        FactsIn &f = in[r];
+        f.ko0 = f.ko1 = f.vo0 = f.vo1 = f.pko = 0;
+        f.kd = f.m = 0;
+        if (e <= n) {
+            f.ko0 = a.key_off[e];
+            f.vo0 = a.val_off[e];
+            if (e < n) {
+                f.kd = a.kind ? a.kind[e] : 0;
+                f.m = a.ts_mask ? a.ts_mask[e] : 0;
+                if (lane == 63) {
+                    f.ko1 = a.key_off[e + 1];
+                    f.vo1 = a.val_off[e + 1];
+                }
+                if (lane == 0 && e > 0) f.pko = a.key_off[e - 1];
             }
-            if (lane == 0 && e > 0) in.pko = a.key_off[e - 1];
         }
     }
-    {
-        const uint64_t nk = wave_next_lane(in.ko0), nv = wave_next_lane(in.vo0);
+#pragma unroll
+    for (uint32_t r = 0; r < kFactsPerT; r++) {
+        FactsIn &f = in[r];
+        const uint64_t nk = wave_next_lane(f.ko0), nv = wave_next_lane(f.vo0);
         if (lane != 63) {
-            in.ko1 = nk;
-            in.vo1 = nv;
+            f.ko1 = nk;
+            f.vo1 = nv;
         }
-    }
-    in.ck0 = in.ck1 = in.pk0 = in.pk1 = 0;
-    if (e < n) {
-        const uint64_t kl = in.ko1 - in.ko0;
-        const uint32_t kn = (uint32_t)(kl < 16 ? kl : 16);
-        if (kn) in.ck0 = load8(a.key_bytes + in.ko0, kn < 8 ? kn : 8);
-        if (kn > 8) in.ck1 = load8(a.key_bytes + in.ko0 + 8, kn - 8);
-        if (lane == 0 && e > 0) {
-            const uint64_t pl = in.ko0 - in.pko;
-            const uint32_t pn = (uint32_t)(pl < 16 ? pl : 16);
-            if (pn) in.pk0 = load8(a.key_bytes + in.pko, pn < 8 ? pn : 8);
-            if (pn > 8) in.pk1 = load8(a.key_bytes + in.pko + 8, pn - 8);
-        }
-    }
-    {
-        const uint64_t pko = wave_prev_lane(in.ko0), pk0 = wave_prev_lane(in.ck0), pk1 = wave_prev_lane(in.ck1);
-        if (lane != 0) {
-            in.pko = pko;
-            in.pk0 = pk0;
-            in.pk1 = pk1;
-        } else if (e == 0) {
-            in.pko = in.ko0;
+        const uint64_t e = e0 + r * kFactsThreads;
+        f.ck0 = f.ck1 = f.pk0 = f.pk1 = 0;
+        if (e < n) {
+            const uint64_t kl = f.ko1 - f.ko0;
+            const uint32_t kn = (uint32_t)(kl < 16 ? kl : 16);
+            if (kn) f.ck0 = load8(a.key_bytes + f.ko0, kn < 8 ? kn : 8);
+            if (kn > 8) f.ck1 = load8(a.key_bytes + f.ko0 + 8, kn - 8);
+            if (lane == 0 && e > 0) {
+                const uint64_t pl = f.ko0 - f.pko;
+                const uint32_t pn = (uint32_t)(pl < 16 ? pl : 16);
+                if (pn) f.pk0 = load8(a.key_bytes + f.pko, pn < 8 ? pn : 8);
+                if (pn > 8) f.pk1 = load8(a.key_bytes + f.pko + 8, pn - 8);
+            }
         }
     }
     uint64_t rk = 0, rv = 0, c = 0;
     uint64_t err = ~0ull;
-    if (e < n) {
-        const EntryFacts f = facts_finish(a, e, in);
-        a.lcp[e] = f.lcp;
-        a.szr[e] = f.s_r;
-        a.sznr[e] = f.s_nr;
-        if (a.bloom_fused) {
-            const uint64_t kl = in.ko1 - in.ko0;
-            const uint64_t h = kl == 16 ? siphash13_16(in.ck0, in.ck1) : siphash13(a.key_bytes + in.ko0, kl);
-            a.hd[e] = (uint64_t)fastmod_u32((uint32_t)h, a.bpl.mmod, a.bpl.m) |
-                      ((uint64_t)fastmod_u32((uint32_t)(h >> 32), a.bpl.mmod, a.bpl.m) << 32);
+    uint32_t hh[kFactsPerT], dd[kFactsPerT];
+#pragma unroll
+    for (uint32_t r = 0; r < kFactsPerT; r++) {
+        FactsIn &f = in[r];
+        const uint64_t e = e0 + r * kFactsThreads;
+        {
+            const uint64_t pko = wave_prev_lane(f.ko0), pk0 = wave_prev_lane(f.ck0), pk1 = wave_prev_lane(f.ck1);
+            if (lane != 0) {
+                f.pko = pko;
+                f.pk0 = pk0;
+                f.pk1 = pk1;
+            } else if (e == 0) {
+                f.pko = f.ko0;
+            }
         }
-        if (f.err) err = (e << 8) | (uint64_t)f.err;
-        rk = f.klen;
-        rv = f.vlen;
-        c = (uint64_t)(f.kind == SDB_KIND_VALUE) | ((uint64_t)(f.kind == SDB_KIND_TOMBSTONE) << 20) |
-            ((uint64_t)(f.kind == SDB_KIND_MERGE) << 40);
+        hh[r] = dd[r] = 0;
+        if (e < n) {
+            const EntryFacts x = facts_finish(a, e, f);
+            a.lcp[e] = x.lcp;
+            a.szr[e] = x.s_r;
+            a.sznr[e] = x.s_nr;
+            if (a.bloom_fused) {  // filter_hash (filter.rs:196-204) -> first probe and step
+                const uint64_t kl = f.ko1 - f.ko0;
+                const uint64_t h = kl == 16 ? siphash13_16(f.ck0, f.ck1) : siphash13(a.key_bytes + f.ko0, kl);
+                hh[r] = fastmod_u32((uint32_t)h, a.bpl.mmod, a.bpl.m);
+                dd[r] = fastmod_u32((uint32_t)(h >> 32), a.bpl.mmod, a.bpl.m);
+            }
+            if (x.err) {
+                const uint64_t ev = (e << 8) | (uint64_t)x.err;
+                err = ev < err ? ev : err;
+            }
+            rk += x.klen;
+            rv += x.vlen;
+            c += (uint64_t)(x.kind == SDB_KIND_VALUE) | ((uint64_t)(x.kind == SDB_KIND_TOMBSTONE) << 20) |
+                 ((uint64_t)(x.kind == SDB_KIND_MERGE) << 40);
+        }
     }
     // SstStats (sst_builder.rs:225-226, 315-317) and the first error: per-workgroup partials
     rk = wave_sum(rk);
@@ -282,6 +302,12 @@ __global__ __launch_bounds__(kFactsThreads) void k_facts(SstSet P) {
         unsigned long long m = ~0ull;
         for (uint32_t q = 0; q < kFactsThreads / 64; q++) m = s_err[q] < m ? s_err[q] : m;
         a.err_part[blockIdx.x] = m;  // every workgroup writes its slot: no initialisation needed
+    }
+    // the fused bloom: this workgroup's kChunk keys are one binning tile (sdb_bloom.h)
+    if (a.bloom_fused) {
+        const uint64_t k0 = (uint64_t)blockIdx.x * kFactsEntries;
+        const uint32_t nk = (uint32_t)((k0 + kFactsEntries < n ? k0 + kFactsEntries : n) - k0);
+        bloom_bin_core<kFactsPerT>(blockIdx.x, hh, dd, nk, a.bpl, a.bq, blds);
     }
 }
 
@@ -1761,7 +1787,6 @@ extern "C" int sdb_diag_phase_times(uint64_t *out, int nblocks) {
 }
 #endif
 
-__global__ void k_bloom_bin_hd(SstSet P);
 __global__ void k_bloom_fill_hd(SstSet P);
 static int g_cus = 0;
 static uint32_t g_emit_threads = kEmitThreads, g_emit_wg_per_cu = kEmitWgPerCu;
@@ -1788,7 +1813,7 @@ static void set_lds_attrs() {
         (void)hipFuncSetAttribute((const void *)k_group, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGroupLds);
         (void)hipFuncSetAttribute((const void *)k_seg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLdsMax);
         (void)hipFuncSetAttribute((const void *)k_bloom_fill_hd, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-        (void)hipFuncSetAttribute((const void *)k_bloom_bin_hd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLds);
+        (void)hipFuncSetAttribute((const void *)k_facts, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLds);
         (void)hipGetLastError();  // an unsupported attribute value must not poison the next launch status
     });
 }
@@ -1799,24 +1824,7 @@ static void set_lds_attrs() {
 // They run on a per-device side stream forked after k_facts and joined after k_emit, so they fill
 // the CUs the latency-bound k_seg / k_group / k_enum leave idle.
 // ------------------------------------------------------------------------------------------------
-static_assert(kChunk == kBinThreads * kHashPerT, "bloom tiles are k_facts hash tiles of kChunk keys");
-__global__ __launch_bounds__(kBinThreads) void k_bloom_bin_hd(SstSet P) {
-    const EncodeArgs a = make_args(P, blockIdx.y);
-    if (!a.bloom_fused || blockIdx.x >= a.bpl.tiles) return;
-    extern __shared__ __attribute__((aligned(16))) uint32_t blds[];
-    const uint32_t tile = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-    const uint64_t k0 = (uint64_t)tile * a.bpl.T;
-    const uint32_t nk = (uint32_t)((k0 + a.bpl.T < a.n ? k0 + a.bpl.T : a.n) - k0);
-    uint32_t hh[kHashPerT], dd[kHashPerT];
-#pragma unroll
-    for (uint32_t r = 0; r < kHashPerT; r++) {
-        const uint32_t x = tid + r * nt;
-        const uint64_t v = x < nk ? a.hd[k0 + x] : 0;
-        hh[r] = (uint32_t)v;
-        dd[r] = (uint32_t)(v >> 32);
-    }
-    bloom_bin_core<kHashPerT>(tile, hh, dd, nk, a.bpl, a.bq, blds);
-}
+static_assert(kChunk == kFactsEntries && kFactsThreads == kBinThreads, "bloom tiles are k_facts' chunks of kChunk keys");
 __global__ __launch_bounds__(kFillThreads) void k_bloom_fill_hd(SstSet P) {
     const EncodeArgs a = make_args(P, blockIdx.y);
     if (!a.bloom_fused || blockIdx.x >= a.bpl.nslices) return;
@@ -1830,13 +1838,8 @@ hipError_t launch_encode_set(const SstSet &P, size_t bin_lds, size_t fill_lds, h
     // every kernel on the caller's stream, in dependency order: the set is large enough to fill the
     // chip at each step, and one stream keeps the sequence capturable into a HIP graph
     stage_mark(st, kStFacts, true);
-    hipLaunchKernelGGL(k_facts, dim3(P.max_facts, P.count), dim3(kFactsThreads), 0, st, P);
+    hipLaunchKernelGGL(k_facts, dim3(P.max_facts, P.count), dim3(kFactsThreads), P.max_tiles ? bin_lds : 0, st, P);
     stage_mark(st, kStFacts, false);
-    if (P.max_tiles) {
-        stage_mark(st, kStBloom, true);
-        hipLaunchKernelGGL(k_bloom_bin_hd, dim3(P.max_tiles, P.count), dim3(kBinThreads), bin_lds, st, P);
-        stage_mark(st, kStBloom, false);
-    }
     stage_mark(st, kStSeg, true);
     hipLaunchKernelGGL(k_seg, dim3(P.max_chunks, P.count), dim3(kSegThreads), kSegLds, st, P);
     stage_mark(st, kStSeg, false);

@@ -109,3 +109,74 @@ def test_no_device_fails_loudly(lib):
     from slatedb_amd import runtime
     with pytest.raises(runtime.SdbError):
         runtime.Encoder()
+
+
+# ------------------------------------------------------------------------------------------------
+# INTEGRATION.md's Rust FFI structs must match the header (names, order, offsets, sizes)
+# ------------------------------------------------------------------------------------------------
+_RUST_PRIM = {"u8": (1, 1), "i8": (1, 1), "u16": (2, 2), "i16": (2, 2), "u32": (4, 4), "i32": (4, 4),
+              "c_int": (4, 4), "u64": (8, 8), "i64": (8, 8), "f64": (8, 8), "usize": (8, 8)}
+
+
+def rust_structs(md_path):
+    txt = open(md_path).read()
+    code = "\n".join(re.findall(r"```rust\n(.*?)```", txt, flags=re.S))
+    out = {}
+    for name, body in re.findall(r"#\[repr\(C\)\]\s*pub struct (\w+)\s*\{(.*?)\}", code, flags=re.S):
+        body = re.sub(r"//[^\n]*", "", body)
+        fields = re.findall(r"pub\s+(\w+)\s*:\s*([^,]+?)\s*(?:,|$)", body)
+        if fields:
+            out[name] = [(f, t.strip()) for f, t in fields]
+    return out
+
+
+def rust_layout(structs, name):
+    """C layout (offsets, size, align) of a #[repr(C)] struct from its Rust field types."""
+    off, align, offs = 0, 1, {}
+    for f, t in structs[name]:
+        if t.startswith("*"):
+            sz = al = 8
+        elif t in _RUST_PRIM:
+            sz, al = _RUST_PRIM[t]
+        else:
+            _, sz, al = rust_layout(structs, t)
+        off = (off + al - 1) // al * al
+        offs[f] = off
+        off += sz
+        align = max(align, al)
+    return offs, (off + align - 1) // align * align, align
+
+
+def test_integration_rust_structs_match_header():
+    structs = rust_structs(os.path.join(ROOT, "INTEGRATION.md"))
+    want = ["sdb_kv_batch", "sdb_sst_params", "sdb_sst_summary", "sdb_sst_out", "sdb_sst_host_result",
+            "sdb_footer_in", "sdb_decode_summary", "sdb_decoded_out", "sdb_decode_host_result"]
+    missing = [w for w in want if w not in structs]
+    assert not missing, missing
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "%s"' % HDR, "int main(void){"]
+    for cname in structs:
+        lines.append('printf("%s %%zu\\n", sizeof(%s));' % (cname, cname))
+        for f, _ in structs[cname]:
+            lines.append('printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (cname, f, cname, f))
+    lines.append("return 0;}")
+    with tempfile.TemporaryDirectory() as d:
+        src, exe = os.path.join(d, "r.c"), os.path.join(d, "r")
+        open(src, "w").write("\n".join(lines))
+        subprocess.check_call(["gcc", "-std=c11", "-o", exe, src])
+        got = dict(l.split() for l in subprocess.check_output([exe]).decode().splitlines())
+    for cname in structs:
+        offs, size, _ = rust_layout(structs, cname)
+        assert int(got[cname]) == size, (cname, "size", size, got[cname])
+        for f, off in offs.items():
+            assert int(got["%s.%s" % (cname, f)]) == off, (cname, f)
+    # every field of the header struct appears in the binding (no field silently missing)
+    hdr = re.sub(r"/\*.*?\*/", "", open(HDR).read(), flags=re.S)
+    for cname in want:
+        m = re.search(r"typedef struct %s\s*\{(.*?)\}\s*%s;" % (cname, cname), hdr, flags=re.S)
+        assert m, cname
+        cfields = []
+        for stmt in m.group(1).split(";"):
+            parts = [x.strip() for x in stmt.split(",") if x.strip()]
+            if parts:
+                cfields += [re.findall(r"(\w+)\s*$", x)[0] for x in parts]
+        assert [f for f, _ in structs[cname]] == cfields, (cname, [f for f, _ in structs[cname]], cfields)
