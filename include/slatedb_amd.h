@@ -227,6 +227,64 @@ sdb_status sdb_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, u
                              uint16_t sst_version, const sdb_decoded_out *out, void *workspace,
                              uint64_t workspace_bytes, void *stream);
 
+/* Decode nblocks blocks placed anywhere in one device arena: block k = arena[block_start[k] ..
+ * block_end[k]).  The read path fetches an SST's blocks as ~2 MiB ranged GETs (read_blocks,
+ * format/sst.rs:919-978; bytes_to_fetch / max_fetch_tasks, config.rs:1323-1337) and splits each per
+ * BlockMeta.offset; uploading many such ranges into one arena and decoding them here costs one launch
+ * sequence instead of one per range.  Same output contract as sdb_decode_blocks; val_off is relative to
+ * `arena`.  Workspace: sdb_decode_workspace_bytes(nblocks). */
+sdb_status sdb_decode_blocks_at(const uint8_t *arena, const uint64_t *block_start, const uint64_t *block_end,
+                                uint64_t nblocks, uint16_t sst_version, const sdb_decoded_out *out,
+                                void *workspace, uint64_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Point lookups / seeks on one encoded SST (device): the read path of Db::get and of an SstIterator
+ * positioned on a key:
+ *   1. filter: BloomFilter::might_contain(filter_hash(key)) (filter.rs:124-136, sst_iter.rs:201-227);
+ *   2. blocks: partitions_covering_range([key, key]) over BlockMeta.first_key (partitioned_keyspace.rs:
+ *      16-110), i.e. [first_partition_including_or_after_key, last_partition_including_key + 1);
+ *   3. the first block of that range in iteration order is seeked (sst_iter.rs:501-516):
+ *      BlockIteratorV2::seek (block_iterator_v2.rs:138-208, 269-313) ascending or
+ *      DescendingBlockIteratorV2::seek (:318-469); BlockIterator::seek for V1 (block_iterator.rs:
+ *      130-190); when it is exhausted the next block of the range is entered at its first entry
+ *      (ascending) or its last (descending);
+ *   4. the entry the iterator returns next is reported, and FOUND if its key equals the query.
+ * Each block read is CRC-checked first (validate_checksum, format/sst.rs:1029-1038).
+ * ------------------------------------------------------------------------------------------- */
+enum { SDB_LOOKUP_FILTERED = 0,     /* the bloom filter rules the key out (no block read) */
+       SDB_LOOKUP_EXHAUSTED = 1,    /* no entry at or past the key in iteration order */
+       SDB_LOOKUP_POSITIONED = 2,   /* positioned on an entry whose key differs from the query */
+       SDB_LOOKUP_FOUND = 3 };      /* positioned on an entry with key == query (newest version) */
+typedef struct sdb_sst_view {       /* device pointers into one encoded SST */
+    const uint8_t *data;            /* data section (blocks ++ crc) */
+    const uint64_t *block_off;      /* num_blocks + 1: BlockMeta.offset, then the data length */
+    uint64_t num_blocks;
+    const uint8_t *index_keys;      /* BlockMeta.first_key of block k = */
+    const uint64_t *index_key_off;  /*   index_keys[index_key_off[k] .. index_key_off[k + 1]) */
+    const uint8_t *bloom;           /* bitmap (filter without its u16 header); NULL = no filter */
+    uint64_t bloom_len;
+    uint32_t num_probes;
+    uint16_t sst_version;           /* 1 or 2 */
+    uint16_t pad;
+} sdb_sst_view;
+typedef struct sdb_lookup_out {     /* device arrays, one element per query */
+    uint8_t *state;                 /* SDB_LOOKUP_* */
+    int32_t *status;                /* sdb_status of the blocks read (CHECKSUM_MISMATCH, ...) */
+    uint32_t *block;                /* block of the positioned entry */
+    uint32_t *entry;                /* index of that entry inside its block (physical order) */
+    uint32_t *key_len;              /* its key length */
+    uint64_t *val_off;              /* its value: data[val_off .. val_off + val_len) (tombstone: 0, 0) */
+    uint32_t *val_len;
+    uint64_t *seq;
+    uint8_t *flags;                 /* RowFlags as the iterator returns them */
+    int64_t *create_ts;             /* valid iff flags & HAS_CREATE_TS */
+    int64_t *expire_ts;             /* valid iff flags & HAS_EXPIRE_TS */
+} sdb_lookup_out;
+uint64_t sdb_sst_lookup_workspace_bytes(uint64_t num_blocks, uint64_t nkeys);
+sdb_status sdb_sst_lookup(const sdb_sst_view *sst, const uint8_t *key_bytes, const uint64_t *key_off,
+                          uint64_t nkeys, int32_t descending, const sdb_lookup_out *out,
+                          void *workspace, uint64_t workspace_bytes, void *stream);
+
 /* ---------------------------------------------------------------------------------------------
  * SST footer (host): everything after the data section, so data ++ footer is the whole SST object
  * EncodedSsTableBuilder::build / EncodedWalSsTableBuilder::build hand to write_sst.

@@ -44,6 +44,7 @@ def _load():
         "orc_bloom_build": (C.c_int, [V, V, C.c_uint64, C.c_uint32, V, C.c_uint64]),
         "orc_bloom_might_contain": (C.c_int, [V, C.c_uint64, C.c_uint32, V, C.c_size_t]),
         "orc_decode_blocks": (C.c_int, [V, V, C.c_uint64, C.c_uint16, P(_abi.DecodedOut)]),
+        "orc_sst_lookup": (C.c_int, [P(_abi.SstView), V, V, C.c_uint64, C.c_int, P(_abi.LookupOut)]),
     }
     for k, (r, a) in sig.items():
         f = getattr(lib, k)
@@ -258,4 +259,53 @@ def _decode_blocks(blocks, block_off, version, cap_entries, key_cap):
     for f in ("val_off", "val_len", "seq", "flags", "create_ts", "expire_ts"):
         setattr(r, f, getattr(r, f)[:n])
     r.bad_block = r.bad_block[:min(sm.num_bad_blocks, max(nb, 1))]
+    return r
+
+
+LOOKUP_FIELDS = (("state", np.uint8), ("status", np.int32), ("block", np.uint32), ("entry", np.uint32),
+                 ("key_len", np.uint32), ("val_off", np.uint64), ("val_len", np.uint32), ("seq", np.uint64),
+                 ("flags", np.uint8), ("create_ts", np.int64), ("expire_ts", np.int64))
+
+
+class LookupResult:
+    pass
+
+
+def sst_index_keys(batch, enc):
+    """BlockMeta.first_key of every block (index key = first key[:index_key_len]) -> (bytes, offsets)."""
+    nb = len(enc.block_off) - 1
+    starts = np.asarray(enc.block_first_entry[:nb], np.int64)
+    ikl = np.asarray(enc.index_key_len[:nb], np.uint64)
+    off = np.zeros(nb + 1, np.uint64)
+    off[1:] = np.cumsum(ikl)
+    parts = [batch.key_bytes[int(batch.key_off[s]):int(batch.key_off[s]) + int(l)] for s, l in zip(starts, ikl)]
+    kb = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    return np.ascontiguousarray(kb, np.uint8), off
+
+
+def sst_lookup(data, block_off, index_keys, index_key_off, keys, descending=False, sst_version=2,
+               bloom=None, num_probes=0):
+    """orc_sst_lookup over host arrays; keys: list of bytes.  Returns a LookupResult of numpy arrays."""
+    data = np.ascontiguousarray(data, np.uint8)
+    block_off = np.ascontiguousarray(block_off, np.uint64)
+    ik = np.ascontiguousarray(index_keys, np.uint8)
+    iko = np.ascontiguousarray(index_key_off, np.uint64)
+    bm = None if bloom is None else np.ascontiguousarray(bloom, np.uint8)
+    v = _abi.SstView(data.ctypes.data if data.size else None, block_off.ctypes.data, len(block_off) - 1,
+                     ik.ctypes.data if ik.size else None, iko.ctypes.data,
+                     bm.ctypes.data if bm is not None and bm.size else (None if bm is None else 1),
+                     0 if bm is None else bm.size, num_probes, sst_version, 0)
+    if bm is not None and not bm.size:
+        v.bloom = C.cast(C.create_string_buffer(1), C.c_void_p).value
+    n = len(keys)
+    koff = np.zeros(n + 1, np.uint64)
+    koff[1:] = np.cumsum([len(k) for k in keys]) if n else []
+    kb = np.frombuffer(b"".join(bytes(k) for k in keys) or b"\0", np.uint8).copy()
+    r = LookupResult()
+    for f, dt in LOOKUP_FIELDS:
+        setattr(r, f, np.zeros(max(n, 1), dt))
+    out = _abi.LookupOut(*[getattr(r, f).ctypes.data for f, _ in LOOKUP_FIELDS])
+    lib().orc_sst_lookup(C.byref(v), kb.ctypes.data, koff.ctypes.data, n, int(bool(descending)), C.byref(out))
+    for f, _ in LOOKUP_FIELDS:
+        setattr(r, f, getattr(r, f)[:n])
     return r

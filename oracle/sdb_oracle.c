@@ -745,3 +745,424 @@ sdb_status orc_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, u
     sm->status = first_err;
     return first_err;
 }
+
+/* ------------------------------------------------------------------------------------------- */
+/* Point lookups: filter -> covering blocks -> block seek (sst_iter.rs:501-516)                  */
+/* ------------------------------------------------------------------------------------------- */
+static int lex_cmp(const uint8_t *a, size_t na, const uint8_t *b, size_t nb) { /* <[u8] as Ord>::cmp */
+    size_t m = na < nb ? na : nb;
+    int c = m ? memcmp(a, b, m) : 0;
+    if (c) return c < 0 ? -1 : 1;
+    return na < nb ? -1 : (na > nb ? 1 : 0);
+}
+
+typedef struct {            /* Block::decode (format/block.rs:28-46) of a CRC-checked block */
+    const uint8_t *d;
+    size_t data_end, count;
+    const uint8_t *offs;
+    uint64_t base;          /* offset of the block in the data section */
+} oblk;
+
+static sdb_status oblk_open(const sdb_sst_view *v, uint64_t k, oblk *b) {
+    uint64_t s = v->block_off[k], e = v->block_off[k + 1];
+    if (e < s || e - s < 4) return SDB_CORRUPT_BLOCK;
+    size_t len = (size_t)(e - s);
+    if (orc_crc32(v->data + s, len - 4) != (uint32_t)rd_be(v->data + e - 4, 4)) return SDB_CHECKSUM_MISMATCH;
+    size_t blen = len - 4;
+    if (blen < 2) return SDB_CORRUPT_BLOCK;
+    b->d = v->data + s;
+    b->base = s;
+    b->count = (size_t)rd_be(b->d + blen - 2, 2);
+    if (2 + 2 * b->count > blen) return SDB_CORRUPT_BLOCK;
+    b->data_end = blen - 2 - 2 * b->count;
+    b->offs = b->d + b->data_end;
+    return SDB_OK;
+}
+static size_t oblk_off(const oblk *b, size_t i) { return (size_t)rd_be(b->offs + 2 * i, 2); }
+
+typedef struct {            /* one decoded row (SstRowCodecV2::decode / SstRowCodecV0::decode) */
+    uint32_t shared, unshared, vlen;
+    size_t suf, vpos, next;
+    uint64_t seq;
+    uint8_t flags;
+    int64_t cts, ets;
+} orow;
+
+static sdb_status v2_row(const oblk *b, size_t pos, orow *r) { /* row_codec_v2.rs:172-220 */
+    const uint8_t *d = b->d;
+    size_t end = b->data_end;
+    if (!rd_varint(d, end, &pos, &r->shared) || !rd_varint(d, end, &pos, &r->unshared) ||
+        !rd_varint(d, end, &pos, &r->vlen))
+        return SDB_CORRUPT_BLOCK;
+    if (pos + (size_t)r->unshared + (size_t)r->vlen + 9 > end) return SDB_CORRUPT_BLOCK;
+    r->suf = pos;
+    pos += r->unshared;
+    r->vpos = pos;
+    pos += r->vlen;
+    r->seq = rd_be(d + pos, 8);
+    pos += 8;
+    r->flags = d[pos++];
+    if (!flags_ok(r->flags)) return SDB_INVALID_ROW_FLAGS;
+    size_t need = ((r->flags & SDB_FLAG_HAS_EXPIRE_TS) ? 8 : 0) + ((r->flags & SDB_FLAG_HAS_CREATE_TS) ? 8 : 0);
+    if (pos + need > end) return SDB_CORRUPT_BLOCK;
+    r->ets = r->cts = 0;
+    if (r->flags & SDB_FLAG_HAS_EXPIRE_TS) { r->ets = (int64_t)rd_be(d + pos, 8); pos += 8; }
+    if (r->flags & SDB_FLAG_HAS_CREATE_TS) { r->cts = (int64_t)rd_be(d + pos, 8); pos += 8; }
+    r->next = pos;
+    return SDB_OK;
+}
+
+/* decode_first_key_at_restart (block_iterator_v2.rs:73-80): asserts shared == 0 */
+static sdb_status v2_restart_key(const oblk *b, size_t ri, const uint8_t **key, size_t *klen) {
+    size_t p = oblk_off(b, ri);
+    uint32_t sh, un, vl;
+    if (p > b->data_end || !rd_varint(b->d, b->data_end, &p, &sh) || !rd_varint(b->d, b->data_end, &p, &un) ||
+        !rd_varint(b->d, b->data_end, &p, &vl) || sh != 0 || p + un > b->data_end)
+        return SDB_CORRUPT_BLOCK;
+    *key = b->d + p;
+    *klen = un;
+    return SDB_OK;
+}
+
+typedef struct { uint8_t *p; size_t n, cap; } okey;
+static void okey_set(okey *k, const uint8_t *pre, size_t npre, const uint8_t *suf, size_t nsuf) {
+    size_t n = npre + nsuf;
+    uint8_t *q = (uint8_t *)malloc(n ? n : 1);
+    if (npre) memcpy(q, pre, npre);
+    if (nsuf) memcpy(q + npre, suf, nsuf);
+    free(k->p);
+    k->p = q;
+    k->n = n;
+}
+
+typedef struct {            /* where a seek left the iterator */
+    int positioned;
+    size_t pos;             /* byte offset of the entry next() returns */
+    okey key;               /* its full key */
+} oseek;
+
+/* binary_search_restarts (block_iterator_v2.rs:138-154): first restart with key >= target */
+static sdb_status v2_bsearch_restarts(const oblk *b, const uint8_t *t, size_t nt, size_t *out) {
+    size_t low = 0, high = b->count;
+    while (low < high) {
+        size_t mid = low + (high - low) / 2;
+        const uint8_t *k;
+        size_t kn;
+        sdb_status st = v2_restart_key(b, mid, &k, &kn);
+        if (st) return st;
+        if (lex_cmp(k, kn, t, nt) < 0) low = mid + 1;
+        else high = mid;
+    }
+    *out = low;
+    return SDB_OK;
+}
+
+static size_t region_end(const oblk *b, size_t ri) { /* restart_region_end (:210-216) */
+    return ri + 1 < b->count ? oblk_off(b, ri + 1) : b->data_end;
+}
+
+/* BlockIteratorV2::seek, ascending (block_iterator_v2.rs:157-176, 269-313) */
+static sdb_status v2_seek_asc(const oblk *b, const uint8_t *t, size_t nt, oseek *s) {
+    s->positioned = 0;
+    if (b->count == 0) return SDB_OK;
+    size_t low;
+    sdb_status st = v2_bsearch_restarts(b, t, nt, &low);
+    if (st) return st;
+    size_t start = low ? low - 1 : 0; /* find_restart_for_key_ascending: low.saturating_sub(1) either way */
+    for (size_t ri = start; ri < b->count; ri++) {
+        const uint8_t *rk;
+        size_t rn;
+        if ((st = v2_restart_key(b, ri, &rk, &rn))) return st;
+        size_t off = oblk_off(b, ri);
+        okey_set(&s->key, rk, rn, NULL, 0);                       /* seek_to_restart */
+        if (off >= b->data_end) return SDB_OK;                    /* exhausted (is_empty) */
+        if (lex_cmp(s->key.p, s->key.n, t, nt) >= 0) { s->positioned = 1; s->pos = off; return SDB_OK; }
+        size_t rend = region_end(b, ri);
+        okey prev = {0, 0, 0};
+        okey_set(&prev, s->key.p, s->key.n, NULL, 0);
+        while (off < rend && off < b->data_end) {
+            orow r;
+            size_t p = off;
+            uint32_t sh, un, vl;                                   /* decode_key_at_offset (:115-126) */
+            if (!rd_varint(b->d, b->data_end, &p, &sh) || !rd_varint(b->d, b->data_end, &p, &un) ||
+                !rd_varint(b->d, b->data_end, &p, &vl) || sh > prev.n || p + un > b->data_end) {
+                free(prev.p);
+                return SDB_CORRUPT_BLOCK;
+            }
+            okey cur = {0, 0, 0};
+            okey_set(&cur, prev.p, sh, b->d + p, un);
+            if (lex_cmp(cur.p, cur.n, t, nt) >= 0) {
+                okey_set(&s->key, cur.p, cur.n, NULL, 0);
+                free(cur.p);
+                free(prev.p);
+                s->positioned = 1;
+                s->pos = off;
+                return SDB_OK;
+            }
+            if ((st = v2_row(b, off, &r))) { free(cur.p); free(prev.p); return st; } /* advance_past_current_entry */
+            off = r.next;
+            free(prev.p);
+            prev = cur;
+        }
+        free(prev.p);
+    }
+    return SDB_OK;
+}
+
+/* DescendingBlockIteratorV2::seek (block_iterator_v2.rs:178-208, 430-469) */
+static sdb_status v2_seek_desc(const oblk *b, const uint8_t *t, size_t nt, oseek *s) {
+    s->positioned = 0;
+    if (b->count == 0) return SDB_OK;
+    size_t low;
+    sdb_status st = v2_bsearch_restarts(b, t, nt, &low);
+    if (st) return st;
+    size_t start = low ? low - 1 : 0;
+    if (low < b->count) {                                          /* find_restart_for_key_descending */
+        const uint8_t *rk;
+        size_t rn;
+        if ((st = v2_restart_key(b, low, &rk, &rn))) return st;
+        if (lex_cmp(rk, rn, t, nt) == 0) {
+            size_t last = low;
+            while (last + 1 < b->count) {
+                if ((st = v2_restart_key(b, last + 1, &rk, &rn))) return st;
+                if (lex_cmp(rk, rn, t, nt) != 0) break;
+                last++;
+            }
+            start = last;
+        }
+    }
+    for (size_t ri = start + 1; ri-- > 0;) {
+        /* load_restart_region (:375-394): entries of region ri, ascending */
+        const uint8_t *rk;
+        size_t rn;
+        if ((st = v2_restart_key(b, ri, &rk, &rn))) return st;
+        okey cur = {0, 0, 0};
+        okey_set(&cur, rk, rn, NULL, 0);
+        size_t off = oblk_off(b, ri), rend = region_end(b, ri);
+        int have = 0;
+        size_t best_pos = 0;
+        okey best = {0, 0, 0};
+        while (off < rend && off < b->data_end) {
+            orow r;
+            if ((st = v2_row(b, off, &r))) { free(cur.p); free(best.p); return st; }
+            if (r.shared > cur.n) { free(cur.p); free(best.p); return SDB_CORRUPT_BLOCK; }
+            okey k = {0, 0, 0};
+            okey_set(&k, cur.p, r.shared, b->d + r.suf, r.unshared);
+            free(cur.p);
+            cur = k;
+            /* the last entry before the first key > target */
+            if (lex_cmp(cur.p, cur.n, t, nt) > 0) break;
+            have = 1;
+            best_pos = off;
+            okey_set(&best, cur.p, cur.n, NULL, 0);
+            off = r.next;
+        }
+        free(cur.p);
+        if (have) {
+            s->positioned = 1;
+            s->pos = best_pos;
+            okey_set(&s->key, best.p, best.n, NULL, 0);
+            free(best.p);
+            return SDB_OK;
+        }
+        free(best.p);
+    }
+    return SDB_OK;
+}
+
+/* V1: decode_key_at_index (block_iterator.rs:249-265): first_key[..prefix] ++ suffix */
+static sdb_status v1_key(const oblk *b, size_t i, okey *k) {
+    if (b->data_end < 4 || rd_be(b->d, 2) != 0) return SDB_CORRUPT_BLOCK; /* decode_first_key */
+    size_t fk = (size_t)rd_be(b->d + 2, 2);
+    if (4 + fk > b->data_end) return SDB_CORRUPT_BLOCK;
+    size_t p = oblk_off(b, i);
+    if (p + 4 > b->data_end) return SDB_CORRUPT_BLOCK;
+    size_t pre = (size_t)rd_be(b->d + p, 2), sl = (size_t)rd_be(b->d + p + 2, 2);
+    if (pre > fk || p + 4 + sl > b->data_end) return SDB_CORRUPT_BLOCK;
+    okey_set(k, b->d + 4, pre, b->d + p + 4, sl);
+    return SDB_OK;
+}
+
+/* BlockIterator::seek (block_iterator.rs:130-190): lower bound (asc) / last key <= target (desc) */
+static sdb_status v1_seek(const oblk *b, const uint8_t *t, size_t nt, int desc, oseek *s, size_t *phys) {
+    s->positioned = 0;
+    size_t n = b->count, low = 0, high = n;
+    okey k = {0, 0, 0};
+    while (low < high) {
+        size_t mid = low + (high - low) / 2;
+        sdb_status st = v1_key(b, mid, &k);
+        if (st) { free(k.p); return st; }
+        int c = lex_cmp(k.p, k.n, t, nt);
+        if (desc ? c <= 0 : c < 0) low = mid + 1;
+        else high = mid;
+    }
+    free(k.p);
+    if (!desc && low < n) { s->positioned = 1; *phys = low; }
+    if (desc && low > 0) { s->positioned = 1; *phys = low - 1; }
+    return SDB_OK;
+}
+
+/* The entry next() returns from a positioned iterator, reported into out[q]. */
+static sdb_status report_entry(const oblk *b, uint16_t version, uint64_t blk, size_t pos_or_idx, const okey *key,
+                               const uint8_t *t, size_t nt, const sdb_lookup_out *out, uint64_t q) {
+    orow r;
+    sdb_status st;
+    uint32_t phys = 0;
+    okey k = {0, 0, 0};
+    if (version == 2) {
+        if ((st = v2_row(b, pos_or_idx, &r))) return st;
+        for (size_t p = 0; p < pos_or_idx; phys++) { /* physical index: rows before pos */
+            orow x;
+            if ((st = v2_row(b, p, &x))) return st;
+            p = x.next;
+        }
+        okey_set(&k, key->p, key->n, NULL, 0);
+        out->val_off[q] = (r.flags & SDB_FLAG_TOMBSTONE) || !r.vlen ? 0 : b->base + r.vpos;
+        out->val_len[q] = (r.flags & SDB_FLAG_TOMBSTONE) ? 0 : r.vlen;
+        out->flags[q] = r.flags;
+    } else {
+        phys = (uint32_t)pos_or_idx;
+        if ((st = v1_key(b, pos_or_idx, &k))) { free(k.p); return st; }
+        size_t p = oblk_off(b, pos_or_idx) + 4;
+        size_t sl = (size_t)rd_be(b->d + p - 2, 2);
+        p += sl;
+        if (p + 9 > b->data_end) { free(k.p); return SDB_CORRUPT_BLOCK; }
+        r.seq = rd_be(b->d + p, 8);
+        p += 8;
+        uint8_t f = b->d[p++];
+        if (!flags_ok(f)) { free(k.p); return SDB_INVALID_ROW_FLAGS; }
+        size_t need = ((f & SDB_FLAG_HAS_EXPIRE_TS) ? 8 : 0) + ((f & SDB_FLAG_HAS_CREATE_TS) ? 8 : 0);
+        if (p + need > b->data_end) { free(k.p); return SDB_CORRUPT_BLOCK; }
+        r.ets = r.cts = 0;
+        if (f & SDB_FLAG_HAS_EXPIRE_TS) { r.ets = (int64_t)rd_be(b->d + p, 8); p += 8; }
+        if (f & SDB_FLAG_HAS_CREATE_TS) { r.cts = (int64_t)rd_be(b->d + p, 8); p += 8; }
+        uint32_t vl = 0;
+        uint64_t vp = 0;
+        if (f & SDB_FLAG_TOMBSTONE) {
+            f = (uint8_t)(f & ~SDB_FLAG_HAS_EXPIRE_TS); /* row.rs:223-231 */
+        } else {
+            if (p + 4 > b->data_end) { free(k.p); return SDB_CORRUPT_BLOCK; }
+            vl = (uint32_t)rd_be(b->d + p, 4);
+            p += 4;
+            if (p + vl > b->data_end) { free(k.p); return SDB_CORRUPT_BLOCK; }
+            vp = b->base + p;
+        }
+        out->val_off[q] = vl ? vp : 0;
+        out->val_len[q] = vl;
+        out->flags[q] = f;
+        r.flags = f;
+    }
+    out->seq[q] = r.seq;
+    out->create_ts[q] = (r.flags & SDB_FLAG_HAS_CREATE_TS) ? r.cts : 0;
+    out->expire_ts[q] = (r.flags & SDB_FLAG_HAS_EXPIRE_TS) ? r.ets : 0;
+    out->block[q] = (uint32_t)blk;
+    out->entry[q] = phys;
+    out->key_len[q] = (uint32_t)k.n;
+    out->state[q] = lex_cmp(k.p, k.n, t, nt) == 0 ? SDB_LOOKUP_FOUND : SDB_LOOKUP_POSITIONED;
+    free(k.p);
+    return SDB_OK;
+}
+
+/* partition_point (partitioned_keyspace.rs:16-39), restated literally; le: first_key <= key, else < */
+static uint64_t o_partition_point(const sdb_sst_view *v, const uint8_t *t, size_t nt, int le) {
+    uint64_t n = v->num_blocks;
+    if (n == 0) return 0;
+    uint64_t low = 0, high = n - 1, pp = 0;
+    while (low <= high) {
+        uint64_t mid = low + (high - low) / 2;
+        const uint8_t *fk = v->index_keys + v->index_key_off[mid];
+        size_t fn = (size_t)(v->index_key_off[mid + 1] - v->index_key_off[mid]);
+        int c = lex_cmp(fk, fn, t, nt);
+        if (le ? c <= 0 : c < 0) {
+            low = mid + 1;
+            pp = mid + 1;
+        } else if (mid > low) {
+            high = mid - 1;
+        } else {
+            break;
+        }
+    }
+    return pp;
+}
+
+sdb_status orc_sst_lookup(const sdb_sst_view *v, const uint8_t *key_bytes, const uint64_t *key_off,
+                          uint64_t nkeys, int descending, const sdb_lookup_out *out) {
+    for (uint64_t q = 0; q < nkeys; q++) {
+        const uint8_t *t = key_bytes + key_off[q];
+        size_t nt = (size_t)(key_off[q + 1] - key_off[q]);
+        out->status[q] = SDB_OK;
+        out->state[q] = SDB_LOOKUP_EXHAUSTED;
+        out->block[q] = out->entry[q] = out->key_len[q] = 0;
+        out->val_off[q] = 0;
+        out->val_len[q] = 0;
+        out->seq[q] = 0;
+        out->flags[q] = 0;
+        out->create_ts[q] = out->expire_ts[q] = 0;
+        if (v->bloom && !orc_bloom_might_contain(v->bloom, v->bloom_len, v->num_probes, t, nt)) {
+            out->state[q] = SDB_LOOKUP_FILTERED;
+            continue;
+        }
+        /* partitions_covering_range(Included(k), Included(k)) */
+        uint64_t pp_lt = o_partition_point(v, t, nt, 0);
+        uint64_t start = pp_lt > 0 ? pp_lt - 1 : 0;
+        uint64_t pp_le = o_partition_point(v, t, nt, 1);
+        uint64_t end = pp_le > 0 ? pp_le : start;
+        sdb_status st = SDB_OK;
+        for (uint64_t i = 0; start < end && i < end - start && out->state[q] == SDB_LOOKUP_EXHAUSTED; i++) {
+            uint64_t blk = descending ? end - 1 - i : start + i;
+            oblk b;
+            if ((st = oblk_open(v, blk, &b))) break;
+            oseek s = {0, 0, {0, 0, 0}};
+            size_t idx = 0;
+            if (i == 0) { /* only the first block is seeked */
+                if (v->sst_version == 2) st = descending ? v2_seek_desc(&b, t, nt, &s) : v2_seek_asc(&b, t, nt, &s);
+                else st = v1_seek(&b, t, nt, descending, &s, &idx);
+            } else if (b.count > 0) { /* a fresh iterator: its first (asc) or last (desc) entry */
+                if (v->sst_version == 1) {
+                    s.positioned = 1;
+                    idx = descending ? b.count - 1 : 0;
+                } else if (!descending) {
+                    const uint8_t *rk;
+                    size_t rn;
+                    if (!(st = v2_restart_key(&b, 0, &rk, &rn)) && b.data_end > 0) {
+                        s.positioned = 1;
+                        s.pos = 0;
+                        okey_set(&s.key, rk, rn, NULL, 0);
+                    }
+                } else {
+                    /* DescendingBlockIteratorV2::init: the last region's last entry */
+                    const uint8_t *rk;
+                    size_t rn;
+                    if (!(st = v2_restart_key(&b, b.count - 1, &rk, &rn))) {
+                        okey cur = {0, 0, 0};
+                        okey_set(&cur, rk, rn, NULL, 0);
+                        size_t off = oblk_off(&b, b.count - 1);
+                        while (!st && off < b.data_end) {
+                            orow r;
+                            if ((st = v2_row(&b, off, &r))) break;
+                            if (r.shared > cur.n) { st = SDB_CORRUPT_BLOCK; break; }
+                            okey k = {0, 0, 0};
+                            okey_set(&k, cur.p, r.shared, b.d + r.suf, r.unshared);
+                            free(cur.p);
+                            cur = k;
+                            s.positioned = 1;
+                            s.pos = off;
+                            okey_set(&s.key, cur.p, cur.n, NULL, 0);
+                            off = r.next;
+                        }
+                        free(cur.p);
+                    }
+                }
+            }
+            if (!st && s.positioned)
+                st = report_entry(&b, v->sst_version, blk, v->sst_version == 2 ? s.pos : idx, &s.key, t, nt, out, q);
+            free(s.key.p);
+            if (st) break;
+        }
+        if (st) {
+            out->status[q] = st;
+            out->state[q] = SDB_LOOKUP_EXHAUSTED;
+        }
+    }
+    return SDB_OK;
+}

@@ -54,6 +54,12 @@ int orc_bloom_might_contain(const uint8_t *bitmap, uint64_t bitmap_bytes, uint32
 sdb_status orc_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
                              uint16_t sst_version, const sdb_decoded_out *out);
 
+/* Point lookups on one SST (host pointers in `sst`): the same contract as sdb_sst_lookup, following
+ * filter.rs:124-136, partitioned_keyspace.rs:16-110, sst_iter.rs:501-516, block_iterator_v2.rs:
+ * 138-469 and block_iterator.rs:130-190 literally (materialised keys). */
+sdb_status orc_sst_lookup(const sdb_sst_view *sst, const uint8_t *key_bytes, const uint64_t *key_off,
+                          uint64_t nkeys, int descending, const sdb_lookup_out *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -120,6 +120,25 @@ class FooterIn(C.Structure):
     ]
 
 
+class SstView(C.Structure):
+    _fields_ = [
+        ("data", C.c_void_p), ("block_off", C.c_void_p), ("num_blocks", C.c_uint64),
+        ("index_keys", C.c_void_p), ("index_key_off", C.c_void_p),
+        ("bloom", C.c_void_p), ("bloom_len", C.c_uint64), ("num_probes", C.c_uint32),
+        ("sst_version", C.c_uint16), ("pad", C.c_uint16),
+    ]
+
+
+class LookupOut(C.Structure):
+    _fields_ = [
+        ("state", C.c_void_p), ("status", C.c_void_p), ("block", C.c_void_p), ("entry", C.c_void_p),
+        ("key_len", C.c_void_p), ("val_off", C.c_void_p), ("val_len", C.c_void_p), ("seq", C.c_void_p),
+        ("flags", C.c_void_p), ("create_ts", C.c_void_p), ("expire_ts", C.c_void_p),
+    ]
+
+
+LOOKUP_FILTERED, LOOKUP_EXHAUSTED, LOOKUP_POSITIONED, LOOKUP_FOUND = 0, 1, 2, 3
+
 SST_COMPACTED, SST_WAL = 0, 1
 
 
@@ -144,6 +163,11 @@ SIGNATURES = {
     "sdb_decode_workspace_bytes": (C.c_uint64, [C.c_uint64]),
     "sdb_decode_blocks": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint16,
                                     C.POINTER(DecodedOut), C.c_void_p, C.c_uint64, C.c_void_p]),
+    "sdb_decode_blocks_at": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint16,
+                                       C.POINTER(DecodedOut), C.c_void_p, C.c_uint64, C.c_void_p]),
+    "sdb_sst_lookup_workspace_bytes": (C.c_uint64, [C.c_uint64, C.c_uint64]),
+    "sdb_sst_lookup": (C.c_int, [C.POINTER(SstView), C.c_void_p, C.c_void_p, C.c_uint64, C.c_int32,
+                                 C.POINTER(LookupOut), C.c_void_p, C.c_uint64, C.c_void_p]),
     "sdb_sst_footer": (C.c_int, [C.POINTER(FooterIn), C.c_void_p, C.c_uint64, u64p]),
     "sdb_sst_footer_bound": (C.c_uint64, [C.POINTER(FooterIn)]),
     "sdb_encoder_create": (C.c_void_p, [C.c_int, C.POINTER(SstParams)]),

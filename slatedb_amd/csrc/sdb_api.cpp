@@ -16,6 +16,22 @@
 #include "sdb_decode.h"
 #include "sdb_bloom.h"
 
+namespace sdb {
+struct LookupArgs {
+    sdb_sst_view v;
+    const uint8_t *key_bytes;
+    const uint64_t *key_off;
+    uint64_t nkeys;
+    uint32_t desc;
+    sdb_lookup_out out;
+    uint32_t *qrange;
+    uint8_t *mark;
+    int32_t *bstat;
+};
+uint64_t lookup_workspace_bytes(uint64_t num_blocks, uint64_t nkeys);
+hipError_t launch_lookup(LookupArgs a, hipStream_t st);
+}  // namespace sdb
+
 using namespace sdb;
 
 namespace {
@@ -297,17 +313,19 @@ sdb_status sdb_bloom_might_contain(const uint8_t *bitmap, uint64_t bitmap_bytes,
 
 uint64_t sdb_decode_workspace_bytes(uint64_t nblocks) { return decode_workspace_layout(nblocks).total; }
 
-sdb_status sdb_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
-                             uint16_t sst_version, const sdb_decoded_out *out, void *workspace,
-                             uint64_t workspace_bytes, void *stream) {
+static sdb_status decode_common(const uint8_t *blocks, const uint64_t *block_off, const uint64_t *block_end,
+                                uint64_t nblocks, uint16_t sst_version, const sdb_decoded_out *out, void *workspace,
+                                uint64_t workspace_bytes, void *stream) {
     if (!out || !out->summary || !out->block_entry_start) return SDB_INVALID_ARGUMENT;
     if (sst_version != 1 && sst_version != 2) return SDB_INVALID_VERSION;  // block_iterator.rs:60-77
+    if (nblocks && (!blocks || !block_off)) return SDB_INVALID_ARGUMENT;
     if (!device_ok()) return SDB_DEVICE_ERROR;
     DecodeWorkspace wl = decode_workspace_layout(nblocks);
     if (!workspace || workspace_bytes < wl.total) return SDB_INVALID_ARGUMENT;
     DecodeArgs a{};
     a.blocks = blocks;
     a.block_off = block_off;
+    a.block_end = block_end;
     a.nblocks = nblocks;
     a.version = sst_version;
     a.out = *out;
@@ -326,6 +344,54 @@ sdb_status sdb_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, u
     a.bad_block = out->bad_block;
     a.bad_cap = out->bad_cap;
     if (launch_decode(a, S(stream)) != hipSuccess) return SDB_DEVICE_ERROR;
+    return SDB_OK;
+}
+
+sdb_status sdb_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                             uint16_t sst_version, const sdb_decoded_out *out, void *workspace,
+                             uint64_t workspace_bytes, void *stream) {
+    return decode_common(blocks, block_off, nullptr, nblocks, sst_version, out, workspace, workspace_bytes, stream);
+}
+
+sdb_status sdb_decode_blocks_at(const uint8_t *arena, const uint64_t *block_start, const uint64_t *block_end,
+                                uint64_t nblocks, uint16_t sst_version, const sdb_decoded_out *out,
+                                void *workspace, uint64_t workspace_bytes, void *stream) {
+    if (nblocks && !block_end) return SDB_INVALID_ARGUMENT;
+    return decode_common(arena, block_start, block_end, nblocks, sst_version, out, workspace, workspace_bytes, stream);
+}
+
+uint64_t sdb_sst_lookup_workspace_bytes(uint64_t num_blocks, uint64_t nkeys) {
+    return lookup_workspace_bytes(num_blocks, nkeys) + 256;
+}
+
+sdb_status sdb_sst_lookup(const sdb_sst_view *sst, const uint8_t *key_bytes, const uint64_t *key_off,
+                          uint64_t nkeys, int32_t descending, const sdb_lookup_out *out, void *workspace,
+                          uint64_t workspace_bytes, void *stream) {
+    if (!sst || !out) return SDB_INVALID_ARGUMENT;
+    if (sst->sst_version != 1 && sst->sst_version != 2) return SDB_INVALID_VERSION;
+    if (sst->num_blocks >= 0xFFFFFFFFull) return SDB_LIMIT_EXCEEDED;
+    if (sst->num_blocks && (!sst->data || !sst->block_off || !sst->index_keys || !sst->index_key_off))
+        return SDB_INVALID_ARGUMENT;
+    if (nkeys && (!key_bytes || !key_off || !out->state || !out->status || !out->block || !out->entry ||
+                  !out->key_len || !out->val_off || !out->val_len || !out->seq || !out->flags || !out->create_ts ||
+                  !out->expire_ts))
+        return SDB_INVALID_ARGUMENT;
+    if (!device_ok()) return SDB_DEVICE_ERROR;
+    if (!workspace || workspace_bytes < sdb_sst_lookup_workspace_bytes(sst->num_blocks, nkeys)) return SDB_INVALID_ARGUMENT;
+    uint8_t *w = (uint8_t *)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+    LookupArgs a{};
+    a.v = *sst;
+    a.key_bytes = key_bytes;
+    a.key_off = key_off;
+    a.nkeys = nkeys;
+    a.desc = descending ? 1 : 0;
+    a.out = *out;
+    a.qrange = (uint32_t *)w;
+    w += (8 * (nkeys + 1) + 255) & ~255ull;
+    a.mark = w;
+    w += (sst->num_blocks + 256) & ~255ull;
+    a.bstat = (int32_t *)w;
+    if (launch_lookup(a, S(stream)) != hipSuccess) return SDB_DEVICE_ERROR;
     return SDB_OK;
 }
 

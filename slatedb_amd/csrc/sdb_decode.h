@@ -9,7 +9,8 @@ namespace sdb {
 
 struct DecodeArgs {
     const uint8_t *blocks;
-    const uint64_t *block_off;  // nblocks+1
+    const uint64_t *block_off;  // nblocks+1 (contiguous) or nblocks starts (with block_end)
+    const uint64_t *block_end;  // nblocks ends, or NULL: block k ends at block_off[k + 1]
     uint64_t nblocks;
     uint32_t version;
     sdb_decoded_out out;  // device pointers

@@ -61,6 +61,10 @@ SDB_DEV bool rd_varint(P d, uint32_t end, uint32_t *pos, uint32_t *v) {
     return true;
 }
 
+// Block k is blocks[block_off[k] .. end): contiguous blocks end where the next begins; scattered
+// blocks (sdb_decode_blocks_at: many read_blocks ranges in one arena) carry their own ends.
+SDB_DEV uint64_t block_end_of(const DecodeArgs &a, uint64_t k) { return a.block_end ? a.block_end[k] : a.block_off[k + 1]; }
+
 SDB_DEV bool flags_ok(uint8_t f) {  // decode_flags (row_codec_v2.rs:234-249)
     return !(f & ~0x0Fu) && !((f & SDB_FLAG_TOMBSTONE) && (f & SDB_FLAG_MERGE_OPERAND));
 }
@@ -233,7 +237,7 @@ typedef BlockViewT<const lu8 *> LdsBlockView;
 // Stage + CRC-check block k; fills the view.  Called by a whole wave.
 SDB_DEV BlockView load_block(const DecodeArgs &a, uint64_t k, uint8_t *stage, const uint32_t (*crc)[256]) {
     BlockView v{};
-    const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
+    const uint64_t s = a.block_off[k], e = block_end_of(a, k);
     const uint64_t len = e - s;
     if (e < s || len < 4) {  // a non-monotone block_off is a corrupt range, never a huge read
         v.status = SDB_CORRUPT_BLOCK;
@@ -618,7 +622,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
     (void)gwave;
     for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave; k < a.nblocks; k += nwaves) {
         DEC_T(t0);
-        const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
+        const uint64_t s = a.block_off[k], e = block_end_of(a, k);
         Tally t{0, 0, 0, false};
         if (lane_id() == 0) a.rcnt[k] = ~0ull;  // row positions not recorded (tally_v2_fast overwrites)
         if (dec_fast(s, e)) {
@@ -1047,7 +1051,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
         if (n_ent == 0) continue;
         const uint64_t kb0 = a.small ? s_kb0 : a.key_start[k];
         const uint64_t kbn = (a.small ? s_kb1 : a.key_start[k + 1]) - kb0;
-        const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
+        const uint64_t s = a.block_off[k], e = block_end_of(a, k);
         const bool seq = a.flag[k] != 0;
         if (dec_fast(s, e)) {
             DEC_T(t0);

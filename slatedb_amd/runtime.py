@@ -449,3 +449,98 @@ def encode_ssts_device(dbatches, outs, prm, workspace, stream=None):
     st = lib().sdb_encode_ssts(len(dbatches), kbs, C.byref(prm), os_, workspace.data_ptr(), workspace.numel(), sp)
     if st:
         raise SdbError(st, "sdb_encode_ssts")
+
+
+class DeviceDecodeOutput:
+    """Caller-owned device outputs + workspace for sdb_decode_blocks / sdb_decode_blocks_at."""
+
+    def __init__(self, nblocks, cap_entries, key_cap, device="cuda"):
+        import torch
+        o = lambda n, dt: torch.empty(max(n, 1), dtype=dt, device=device)
+        self.nblocks = nblocks
+        self.block_entry_start = o(nblocks + 1, torch.int64)
+        self.key_arena = o(key_cap + 16, torch.uint8)
+        self.key_off = o(cap_entries + 1, torch.int64)
+        self.val_off = o(cap_entries, torch.int64)
+        self.val_len = o(cap_entries, torch.int32)
+        self.seq = o(cap_entries, torch.int64)
+        self.flags = o(cap_entries, torch.uint8)
+        self.create_ts = o(cap_entries, torch.int64)
+        self.expire_ts = o(cap_entries, torch.int64)
+        self.bad_block = o(nblocks + 1, torch.int32)
+        self.summary = torch.zeros(64, dtype=torch.uint8, device=device)
+        self.out = _abi.DecodedOut(self.block_entry_start.data_ptr(), self.key_arena.data_ptr(), key_cap,
+                                   self.key_off.data_ptr(), self.val_off.data_ptr(), self.val_len.data_ptr(),
+                                   self.seq.data_ptr(), self.flags.data_ptr(), self.create_ts.data_ptr(),
+                                   self.expire_ts.data_ptr(), cap_entries, self.bad_block.data_ptr(),
+                                   nblocks + 1, self.summary.data_ptr())
+        wsb = lib().sdb_decode_workspace_bytes(nblocks)
+        self.workspace = torch.empty(max(wsb, 256), dtype=torch.uint8, device=device)
+
+    def summary_host(self):
+        return _abi.DecodeSummary.from_buffer_copy(self.summary.cpu().numpy().tobytes()[:C.sizeof(_abi.DecodeSummary)])
+
+    def to_host(self):
+        """A Decoded with the same fields as Decoder.decode (numpy)."""
+        sm = self.summary_host()
+        d = Decoded()
+        d.status = sm.status
+        d.summary = {f: getattr(sm, f) for f, _ in _abi.DecodeSummary._fields_}
+        n = sm.num_entries if sm.status in (0, 3, 4, 9) else 0
+        d.n = n
+        v = lambda t, k, dt: t[:k].cpu().numpy().view(dt)
+        d.block_entry_start = v(self.block_entry_start, self.nblocks + 1, np.uint64)
+        d.key_off = v(self.key_off, n + 1, np.uint64)
+        d.key_arena = v(self.key_arena, sm.key_bytes, np.uint8)
+        d.val_off = v(self.val_off, n, np.uint64)
+        d.val_len = v(self.val_len, n, np.uint32)
+        d.seq = v(self.seq, n, np.uint64)
+        d.flags = v(self.flags, n, np.uint8)
+        d.create_ts = v(self.create_ts, n, np.int64)
+        d.expire_ts = v(self.expire_ts, n, np.int64)
+        d.bad_block = v(self.bad_block, min(sm.num_bad_blocks, self.nblocks + 1), np.uint32)
+        return d
+
+
+def decode_blocks_at_device(arena, block_start, block_end, nblocks, out, sst_version=2, stream=None):
+    """Enqueue sdb_decode_blocks_at: blocks at arbitrary places of one device arena (torch tensors)."""
+    sp = None
+    if stream is not None:
+        sp = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    st = lib().sdb_decode_blocks_at(arena.data_ptr(), block_start.data_ptr(), block_end.data_ptr(), nblocks,
+                                    sst_version, C.byref(out.out), out.workspace.data_ptr(), out.workspace.numel(), sp)
+    if st:
+        raise SdbError(st, "sdb_decode_blocks_at")
+
+
+LOOKUP_FIELDS = (("state", "uint8"), ("status", "int32"), ("block", "int32"), ("entry", "int32"),
+                 ("key_len", "int32"), ("val_off", "int64"), ("val_len", "int32"), ("seq", "int64"),
+                 ("flags", "uint8"), ("create_ts", "int64"), ("expire_ts", "int64"))
+
+
+def sst_lookup_device(view_tensors, key_bytes, key_off, nkeys, descending=False, stream=None):
+    """sdb_sst_lookup over device tensors.  view_tensors: dict with data, block_off, index_keys,
+    index_key_off (torch device tensors), num_blocks, sst_version and optionally bloom (device
+    tensor) + num_probes.  Returns a dict of device result tensors (LOOKUP_FIELDS)."""
+    import torch
+    dev = key_bytes.device
+    vt = view_tensors
+    bloom = vt.get("bloom")
+    v = _abi.SstView(vt["data"].data_ptr(), vt["block_off"].data_ptr(), vt["num_blocks"],
+                     vt["index_keys"].data_ptr(), vt["index_key_off"].data_ptr(),
+                     bloom.data_ptr() if bloom is not None else None,
+                     int(vt.get("bloom_len", 0)) if bloom is not None else 0, int(vt.get("num_probes", 0)),
+                     int(vt.get("sst_version", 2)), 0)
+    res = {f: torch.zeros(max(nkeys, 1), dtype=getattr(torch, dt), device=dev) for f, dt in LOOKUP_FIELDS}
+    out = _abi.LookupOut(*[res[f].data_ptr() for f, _ in LOOKUP_FIELDS])
+    wsb = lib().sdb_sst_lookup_workspace_bytes(vt["num_blocks"], nkeys)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    sp = None
+    if stream is not None:
+        sp = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    st = lib().sdb_sst_lookup(C.byref(v), key_bytes.data_ptr(), key_off.data_ptr(), nkeys, int(bool(descending)),
+                              C.byref(out), ws.data_ptr(), wsb, sp)
+    if st:
+        raise SdbError(st, "sdb_sst_lookup")
+    res["_ws"] = ws
+    return res

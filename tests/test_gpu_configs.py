@@ -200,3 +200,48 @@ def test_encode_graph_capture_replay(rt):
     torch.cuda.synchronize()
     for x, o in zip(batches, outs):
         assert_same(O.encode_sst(x, O.params()), _host_view(o.to_host()), "graph replay")
+
+
+# ------------------------------------------------------------------------------------------------
+# many read_blocks ranges in one arena (sdb_decode_blocks_at): §8 C1 at the 2 MiB GET granularity
+# ------------------------------------------------------------------------------------------------
+def test_decode_blocks_at_scattered_ranges(rt):
+    import torch
+    rng = np.random.default_rng(17)
+    encs = [O.encode_sst(datasets.d1(n=30000, sst_index=50 + j), O.params()) for j in range(3)]
+    encs.append(O.encode_sst(datasets.d3(n=2500), O.params(block_size=1024)))
+    # ranges of ~520 blocks (one 2 MiB GET each), placed in the arena in shuffled order with gaps
+    ranges = []
+    for e in encs:
+        nb = len(e.block_off) - 1
+        for b0 in range(0, nb, 520):
+            ranges.append((e, b0, min(nb, b0 + 520)))
+    order = rng.permutation(len(ranges))
+    arena = np.zeros(0, np.uint8)
+    starts, ends, contig, coff = [], [], [], [0]
+    for i in order:
+        e, b0, b1 = ranges[i]
+        lo, hi = int(e.block_off[b0]), int(e.block_off[b1])
+        base = len(arena) + int(rng.integers(1, 300))                  # a gap before every range
+        arena = np.concatenate([arena, rng.integers(0, 256, base - len(arena), dtype=np.uint8), e.data[lo:hi]])
+        starts += [base + int(e.block_off[k]) - lo for k in range(b0, b1)]
+        ends += [base + int(e.block_off[k + 1]) - lo for k in range(b0, b1)]
+        contig.append(e.data[lo:hi])
+    nb = len(starts)
+    # the oracle decodes the same blocks laid out back to back
+    cdata = np.concatenate(contig)
+    cl = np.array([e - s for s, e in zip(starts, ends)], np.uint64)
+    coff = np.concatenate([[0], np.cumsum(cl)]).astype(np.uint64)
+    ref = O.decode_blocks(cdata, coff, 2)
+    assert ref.status == 0
+    dev = torch.device("cuda")
+    out = rt.DeviceDecodeOutput(nb, ref.n + 16, len(ref.key_arena) + 16)
+    rt.decode_blocks_at_device(torch.from_numpy(arena).to(dev), torch.from_numpy(np.array(starts, np.uint64).view(np.int64)).to(dev),
+                               torch.from_numpy(np.array(ends, np.uint64).view(np.int64)).to(dev), nb, out)
+    torch.cuda.synchronize()
+    got = out.to_host()
+    # value references are arena offsets: map them back to the contiguous layout block by block
+    blk = np.searchsorted(ref.block_entry_start, np.arange(ref.n), side="right") - 1
+    shift = np.array(starts, np.uint64)[blk] - coff[:-1][blk]
+    got.val_off = np.where(got.val_len > 0, got.val_off - shift, got.val_off)
+    assert_decode_same(ref, got, "scattered ranges")
