@@ -89,9 +89,19 @@ typedef struct sdb_kv_batch {
     const int64_t *create_ts;   /* n (NULL = none); used where ts_mask & SDB_TS_CREATE, any entry may be read */
     const int64_t *expire_ts;   /* n (NULL = none); used where ts_mask & SDB_TS_EXPIRE, any entry may be read */
     const uint8_t *ts_mask;     /* n; NULL = no timestamps */
+    const int32_t *prefix_len;  /* n; SDB_PREFIX_LENGTHS only: PrefixExtractor::prefix_len(Point(key))
+                                   computed by the caller's extractor (-1 = None); else NULL */
 } sdb_kv_batch;
 
 enum { SDB_SST_COMPACTED = 0, SDB_SST_WAL = 1 };   /* SstType (schemas/sst.fbs) */
+/* Prefix extractor of BloomFilterPolicy::with_prefix_extractor (filter_policy.rs:213-224, filter.rs:
+ * 40-63, prefix_extractor.rs:41-95).  The extractor is a user trait object in the reference; the
+ * device evaluates the two stateless families the reference's tests use, or takes the lengths the
+ * caller's own extractor returned (SDB_PREFIX_LENGTHS), which covers any extractor. */
+enum { SDB_PREFIX_NONE = 0,
+       SDB_PREFIX_FIXED = 1,    /* prefix_len = key.len() >= arg ? Some(arg) : None */
+       SDB_PREFIX_DELIM = 2,    /* first byte == arg at i: Some(i + 1), else None */
+       SDB_PREFIX_LENGTHS = 3 };/* sdb_kv_batch.prefix_len / the query lengths */
 
 /* SsTableFormat knobs on this path (format/sst.rs:620-643, db/builder.rs:439-531). */
 typedef struct sdb_sst_params {
@@ -103,6 +113,11 @@ typedef struct sdb_sst_params {
     uint32_t sst_type;           /* SDB_SST_COMPACTED, or SDB_SST_WAL: EncodedWalSsTableBuilder
                                     (wal/slatedb/sst_builder.rs:68-205): entries in insertion order,
                                     no compute_index_key (so no prefix panic), no filter; V2 only */
+    uint32_t prefix_kind;        /* SDB_PREFIX_*: prefix hashes (deduplicated against the previous
+                                    key's prefix) join the filter (filter.rs:40-58) */
+    uint32_t prefix_arg;         /* FIXED: the length; DELIM: the delimiter byte */
+    uint32_t no_whole_key;       /* 1 = with_whole_key_filtering(false) (filter_policy.rs:226-235):
+                                    full keys are not hashed; 0 (default) = they are */
 } sdb_sst_params;
 
 /* Scalar results of one SST encode, written by the device. */
@@ -184,6 +199,27 @@ uint64_t sdb_bloom_workspace_bytes(uint64_t num_keys, uint32_t bits_per_key);
 sdb_status sdb_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
                            uint32_t bits_per_key, uint8_t *bitmap, uint64_t bitmap_bytes,
                            void *workspace, uint64_t workspace_bytes, void *stream);
+
+/* Filter over whole keys and/or extracted prefixes (BloomFilterBuilder::add_key with a prefix
+ * extractor, filter.rs:40-90): the filter's size follows the number of hashes (full keys + distinct
+ * consecutive prefixes), which the device counts, so the byte length is written to *bloom_len (device
+ * u64).  bitmap: 4-byte aligned, >= sdb_bloom_filter_bytes(2 n, bpk) bytes (the bound).  prefix_len:
+ * per-key lengths for SDB_PREFIX_LENGTHS (else NULL).  Keys must be sorted for the prefix dedup. */
+uint64_t sdb_bloom_prefix_workspace_bytes(uint64_t n);
+sdb_status sdb_bloom_build_prefix(const uint8_t *key_bytes, const uint64_t *key_off, const int32_t *prefix_len,
+                                  uint64_t n, uint32_t bits_per_key, uint32_t prefix_kind,
+                                  uint32_t prefix_arg, uint32_t whole_key, uint8_t *bitmap,
+                                  uint64_t bitmap_cap, uint64_t *bloom_len, void *workspace,
+                                  uint64_t workspace_bytes, void *stream);
+/* Filter::might_match (filter.rs:149-175) for FilterQuery targets: is_prefix[i] = 0 -> Point(key),
+ * 1 -> Prefix(key) (a scan prefix; NULL = all points).  With whole-key filtering a point probes the
+ * full key; otherwise the extracted prefix (query_prefix_len for SDB_PREFIX_LENGTHS, -1 = None); no
+ * extractable prefix answers 1 (no false negative).  result[i] = 1 iff the key may be present. */
+sdb_status sdb_bloom_might_match(const uint8_t *bitmap, uint64_t bitmap_bytes, uint32_t num_probes,
+                                 uint32_t whole_key, uint32_t prefix_kind, uint32_t prefix_arg,
+                                 const uint8_t *key_bytes, const uint64_t *key_off,
+                                 const uint8_t *is_prefix, const int32_t *query_prefix_len, uint64_t n,
+                                 uint8_t *result, void *stream);
 
 /* Batched BloomFilter::might_contain(filter_hash(key)) (filter.rs:124-136, 150-175): result[i]=1
  * iff every probe bit is set.  An empty bitmap answers 0.  The bitmap may start at any byte address
@@ -312,6 +348,8 @@ typedef struct sdb_footer_in {
     const uint16_t *block_stats;      /* 3 per block (puts, deletes, merges) */
     const uint8_t *bloom;             /* bitmap (has_filter) */
     uint64_t bloom_len;
+    const char *filter_name;          /* FilterPolicy::name: NULL = "_bf"; a prefix / no-whole-key policy
+                                         is "_bf:p=<extractor>[:wh=0]" (filter_policy.rs:237-250) */
 } sdb_footer_in;
 /* Writes the footer into out[0..cap) and its length into *len.  out == NULL: size query only.
  * cap too small: SDB_LIMIT_EXCEEDED (with *len set). */

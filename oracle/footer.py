@@ -195,7 +195,7 @@ def info_block(first_entry, last_entry, index_offset, index_len, filter_offset, 
 
 
 def sst_footer(data_len, first_keys, block_off, sst_version=2, sst_type=0, first_entry=None,
-               last_entry=None, stats=None, bloom=None, num_probes=0):
+               last_entry=None, stats=None, bloom=None, num_probes=0, filter_name=b"_bf"):
     """EncodedSsTableFooterBuilder::build.  stats = (puts, deletes, merges, raw_key, raw_val,
     block_stats) or None; bloom = bitmap bytes (a `_bf` filter is written) or None."""
     buf = b""
@@ -203,7 +203,7 @@ def sst_footer(data_len, first_keys, block_off, sst_version=2, sst_type=0, first
     filter_len = 0
     if bloom is not None:
         enc = struct.pack(">H", num_probes) + bytes(bloom)                       # filter.rs:177-180
-        comp = struct.pack(">HH", 1, 3) + b"_bf" + struct.pack(">Q", len(enc)) + enc
+        comp = struct.pack(">HH", 1, len(filter_name)) + filter_name + struct.pack(">Q", len(enc)) + enc
         buf += _checksummed(comp)
         filter_len = len(comp) + 4
     idx = index_block(first_keys, block_off)
@@ -317,7 +317,7 @@ def parse_sst(obj):
     return version, info, index, stats, filt
 
 
-def sst_object(batch, res, sst_version=2, sst_type=0, bloom_bits_per_key=10):
+def sst_object(batch, res, sst_version=2, sst_type=0, bloom_bits_per_key=10, filter_name=b"_bf"):
     """Whole SST object (data section ++ footer) from an encode result (oracle.SstResult or the
     device result as host arrays): what EncodedSsTableBuilder::build + write_sst store.
     sst_type 1 = WAL (wal/slatedb/sst_builder.rs): first_key = first seq BE, no last entry,
@@ -339,5 +339,6 @@ def sst_object(batch, res, sst_version=2, sst_type=0, bloom_bits_per_key=10):
                  [tuple(int(v) for v in row) for row in res.block_stats])
         bloom = bytes(res.bloom) if sm.filter_built else None
     foot, _ = sst_footer(int(res.summary.data_len), fks, [int(x) for x in res.block_off[:nb]],
-                         sst_version, sst_type, first, last, stats, bloom, int(res.summary.num_probes))
+                         sst_version, sst_type, first, last, stats, bloom, int(res.summary.num_probes),
+                         filter_name)
     return bytes(res.data) + foot

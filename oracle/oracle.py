@@ -45,6 +45,11 @@ def _load():
         "orc_bloom_might_contain": (C.c_int, [V, C.c_uint64, C.c_uint32, V, C.c_size_t]),
         "orc_decode_blocks": (C.c_int, [V, V, C.c_uint64, C.c_uint16, P(_abi.DecodedOut)]),
         "orc_sst_lookup": (C.c_int, [P(_abi.SstView), V, V, C.c_uint64, C.c_int, P(_abi.LookupOut)]),
+        "orc_bloom_build_prefix": (C.c_int, [V, V, V, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, V,
+                                             C.c_uint64, P(C.c_uint64)]),
+        "orc_bloom_might_match": (C.c_int, [V, C.c_uint64, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, V,
+                                            C.c_size_t, C.c_int, C.c_int64]),
+        "orc_prefix_len": (C.c_int64, [C.c_uint32, C.c_uint32, V, C.c_size_t, C.c_int64]),
     }
     for k, (r, a) in sig.items():
         f = getattr(lib, k)
@@ -164,14 +169,38 @@ def bounds(batch, params):
     vb = int(batch.val_off[-1] - batch.val_off[0])
     data_cap = kb + vb + n * 64 + 64
     block_cap = n + 1
-    bloom_cap = filter_size_bytes(n, params.bloom_bits_per_key) + 16 if params.bloom_bits_per_key else 16
+    hashes = (n if params.prefix_kind else 0) + (0 if params.no_whole_key else n)
+    bloom_cap = filter_size_bytes(hashes, params.bloom_bits_per_key) + 16 if params.bloom_bits_per_key else 16
     return data_cap, block_cap, bloom_cap
 
 
 def params(block_size=4096, sst_version=2, restart_interval=16, bloom_bits_per_key=10,
-           min_filter_keys=0, sst_type=0):
+           min_filter_keys=0, sst_type=0, prefix_kind=0, prefix_arg=0, no_whole_key=0):
     return _abi.SstParams(block_size, sst_version, restart_interval, bloom_bits_per_key,
-                          min_filter_keys, sst_type)
+                          min_filter_keys, sst_type, prefix_kind, prefix_arg, no_whole_key)
+
+
+def bloom_build_prefix(key_bytes, key_off, bpk, kind, arg=0, whole=True, prefix_len=None):
+    """BloomFilterBuilder with a prefix extractor (filter.rs:40-90): the bitmap (size from the hash count)."""
+    n = len(key_off) - 1
+    cap = filter_size_bytes(2 * n, bpk) + 16
+    bm = np.zeros(max(cap, 1), np.uint8)
+    ln = C.c_uint64(0)
+    pl = None if prefix_len is None else np.ascontiguousarray(prefix_len, np.int32)
+    kb = np.ascontiguousarray(key_bytes, np.uint8)
+    st = lib().orc_bloom_build_prefix(kb.ctypes.data if kb.size else None, np.ascontiguousarray(key_off, np.uint64).ctypes.data,
+                                      None if pl is None else pl.ctypes.data, n, bpk, kind, arg, int(whole),
+                                      bm.ctypes.data, cap, C.byref(ln))
+    assert st == 0, st
+    return bm[:ln.value].copy()
+
+
+def might_match(bitmap, num_probes, whole, kind, arg, query, is_prefix=False, given=-1):
+    """Filter::might_match (filter.rs:149-175) for FilterQuery::point / ::prefix."""
+    bq, nq = _buf(query)
+    bm = np.ascontiguousarray(bitmap, np.uint8)
+    return bool(lib().orc_bloom_might_match(bm.ctypes.data if bm.size else None, bm.size, num_probes, int(whole),
+                                            kind, arg, bq, nq, int(is_prefix), given))
 
 
 def encode_sst(batch, prm):

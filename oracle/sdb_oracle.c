@@ -203,6 +203,75 @@ sdb_status orc_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, ui
     return SDB_OK;
 }
 
+/* PrefixExtractor::prefix_len for the device-supported families (prefix_extractor.rs:41-95): -1 = None */
+int64_t orc_prefix_len(uint32_t kind, uint32_t arg, const uint8_t *key, size_t klen, int64_t given) {
+    if (kind == SDB_PREFIX_FIXED) return klen >= arg ? (int64_t)arg : -1;
+    if (kind == SDB_PREFIX_DELIM) {
+        for (size_t i = 0; i < klen; i++)
+            if (key[i] == (uint8_t)arg) return (int64_t)i + 1;
+        return -1;
+    }
+    if (kind == SDB_PREFIX_LENGTHS) return given;
+    return -1;
+}
+
+static void set_probes(uint8_t *bitmap, uint32_t m, uint16_t k, uint64_t h) {
+    uint32_t pr[64];
+    uint32_t *p = k <= 64 ? pr : (uint32_t *)malloc(sizeof(uint32_t) * k);
+    orc_probes_for_key(h, k, m, p);
+    for (uint16_t j = 0; j < k; j++) bitmap[p[j] / 8] |= (uint8_t)(1u << (p[j] % 8)); /* set_bit */
+    if (p != pr) free(p);
+}
+
+/* BloomFilterBuilder::add_key (filter.rs:40-63) over a sorted run + build_filter (:71-90): the
+ * extracted prefix is hashed when it differs from the last stored prefix (keys without a prefix do
+ * not reset it), the full key when whole_key.  The size follows the hash count. */
+sdb_status orc_bloom_build_prefix(const uint8_t *key_bytes, const uint64_t *key_off, const int32_t *plens,
+                                  uint64_t n, uint32_t bpk, uint32_t kind, uint32_t arg, int whole,
+                                  uint8_t *bitmap, uint64_t cap, uint64_t *len) {
+    uint64_t *h = (uint64_t *)malloc(sizeof(uint64_t) * (2 * n + 1));
+    uint64_t nh = 0;
+    const uint8_t *last = NULL;
+    size_t last_n = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint8_t *k = key_bytes + key_off[i];
+        size_t kl = (size_t)(key_off[i + 1] - key_off[i]);
+        if (kind != SDB_PREFIX_NONE) {
+            int64_t pl = orc_prefix_len(kind, arg, k, kl, plens ? plens[i] : -1);
+            if (pl >= 0) {
+                if ((size_t)pl > kl) { free(h); return SDB_INVALID_ARGUMENT; } /* the reference asserts */
+                int same = last && last_n == (size_t)pl && memcmp(last, k, (size_t)pl) == 0;
+                if (!same) {
+                    h[nh++] = orc_filter_hash(k, (size_t)pl);
+                    last = k;
+                    last_n = (size_t)pl;
+                }
+            }
+        }
+        if (whole) h[nh++] = orc_filter_hash(k, kl);
+    }
+    uint64_t fb = orc_filter_size_bytes(nh, bpk); /* key_hashes.len() as u32 */
+    *len = fb;
+    if (fb > cap) { free(h); return SDB_INVALID_ARGUMENT; }
+    memset(bitmap, 0, fb);
+    uint16_t kp = orc_optimal_num_probes(bpk);
+    if (fb)
+        for (uint64_t i = 0; i < nh; i++) set_probes(bitmap, (uint32_t)(fb * 8), kp, h[i]);
+    free(h);
+    return SDB_OK;
+}
+
+/* Filter::might_match (filter.rs:149-175) */
+int orc_bloom_might_match(const uint8_t *bitmap, uint64_t bitmap_bytes, uint32_t num_probes, int whole,
+                          uint32_t kind, uint32_t arg, const uint8_t *q, size_t qn, int is_prefix,
+                          int64_t given) {
+    if (!is_prefix && whole) return orc_bloom_might_contain(bitmap, bitmap_bytes, num_probes, q, qn);
+    if (kind == SDB_PREFIX_NONE) return 1;
+    int64_t pl = orc_prefix_len(kind, arg, q, qn, given);
+    if (pl < 0) return 1;
+    return orc_bloom_might_contain(bitmap, bitmap_bytes, num_probes, q, (size_t)pl);
+}
+
 int orc_bloom_might_contain(const uint8_t *bitmap, uint64_t bitmap_bytes, uint32_t num_probes,
                             const uint8_t *key, size_t klen) {
     if (bitmap_bytes == 0) return 0; /* filter.rs:124-129 */
@@ -562,8 +631,14 @@ sdb_status orc_encode_sst(const sdb_kv_batch *batch, const sdb_sst_params *param
     /* Filters (sst_builder.rs:388-403): one bloom per SST when num_rows >= min_filter_keys. */
     if (params->sst_type != SDB_SST_WAL && params->bloom_bits_per_key > 0 && n >= params->min_filter_keys) {
         uint64_t fb = orc_filter_size_bytes(n, params->bloom_bits_per_key);
-        if (fb > out->bloom_cap) { st = SDB_INVALID_ARGUMENT; goto done; }
-        orc_bloom_build(batch->key_bytes, batch->key_off, n, params->bloom_bits_per_key, out->bloom, fb);
+        if (params->prefix_kind != SDB_PREFIX_NONE || params->no_whole_key) {
+            if (orc_bloom_build_prefix(batch->key_bytes, batch->key_off, batch->prefix_len, n, params->bloom_bits_per_key,
+                                       params->prefix_kind, params->prefix_arg, !params->no_whole_key, out->bloom,
+                                       out->bloom_cap, &fb) != SDB_OK) { st = SDB_INVALID_ARGUMENT; goto done; }
+        } else {
+            if (fb > out->bloom_cap) { st = SDB_INVALID_ARGUMENT; goto done; }
+            orc_bloom_build(batch->key_bytes, batch->key_off, n, params->bloom_bits_per_key, out->bloom, fb);
+        }
         sm->bloom_len = fb;
         sm->filter_built = 1;
         sm->num_probes = orc_optimal_num_probes(params->bloom_bits_per_key);

@@ -49,6 +49,14 @@ sdb_status orc_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, ui
                            uint32_t bpk, uint8_t *bitmap, uint64_t bitmap_bytes);
 int orc_bloom_might_contain(const uint8_t *bitmap, uint64_t bitmap_bytes, uint32_t num_probes,
                             const uint8_t *key, size_t klen);
+/* Prefix filters (filter.rs:40-90, 149-175; prefix_extractor.rs:41-95). */
+int64_t orc_prefix_len(uint32_t kind, uint32_t arg, const uint8_t *key, size_t klen, int64_t given);
+sdb_status orc_bloom_build_prefix(const uint8_t *key_bytes, const uint64_t *key_off, const int32_t *plens,
+                                  uint64_t n, uint32_t bpk, uint32_t kind, uint32_t arg, int whole,
+                                  uint8_t *bitmap, uint64_t cap, uint64_t *len);
+int orc_bloom_might_match(const uint8_t *bitmap, uint64_t bitmap_bytes, uint32_t num_probes, int whole,
+                          uint32_t kind, uint32_t arg, const uint8_t *q, size_t qn, int is_prefix,
+                          int64_t given);
 
 /* read_blocks/decode_block + DataBlockIterator (format/sst.rs:938-1038, block_iterator*.rs). */
 sdb_status orc_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,

@@ -41,6 +41,7 @@ class KvBatch(C.Structure):
         ("val_bytes", C.c_void_p), ("val_off", C.c_void_p),
         ("kind", C.c_void_p), ("seq", C.c_void_p),
         ("create_ts", C.c_void_p), ("expire_ts", C.c_void_p), ("ts_mask", C.c_void_p),
+        ("prefix_len", C.c_void_p),
     ]
 
 
@@ -48,6 +49,7 @@ class SstParams(C.Structure):
     _fields_ = [
         ("block_size", C.c_uint32), ("sst_version", C.c_uint16), ("restart_interval", C.c_uint16),
         ("bloom_bits_per_key", C.c_uint32), ("min_filter_keys", C.c_uint32), ("sst_type", C.c_uint32),
+        ("prefix_kind", C.c_uint32), ("prefix_arg", C.c_uint32), ("no_whole_key", C.c_uint32),
     ]
 
 
@@ -116,7 +118,7 @@ class FooterIn(C.Structure):
         ("first_entry", C.c_char_p), ("first_entry_len", C.c_uint64),
         ("last_entry", C.c_char_p), ("last_entry_len", C.c_uint64),
         ("stats", C.c_void_p), ("block_stats", C.c_void_p), ("bloom", C.c_void_p),
-        ("bloom_len", C.c_uint64),
+        ("bloom_len", C.c_uint64), ("filter_name", C.c_char_p),
     ]
 
 
@@ -158,6 +160,13 @@ SIGNATURES = {
     "sdb_bloom_workspace_bytes": (C.c_uint64, [C.c_uint64, C.c_uint32]),
     "sdb_bloom_build": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p,
                                   C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]),
+    "sdb_bloom_prefix_workspace_bytes": (C.c_uint64, [C.c_uint64]),
+    "sdb_bloom_build_prefix": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                         C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                         C.c_uint64, C.c_void_p]),
+    "sdb_bloom_might_match": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                        C.c_void_p]),
     "sdb_bloom_might_contain": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p,
                                           C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
     "sdb_decode_workspace_bytes": (C.c_uint64, [C.c_uint64]),

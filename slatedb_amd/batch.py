@@ -14,10 +14,10 @@ from . import _abi
 
 class Batch:
     __slots__ = ("key_bytes", "key_off", "val_bytes", "val_off", "kind", "seq", "create_ts",
-                 "expire_ts", "ts_mask")
+                 "expire_ts", "ts_mask", "prefix_len")
 
     def __init__(self, key_bytes, key_off, val_bytes, val_off, kind=None, seq=None,
-                 create_ts=None, expire_ts=None, ts_mask=None):
+                 create_ts=None, expire_ts=None, ts_mask=None, prefix_len=None):
         self.key_bytes = np.ascontiguousarray(key_bytes, dtype=np.uint8)
         self.key_off = np.ascontiguousarray(key_off, dtype=np.uint64)
         self.val_bytes = np.ascontiguousarray(val_bytes, dtype=np.uint8)
@@ -27,9 +27,10 @@ class Batch:
         self.create_ts = None if create_ts is None else np.ascontiguousarray(create_ts, dtype=np.int64)
         self.expire_ts = None if expire_ts is None else np.ascontiguousarray(expire_ts, dtype=np.int64)
         self.ts_mask = None if ts_mask is None else np.ascontiguousarray(ts_mask, dtype=np.uint8)
+        self.prefix_len = None if prefix_len is None else np.ascontiguousarray(prefix_len, dtype=np.int32)
         n = len(self.key_off) - 1
         assert len(self.val_off) == n + 1, "val_off must have n+1 entries"
-        for name in ("kind", "seq", "create_ts", "expire_ts", "ts_mask"):
+        for name in ("kind", "seq", "create_ts", "expire_ts", "ts_mask", "prefix_len"):
             a = getattr(self, name)
             assert a is None or len(a) == n, name
 
@@ -71,7 +72,7 @@ class Batch:
         vb = self.val_bytes[int(vo[0]):int(vo[-1])]
         pick = lambda a: None if a is None else a[lo:hi]
         return Batch(kb, ko - ko[0], vb, vo - vo[0], pick(self.kind), pick(self.seq),
-                     pick(self.create_ts), pick(self.expire_ts), pick(self.ts_mask))
+                     pick(self.create_ts), pick(self.expire_ts), pick(self.ts_mask), pick(self.prefix_len))
 
     def logical_bytes(self):
         """Σ(|key| + |value|) — the headline GiB/s numerator."""
@@ -90,7 +91,7 @@ class Batch:
         p = lambda a: None if a is None else a.ctypes.data
         return _abi.KvBatch(self.n, p(self.key_bytes), p(self.key_off), p(self.val_bytes),
                             p(self.val_off), p(self.kind), p(self.seq), p(self.create_ts),
-                            p(self.expire_ts), p(self.ts_mask))
+                            p(self.expire_ts), p(self.ts_mask), p(self.prefix_len))
 
     def to_device(self, device="cuda"):
         return DeviceBatch(self, device)
@@ -112,9 +113,10 @@ class DeviceBatch:
         self.create_ts = t(host.create_ts)
         self.expire_ts = t(host.expire_ts)
         self.ts_mask = t(host.ts_mask)
+        self.prefix_len = t(host.prefix_len)
 
     def to_ctypes(self):
         p = lambda a: None if a is None else a.data_ptr()
         return _abi.KvBatch(self.n, p(self.key_bytes), p(self.key_off), p(self.val_bytes),
                             p(self.val_off), p(self.kind), p(self.seq), p(self.create_ts),
-                            p(self.expire_ts), p(self.ts_mask))
+                            p(self.expire_ts), p(self.ts_mask), p(self.prefix_len))

@@ -57,6 +57,9 @@ sdb_status check_params(const sdb_sst_params *p) {
     if (p->block_size == 0) return SDB_INVALID_ARGUMENT;
     if (p->sst_version == 2 && p->restart_interval == 0) return SDB_INVALID_ARGUMENT;
     if (p->sst_type > SDB_SST_WAL || (p->sst_type == SDB_SST_WAL && p->sst_version != 2)) return SDB_INVALID_ARGUMENT;
+    if (p->prefix_kind > SDB_PREFIX_LENGTHS || (p->prefix_kind == SDB_PREFIX_DELIM && p->prefix_arg > 255))
+        return SDB_INVALID_ARGUMENT;
+    if (p->no_whole_key && p->prefix_kind == SDB_PREFIX_NONE) return SDB_INVALID_ARGUMENT;  // nothing to hash
     return SDB_OK;
 }
 
@@ -108,8 +111,10 @@ sdb_status sdb_encode_bounds(uint64_t n, uint64_t total_key_bytes, uint64_t tota
     // block (+2 offset +2 count +4 crc).  V0 rows: 4 + key + 9 + 16 + 4 + value, +2 offset.
     if (data_cap) *data_cap = total_key_bytes + total_val_bytes + 64 * n + 64;
     if (block_cap) *block_cap = n + 1;
+    // a prefix-extractor filter holds up to one prefix hash per key besides the full-key hash
+    const uint64_t hashes = (params->prefix_kind ? n : 0) + (params->no_whole_key ? 0 : n);
     if (bloom_cap)
-        *bloom_cap = params->bloom_bits_per_key ? ((filter_bytes_for(n, params->bloom_bits_per_key) + 3) & ~3ull) + 16
+        *bloom_cap = params->bloom_bits_per_key ? ((filter_bytes_for(hashes, params->bloom_bits_per_key) + 3) & ~3ull) + 16
                                                 : 16;
     return SDB_OK;
 }
@@ -118,7 +123,10 @@ sdb_status sdb_encode_bounds(uint64_t n, uint64_t total_key_bytes, uint64_t tota
 
 namespace {
 // One SST's workspace region (256-byte multiple) inside a set's workspace.
+bool prefix_filter(const sdb_sst_params *p) { return p->prefix_kind != SDB_PREFIX_NONE || p->no_whole_key; }
 uint64_t sst_ws_bytes(uint64_t n, const sdb_sst_params *p) {
+    if (prefix_filter(p))  // the prefix filter's scratch instead of the fused bloom's slots
+        return (encode_workspace_offsets(n, false).bloom_rep + prefix_workspace_bytes(n) + 511) & ~255ull;
     const uint64_t fb = p->bloom_bits_per_key ? filter_bytes_for(n, p->bloom_bits_per_key) : 0;
     return (encode_workspace_layout(n, fb, num_probes_for(p->bloom_bits_per_key)).total + 255) & ~255ull;
 }
@@ -129,8 +137,11 @@ sdb_status check_sst(const sdb_kv_batch *b, const sdb_sst_params *p, const sdb_s
     if (n >= (1ull << 31)) return SDB_LIMIT_EXCEEDED;
     if (n && (!b->key_bytes || !b->key_off || !b->val_off)) return SDB_INVALID_ARGUMENT;
     const bool want_filter = p->sst_type != SDB_SST_WAL && p->bloom_bits_per_key > 0 && n >= p->min_filter_keys;
-    const uint64_t fb = want_filter ? filter_bytes_for(n, p->bloom_bits_per_key) : 0;
+    const uint64_t hashes = prefix_filter(p) ? (p->prefix_kind ? n : 0) + (p->no_whole_key ? 0 : n) : n;
+    const uint64_t fb = want_filter ? filter_bytes_for(hashes, p->bloom_bits_per_key) : 0;
     if (want_filter && fb && (!out->bloom || out->bloom_cap < fb)) return SDB_INVALID_ARGUMENT;
+    if (want_filter && prefix_filter(p) && ((uintptr_t)out->bloom & 3)) return SDB_INVALID_ARGUMENT;
+    if (want_filter && p->prefix_kind == SDB_PREFIX_LENGTHS && n && !b->prefix_len) return SDB_INVALID_ARGUMENT;
     if (n && (!out->data || !out->block_off || !out->block_first_entry || !out->index_key_len || !out->block_stats))
         return SDB_INVALID_ARGUMENT;
     return SDB_OK;
@@ -175,7 +186,11 @@ SstSlot plan_slot(const sdb_kv_batch *b, const sdb_sst_params *p, const sdb_sst_
         s.group = g;
     }
     *standalone_bloom = false;
-    if (want_filter && n) {
+    if (want_filter && prefix_filter(p)) {  // device-counted size: built before the set (sdb_bloom.hip)
+        s.prefix_bloom = 1;
+        s.bloom_len = 0;
+        *standalone_bloom = true;
+    } else if (want_filter && n) {
         // the bloom is fused with the encode (k_facts hashes, binned per chunk) when the binned build
         // fits; otherwise the standalone build runs before the set
         const BloomPlan pl = bloom_plan(n, s.num_probes, fb, kChunk);
@@ -248,9 +263,15 @@ sdb_status sdb_encode_ssts(uint32_t count, const sdb_kv_batch *batches, const sd
             one.s[0] = slot;
             const EncodeArgs a = make_args(one, 0);
             stage_mark(s, kStBloom, true);
-            if (launch_bloom_build(slot.key_bytes, slot.key_off, slot.n, slot.num_probes, slot.bloom_out, slot.bloom_len,
-                                   (void *)a.bq.count, s) != hipSuccess)
-                return SDB_DEVICE_ERROR;
+            hipError_t e;
+            if (slot.prefix_bloom)
+                e = launch_bloom_prefix(slot.key_bytes, slot.key_off, batches[i].prefix_len, slot.n, p->bloom_bits_per_key,
+                                        p->prefix_kind, p->prefix_arg, p->no_whole_key ? 0 : 1, slot.bloom_out,
+                                        outs[i].bloom_cap, (uint64_t *)a.bloom_len_dev, (void *)a.bq.count, s);
+            else
+                e = launch_bloom_build(slot.key_bytes, slot.key_off, slot.n, slot.num_probes, slot.bloom_out, slot.bloom_len,
+                                       (void *)a.bq.count, s);
+            if (e != hipSuccess) return SDB_DEVICE_ERROR;
             stage_mark(s, kStBloom, false);
         }
         if (!slot.n) {  // empty SST: summary only (a filter of an empty SST has no bytes)
@@ -297,6 +318,38 @@ sdb_status sdb_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, ui
     if (((uintptr_t)bitmap & 3) || (!workspace && fb && bitmap_bytes < ((fb + 3) & ~3ull))) return SDB_INVALID_ARGUMENT;
     if (workspace && workspace_bytes < sdb_bloom_workspace_bytes(n, bits_per_key)) return SDB_INVALID_ARGUMENT;
     if (launch_bloom_build(key_bytes, key_off, n, num_probes_for(bits_per_key), bitmap, fb, workspace, S(stream)) != hipSuccess)
+        return SDB_DEVICE_ERROR;
+    return SDB_OK;
+}
+
+uint64_t sdb_bloom_prefix_workspace_bytes(uint64_t n) { return prefix_workspace_bytes(n) + 256; }
+
+sdb_status sdb_bloom_build_prefix(const uint8_t *key_bytes, const uint64_t *key_off, const int32_t *prefix_len,
+                                  uint64_t n, uint32_t bits_per_key, uint32_t prefix_kind, uint32_t prefix_arg,
+                                  uint32_t whole_key, uint8_t *bitmap, uint64_t bitmap_cap, uint64_t *bloom_len,
+                                  void *workspace, uint64_t workspace_bytes, void *stream) {
+    if (!device_ok()) return SDB_DEVICE_ERROR;
+    if (prefix_kind > SDB_PREFIX_LENGTHS || (prefix_kind == SDB_PREFIX_NONE && !whole_key) || !bloom_len ||
+        (n && (!key_bytes || !key_off)) || (prefix_kind == SDB_PREFIX_LENGTHS && n && !prefix_len) ||
+        (prefix_kind == SDB_PREFIX_DELIM && prefix_arg > 255) || !bitmap || ((uintptr_t)bitmap & 3) ||
+        !workspace || workspace_bytes < sdb_bloom_prefix_workspace_bytes(n))
+        return SDB_INVALID_ARGUMENT;
+    if (launch_bloom_prefix(key_bytes, key_off, prefix_len, n, bits_per_key, prefix_kind, prefix_arg, whole_key ? 1 : 0,
+                            bitmap, bitmap_cap, bloom_len, workspace, S(stream)) != hipSuccess)
+        return SDB_DEVICE_ERROR;
+    return SDB_OK;
+}
+
+sdb_status sdb_bloom_might_match(const uint8_t *bitmap, uint64_t bitmap_bytes, uint32_t num_probes, uint32_t whole_key,
+                                 uint32_t prefix_kind, uint32_t prefix_arg, const uint8_t *key_bytes,
+                                 const uint64_t *key_off, const uint8_t *is_prefix, const int32_t *query_prefix_len,
+                                 uint64_t n, uint8_t *result, void *stream) {
+    if (!device_ok()) return SDB_DEVICE_ERROR;
+    if (prefix_kind > SDB_PREFIX_LENGTHS || (n && (!key_bytes || !key_off || !result)) ||
+        (prefix_kind == SDB_PREFIX_LENGTHS && n && !query_prefix_len) || (bitmap_bytes && !bitmap))
+        return SDB_INVALID_ARGUMENT;
+    if (launch_bloom_match(bitmap, bitmap_bytes, num_probes, whole_key ? 1 : 0, prefix_kind, prefix_arg, key_bytes, key_off,
+                           is_prefix, query_prefix_len, n, result, S(stream)) != hipSuccess)
         return SDB_DEVICE_ERROR;
     return SDB_OK;
 }
@@ -509,7 +562,7 @@ struct sdb_encoder {
 namespace {
 
 struct InLayout {  // packed input arrays inside one allocation (256-byte aligned pieces)
-    uint64_t key_bytes, key_off, val_bytes, val_off, kind, seq, cts, ets, mask, total;
+    uint64_t key_bytes, key_off, val_bytes, val_off, kind, seq, cts, ets, mask, plen, total;
 };
 InLayout in_layout(uint64_t n, uint64_t kb, uint64_t vb) {
     InLayout l{};
@@ -528,6 +581,7 @@ InLayout in_layout(uint64_t n, uint64_t kb, uint64_t vb) {
     l.cts = take(8 * (n + 1));
     l.ets = take(8 * (n + 1));
     l.mask = take(n + 1);
+    l.plen = take(4 * (n + 1));
     l.total = off;
     return l;
 }
@@ -610,6 +664,7 @@ sdb_status sdb_encoder_encode_host(sdb_encoder *e, const sdb_kv_batch *hb, sdb_s
         if (hb->create_ts) memcpy(hi + il.cts, hb->create_ts, 8 * n);
         if (hb->expire_ts) memcpy(hi + il.ets, hb->expire_ts, 8 * n);
         if (hb->ts_mask) memcpy(hi + il.mask, hb->ts_mask, n);
+        if (hb->prefix_len) memcpy(hi + il.plen, hb->prefix_len, 4 * n);
     }
     uint8_t *di = (uint8_t *)e->d_in.p, *dout = (uint8_t *)e->d_out.p;
     hipEventRecord(e->ev[0], e->stream);
@@ -626,6 +681,7 @@ sdb_status sdb_encoder_encode_host(sdb_encoder *e, const sdb_kv_batch *hb, sdb_s
     db.create_ts = hb->create_ts ? (const int64_t *)(di + il.cts) : nullptr;
     db.expire_ts = hb->expire_ts ? (const int64_t *)(di + il.ets) : nullptr;
     db.ts_mask = hb->ts_mask ? di + il.mask : nullptr;
+    db.prefix_len = hb->prefix_len ? (const int32_t *)(di + il.plen) : nullptr;
     sdb_sst_out o{};
     o.data = dout + ol.data;
     o.data_cap = data_cap;

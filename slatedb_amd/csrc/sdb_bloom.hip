@@ -176,3 +176,258 @@ uint64_t encode_bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_by
     return a > b ? a : b;
 }
 }  // namespace sdb
+
+namespace sdb {
+
+// ------------------------------------------------------------------------------------------------
+// Prefix-extractor filters (BloomFilterBuilder::add_key with an extractor, filter.rs:40-63; build
+// filter.rs:71-90): every stored key contributes hash(key[..prefix_len]) when that prefix differs from
+// the last stored prefix (keys without a prefix do not reset it) and hash(key) under whole-key
+// filtering.  The filter size follows the hash count, so the device counts before it sizes:
+//   k_pf_last   per 1024-entry chunk: the last entry that has a prefix
+//   k_pf_count  per entry: the previous entry with a prefix (in-chunk scan, else the chunks before),
+//               new-prefix flag; per chunk: hashes
+//   k_pf_plan   one workgroup: total hashes -> filter_size_bytes (u32 arithmetic), m, fastmod constant
+//   k_pf_set    per entry: the probes of its hashes, device-scope atomicOr into the zeroed bitmap
+// ------------------------------------------------------------------------------------------------
+struct PrefixSpec {
+    uint32_t kind, arg, whole, pad;
+    const int32_t *lens;  // SDB_PREFIX_LENGTHS
+};
+struct PrefixWs {
+    int64_t *chunk_last;   // per chunk: last entry with a prefix (-1: none)
+    int64_t *prev_last;    // per chunk: last entry with a prefix before the chunk
+    uint64_t *chunk_cnt;   // per chunk: hashes
+    uint8_t *is_new;       // per entry: its prefix hash is stored
+    uint64_t *plan;        // [0] hashes, [1] filter bytes, [2] m, [3] fastmod constant, [4] error
+};
+constexpr uint32_t kPfChunk = 1024;
+
+SDB_DEV int64_t pf_len(const PrefixSpec &ps, const uint8_t *k, uint32_t kl, uint64_t i) {  // -1 = None
+    if (ps.kind == SDB_PREFIX_FIXED) return kl >= ps.arg ? (int64_t)ps.arg : -1;
+    if (ps.kind == SDB_PREFIX_DELIM) {
+        for (uint32_t x = 0; x < kl; x++)
+            if (k[x] == (uint8_t)ps.arg) return (int64_t)x + 1;
+        return -1;
+    }
+    if (ps.kind == SDB_PREFIX_LENGTHS) return ps.lens ? (int64_t)ps.lens[i] : -1;
+    return -1;
+}
+
+// Entry indices travel as i + 1 (0 = none) so the scans are unsigned maxima with identity 0 (the DPP
+// lanes without a source read 0).
+SDB_DEV uint64_t umax64(uint64_t x, uint64_t y) { return x > y ? x : y; }
+SDB_DEV int64_t block_max_i64(int64_t v, int64_t *s_w) {  // every thread gets the workgroup max (v >= -1)
+    const uint32_t tid = threadIdx.x, w = tid >> 6, nw = (blockDim.x + 63) >> 6;
+    const uint64_t u = wave_readlane(wave_incl_scan_op((uint64_t)(v + 1), umax64), 63);
+    __syncthreads();
+    if ((tid & 63) == 0) s_w[w] = (int64_t)u;
+    __syncthreads();
+    uint64_t r = (uint64_t)s_w[0];
+    for (uint32_t q = 1; q < nw; q++) r = umax64(r, (uint64_t)s_w[q]);
+    __syncthreads();
+    return (int64_t)r - 1;
+}
+
+__global__ __launch_bounds__(kPfChunk) void k_pf_last(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
+                                                      PrefixSpec ps, PrefixWs w) {
+    __shared__ int64_t s_w[16];
+    const uint64_t i = (uint64_t)blockIdx.x * kPfChunk + threadIdx.x;
+    int64_t v = -1;
+    if (i < n) {
+        const uint64_t ko = key_off[i];
+        if (pf_len(ps, key_bytes + ko, (uint32_t)(key_off[i + 1] - ko), i) >= 0) v = (int64_t)i;
+    }
+    v = block_max_i64(v, s_w);
+    if (threadIdx.x == 0) w.chunk_last[blockIdx.x] = v;
+}
+
+__global__ __launch_bounds__(1024) void k_pf_prev(uint64_t nchunks, PrefixWs w) {  // exclusive max-scan
+    if (threadIdx.x == 0) {
+        int64_t m = -1;
+        for (uint64_t c = 0; c < nchunks; c++) {
+            w.prev_last[c] = m;
+            const int64_t x = w.chunk_last[c];
+            m = x > m ? x : m;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kPfChunk) void k_pf_count(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
+                                                       PrefixSpec ps, PrefixWs w) {
+    __shared__ int64_t s_last[16];
+    __shared__ uint64_t s_w[17];
+    const uint32_t tid = threadIdx.x, lane = (uint32_t)lane_id(), wv = tid >> 6;
+    const uint64_t i = (uint64_t)blockIdx.x * kPfChunk + tid;
+    int64_t pl = -1;
+    uint64_t ko = 0;
+    uint32_t kl = 0;
+    if (i < n) {
+        ko = key_off[i];
+        kl = (uint32_t)(key_off[i + 1] - ko);
+        pl = pf_len(ps, key_bytes + ko, kl, i);
+    }
+    // j = the last entry < i with a prefix: inclusive max-scan of (has ? i : -1), shifted by one
+    const uint64_t mine = pl >= 0 ? i + 1 : 0;  // i + 1, 0 = none
+    const uint64_t inc = wave_incl_scan_op(mine, umax64);
+    if (lane == 63) s_last[wv] = (int64_t)inc;
+    __syncthreads();
+    uint64_t before = (uint64_t)(w.prev_last[blockIdx.x] + 1);
+    for (uint32_t q = 0; q < wv; q++) before = umax64(before, (uint64_t)s_last[q]);
+    uint64_t jp = wave_prev_lane(inc);
+    if (lane == 0) jp = 0;
+    const int64_t j = (int64_t)umax64(jp, before) - 1;
+    uint64_t cnt = 0;
+    uint8_t isnew = 0;
+    if (i < n) {
+        if (pl >= 0) {
+            if (pl > kl) atomicMax((unsigned long long *)&w.plan[4], 1ull);  // the reference asserts
+            isnew = 1;
+            if (j >= 0) {
+                const uint64_t jo = key_off[j];
+                const uint32_t jl = (uint32_t)(key_off[j + 1] - jo);
+                const int64_t pj = pf_len(ps, key_bytes + jo, jl, (uint64_t)j);
+                if (pj == pl && pl <= kl && pj <= jl &&
+                    lcp_bytes(key_bytes + ko, (uint32_t)pl, key_bytes + jo, (uint32_t)pj) == (uint32_t)pl)
+                    isnew = 0;
+            }
+        }
+        w.is_new[i] = isnew;
+        cnt = isnew + (ps.whole ? 1 : 0);
+    }
+    uint64_t tot;
+    block_excl_scan_u64(cnt, s_w, &tot);
+    if (tid == 0) w.chunk_cnt[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(64) void k_pf_plan(uint64_t nchunks, uint32_t bpk, uint64_t cap, uint64_t *bloom_len,
+                                                PrefixWs w) {
+    if (threadIdx.x) return;
+    uint64_t h = 0;
+    for (uint64_t c = 0; c < nchunks; c++) h += w.chunk_cnt[c];
+    const uint32_t bits = (uint32_t)h * bpk;  // key_hashes.len() as u32 (filter.rs:65-69)
+    const uint64_t fb = bits / 8u + (bits % 8u != 0);
+    const uint64_t m = fb * 8;
+    w.plan[0] = h;
+    w.plan[1] = fb;
+    w.plan[2] = m;
+    w.plan[3] = m ? ~0ull / m + 1 : 0;
+    if (fb > cap) w.plan[4] = 1;
+    *bloom_len = w.plan[4] ? ~0ull : fb;  // ~0: a prefix longer than its key, or the bitmap too small
+}
+
+__global__ __launch_bounds__(256) void k_pf_zero(uint8_t *bitmap, uint64_t cap, PrefixWs w) {
+    const uint64_t fb = w.plan[4] ? 0 : w.plan[1];
+    for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; 4 * x < fb && 4 * x < cap;
+         x += (uint64_t)gridDim.x * blockDim.x)
+        ((uint32_t *)bitmap)[x] = 0;
+}
+
+SDB_DEV void pf_set_hash(uint32_t *bm, uint64_t h, uint32_t k, uint32_t m, uint64_t mmod) {
+    const uint32_t h0 = fastmod_u32((uint32_t)h, mmod, m), d0 = fastmod_u32((uint32_t)(h >> 32), mmod, m);
+    probes_hd(h0, d0, k, m, [&](uint32_t p) { atomicOr(bm + (p >> 5), 1u << (p & 31)); });
+}
+
+__global__ __launch_bounds__(256) void k_pf_set(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
+                                                PrefixSpec ps, uint32_t k, uint8_t *bitmap, PrefixWs w) {
+    if (w.plan[4]) return;
+    const uint32_t m = (uint32_t)w.plan[2];
+    const uint64_t mmod = w.plan[3];
+    if (!m) return;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t ko = key_off[i];
+        const uint32_t kl = (uint32_t)(key_off[i + 1] - ko);
+        if (w.is_new[i]) {
+            const int64_t pl = pf_len(ps, key_bytes + ko, kl, i);
+            pf_set_hash((uint32_t *)bitmap, siphash13(key_bytes + ko, (uint64_t)pl), k, m, mmod);
+        }
+        if (ps.whole) pf_set_hash((uint32_t *)bitmap, siphash13(key_bytes + ko, kl), k, m, mmod);
+    }
+}
+
+uint64_t prefix_workspace_bytes(uint64_t n) {
+    const uint64_t nc = (n + kPfChunk - 1) / kPfChunk + 1;
+    return 3 * ((8 * nc + 255) & ~255ull) + ((n + 256) & ~255ull) + 256;
+}
+static PrefixWs prefix_ws(void *ws, uint64_t n) {
+    const uint64_t nc = (n + kPfChunk - 1) / kPfChunk + 1, a = (8 * nc + 255) & ~255ull;
+    uint8_t *b = (uint8_t *)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
+    PrefixWs w;
+    w.plan = (uint64_t *)b;
+    w.chunk_last = (int64_t *)(b + 256);
+    w.prev_last = (int64_t *)(b + 256 + a);
+    w.chunk_cnt = (uint64_t *)(b + 256 + 2 * a);
+    w.is_new = b + 256 + 3 * a;
+    return w;
+}
+
+hipError_t launch_bloom_prefix(const uint8_t *key_bytes, const uint64_t *key_off, const int32_t *lens, uint64_t n,
+                               uint32_t bpk, uint32_t kind, uint32_t arg, uint32_t whole, uint8_t *bitmap, uint64_t cap,
+                               uint64_t *bloom_len, void *ws, hipStream_t st) {
+    PrefixSpec ps{kind, arg, whole, 0, lens};
+    PrefixWs w = prefix_ws(ws, n);
+    const uint64_t nc = (n + kPfChunk - 1) / kPfChunk;
+    hipError_t e = hipMemsetAsync(w.plan, 0, 64, st);
+    if (e != hipSuccess) return e;
+    const uint32_t k = (uint32_t)((float)bpk * 0.69f);  // optimal_num_probes (filter.rs:235-239)
+    if (nc) {
+        hipLaunchKernelGGL(k_pf_last, dim3((uint32_t)nc), dim3(kPfChunk), 0, st, key_bytes, key_off, n, ps, w);
+        hipLaunchKernelGGL(k_pf_prev, dim3(1), dim3(1024), 0, st, nc, w);
+        hipLaunchKernelGGL(k_pf_count, dim3((uint32_t)nc), dim3(kPfChunk), 0, st, key_bytes, key_off, n, ps, w);
+    }
+    hipLaunchKernelGGL(k_pf_plan, dim3(1), dim3(64), 0, st, nc, bpk, cap, bloom_len, w);
+    uint64_t zb = (cap / 4 + 255) / 256;
+    zb = zb < 1 ? 1 : (zb > 8192 ? 8192 : zb);
+    hipLaunchKernelGGL(k_pf_zero, dim3((uint32_t)zb), dim3(256), 0, st, bitmap, cap, w);
+    if (n) {
+        uint64_t sb = (n + 255) / 256;
+        sb = sb > 65536 ? 65536 : sb;
+        hipLaunchKernelGGL(k_pf_set, dim3((uint32_t)sb), dim3(256), 0, st, key_bytes, key_off, n, ps, k, bitmap, w);
+    }
+    return hipGetLastError();
+}
+
+// Filter::might_match (filter.rs:149-175)
+__global__ __launch_bounds__(256) void k_bloom_match(const uint8_t *bitmap, uint64_t bytes, uint32_t k, uint32_t whole,
+                                                     PrefixSpec ps, const uint8_t *key_bytes, const uint64_t *key_off,
+                                                     const uint8_t *is_prefix, uint64_t n, uint8_t *result) {
+    const uint32_t m = (uint32_t)(bytes * 8);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t ko = key_off[i];
+        const uint32_t kl = (uint32_t)(key_off[i + 1] - ko);
+        const bool pfx = is_prefix && is_prefix[i];
+        int64_t len = -1;
+        if (!pfx && whole) len = kl;
+        else if (ps.kind != SDB_PREFIX_NONE) len = pf_len(ps, key_bytes + ko, kl, i);
+        uint8_t r = 1;  // nothing to probe: no false negative
+        if (len >= 0) {
+            r = 0;
+            if (m) {  // might_contain: an empty bitmap answers false
+                r = 1;
+                const uint64_t h = siphash13(key_bytes + ko, (uint64_t)len);
+                for_each_probe(h, k, m, [&](uint32_t p) {
+                    if (!((bitmap[p >> 3] >> (p & 7)) & 1u)) {
+                        r = 0;
+                        return false;
+                    }
+                    return true;
+                });
+            }
+        }
+        result[i] = r;
+    }
+}
+
+hipError_t launch_bloom_match(const uint8_t *bitmap, uint64_t bytes, uint32_t k, uint32_t whole, uint32_t kind,
+                              uint32_t arg, const uint8_t *key_bytes, const uint64_t *key_off, const uint8_t *is_prefix,
+                              const int32_t *qlens, uint64_t n, uint8_t *result, hipStream_t st) {
+    if (!n) return hipSuccess;
+    PrefixSpec ps{kind, arg, whole, 0, qlens};
+    uint64_t b = (n + 255) / 256;
+    b = b > 65536 ? 65536 : b;
+    hipLaunchKernelGGL(k_bloom_match, dim3((uint32_t)b), dim3(256), 0, st, bitmap, bytes, k, whole, ps, key_bytes, key_off,
+                       is_prefix, n, result);
+    return hipGetLastError();
+}
+
+}  // namespace sdb

@@ -118,6 +118,7 @@ struct EncodeArgs {
     sdb_sst_summary *summary;
     uint64_t bloom_len;
     uint32_t num_probes, filter_built;
+    const uint64_t *bloom_len_dev;  // prefix-extractor filter: the device-counted length (~0: error)
 };
 
 // Workspace layout for n entries (all offsets 256-byte aligned).  Everything up to `bloom_rep` depends
@@ -126,7 +127,7 @@ struct EncodeArgs {
 struct EncodeWorkspace {
     uint64_t lcp, szr, sznr, hd, row_scratch, next, bbytes, tab_exit, tab_cnt, tab_bytes;
     uint64_t anchor_e, anchor_blk, anchor_byte, err, wmax, slow_count, slow_list, desc, stat_part, wmax_part, bloom_rep;
-    uint64_t err_part, done, gtab_exit, gtab_cnt, gtab_bytes, mode;
+    uint64_t err_part, done, gtab_exit, gtab_cnt, gtab_bytes, mode, blen;
     uint64_t total;
 };
 uint64_t bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes);
@@ -168,7 +169,8 @@ __host__ __device__ inline EncodeWorkspace encode_workspace_offsets(uint64_t n, 
     w.gtab_cnt = take(4 * (nc * kSegLook + 1));
     w.gtab_bytes = take(8 * (nc * kSegLook + 1));
     w.mode = take(4);
-    w.bloom_rep = off;  // bloom slots (host-sized) last
+    w.blen = take(8);   // prefix-extractor filters: the filter length the device counted
+    w.bloom_rep = off;  // bloom slots or the prefix filter's scratch (host-sized) last
     w.total = off;
     return w;
 }
@@ -177,6 +179,13 @@ inline EncodeWorkspace encode_workspace_layout(uint64_t n, uint64_t filter_bytes
     w.total = w.bloom_rep + ((filter_bytes ? encode_bloom_workspace_bytes(n, num_probes, filter_bytes) : 0) + 255) / 256 * 256;
     return w;
 }
+uint64_t prefix_workspace_bytes(uint64_t n);
+hipError_t launch_bloom_prefix(const uint8_t *key_bytes, const uint64_t *key_off, const int32_t *lens, uint64_t n,
+                               uint32_t bpk, uint32_t kind, uint32_t arg, uint32_t whole, uint8_t *bitmap, uint64_t cap,
+                               uint64_t *bloom_len, void *ws, hipStream_t st);
+hipError_t launch_bloom_match(const uint8_t *bitmap, uint64_t bytes, uint32_t k, uint32_t whole, uint32_t kind,
+                              uint32_t arg, const uint8_t *key_bytes, const uint64_t *key_off, const uint8_t *is_prefix,
+                              const int32_t *qlens, uint64_t n, uint8_t *result, hipStream_t st);
 
 // ------------------------------------------------------------------------------------------------
 // A launch set: up to kMaxSsts independent SSTs with the same SsTableFormat knobs encoded by ONE
@@ -209,6 +218,7 @@ struct SstSlot {
     uint8_t *ws;              // this SST's workspace (256-byte aligned)
     uint32_t num_probes, filter_built, bloom_fused, has_filter_ws;  // has_filter_ws: hd in the layout
     uint32_t nchunks, nfacts, group, slot_cap;
+    uint32_t prefix_bloom, pad2;  // the filter is a prefix-extractor one: its length is device-counted
     BloomPlan bpl;            // fused bloom plan (bloom_fused)
 };
 struct SstSet {
@@ -290,6 +300,7 @@ __host__ __device__ inline EncodeArgs make_args(const SstSet &P, uint32_t i) {
     a.bloom_len = s.bloom_len;
     a.num_probes = s.num_probes;
     a.filter_built = s.filter_built;
+    a.bloom_len_dev = s.prefix_bloom ? (uint64_t *)(b + w.blen) : nullptr;
     return a;
 }
 

@@ -1431,7 +1431,18 @@ SDB_DEV void finish_summary(const EncodeArgs &a) {
     sdb_sst_summary *s = a.summary;
     const unsigned long long e = atomicOr(a.err, 0ull);  // device-scope read of the error word
     s->max_block_entries = *a.wmax;
-    s->bloom_len = a.bloom_len;
+    uint64_t bl = a.bloom_len;
+    if (a.bloom_len_dev) {
+        bl = *a.bloom_len_dev;
+        if (bl == ~0ull) {  // a prefix longer than its key (the reference asserts) or a short bitmap
+            bl = 0;
+            if (e == ~0ull) {
+                s->status = SDB_INVALID_ARGUMENT;
+                s->first_error_entry = 0;
+            }
+        }
+    }
+    s->bloom_len = bl;
     s->num_probes = a.num_probes;
     s->filter_built = a.filter_built;
     if (e != ~0ull) {

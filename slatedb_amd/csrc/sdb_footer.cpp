@@ -197,7 +197,7 @@ extern "C" uint64_t sdb_sst_footer_bound(const sdb_footer_in *in) {
     const uint64_t nb = in->num_blocks;
     const uint64_t keys = nb && in->first_key_off ? in->first_key_off[nb] - in->first_key_off[0] : 0;
     uint64_t b = 256 + in->first_entry_len + in->last_entry_len;  // SsTableInfo, crcs, trailer
-    if (in->has_filter) b += 32 + in->bloom_len;                  // composite filter block
+    if (in->has_filter) b += 32 + in->bloom_len + (in->filter_name ? strlen(in->filter_name) : 3);  // composite filter block
     b += 64 + keys + 48 * nb;                                      // index: key, len, pads, BlockMeta, vtable, slot
     if (in->stats) b += 128 + 32 * nb;                             // stats: BlockStats tables + vector
     return b;
@@ -221,12 +221,13 @@ extern "C" sdb_status sdb_sst_footer(const sdb_footer_in *in, uint8_t *out, uint
     uint64_t filter_len = 0;
     if (in->has_filter) {
         std::vector<uint8_t> c;
-        c.reserve(in->bloom_len + 17);
+        const char *name = in->filter_name ? in->filter_name : "_bf";
+        const size_t nl = strlen(name);
+        if (nl > 0xFFFF) return SDB_INVALID_ARGUMENT;
+        c.reserve(in->bloom_len + 14 + nl);
         put_be(c, 1, 2);
-        put_be(c, 3, 2);
-        c.push_back('_');
-        c.push_back('b');
-        c.push_back('f');
+        put_be(c, nl, 2);
+        c.insert(c.end(), (const uint8_t *)name, (const uint8_t *)name + nl);
         put_be(c, in->bloom_len + 2, 8);
         put_be(c, in->num_probes, 2);
         if (in->bloom_len) c.insert(c.end(), in->bloom, in->bloom + in->bloom_len);

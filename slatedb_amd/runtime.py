@@ -65,9 +65,58 @@ def require_device():
 
 
 def params(block_size=4096, sst_version=2, restart_interval=16, bloom_bits_per_key=10,
-           min_filter_keys=0, sst_type=_abi.SST_COMPACTED):
+           min_filter_keys=0, sst_type=_abi.SST_COMPACTED, prefix_kind=0, prefix_arg=0, no_whole_key=0):
     return _abi.SstParams(block_size, sst_version, restart_interval, bloom_bits_per_key,
-                          min_filter_keys, sst_type)
+                          min_filter_keys, sst_type, prefix_kind, prefix_arg, no_whole_key)
+
+
+def filter_name(prm, extractor_name=None):
+    """FilterPolicy::name of BloomFilterPolicy (filter_policy.rs:237-250): "_bf[:p=<extractor>][:wh=0]"."""
+    name = "_bf"
+    if prm.prefix_kind:
+        name += ":p=" + (extractor_name or {1: "fixed%d" % prm.prefix_arg, 2: "delim%d" % prm.prefix_arg,
+                                            3: "custom"}[prm.prefix_kind])
+    if prm.no_whole_key:
+        name += ":wh=0"
+    return name.encode()
+
+
+def bloom_build_prefix_device(key_bytes, key_off, n, bpk, kind, arg=0, whole=True, prefix_len=None, stream=None):
+    """sdb_bloom_build_prefix over device tensors -> the bitmap (torch uint8, device-counted length)."""
+    import torch
+    dev = key_bytes.device
+    cap = lib().sdb_bloom_filter_bytes(2 * n, bpk) + 16
+    bm = torch.empty((cap + 3) // 4 * 4, dtype=torch.uint8, device=dev)
+    ln = torch.zeros(1, dtype=torch.int64, device=dev)
+    wsb = lib().sdb_bloom_prefix_workspace_bytes(n)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    sp = None if stream is None else (stream.cuda_stream if hasattr(stream, "cuda_stream") else stream)
+    st = lib().sdb_bloom_build_prefix(key_bytes.data_ptr(), key_off.data_ptr(),
+                                      None if prefix_len is None else prefix_len.data_ptr(), n, bpk, kind, arg,
+                                      int(whole), bm.data_ptr(), cap, ln.data_ptr(), ws.data_ptr(), wsb, sp)
+    if st:
+        raise SdbError(st, "sdb_bloom_build_prefix")
+    torch.cuda.synchronize()
+    L = int(ln.item())
+    if L < 0:
+        raise SdbError(_abi.SDB_INVALID_ARGUMENT, "sdb_bloom_build_prefix (prefix longer than its key)")
+    return bm[:L]
+
+
+def might_match_device(bitmap, num_probes, whole, kind, arg, key_bytes, key_off, n, is_prefix=None,
+                       query_prefix_len=None, stream=None):
+    """sdb_bloom_might_match over device tensors -> torch uint8 results."""
+    import torch
+    res = torch.zeros(max(n, 1), dtype=torch.uint8, device=key_bytes.device)
+    sp = None if stream is None else (stream.cuda_stream if hasattr(stream, "cuda_stream") else stream)
+    st = lib().sdb_bloom_might_match(bitmap.data_ptr() if bitmap.numel() else None, bitmap.numel(), num_probes,
+                                     int(whole), kind, arg, key_bytes.data_ptr(), key_off.data_ptr(),
+                                     None if is_prefix is None else is_prefix.data_ptr(),
+                                     None if query_prefix_len is None else query_prefix_len.data_ptr(), n,
+                                     res.data_ptr(), sp)
+    if st:
+        raise SdbError(st, "sdb_bloom_might_match")
+    return res[:n]
 
 
 def _u8(ptr, n):
@@ -128,7 +177,7 @@ class EncodedSst:
         return comp + struct.pack(">I", zlib.crc32(comp))
 
 
-def sst_footer(batch, enc, sst_version=2, sst_type=_abi.SST_COMPACTED):
+def sst_footer(batch, enc, sst_version=2, sst_type=_abi.SST_COMPACTED, filter_name=None):
     """Footer bytes after the data section (sdb_sst_footer; EncodedSsTableFooterBuilder::build,
     format/sst.rs:383-487).  `enc` is an encode result with host arrays (EncodedSst, the
     DeviceSstOutput.to_host() dict wrapped by `_FooterView`, or anything with data/block_off/
@@ -162,7 +211,8 @@ def sst_footer(batch, enc, sst_version=2, sst_type=_abi.SST_COMPACTED):
                        int(sm.data_len), nb, boff.ctypes.data, fk.ctypes.data, fko.ctypes.data,
                        first, len(first or b""), last, len(last or b""),
                        None if wal else C.addressof(sm), bst.ctypes.data if len(bst) else None,
-                       bloom.ctypes.data if len(bloom) else None, 0 if wal else int(sm.bloom_len))
+                       bloom.ctypes.data if len(bloom) else None, 0 if wal else int(sm.bloom_len),
+                       filter_name)
     n = C.c_uint64(0)
     cap = lib().sdb_sst_footer_bound(C.byref(fi))
     out = np.empty(max(cap, 1), np.uint8)
@@ -172,9 +222,9 @@ def sst_footer(batch, enc, sst_version=2, sst_type=_abi.SST_COMPACTED):
     return out[:n.value].tobytes()
 
 
-def sst_object(batch, enc, sst_version=2, sst_type=_abi.SST_COMPACTED):
+def sst_object(batch, enc, sst_version=2, sst_type=_abi.SST_COMPACTED, filter_name=None):
     """The whole SST object (data section ++ footer) that write_sst stores."""
-    return np.asarray(enc.data, np.uint8).tobytes() + sst_footer(batch, enc, sst_version, sst_type)
+    return np.asarray(enc.data, np.uint8).tobytes() + sst_footer(batch, enc, sst_version, sst_type, filter_name)
 
 
 class Encoder:

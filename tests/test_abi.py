@@ -40,6 +40,9 @@ def test_exports_every_declared_symbol(lib):
 
 
 STRUCTS = {
+    "sdb_sst_view": _abi.SstView,
+    "sdb_lookup_out": _abi.LookupOut,
+    "sdb_footer_in": _abi.FooterIn,
     "sdb_kv_batch": _abi.KvBatch,
     "sdb_sst_params": _abi.SstParams,
     "sdb_sst_summary": _abi.SstSummary,
@@ -150,7 +153,8 @@ def rust_layout(structs, name):
 def test_integration_rust_structs_match_header():
     structs = rust_structs(os.path.join(ROOT, "INTEGRATION.md"))
     want = ["sdb_kv_batch", "sdb_sst_params", "sdb_sst_summary", "sdb_sst_out", "sdb_sst_host_result",
-            "sdb_footer_in", "sdb_decode_summary", "sdb_decoded_out", "sdb_decode_host_result"]
+            "sdb_footer_in", "sdb_decode_summary", "sdb_decoded_out", "sdb_decode_host_result", "sdb_sst_view",
+            "sdb_lookup_out"]
     missing = [w for w in want if w not in structs]
     assert not missing, missing
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "%s"' % HDR, "int main(void){"]
@@ -180,3 +184,13 @@ def test_integration_rust_structs_match_header():
             if parts:
                 cfields += [re.findall(r"(\w+)\s*$", x)[0] for x in parts]
         assert [f for f, _ in structs[cname]] == cfields, (cname, [f for f, _ in structs[cname]], cfields)
+
+
+def test_integration_declares_every_entry_point():
+    """Every function of include/slatedb_amd.h (diagnostics aside) has a Rust declaration in INTEGRATION.md."""
+    txt = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    code = "\n".join(re.findall(r"```rust\n(.*?)```", txt, flags=re.S))
+    declared = set(re.findall(r"pub fn (sdb_\w+)\s*\(", code))
+    want = {f for f in header_functions() if not f.startswith("sdb_diag_")}
+    missing = sorted(want - declared)
+    assert not missing, missing
