@@ -66,6 +66,7 @@ typedef enum sdb_status {
     SDB_UNSUPPORTED = 7,            /* compression / block transformer (not on this path) */
     SDB_INVALID_ARGUMENT = 8,       /* bad kind byte, capacity too small, NULL pointer, ... */
     SDB_CORRUPT_BLOCK = 9,          /* block bytes that the reference would panic on while parsing */
+    SDB_MERGE_OPERATOR_MISSING = 10,/* SlateDBError::MergeOperatorMissing (merge_operator.rs:213-223) */
     SDB_DEVICE_ERROR = 100          /* no HIP device / launch failure */
 } sdb_status;
 
@@ -320,6 +321,112 @@ uint64_t sdb_sst_lookup_workspace_bytes(uint64_t num_blocks, uint64_t nkeys);
 sdb_status sdb_sst_lookup(const sdb_sst_view *sst, const uint8_t *key_bytes, const uint64_t *key_off,
                           uint64_t nkeys, int32_t descending, const sdb_lookup_out *out,
                           void *workspace, uint64_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Compaction (device): the output side of CompactionExecutor::run_subcompaction_merge
+ * (compactor_executor.rs:386-410, 818-871) over decoded inputs:
+ *   1. MergeIterator over the sorted runs, dedup off (merge_iterator.rs:56-69): key ascending, seq
+ *      descending; equal (key, seq) pairs (which the store never writes) in run order;
+ *   2. MergeOperatorRequiredIterator (merge_operator.rs:213-223): a merge operand fails the job with
+ *      SDB_MERGE_OPERATOR_MISSING, unless `merge_operands` passes operands on unmerged;
+ *   3. RetentionIterator (retention_iterator.rs:91-204, 381-398): per key, versions newest first,
+ *      a later equal-seq version replacing an earlier one (BTreeMap::insert); expired merges are
+ *      skipped, expired values / tombstones become tombstones without expire_ts; the walk stops
+ *      after the first non-merge version outside both the seq and the time window; trailing
+ *      tombstones are dropped when filter_tombstone;
+ *   4. output SSTs cut where the bytes of the blocks the writer finished exceed max_sst_size: the
+ *      entry whose add finished that block closes the SST as its one-entry tail block
+ *      (compactor_executor.rs:833-858, sst_builder.rs:224-325); every SST then encodes as above.
+ * sdb_merge_runs and sdb_sst_cuts are asynchronous on the caller's stream; sdb_compactor_run
+ * orchestrates the whole job (two host synchronisations: the merged entry count, the cut list).
+ * ------------------------------------------------------------------------------------------- */
+/* One sorted input run in the layout sdb_decode_blocks produces (a decoded SST, or a sorted run's
+ * SSTs decoded into one output): value i = val_base[val_off[i] .. val_off[i] + val_len[i]). */
+typedef struct sdb_run {
+    uint64_t n;
+    const uint8_t *key_arena;
+    const uint64_t *key_off;        /* n+1 */
+    const uint8_t *val_base;
+    const uint64_t *val_off;        /* n */
+    const uint32_t *val_len;        /* n */
+    const uint64_t *seq;            /* n */
+    const uint8_t *flags;           /* n: RowFlags (SDB_FLAG_*) */
+    const int64_t *create_ts;       /* n: valid iff flags & HAS_CREATE_TS (NULL: none anywhere) */
+    const int64_t *expire_ts;       /* n: valid iff flags & HAS_EXPIRE_TS (NULL: none anywhere) */
+} sdb_run;
+enum { SDB_MAX_RUNS = 32 };
+typedef struct sdb_retention {
+    uint64_t min_seq;               /* retention_min_seq: the walk continues past seq > min_seq
+                                       (retention_iterator.rs:188-190) when has_min_seq */
+    uint64_t time_seq;              /* retention_timeout resolved on the host: the walk continues past
+                                       seq >= time_seq when has_time_window (create_sys_ts + timeout > now,
+                                       :171-187; SequenceTracker::find_ts(.., RoundUp) is monotone in seq,
+                                       so the seqs inside the window are an up-set; 0 = every seq) */
+    int64_t compaction_start_ts;    /* compaction_clock_tick: expire_ts <= this has expired */
+    uint8_t has_min_seq, has_time_window;
+    uint8_t filter_tombstone;       /* is_dest_last_run */
+    uint8_t merge_operands;         /* 0: MergeOperatorRequiredIterator; 1: operands pass unmerged */
+    uint32_t pad;
+} sdb_retention;
+typedef struct sdb_merge_summary {
+    uint64_t num_in;                /* entries of all runs */
+    uint64_t num_out;               /* entries after retention */
+    uint64_t key_bytes, val_bytes;  /* bytes written to the output arenas */
+    uint64_t expired_values;        /* RetentionMetrics::expired_entries_purged_value */
+    uint64_t expired_merges;        /* RetentionMetrics::expired_entries_purged_merge */
+    int32_t status;                 /* SDB_OK | SDB_MERGE_OPERATOR_MISSING | SDB_INVALID_ARGUMENT (a run
+                                       out of order: first_error_entry = its global index) */
+    uint32_t pad;
+    uint64_t first_error_entry;     /* merged position (or run entry) that raised status */
+} sdb_merge_summary;
+/* Merged, retained stream: an sdb_kv_batch (n = summary.num_out) in caller-owned device memory.
+ * Capacities: cap_entries >= sum n, key_cap >= sum key bytes, val_cap >= sum value bytes. */
+typedef struct sdb_merged_out {
+    uint8_t *key_bytes;
+    uint64_t key_cap;
+    uint64_t *key_off;              /* cap_entries + 1 */
+    uint8_t *val_bytes;
+    uint64_t val_cap;
+    uint64_t *val_off;              /* cap_entries + 1 */
+    uint8_t *kind;
+    uint64_t *seq;
+    int64_t *create_ts;
+    int64_t *expire_ts;
+    uint8_t *ts_mask;
+    uint64_t cap_entries;
+    sdb_merge_summary *summary;     /* device-writable */
+} sdb_merged_out;
+uint64_t sdb_merge_runs_workspace_bytes(const sdb_run *runs, uint32_t nruns);
+sdb_status sdb_merge_runs(const sdb_run *runs, uint32_t nruns, const sdb_retention *retention,
+                          const sdb_merged_out *out, void *workspace, uint64_t workspace_bytes, void *stream);
+/* SST boundaries of a compaction output stream: cut_start[0..*num_ssts] (device) are entry indices
+ * with cut_start[0] = 0 and cut_start[*num_ssts] = n; SST i = entries [cut_start[i], cut_start[i+1]).
+ * cut_cap >= n + 1 always suffices.  params: the output format (block size, restart interval). */
+uint64_t sdb_sst_cuts_workspace_bytes(uint64_t n, const sdb_sst_params *params);
+sdb_status sdb_sst_cuts(const sdb_kv_batch *batch, const sdb_sst_params *params, uint64_t max_sst_size,
+                        uint64_t *cut_start, uint64_t cut_cap, uint64_t *num_ssts, void *workspace,
+                        uint64_t workspace_bytes, void *stream);
+
+/* A compaction job on the device: merge + retention + cuts + encode of every output SST, with the
+ * outputs in the handle's device memory (valid until the next run or destroy). */
+typedef struct sdb_compactor sdb_compactor;
+typedef struct sdb_compacted_sst {
+    uint64_t entry_start, entry_end;   /* range of the merged stream (sdb_compactor_merged) */
+    const uint8_t *data;               /* device: the SST's data section */
+    const uint64_t *block_off;         /* device: num_blocks + 1 */
+    const uint32_t *block_first_entry; /* device: num_blocks + 1 (relative to entry_start) */
+    const uint32_t *index_key_len;     /* device: num_blocks */
+    const uint16_t *block_stats;       /* device: 3 per block */
+    const uint8_t *bloom;              /* device: summary.bloom_len bytes */
+    sdb_sst_summary summary;           /* host copy */
+} sdb_compacted_sst;
+sdb_compactor *sdb_compactor_create(int device);
+void sdb_compactor_destroy(sdb_compactor *c);
+sdb_status sdb_compactor_run(sdb_compactor *c, const sdb_run *runs, uint32_t nruns, const sdb_retention *retention,
+                             const sdb_sst_params *params, uint64_t max_sst_size, void *stream, uint32_t *num_ssts);
+sdb_status sdb_compactor_sst(const sdb_compactor *c, uint32_t i, sdb_compacted_sst *out);
+/* The merged stream of the last run (device batch view) and its summary (host copy). */
+sdb_status sdb_compactor_merged(const sdb_compactor *c, sdb_kv_batch *batch, sdb_merge_summary *summary);
 
 /* ---------------------------------------------------------------------------------------------
  * SST footer (host): everything after the data section, so data ++ footer is the whole SST object

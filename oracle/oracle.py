@@ -50,6 +50,8 @@ def _load():
         "orc_bloom_might_match": (C.c_int, [V, C.c_uint64, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, V,
                                             C.c_size_t, C.c_int, C.c_int64]),
         "orc_prefix_len": (C.c_int64, [C.c_uint32, C.c_uint32, V, C.c_size_t, C.c_int64]),
+        "orc_merge_runs": (C.c_int, [P(_abi.Run), C.c_uint32, P(_abi.Retention), P(_abi.MergedOut)]),
+        "orc_sst_cuts": (C.c_int, [P(_abi.KvBatch), P(_abi.SstParams), C.c_uint64, V, C.c_uint64, P(C.c_uint64)]),
     }
     for k, (r, a) in sig.items():
         f = getattr(lib, k)
@@ -338,3 +340,52 @@ def sst_lookup(data, block_off, index_keys, index_key_off, keys, descending=Fals
     for f, _ in LOOKUP_FIELDS:
         setattr(r, f, getattr(r, f)[:n])
     return r
+
+
+def retention(min_seq=None, time_seq=None, compaction_start_ts=0, filter_tombstone=False, merge_operands=False):
+    """sdb_retention: min_seq = retention_min_seq (None: no seq window); time_seq = the first seq inside the
+    retention_timeout window (None: no time window, 0: every seq)."""
+    return _abi.Retention(min_seq or 0, time_seq or 0, compaction_start_ts, int(min_seq is not None),
+                          int(time_seq is not None), int(bool(filter_tombstone)), int(bool(merge_operands)), 0)
+
+
+def merge_runs(runs, ret):
+    """orc_merge_runs over host Runs -> (Batch of the merged, retained stream, MergeSummary)."""
+    from slatedb_amd.batch import Batch
+    total = sum(r.n for r in runs)
+    kcap = sum(int(r.key_off[-1]) for r in runs) + 1
+    vcap = sum(int(r.val_len.sum()) for r in runs) + 1
+    kb, vb = np.zeros(kcap, np.uint8), np.zeros(vcap, np.uint8)
+    ko, vo = np.zeros(total + 1, np.uint64), np.zeros(total + 1, np.uint64)
+    kind, seq = np.zeros(max(total, 1), np.uint8), np.zeros(max(total, 1), np.uint64)
+    cts, ets, mask = np.zeros(max(total, 1), np.int64), np.zeros(max(total, 1), np.int64), np.zeros(max(total, 1), np.uint8)
+    sm = _abi.MergeSummary()
+    out = _abi.MergedOut(kb.ctypes.data, kcap, ko.ctypes.data, vb.ctypes.data, vcap, vo.ctypes.data, kind.ctypes.data,
+                         seq.ctypes.data, cts.ctypes.data, ets.ctypes.data, mask.ctypes.data, total, C.addressof(sm))
+    cr = (_abi.Run * max(len(runs), 1))(*[r.to_ctypes() for r in runs])
+    lib().orc_merge_runs(cr, len(runs), C.byref(ret), C.byref(out))
+    n = sm.num_out
+    b = Batch(kb[:sm.key_bytes], ko[:n + 1], vb[:sm.val_bytes], vo[:n + 1], kind[:n], seq[:n], cts[:n], ets[:n], mask[:n])
+    return b, sm
+
+
+def sst_cuts(batch, prm, max_sst_size):
+    """orc_sst_cuts -> (status, list of SST start entries + [n])."""
+    cap = batch.n + 2
+    cuts = np.zeros(cap, np.uint64)
+    ns = C.c_uint64(0)
+    kb = batch.to_ctypes()
+    st = lib().orc_sst_cuts(C.byref(kb), C.byref(prm), max_sst_size, cuts.ctypes.data, cap, C.byref(ns))
+    return st, [int(x) for x in cuts[:ns.value + 1]] if ns.value else []
+
+
+def compact(runs, ret, prm, max_sst_size):
+    """The compaction output side: merge + retention, cuts, then encode_sst per output SST.
+    Returns (merged Batch, MergeSummary, cuts, [SstResult])."""
+    merged, sm = merge_runs(runs, ret)
+    if sm.status:
+        return merged, sm, [], []
+    st, cuts = sst_cuts(merged, prm, max_sst_size)
+    assert st == 0, st
+    ssts = [encode_sst(merged.slice(cuts[i], cuts[i + 1]), prm) for i in range(len(cuts) - 1)]
+    return merged, sm, cuts, ssts

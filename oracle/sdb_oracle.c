@@ -1241,3 +1241,183 @@ sdb_status orc_sst_lookup(const sdb_sst_view *v, const uint8_t *key_bytes, const
     }
     return SDB_OK;
 }
+
+/* ------------------------------------------------------------------------------------------- */
+/* Compaction output side (compactor_executor.rs:386-410, 818-871)                              */
+/* ------------------------------------------------------------------------------------------- */
+/* MergeIteratorHeapEntry::cmp (merge_iterator.rs:55-69), ascending: key, then seq descending; the
+ * heap's order between equal (key, seq) heads is unspecified, the restatement takes run order. */
+static int run_before(const sdb_run *ra, uint64_t ia, uint32_t a, const sdb_run *rb, uint64_t ib, uint32_t b) {
+    const uint8_t *ka = ra->key_arena + ra->key_off[ia], *kb = rb->key_arena + rb->key_off[ib];
+    int c = lex_cmp(ka, (size_t)(ra->key_off[ia + 1] - ra->key_off[ia]), kb, (size_t)(rb->key_off[ib + 1] - rb->key_off[ib]));
+    if (c) return c < 0;
+    if (ra->seq[ia] != rb->seq[ib]) return ra->seq[ia] > rb->seq[ib];
+    return a < b;
+}
+
+typedef struct { uint32_t r; uint64_t i; } mpos;
+
+static int same_key(const sdb_run *runs, mpos x, mpos y) {
+    const sdb_run *a = &runs[x.r], *b = &runs[y.r];
+    size_t na = (size_t)(a->key_off[x.i + 1] - a->key_off[x.i]), nb = (size_t)(b->key_off[y.i + 1] - b->key_off[y.i]);
+    return na == nb && memcmp(a->key_arena + a->key_off[x.i], b->key_arena + b->key_off[y.i], na) == 0;
+}
+
+sdb_status orc_merge_runs(const sdb_run *runs, uint32_t nruns, const sdb_retention *ret, const sdb_merged_out *out) {
+    sdb_merge_summary *sm = out->summary;
+    memset(sm, 0, sizeof *sm);
+    sm->first_error_entry = UINT64_MAX;
+    uint64_t total = 0;
+    for (uint32_t r = 0; r < nruns; r++) total += runs[r].n;
+    sm->num_in = total;
+    if (total > out->cap_entries) return (sdb_status)(sm->status = SDB_INVALID_ARGUMENT);
+    /* sorted-run precondition (a run out of order: INVALID_ARGUMENT at its global index) */
+    uint64_t base = 0;
+    for (uint32_t r = 0; r < nruns; r++) {
+        for (uint64_t i = 1; i < runs[r].n; i++) {
+            const sdb_run *R = &runs[r];
+            int c = lex_cmp(R->key_arena + R->key_off[i - 1], (size_t)(R->key_off[i] - R->key_off[i - 1]),
+                            R->key_arena + R->key_off[i], (size_t)(R->key_off[i + 1] - R->key_off[i]));
+            if (c > 0 || (c == 0 && R->seq[i - 1] < R->seq[i])) {
+                sm->first_error_entry = base + i;
+                return (sdb_status)(sm->status = SDB_INVALID_ARGUMENT);
+            }
+        }
+        base += runs[r].n;
+    }
+    /* 1. the merged order: repeatedly pop the smallest head (BinaryHeap<Reverse<..>>) */
+    mpos *m = (mpos *)malloc(sizeof(mpos) * (total + 1));
+    uint64_t *head = (uint64_t *)calloc(nruns + 1, sizeof(uint64_t));
+    for (uint64_t p = 0; p < total; p++) {
+        int best = -1;
+        for (uint32_t r = 0; r < nruns; r++) {
+            if (head[r] >= runs[r].n) continue;
+            if (best < 0 || run_before(&runs[r], head[r], r, &runs[best], head[best], (uint32_t)best)) best = (int)r;
+        }
+        m[p].r = (uint32_t)best;
+        m[p].i = head[best]++;
+    }
+    free(head);
+    /* 2. MergeOperatorRequiredIterator: the first merge operand in merged order fails the job */
+    if (!ret->merge_operands)
+        for (uint64_t p = 0; p < total; p++)
+            if (runs[m[p].r].flags[m[p].i] & SDB_FLAG_MERGE_OPERAND) {
+                sm->first_error_entry = p;
+                free(m);
+                return (sdb_status)(sm->status = SDB_MERGE_OPERATOR_MISSING);
+            }
+    /* 3. RetentionIterator per key group: dec 0 drop, 1 keep, 2 keep as a tombstone */
+    uint8_t *dec = (uint8_t *)calloc(total + 1, 1);
+    for (uint64_t g = 0; g < total;) {
+        uint64_t ge = g + 1;
+        while (ge < total && same_key(runs, m[g], m[ge])) ge++;
+        for (uint64_t q = g; q < ge; q++) {
+            const sdb_run *R = &runs[m[q].r];
+            const uint64_t i = m[q].i;
+            /* RetentionBuffer::push: BTreeMap::insert, a later equal-seq version replaces this one */
+            if (q + 1 < ge && runs[m[q + 1].r].seq[m[q + 1].i] == R->seq[i]) continue;
+            const uint8_t f = R->flags[i];
+            const int is_merge = (f & SDB_FLAG_MERGE_OPERAND) != 0;
+            if ((f & SDB_FLAG_HAS_EXPIRE_TS) && R->expire_ts[i] <= ret->compaction_start_ts) {
+                if (is_merge) { sm->expired_merges++; continue; }  /* skip expired merges */
+                sm->expired_values++;
+                dec[q] = 2;
+            } else {
+                dec[q] = 1;
+            }
+            const int cont = (ret->has_time_window && R->seq[i] >= ret->time_seq) ||
+                             (ret->has_min_seq && R->seq[i] > ret->min_seq) || is_merge;
+            if (!cont) break;
+        }
+        if (ret->filter_tombstone) /* pop the tombstones in the tail */
+            for (uint64_t q = ge; q-- > g;) {
+                if (!dec[q]) continue;
+                if (dec[q] == 2 || (runs[m[q].r].flags[m[q].i] & SDB_FLAG_TOMBSTONE)) dec[q] = 0;
+                else break;
+            }
+        g = ge;
+    }
+    /* 4. the output batch */
+    uint64_t n = 0, kb = 0, vb = 0;
+    sdb_status st = SDB_OK;
+    for (uint64_t p = 0; p < total && !st; p++) {
+        if (!dec[p]) continue;
+        const sdb_run *R = &runs[m[p].r];
+        const uint64_t i = m[p].i;
+        const uint8_t f = R->flags[i];
+        const int tomb = dec[p] == 2 || (f & SDB_FLAG_TOMBSTONE);
+        const uint64_t kl = R->key_off[i + 1] - R->key_off[i], vl = tomb ? 0 : R->val_len[i];
+        if (kb + kl > out->key_cap || vb + vl > out->val_cap) { st = SDB_INVALID_ARGUMENT; break; }
+        out->key_off[n] = kb;
+        memcpy(out->key_bytes + kb, R->key_arena + R->key_off[i], kl);
+        kb += kl;
+        out->val_off[n] = vb;
+        if (vl) memcpy(out->val_bytes + vb, R->val_base + R->val_off[i], vl);
+        vb += vl;
+        out->kind[n] = tomb ? SDB_KIND_TOMBSTONE : (f & SDB_FLAG_MERGE_OPERAND) ? SDB_KIND_MERGE : SDB_KIND_VALUE;
+        out->seq[n] = R->seq[i];
+        uint8_t mask = 0;
+        if (f & SDB_FLAG_HAS_CREATE_TS) mask |= SDB_TS_CREATE;
+        if ((f & SDB_FLAG_HAS_EXPIRE_TS) && dec[p] == 1) mask |= SDB_TS_EXPIRE; /* converted: expire_ts None */
+        out->ts_mask[n] = mask;
+        out->create_ts[n] = (mask & SDB_TS_CREATE) ? R->create_ts[i] : 0;
+        out->expire_ts[n] = (mask & SDB_TS_EXPIRE) ? R->expire_ts[i] : 0;
+        n++;
+    }
+    out->key_off[n] = kb;
+    out->val_off[n] = vb;
+    sm->num_out = n;
+    sm->key_bytes = kb;
+    sm->val_bytes = vb;
+    sm->status = st;
+    free(dec);
+    free(m);
+    return st;
+}
+
+/* EncodedSsTableWriter::add per entry (sst_builder.rs:224-260, 284-325) with the compactor's cut
+ * rule (compactor_executor.rs:833-858): bytes_written += the finished block's encoded length (incl.
+ * CRC); past max_sst_size the writer closes, its builder holding only the entry just added. */
+sdb_status orc_sst_cuts(const sdb_kv_batch *batch, const sdb_sst_params *p, uint64_t max_sst_size,
+                        uint64_t *cut_start, uint64_t cap, uint64_t *num_ssts) {
+    blk_t b;
+    memset(&b, 0, sizeof b);
+    b.version = p->sst_version;
+    b.block_size = p->block_size;
+    b.restart_interval = p->sst_version == 2 ? p->restart_interval : 1;
+    uint64_t ns = 0, acc = 0;
+    sdb_status st = SDB_OK;
+    const uint64_t n = batch->n;
+    if (cap < 1) return SDB_INVALID_ARGUMENT;
+    cut_start[0] = 0;
+    vbuf enc = {0};
+    for (uint64_t i = 0; i < n; i++) {
+        entry_t e;
+        if (!get_entry(batch, i, &e)) { st = SDB_INVALID_ARGUMENT; break; }
+        if (!blk_would_fit(&b, &e)) { /* finish_block: its encoded length + 4 bytes of CRC */
+            enc.len = 0;
+            blk_encode(&b, &enc);
+            acc += enc.len + 4;
+            blk_reset(&b);
+        }
+        int r = blk_add(&b, &e);
+        if (r < 0) { st = (sdb_status)(-r); break; }
+        if (acc > max_sst_size) {
+            if (i + 1 < n) {
+                if (ns + 2 > cap) { st = SDB_INVALID_ARGUMENT; break; }
+                cut_start[++ns] = i + 1;
+            }
+            acc = 0;
+            blk_reset(&b);
+        }
+    }
+    if (!st) {
+        if (ns + 2 > cap) st = SDB_INVALID_ARGUMENT;
+        else cut_start[++ns] = n;
+    }
+    *num_ssts = n ? ns : 0;
+    if (!n) cut_start[0] = 0;
+    blk_free(&b);
+    free(enc.p);
+    return st;
+}

@@ -68,6 +68,15 @@ sdb_status orc_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, u
 sdb_status orc_sst_lookup(const sdb_sst_view *sst, const uint8_t *key_bytes, const uint64_t *key_off,
                           uint64_t nkeys, int descending, const sdb_lookup_out *out);
 
+/* Compaction output side over host runs: MergeIterator (merge_iterator.rs:55-69, dedup off) ->
+ * MergeOperatorRequiredIterator (merge_operator.rs:213-223) -> RetentionIterator
+ * (retention_iterator.rs:91-204, 381-398); the same contract as sdb_merge_runs. */
+sdb_status orc_merge_runs(const sdb_run *runs, uint32_t nruns, const sdb_retention *ret, const sdb_merged_out *out);
+/* Output SST boundaries by EncodedSsTableWriter::add and the compactor's max_sst_size rule
+ * (compactor_executor.rs:833-858, sst_builder.rs:224-325); the same contract as sdb_sst_cuts. */
+sdb_status orc_sst_cuts(const sdb_kv_batch *batch, const sdb_sst_params *p, uint64_t max_sst_size,
+                        uint64_t *cut_start, uint64_t cap, uint64_t *num_ssts);
+
 #ifdef __cplusplus
 }
 #endif

@@ -15,12 +15,13 @@ SDB_LIMIT_EXCEEDED = 6
 SDB_UNSUPPORTED = 7
 SDB_INVALID_ARGUMENT = 8
 SDB_CORRUPT_BLOCK = 9
+SDB_MERGE_OPERATOR_MISSING = 10
 SDB_DEVICE_ERROR = 100
 
 STATUS_NAMES = {
     0: "OK", 1: "EMPTY_KEY", 2: "EMPTY_BLOCK", 3: "CHECKSUM_MISMATCH", 4: "INVALID_ROW_FLAGS",
     5: "INVALID_VERSION", 6: "LIMIT_EXCEEDED", 7: "UNSUPPORTED", 8: "INVALID_ARGUMENT",
-    9: "CORRUPT_BLOCK", 100: "DEVICE_ERROR",
+    9: "CORRUPT_BLOCK", 10: "MERGE_OPERATOR_MISSING", 100: "DEVICE_ERROR",
 }
 
 KIND_VALUE, KIND_MERGE, KIND_TOMBSTONE = 0, 1, 2
@@ -139,6 +140,52 @@ class LookupOut(C.Structure):
     ]
 
 
+class Run(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint64), ("key_arena", C.c_void_p), ("key_off", C.c_void_p),
+        ("val_base", C.c_void_p), ("val_off", C.c_void_p), ("val_len", C.c_void_p),
+        ("seq", C.c_void_p), ("flags", C.c_void_p), ("create_ts", C.c_void_p), ("expire_ts", C.c_void_p),
+    ]
+
+
+MAX_RUNS = 32
+U64_MAX = (1 << 64) - 1
+
+
+class Retention(C.Structure):
+    _fields_ = [
+        ("min_seq", C.c_uint64), ("time_seq", C.c_uint64), ("compaction_start_ts", C.c_int64),
+        ("has_min_seq", C.c_uint8), ("has_time_window", C.c_uint8), ("filter_tombstone", C.c_uint8),
+        ("merge_operands", C.c_uint8), ("pad", C.c_uint32),
+    ]
+
+
+class MergeSummary(C.Structure):
+    _fields_ = [
+        ("num_in", C.c_uint64), ("num_out", C.c_uint64), ("key_bytes", C.c_uint64), ("val_bytes", C.c_uint64),
+        ("expired_values", C.c_uint64), ("expired_merges", C.c_uint64),
+        ("status", C.c_int32), ("pad", C.c_uint32), ("first_error_entry", C.c_uint64),
+    ]
+
+
+class MergedOut(C.Structure):
+    _fields_ = [
+        ("key_bytes", C.c_void_p), ("key_cap", C.c_uint64), ("key_off", C.c_void_p),
+        ("val_bytes", C.c_void_p), ("val_cap", C.c_uint64), ("val_off", C.c_void_p),
+        ("kind", C.c_void_p), ("seq", C.c_void_p), ("create_ts", C.c_void_p), ("expire_ts", C.c_void_p),
+        ("ts_mask", C.c_void_p), ("cap_entries", C.c_uint64), ("summary", C.c_void_p),
+    ]
+
+
+class CompactedSst(C.Structure):
+    _fields_ = [
+        ("entry_start", C.c_uint64), ("entry_end", C.c_uint64),
+        ("data", C.c_void_p), ("block_off", C.c_void_p), ("block_first_entry", C.c_void_p),
+        ("index_key_len", C.c_void_p), ("block_stats", C.c_void_p), ("bloom", C.c_void_p),
+        ("summary", SstSummary),
+    ]
+
+
 LOOKUP_FILTERED, LOOKUP_EXHAUSTED, LOOKUP_POSITIONED, LOOKUP_FOUND = 0, 1, 2, 3
 
 SST_COMPACTED, SST_WAL = 0, 1
@@ -177,6 +224,18 @@ SIGNATURES = {
     "sdb_sst_lookup_workspace_bytes": (C.c_uint64, [C.c_uint64, C.c_uint64]),
     "sdb_sst_lookup": (C.c_int, [C.POINTER(SstView), C.c_void_p, C.c_void_p, C.c_uint64, C.c_int32,
                                  C.POINTER(LookupOut), C.c_void_p, C.c_uint64, C.c_void_p]),
+    "sdb_merge_runs_workspace_bytes": (C.c_uint64, [C.POINTER(Run), C.c_uint32]),
+    "sdb_merge_runs": (C.c_int, [C.POINTER(Run), C.c_uint32, C.POINTER(Retention), C.POINTER(MergedOut),
+                                 C.c_void_p, C.c_uint64, C.c_void_p]),
+    "sdb_sst_cuts_workspace_bytes": (C.c_uint64, [C.c_uint64, C.POINTER(SstParams)]),
+    "sdb_sst_cuts": (C.c_int, [C.POINTER(KvBatch), C.POINTER(SstParams), C.c_uint64, C.c_void_p, C.c_uint64,
+                               C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    "sdb_compactor_create": (C.c_void_p, [C.c_int]),
+    "sdb_compactor_destroy": (None, [C.c_void_p]),
+    "sdb_compactor_run": (C.c_int, [C.c_void_p, C.POINTER(Run), C.c_uint32, C.POINTER(Retention),
+                                    C.POINTER(SstParams), C.c_uint64, C.c_void_p, u32p]),
+    "sdb_compactor_sst": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(CompactedSst)]),
+    "sdb_compactor_merged": (C.c_int, [C.c_void_p, C.POINTER(KvBatch), C.POINTER(MergeSummary)]),
     "sdb_sst_footer": (C.c_int, [C.POINTER(FooterIn), C.c_void_p, C.c_uint64, u64p]),
     "sdb_sst_footer_bound": (C.c_uint64, [C.POINTER(FooterIn)]),
     "sdb_encoder_create": (C.c_void_p, [C.c_int, C.POINTER(SstParams)]),

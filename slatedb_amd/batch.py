@@ -120,3 +120,51 @@ class DeviceBatch:
         return _abi.KvBatch(self.n, p(self.key_bytes), p(self.key_off), p(self.val_bytes),
                             p(self.val_off), p(self.kind), p(self.seq), p(self.create_ts),
                             p(self.expire_ts), p(self.ts_mask), p(self.prefix_len))
+
+
+class Run:
+    """A sorted input run of a compaction in the decoded layout (`sdb_run`): value i is
+    val_base[val_off[i]:val_off[i] + val_len[i]], flags are RowFlags (row_codec_v2.rs:67-80)."""
+    __slots__ = ("key_arena", "key_off", "val_base", "val_off", "val_len", "seq", "flags", "create_ts",
+                 "expire_ts")
+
+    def __init__(self, key_arena, key_off, val_base, val_off, val_len, seq, flags, create_ts, expire_ts):
+        self.key_arena = np.ascontiguousarray(key_arena, dtype=np.uint8)
+        self.key_off = np.ascontiguousarray(key_off, dtype=np.uint64)
+        self.val_base = np.ascontiguousarray(val_base, dtype=np.uint8)
+        self.val_off = np.ascontiguousarray(val_off, dtype=np.uint64)
+        self.val_len = np.ascontiguousarray(val_len, dtype=np.uint32)
+        self.seq = np.ascontiguousarray(seq, dtype=np.uint64)
+        self.flags = np.ascontiguousarray(flags, dtype=np.uint8)
+        self.create_ts = np.ascontiguousarray(create_ts, dtype=np.int64)
+        self.expire_ts = np.ascontiguousarray(expire_ts, dtype=np.int64)
+
+    @property
+    def n(self):
+        return len(self.key_off) - 1
+
+    @classmethod
+    def from_batch(cls, b):
+        n = b.n
+        kind = b.kind if b.kind is not None else np.zeros(n, np.uint8)
+        mask = b.ts_mask if b.ts_mask is not None else np.zeros(n, np.uint8)
+        flags = np.where(kind == _abi.KIND_TOMBSTONE, _abi.FLAG_TOMBSTONE,
+                         np.where(kind == _abi.KIND_MERGE, _abi.FLAG_MERGE_OPERAND, 0)).astype(np.uint8)
+        flags |= np.where(mask & _abi.TS_CREATE, _abi.FLAG_HAS_CREATE_TS, 0).astype(np.uint8)
+        flags |= np.where(mask & _abi.TS_EXPIRE, _abi.FLAG_HAS_EXPIRE_TS, 0).astype(np.uint8)
+        vlen = np.diff(b.val_off).astype(np.uint32)
+        vlen[kind == _abi.KIND_TOMBSTONE] = 0
+        zeros = np.zeros(n, np.int64)
+        cts = b.create_ts if b.create_ts is not None else zeros
+        ets = b.expire_ts if b.expire_ts is not None else zeros
+        return cls(b.key_bytes, b.key_off, b.val_bytes, b.val_off[:n], vlen,
+                   b.seq if b.seq is not None else np.zeros(n, np.uint64), flags, cts, ets)
+
+    @classmethod
+    def from_entries(cls, entries):
+        return cls.from_batch(Batch.from_entries(entries))
+
+    def to_ctypes(self):
+        p = lambda a: a.ctypes.data if a.size else None
+        return _abi.Run(self.n, p(self.key_arena), self.key_off.ctypes.data, p(self.val_base), p(self.val_off),
+                        p(self.val_len), p(self.seq), p(self.flags), p(self.create_ts), p(self.expire_ts))

@@ -15,6 +15,7 @@
 #include "../../include/slatedb_amd.h"
 #include "sdb_decode.h"
 #include "sdb_bloom.h"
+#include "sdb_compact.h"
 
 namespace sdb {
 struct LookupArgs {
@@ -92,6 +93,7 @@ const char *sdb_status_name(int s) {
         case SDB_UNSUPPORTED: return "UNSUPPORTED";
         case SDB_INVALID_ARGUMENT: return "INVALID_ARGUMENT";
         case SDB_CORRUPT_BLOCK: return "CORRUPT_BLOCK";
+        case SDB_MERGE_OPERATOR_MISSING: return "MERGE_OPERATOR_MISSING";
         case SDB_DEVICE_ERROR: return "DEVICE_ERROR";
         default: return "UNKNOWN";
     }
@@ -411,6 +413,71 @@ sdb_status sdb_decode_blocks_at(const uint8_t *arena, const uint64_t *block_star
                                 void *workspace, uint64_t workspace_bytes, void *stream) {
     if (nblocks && !block_end) return SDB_INVALID_ARGUMENT;
     return decode_common(arena, block_start, block_end, nblocks, sst_version, out, workspace, workspace_bytes, stream);
+}
+
+uint64_t sdb_merge_runs_workspace_bytes(const sdb_run *runs, uint32_t nruns) {
+    if (nruns && !runs) return 0;
+    uint64_t total = 0;
+    for (uint32_t r = 0; r < nruns; r++) total += runs[r].n;
+    return merge_workspace_layout(total).total + 256;
+}
+
+sdb_status sdb_merge_runs(const sdb_run *runs, uint32_t nruns, const sdb_retention *ret, const sdb_merged_out *out,
+                          void *workspace, uint64_t workspace_bytes, void *stream) {
+    MergeArgs a;
+    sdb_status st = build_merge_args(runs, nruns, ret, out, workspace, workspace_bytes, &a);
+    if (st) return st;
+    if (!device_ok()) return SDB_DEVICE_ERROR;
+    if (launch_merge(a, true, S(stream)) != hipSuccess) return SDB_DEVICE_ERROR;
+    return SDB_OK;
+}
+
+uint64_t sdb_sst_cuts_workspace_bytes(uint64_t n, const sdb_sst_params *params) {
+    if (!params) return 0;
+    sdb_sst_params p = *params;
+    p.bloom_bits_per_key = 0;
+    p.prefix_kind = SDB_PREFIX_NONE;
+    p.no_whole_key = 0;
+    return sst_ws_bytes(n, &p) + 512 + 256;
+}
+
+sdb_status sdb_sst_cuts(const sdb_kv_batch *batch, const sdb_sst_params *params, uint64_t max_sst_size,
+                        uint64_t *cut_start, uint64_t cut_cap, uint64_t *num_ssts, void *workspace,
+                        uint64_t workspace_bytes, void *stream) {
+    if (!batch || !params || !cut_start || !num_ssts) return SDB_INVALID_ARGUMENT;
+    sdb_sst_params p = *params;  // the chain only: no filter
+    p.bloom_bits_per_key = 0;
+    p.prefix_kind = SDB_PREFIX_NONE;
+    p.no_whole_key = 0;
+    sdb_status st = check_params(&p);
+    if (st) return st;
+    const uint64_t n = batch->n;
+    if (n >= (1ull << 31)) return SDB_LIMIT_EXCEEDED;
+    if (cut_cap < n + 1 || (n && (!batch->key_bytes || !batch->key_off || !batch->val_off))) return SDB_INVALID_ARGUMENT;
+    if (!device_ok()) return SDB_DEVICE_ERROR;
+    if (!workspace || workspace_bytes < sdb_sst_cuts_workspace_bytes(n, params)) return SDB_INVALID_ARGUMENT;
+    hipStream_t s = S(stream);
+    uint8_t *ws = (uint8_t *)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+    if (!n) {
+        if (hipMemsetAsync(cut_start, 0, 8, s) != hipSuccess || hipMemsetAsync(num_ssts, 0, 8, s) != hipSuccess)
+            return SDB_DEVICE_ERROR;
+        return SDB_OK;
+    }
+    // the prep kernels write an SST summary: a scratch one after the encode workspace
+    sdb_sst_summary *scratch = (sdb_sst_summary *)(ws + sst_ws_bytes(n, &p));
+    sdb_sst_out out{};
+    out.data_cap = ~0ull;
+    out.block_cap = ~0ull;
+    out.summary = scratch;
+    bool standalone = false;
+    SstSet P = set_header(&p);
+    P.s[0] = plan_slot(batch, &p, &out, ws, &standalone);
+    P.count = 1;
+    P.max_facts = P.s[0].nfacts;
+    P.max_chunks = P.s[0].nchunks;
+    P.max_groups = (P.s[0].nchunks + P.s[0].group - 1) / P.s[0].group;
+    if (launch_cuts(P, max_sst_size, cut_start, cut_cap, num_ssts, s) != hipSuccess) return SDB_DEVICE_ERROR;
+    return SDB_OK;
 }
 
 uint64_t sdb_sst_lookup_workspace_bytes(uint64_t num_blocks, uint64_t nkeys) {

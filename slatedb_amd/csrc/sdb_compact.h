@@ -1,0 +1,84 @@
+// sdb_compact.h — kernel arguments of the compaction output side (sdb_compact.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/slatedb_amd.h"
+#include "sdb_encode.h"
+
+namespace sdb {
+
+constexpr uint32_t kMaxRuns = SDB_MAX_RUNS;
+constexpr uint32_t kMergeTile = 4096;      // merged positions per k_mg_tiles / k_mg_emit workgroup
+constexpr uint32_t kMergeThreads = 1024;
+
+struct RunDesc {  // sdb_run + the run's first global entry index
+    uint64_t n, base;
+    const uint8_t *key_arena;
+    const uint64_t *key_off;
+    const uint8_t *val_base;
+    const uint64_t *val_off;
+    const uint32_t *val_len;
+    const uint64_t *seq;
+    const uint8_t *flags;
+    const int64_t *create_ts;
+    const int64_t *expire_ts;
+};
+
+struct MergeArgs {
+    uint32_t nruns, ntiles;
+    uint64_t total;
+    sdb_retention ret;
+    sdb_merged_out out;
+    // workspace
+    uint64_t *pfx;               // per global entry: first 8 key bytes, big-endian, zero padded
+    uint64_t *perm;              // merged position -> global entry
+    uint8_t *start;              // merged position: first version of its key
+    uint8_t *dec;                // merged position: 0 drop, 1 keep, 2 keep as a tombstone
+    uint64_t *tile_sum;          // per tile: kept entries, key bytes, value bytes (exclusive offsets after k_mg_scan)
+    unsigned long long *err;     // run order violations: min (global entry << 8 | code)
+    unsigned long long *err_merge;  // merge operands (MergeOperatorRequiredIterator): min merged position << 8 | code
+    unsigned long long *metric;  // expired values, expired merges
+    RunDesc r[kMaxRuns];
+};
+static_assert(sizeof(MergeArgs) < 4000, "MergeArgs is passed as kernel arguments");
+
+struct MergeWorkspace {
+    uint64_t pfx, perm, start, dec, tile_sum, err, err_merge, metric, total;
+};
+inline MergeWorkspace merge_workspace_layout(uint64_t total) {
+    MergeWorkspace w{};
+    uint64_t off = 0;
+    auto take = [&](uint64_t bytes) {
+        uint64_t r = off;
+        off += (bytes + 255) & ~255ull;
+        return r;
+    };
+    const uint64_t ntiles = (total + kMergeTile - 1) / kMergeTile;
+    w.pfx = take(8 * (total + 1));
+    w.perm = take(8 * (total + 1));
+    w.start = take(total + 1);
+    w.dec = take(total + 1);
+    w.tile_sum = take(24 * (ntiles + 1));
+    w.err = take(8);
+    w.err_merge = take(8);
+    w.metric = take(16);
+    w.total = off;
+    return w;
+}
+
+sdb_status build_merge_args(const sdb_run *runs, uint32_t nruns, const sdb_retention *ret, const sdb_merged_out *out,
+                            void *workspace, uint64_t workspace_bytes, MergeArgs *a);
+// merge + retention (+ emit when `emit`), all on `st`
+hipError_t launch_merge(const MergeArgs &a, bool emit, hipStream_t st);
+hipError_t launch_merge_emit(const MergeArgs &a, hipStream_t st);
+
+// SST cuts over the chain tables of a prep-only encode set of one slot (launch_encode_prep)
+hipError_t launch_cuts(const SstSet &P, uint64_t max_sst_size, uint64_t *cut, uint64_t cap, uint64_t *num,
+                       hipStream_t st);
+
+// out[2i], out[2i+1] = key_off[cut[i]], val_off[cut[i]] for i <= ns
+hipError_t launch_cut_offsets(const uint64_t *cut, uint64_t ns, const uint64_t *key_off, const uint64_t *val_off,
+                              uint64_t *out, hipStream_t st);
+
+}  // namespace sdb

@@ -1,0 +1,492 @@
+// sdb_compact.hip — the compaction output side on the device: merge of sorted runs, retention, and
+// the SST cuts of the output stream (include/slatedb_amd.h, "Compaction").
+//
+//   k_mg_prefix   per input entry: 8-byte big-endian key prefix; run order check
+//   k_mg_rank     per input entry: its merged position = own index + one binary search per other run
+//                 (MergeIterator order, merge_iterator.rs:55-69: key asc, seq desc, then run)
+//   k_mg_group    per merged position: first version of its key?; merge operand check
+//                 (MergeOperatorRequiredIterator, merge_operator.rs:213-223)
+//   k_mg_retain   per key: apply_retention_filter (retention_iterator.rs:91-204) -> keep / drop /
+//                 keep as a tombstone per version
+//   k_mg_tiles    per 4096 positions: kept entries, key bytes, value bytes
+//   k_mg_scan     one workgroup: tile offsets, the summary
+//   k_mg_emit     per 4096 positions: the output batch (metadata + key / value bytes)
+//   k_cut         one lane: the compactor's max_sst_size walk (compactor_executor.rs:833-858) over
+//                 the chain tables of the encoder's k_seg / k_group (group, chunk, then block steps)
+//
+// The work here is integer / byte movement bound by HBM and by the dependent loads of the binary
+// searches; nothing is GEMM-shaped.
+#include <hip/hip_runtime.h>
+
+#include "sdb_compact.h"
+#include "sdb_device.h"
+
+namespace sdb {
+
+namespace {
+
+constexpr uint32_t kPfxThreads = 256;
+
+SDB_DEV uint32_t run_of(const MergeArgs &a, uint64_t g) {
+    uint32_t r = 0;
+    while (r + 1 < a.nruns && g >= a.r[r + 1].base) r++;
+    return r;
+}
+
+SDB_DEV uint64_t key_prefix(const uint8_t *p, uint32_t n) {  // first 8 bytes, big-endian, zero padded
+    if (!n) return 0;
+    const uint32_t need = n < 8 ? n : 8;
+    uint64_t v = load8(p, need);
+    if (need < 8) v &= (~0ull) >> (8 * (8 - need));
+    return bswap64(v);
+}
+
+// <[u8] as Ord>::cmp given the prefixes: -1, 0, 1
+SDB_DEV int cmp_key(uint64_t pa, const uint8_t *a, uint32_t na, uint64_t pb, const uint8_t *b, uint32_t nb) {
+    if (pa != pb) return pa < pb ? -1 : 1;
+    if (na > 8 && nb > 8) {
+        const uint32_t l = lcp_bytes(a + 8, na - 8, b + 8, nb - 8), m = (na < nb ? na : nb) - 8;
+        if (l < m) return a[8 + l] < b[8 + l] ? -1 : 1;
+    }
+    return na < nb ? -1 : (na > nb ? 1 : 0);
+}
+
+struct KeyAt {
+    const uint8_t *p;
+    uint32_t n;
+};
+SDB_DEV KeyAt key_at(const RunDesc &R, uint64_t i) {
+    const uint64_t o = R.key_off[i];
+    return {R.key_arena + o, (uint32_t)(R.key_off[i + 1] - o)};
+}
+
+__global__ __launch_bounds__(kPfxThreads) void k_mg_prefix(MergeArgs a) {
+    const uint64_t g = (uint64_t)blockIdx.x * kPfxThreads + threadIdx.x;
+    if (g >= a.total) return;
+    const uint32_t r = run_of(a, g);
+    const RunDesc &R = a.r[r];
+    const uint64_t i = g - R.base;
+    const KeyAt k = key_at(R, i);
+    const uint64_t pk = key_prefix(k.p, k.n);
+    a.pfx[g] = pk;
+    if (i > 0) {  // sorted-run precondition: key asc, seq desc
+        const KeyAt q = key_at(R, i - 1);
+        const int c = cmp_key(key_prefix(q.p, q.n), q.p, q.n, pk, k.p, k.n);
+        if (c > 0 || (c == 0 && R.seq[i - 1] < R.seq[i])) report_error(a.err, g, SDB_INVALID_ARGUMENT);
+    }
+}
+
+__global__ __launch_bounds__(kPfxThreads) void k_mg_rank(MergeArgs a) {
+    const uint64_t g = (uint64_t)blockIdx.x * kPfxThreads + threadIdx.x;
+    if (g >= a.total || *a.err != ~0ull) return;
+    const uint32_t r = run_of(a, g);
+    const RunDesc &R = a.r[r];
+    const uint64_t i = g - R.base;
+    const KeyAt k = key_at(R, i);
+    const uint64_t pk = a.pfx[g], sq = R.seq[i];
+    uint64_t pos = i;
+    for (uint32_t r2 = 0; r2 < a.nruns; r2++) {
+        if (r2 == r) continue;
+        const RunDesc &Q = a.r[r2];
+        // entries of run r2 that come before (key, seq, r): key less, or equal with a larger seq, or
+        // an equal seq in an earlier run
+        uint64_t lo = 0, hi = Q.n;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            const KeyAt f = key_at(Q, mid);
+            const int c = cmp_key(a.pfx[Q.base + mid], f.p, f.n, pk, k.p, k.n);
+            bool before = c < 0;
+            if (c == 0) {
+                const uint64_t s2 = Q.seq[mid];
+                before = s2 > sq || (s2 == sq && r2 < r);
+            }
+            if (before) lo = mid + 1;
+            else hi = mid;
+        }
+        pos += lo;
+    }
+    a.perm[pos] = g;
+}
+
+__global__ __launch_bounds__(kPfxThreads) void k_mg_group(MergeArgs a) {
+    const uint64_t p = (uint64_t)blockIdx.x * kPfxThreads + threadIdx.x;
+    if (p >= a.total || *a.err != ~0ull) return;
+    const uint64_t g = a.perm[p];
+    const uint32_t r = run_of(a, g);
+    const RunDesc &R = a.r[r];
+    const uint64_t i = g - R.base;
+    uint8_t st = 1;
+    if (p > 0) {
+        const uint64_t h = a.perm[p - 1];
+        const RunDesc &Q = a.r[run_of(a, h)];
+        const KeyAt x = key_at(Q, h - Q.base), y = key_at(R, i);
+        st = cmp_key(a.pfx[h], x.p, x.n, a.pfx[g], y.p, y.n) != 0;
+    }
+    a.start[p] = st;
+    if (!a.ret.merge_operands && (R.flags[i] & SDB_FLAG_MERGE_OPERAND))
+        report_error(a.err_merge, p, SDB_MERGE_OPERATOR_MISSING);
+}
+
+struct Ver {
+    uint64_t seq;
+    int64_t ets;
+    uint8_t flags;
+};
+SDB_DEV Ver ver_at(const MergeArgs &a, uint64_t p) {
+    const uint64_t g = a.perm[p];
+    const RunDesc &R = a.r[run_of(a, g)];
+    const uint64_t i = g - R.base;
+    Ver v;
+    v.seq = R.seq[i];
+    v.flags = R.flags[i];
+    v.ets = (v.flags & SDB_FLAG_HAS_EXPIRE_TS) ? R.expire_ts[i] : 0;
+    return v;
+}
+
+// One thread per key (the thread of its first version): the versions newest first
+// (retention_iterator.rs:91-204 over the RetentionBuffer's BTreeMap, :381-398).
+__global__ __launch_bounds__(kPfxThreads) void k_mg_retain(MergeArgs a) {
+    const uint64_t p = (uint64_t)blockIdx.x * kPfxThreads + threadIdx.x;
+    if (p >= a.total || !a.start[p] || *a.err != ~0ull || *a.err_merge != ~0ull) return;
+    uint64_t end = p + 1;
+    while (end < a.total && !a.start[end]) end++;
+    const sdb_retention &rt = a.ret;
+    uint64_t nv = 0, nm = 0;
+    bool broken = false;
+    Ver cur = ver_at(a, p);
+    for (uint64_t q = p; q < end; q++) {
+        Ver nxt{};
+        if (q + 1 < end) nxt = ver_at(a, q + 1);
+        uint8_t d = 0;
+        // a later version with the same seq replaces this one (BTreeMap::insert)
+        if (!broken && !(q + 1 < end && nxt.seq == cur.seq)) {
+            const bool is_merge = (cur.flags & SDB_FLAG_MERGE_OPERAND) != 0;
+            bool skip = false;
+            d = 1;
+            if ((cur.flags & SDB_FLAG_HAS_EXPIRE_TS) && cur.ets <= rt.compaction_start_ts) {
+                if (is_merge) {  // expired merge operands are skipped
+                    nm++;
+                    skip = true;
+                    d = 0;
+                } else {         // expired values / tombstones become tombstones
+                    nv++;
+                    d = 2;
+                }
+            }
+            if (!skip) {
+                const bool cont = (rt.has_time_window && cur.seq >= rt.time_seq) ||
+                                  (rt.has_min_seq && cur.seq > rt.min_seq) || is_merge;
+                if (!cont) broken = true;
+            }
+        }
+        a.dec[q] = d;
+        cur = nxt;
+    }
+    if (rt.filter_tombstone) {  // pop the tombstones in the tail
+        for (uint64_t q = end; q-- > p;) {
+            const uint8_t d = a.dec[q];
+            if (!d) continue;
+            if (d == 2 || (ver_at(a, q).flags & SDB_FLAG_TOMBSTONE)) a.dec[q] = 0;
+            else break;
+        }
+    }
+    if (nv) atomicAdd(&a.metric[0], (unsigned long long)nv);
+    if (nm) atomicAdd(&a.metric[1], (unsigned long long)nm);
+}
+
+struct OutSizes {
+    uint64_t keep, kb, vb;
+};
+SDB_DEV OutSizes out_sizes(const MergeArgs &a, uint64_t p) {
+    OutSizes s{0, 0, 0};
+    if (p >= a.total) return s;
+    const uint8_t d = a.dec[p];
+    if (!d) return s;
+    const uint64_t g = a.perm[p];
+    const RunDesc &R = a.r[run_of(a, g)];
+    const uint64_t i = g - R.base;
+    s.keep = 1;
+    s.kb = R.key_off[i + 1] - R.key_off[i];
+    s.vb = (d == 1 && !(R.flags[i] & SDB_FLAG_TOMBSTONE)) ? R.val_len[i] : 0;
+    return s;
+}
+
+constexpr uint32_t kPerT = kMergeTile / kMergeThreads;
+
+__global__ __launch_bounds__(kMergeThreads) void k_mg_tiles(MergeArgs a) {
+    if (*a.err != ~0ull || *a.err_merge != ~0ull) return;
+    __shared__ uint64_t s_w[17];
+    const uint64_t p0 = (uint64_t)blockIdx.x * kMergeTile + (uint64_t)threadIdx.x * kPerT;
+    uint64_t c = 0, kb = 0, vb = 0, t;
+    for (uint32_t u = 0; u < kPerT; u++) {
+        const OutSizes s = out_sizes(a, p0 + u);
+        c += s.keep;
+        kb += s.kb;
+        vb += s.vb;
+    }
+    uint64_t tc, tk, tv;
+    block_excl_scan_u64(c, s_w, &tc);
+    block_excl_scan_u64(kb, s_w, &tk);
+    block_excl_scan_u64(vb, s_w, &tv);
+    (void)t;
+    if (threadIdx.x == 0) {
+        a.tile_sum[3 * (uint64_t)blockIdx.x + 0] = tc;
+        a.tile_sum[3 * (uint64_t)blockIdx.x + 1] = tk;
+        a.tile_sum[3 * (uint64_t)blockIdx.x + 2] = tv;
+    }
+}
+
+// One workgroup: exclusive tile offsets, the totals and the summary.
+__global__ __launch_bounds__(kMergeThreads) void k_mg_scan(MergeArgs a) {
+    __shared__ uint64_t s_w[17];
+    sdb_merge_summary *sm = a.out.summary;
+    const unsigned long long e1 = *a.err, e2 = *a.err_merge;
+    uint64_t carry[3] = {0, 0, 0};
+    if (e1 == ~0ull && e2 == ~0ull) {
+        for (uint32_t base = 0; base < a.ntiles; base += kMergeThreads) {
+            const uint32_t t = base + threadIdx.x;
+#pragma unroll
+            for (int f = 0; f < 3; f++) {
+                const uint64_t v = t < a.ntiles ? a.tile_sum[3 * (uint64_t)t + f] : 0;
+                uint64_t tot;
+                const uint64_t ex = block_excl_scan_u64(v, s_w, &tot);
+                if (t < a.ntiles) a.tile_sum[3 * (uint64_t)t + f] = carry[f] + ex;
+                carry[f] += tot;
+            }
+        }
+    }
+    if (threadIdx.x) return;
+    sm->num_in = a.total;
+    sm->expired_values = a.metric[0];
+    sm->expired_merges = a.metric[1];
+    sm->pad = 0;
+    sm->first_error_entry = ~0ull;
+    int32_t st = SDB_OK;
+    if (e1 != ~0ull) {
+        st = (int32_t)(e1 & 0xFF);
+        sm->first_error_entry = e1 >> 8;
+    } else if (e2 != ~0ull) {
+        st = (int32_t)(e2 & 0xFF);
+        sm->first_error_entry = e2 >> 8;
+    } else if (carry[0] > a.out.cap_entries || carry[1] > a.out.key_cap || carry[2] > a.out.val_cap) {
+        st = SDB_INVALID_ARGUMENT;
+    }
+    sm->status = st;
+    // a capacity failure still reports the sizes the output needs
+    const bool sized = e1 == ~0ull && e2 == ~0ull;
+    sm->num_out = sized ? carry[0] : 0;
+    sm->key_bytes = sized ? carry[1] : 0;
+    sm->val_bytes = sized ? carry[2] : 0;
+    if (!st) {
+        a.out.key_off[carry[0]] = carry[1];
+        a.out.val_off[carry[0]] = carry[2];
+    }
+}
+
+SDB_DEV void copy_bytes(uint8_t *dst, const uint8_t *src, uint64_t n) {
+    uint64_t o = 0;
+    // align the destination to 4 bytes, then dword stores from unaligned 8-byte loads
+    while (o < n && ((uintptr_t)(dst + o) & 3)) {
+        dst[o] = src[o];
+        o++;
+    }
+    for (; o + 4 <= n; o += 4) *(uint32_t *)(dst + o) = (uint32_t)load8(src + o, 4);
+    for (; o < n; o++) dst[o] = src[o];
+}
+
+__global__ __launch_bounds__(kMergeThreads) void k_mg_emit(MergeArgs a) {
+    if (a.out.summary->status != SDB_OK) return;
+    __shared__ uint64_t s_w[17];
+    const uint64_t p0 = (uint64_t)blockIdx.x * kMergeTile + (uint64_t)threadIdx.x * kPerT;
+    OutSizes s[kPerT];
+    uint64_t c = 0, kb = 0, vb = 0, tot;
+#pragma unroll
+    for (uint32_t u = 0; u < kPerT; u++) {
+        s[u] = out_sizes(a, p0 + u);
+        c += s[u].keep;
+        kb += s[u].kb;
+        vb += s[u].vb;
+    }
+    uint64_t j = a.tile_sum[3 * (uint64_t)blockIdx.x + 0] + block_excl_scan_u64(c, s_w, &tot);
+    uint64_t ko = a.tile_sum[3 * (uint64_t)blockIdx.x + 1] + block_excl_scan_u64(kb, s_w, &tot);
+    uint64_t vo = a.tile_sum[3 * (uint64_t)blockIdx.x + 2] + block_excl_scan_u64(vb, s_w, &tot);
+    const sdb_merged_out &o = a.out;
+#pragma unroll
+    for (uint32_t u = 0; u < kPerT; u++) {
+        if (!s[u].keep) continue;
+        const uint64_t p = p0 + u, g = a.perm[p];
+        const RunDesc &R = a.r[run_of(a, g)];
+        const uint64_t i = g - R.base;
+        const uint8_t d = a.dec[p], f = R.flags[i];
+        const bool tomb = d == 2 || (f & SDB_FLAG_TOMBSTONE);
+        uint8_t mask = 0;
+        if (f & SDB_FLAG_HAS_CREATE_TS) mask |= SDB_TS_CREATE;
+        if ((f & SDB_FLAG_HAS_EXPIRE_TS) && d == 1) mask |= SDB_TS_EXPIRE;  // converted: expire_ts None
+        o.key_off[j] = ko;
+        o.val_off[j] = vo;
+        o.kind[j] = tomb ? SDB_KIND_TOMBSTONE : (f & SDB_FLAG_MERGE_OPERAND) ? SDB_KIND_MERGE : SDB_KIND_VALUE;
+        o.seq[j] = R.seq[i];
+        o.ts_mask[j] = mask;
+        o.create_ts[j] = (mask & SDB_TS_CREATE) ? R.create_ts[i] : 0;
+        o.expire_ts[j] = (mask & SDB_TS_EXPIRE) ? R.expire_ts[i] : 0;
+        copy_bytes(o.key_bytes + ko, R.key_arena + R.key_off[i], s[u].kb);
+        if (s[u].vb) copy_bytes(o.val_bytes + vo, R.val_base + R.val_off[i], s[u].vb);
+        j++;
+        ko += s[u].kb;
+        vo += s[u].vb;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// SST cuts: one lane walks the block chain the writer builds, restarting it after every cut.  A
+// chain that enters a chunk (or a group of chunks) from the one before sits at one of the table
+// entry points, so whole chunks / groups whose bytes keep the SST at or under max_sst_size are
+// skipped with one lookup; near a cut the walk steps block by block through next() / bbytes.
+// ------------------------------------------------------------------------------------------------
+__global__ void k_cut(SstSet P, uint64_t max_sst, uint64_t *cut, uint64_t *num) {
+    if (threadIdx.x || blockIdx.x) return;
+    const EncodeArgs a = make_args(P, 0);
+    const uint64_t n = a.n;
+    const bool fast = *a.mode == 1;
+    const uint32_t W = *a.wmax, G = a.group, L = a.seg_look;
+    uint64_t e = 0, acc = 0, ns = 0;
+    bool entry_pt = true;  // reached from the previous chunk (or the stream start): the tables apply
+    cut[0] = 0;
+    while (e < n) {
+        const uint64_t k = e / kChunk, o = e - k * kChunk;
+        if (fast && entry_pt && o < W) {
+            if (k % G == 0) {
+                const uint64_t t = (k / G) * L + o, b = a.gtab_bytes[t];
+                if (acc + b <= max_sst) {
+                    acc += b;
+                    e = (k + G) * kChunk + a.gtab_exit[t];
+                    continue;
+                }
+            }
+            const uint64_t t = k * L + o;
+            const uint32_t ex = a.tab_exit[t];
+            if (ex != 0xFFFFFFFFu) {
+                const uint64_t b = a.tab_bytes[t];
+                if (acc + b <= max_sst) {
+                    acc += b;
+                    e = ex;
+                    continue;
+                }
+            }
+        }
+        const uint64_t j = a.next[e];
+        if (j >= n) break;  // the tail block: built by close(), never counted
+        acc += a.bbytes[e];
+        if (acc > max_sst) {
+            // entry j's add finished the block: the writer closes with j as its one-entry tail
+            if (j + 1 < n) cut[++ns] = j + 1;
+            acc = 0;
+            e = j + 1;
+            entry_pt = (e % kChunk) == 0;
+            continue;
+        }
+        entry_pt = j / kChunk != k;
+        e = j;
+    }
+    if (n) cut[++ns] = n;
+    *num = ns;
+}
+
+__global__ void k_cut_offsets(const uint64_t *cut, uint64_t ns, const uint64_t *key_off, const uint64_t *val_off,
+                              uint64_t *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > ns) return;
+    const uint64_t c = cut[i];
+    out[2 * i] = key_off[c];
+    out[2 * i + 1] = val_off[c];
+}
+
+}  // namespace
+
+hipError_t launch_cut_offsets(const uint64_t *cut, uint64_t ns, const uint64_t *key_off, const uint64_t *val_off,
+                              uint64_t *out, hipStream_t st) {
+    hipLaunchKernelGGL(k_cut_offsets, dim3((uint32_t)((ns + 256) / 256)), dim3(256), 0, st, cut, ns, key_off, val_off, out);
+    return hipGetLastError();
+}
+
+sdb_status build_merge_args(const sdb_run *runs, uint32_t nruns, const sdb_retention *ret, const sdb_merged_out *out,
+                            void *workspace, uint64_t workspace_bytes, MergeArgs *pa) {
+    if ((nruns && !runs) || !ret || !out || !out->summary || !out->key_off || !out->val_off || !pa)
+        return SDB_INVALID_ARGUMENT;
+    if (nruns > kMaxRuns) return SDB_LIMIT_EXCEEDED;
+    MergeArgs &a = *pa;
+    a = MergeArgs{};
+    a.nruns = nruns;
+    uint64_t total = 0;
+    for (uint32_t r = 0; r < nruns; r++) {
+        const sdb_run &R = runs[r];
+        if (R.n && (!R.key_arena || !R.key_off || !R.val_off || !R.val_len || !R.seq || !R.flags))
+            return SDB_INVALID_ARGUMENT;
+        RunDesc &d = a.r[r];
+        d.n = R.n;
+        d.base = total;
+        d.key_arena = R.key_arena;
+        d.key_off = R.key_off;
+        d.val_base = R.val_base;
+        d.val_off = R.val_off;
+        d.val_len = R.val_len;
+        d.seq = R.seq;
+        d.flags = R.flags;
+        d.create_ts = R.create_ts;
+        d.expire_ts = R.expire_ts;
+        total += R.n;
+    }
+    if (total >= (1ull << 40)) return SDB_LIMIT_EXCEEDED;
+    if (total && (!out->kind || !out->seq || !out->create_ts || !out->expire_ts || !out->ts_mask)) return SDB_INVALID_ARGUMENT;
+    const MergeWorkspace w = merge_workspace_layout(total);
+    if (!workspace || workspace_bytes < w.total + 256) return SDB_INVALID_ARGUMENT;
+    uint8_t *ws = (uint8_t *)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+    a.total = total;
+    a.ntiles = (uint32_t)((total + kMergeTile - 1) / kMergeTile);
+    a.ret = *ret;
+    a.out = *out;
+    a.pfx = (uint64_t *)(ws + w.pfx);
+    a.perm = (uint64_t *)(ws + w.perm);
+    a.start = ws + w.start;
+    a.dec = ws + w.dec;
+    a.tile_sum = (uint64_t *)(ws + w.tile_sum);
+    a.err = (unsigned long long *)(ws + w.err);
+    a.err_merge = (unsigned long long *)(ws + w.err_merge);
+    a.metric = (unsigned long long *)(ws + w.metric);
+    return SDB_OK;
+}
+
+hipError_t launch_merge(const MergeArgs &a, bool emit, hipStream_t st) {
+    if (hipMemsetAsync(a.err, 0xFF, 8, st) != hipSuccess || hipMemsetAsync(a.err_merge, 0xFF, 8, st) != hipSuccess ||
+        hipMemsetAsync(a.metric, 0, 16, st) != hipSuccess)
+        return hipErrorUnknown;
+    const uint32_t gb = (uint32_t)((a.total + kPfxThreads - 1) / kPfxThreads);
+    if (gb) {
+        hipLaunchKernelGGL(k_mg_prefix, dim3(gb), dim3(kPfxThreads), 0, st, a);
+        hipLaunchKernelGGL(k_mg_rank, dim3(gb), dim3(kPfxThreads), 0, st, a);
+        hipLaunchKernelGGL(k_mg_group, dim3(gb), dim3(kPfxThreads), 0, st, a);
+        hipLaunchKernelGGL(k_mg_retain, dim3(gb), dim3(kPfxThreads), 0, st, a);
+    }
+    if (a.ntiles) hipLaunchKernelGGL(k_mg_tiles, dim3(a.ntiles), dim3(kMergeThreads), 0, st, a);
+    hipLaunchKernelGGL(k_mg_scan, dim3(1), dim3(kMergeThreads), 0, st, a);
+    if (emit && a.ntiles) hipLaunchKernelGGL(k_mg_emit, dim3(a.ntiles), dim3(kMergeThreads), 0, st, a);
+    return hipGetLastError();
+}
+
+// The emit alone, after launch_merge(a, false) sized the output with unbounded capacities (the
+// caller then points a.out at buffers of exactly the reported sizes).
+hipError_t launch_merge_emit(const MergeArgs &a, hipStream_t st) {
+    if (a.ntiles) hipLaunchKernelGGL(k_mg_emit, dim3(a.ntiles), dim3(kMergeThreads), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_cuts(const SstSet &P, uint64_t max_sst_size, uint64_t *cut, uint64_t cap, uint64_t *num,
+                       hipStream_t st) {
+    (void)cap;  // the host checks cap >= n + 1
+    hipError_t e = launch_encode_prep(P, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_cut, dim3(1), dim3(64), 0, st, P, max_sst_size, cut, num);
+    return hipGetLastError();
+}
+
+}  // namespace sdb

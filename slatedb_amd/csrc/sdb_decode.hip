@@ -264,9 +264,10 @@ SDB_DEV BlockView load_block(const DecodeArgs &a, uint64_t k, uint8_t *stage, co
         for (uint64_t w = 0; w < nwin; w++) {
             uint64_t wbeg = (w == 0) ? 0 : first + ((w - 1) << 12);
             uint32_t wlen = (uint32_t)((w == 0) ? first : 4096);
-            for (uint32_t q = lane_id(); q < wlen; q += 64) stage[16 + q] = g[wbeg + q];
+            // the init fold inverts message bytes [0, 4), which may straddle the first two windows
+            for (uint32_t q = lane_id(); q < wlen; q += 64) stage[16 + q] = g[wbeg + q] ^ (wbeg + q < 4 ? 0xFF : 0);
             wave_sync_d();
-            uint32_t raw = wave_crc_raw_lds(stage + 16, wlen, crc, w == 0);
+            uint32_t raw = wave_crc_raw_lds(stage + 16, wlen, crc, false);
             acc = (w == 0) ? raw : (gf_mul(c_shift.window, acc) ^ raw);
             wave_sync_d();
         }

@@ -307,6 +307,7 @@ __host__ __device__ inline EncodeArgs make_args(const SstSet &P, uint32_t i) {
 // Enqueue the encode of every SST of the set on `st` (one launch sequence).
 hipError_t launch_encode_set(const SstSet &P, size_t bin_lds, size_t fill_lds, hipStream_t st);
 hipError_t launch_encode_empty(EncodeArgs a, hipStream_t st);
+hipError_t launch_encode_prep(const SstSet &P, hipStream_t st);  // k_facts, k_seg, k_group only
 
 // stage timing (diagnostics)
 enum Stage { kStBloom = 0, kStFacts, kStSeg, kStGroup, kStEnum, kStEmit, kStEmitSlow, kStBloomFill, kNumStages };

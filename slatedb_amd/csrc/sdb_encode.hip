@@ -1714,9 +1714,13 @@ SDB_DEV void emit_slow_blocks(const EncodeArgs &a, uint8_t *scratch, const uint3
             for (uint64_t w = 0; w < nwin; w++) {
                 uint64_t wbeg = (w == 0) ? 0 : first + ((w - 1) << 12);
                 uint32_t wlen = (uint32_t)((w == 0) ? first : 4096);
-                for (uint32_t q = threadIdx.x; q < wlen; q += 64) s_win[16 + q] = dst[wbeg + q];
+                // crc32fast's 0xFFFFFFFF init = inverting message bytes [0, 4), which straddle the
+                // first two windows when the first holds fewer than 4 bytes (V1 blocks of
+                // block_size + 1 or + 2 bytes: the new entry's offset is not counted, block.rs:117-123)
+                for (uint32_t q = threadIdx.x; q < wlen; q += 64)
+                    s_win[16 + q] = dst[wbeg + q] ^ (wbeg + q < 4 ? 0xFF : 0);
                 wave_sync();
-                uint32_t raw = wave_crc_raw_lds(s_win + 16, wlen, (const uint32_t(*)[256])s_crc, w == 0);
+                uint32_t raw = wave_crc_raw_lds(s_win + 16, wlen, (const uint32_t(*)[256])s_crc, false);
                 // R(A || B) = R(A) * x^(8|B|) + R(B); every window after the first is 4096 bytes
                 acc = (w == 0) ? raw : (gf_mul(c_shift.window, acc) ^ raw);
                 wave_sync();
@@ -1869,6 +1873,18 @@ hipError_t launch_encode_set(const SstSet &P, size_t bin_lds, size_t fill_lds, h
     if (P.version == 2) hipLaunchKernelGGL(k_emit<2>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, P);
     else hipLaunchKernelGGL(k_emit<1>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, P);
     stage_mark(st, kStEmit, false);
+    return hipGetLastError();
+}
+
+// The block chain alone (k_facts -> k_seg -> k_group): per-entry next() / block bytes, the chunk and
+// group transfer tables and the walk mode, for the compactor's SST cuts (sdb_compact.hip).  The slot
+// builds no filter.
+hipError_t launch_encode_prep(const SstSet &P, hipStream_t st) {
+    set_lds_attrs();
+    if (!P.count) return hipSuccess;
+    hipLaunchKernelGGL(k_facts, dim3(P.max_facts, P.count), dim3(kFactsThreads), 0, st, P);
+    hipLaunchKernelGGL(k_seg, dim3(P.max_chunks, P.count), dim3(kSegThreads), kSegLds, st, P);
+    hipLaunchKernelGGL(k_group, dim3(P.max_groups, P.count), dim3(kGroupThreads), kGroupLds, st, P);
     return hipGetLastError();
 }
 

@@ -594,3 +594,177 @@ def sst_lookup_device(view_tensors, key_bytes, key_off, nkeys, descending=False,
         raise SdbError(st, "sdb_sst_lookup")
     res["_ws"] = ws
     return res
+
+
+# ------------------------------------------------------------------------------------------------
+# Compaction (sdb_merge_runs / sdb_sst_cuts / sdb_compactor_*)
+# ------------------------------------------------------------------------------------------------
+def _sp(stream):
+    if stream is None:
+        return None
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+
+
+_hip = None
+
+
+def _d2h(ptr, nbytes):
+    """Copy nbytes at a raw device pointer to a host numpy uint8 array (hipMemcpy D2H)."""
+    global _hip
+    if _hip is None:
+        _hip = C.CDLL("libamdhip64.so")
+        _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        _hip.hipMemcpy.restype = C.c_int
+    out = np.empty(max(nbytes, 1), np.uint8)
+    if nbytes:
+        st = _hip.hipMemcpy(out.ctypes.data, ptr, nbytes, 2)
+        if st:
+            raise SdbError(_abi.SDB_DEVICE_ERROR, "hipMemcpy D2H")
+    return out[:nbytes]
+
+
+class DeviceRun:
+    """A sorted run on the device in the sdb_run layout (torch tensors)."""
+
+    def __init__(self, n, key_arena, key_off, val_base, val_off, val_len, seq, flags, create_ts, expire_ts,
+                 key_bytes, val_bytes):
+        self.n = n
+        self.t = (key_arena, key_off, val_base, val_off, val_len, seq, flags, create_ts, expire_ts)
+        self.key_bytes, self.val_bytes = key_bytes, val_bytes
+
+    @classmethod
+    def from_host(cls, run, device="cuda"):
+        import torch
+        up = lambda a: torch.from_numpy(np.concatenate([np.ascontiguousarray(a).view(np.uint8),
+                                                        np.zeros(16, np.uint8)])).to(device)
+        return cls(run.n, up(run.key_arena), up(run.key_off), up(run.val_base), up(run.val_off), up(run.val_len),
+                   up(run.seq), up(run.flags), up(run.create_ts), up(run.expire_ts),
+                   int(run.key_off[-1]) if run.n else 0, int(run.val_len.sum()))
+
+    @classmethod
+    def from_decoded(cls, dout, blocks, n):
+        """A DeviceDecodeOutput of `n` entries whose values live in the `blocks` device tensor."""
+        sm = dout.summary_host()
+        vb = int(dout.val_len[:n].to(dtype=__import__("torch").int64).sum().item()) if n else 0
+        return cls(n, dout.key_arena, dout.key_off, blocks, dout.val_off, dout.val_len, dout.seq, dout.flags,
+                   dout.create_ts, dout.expire_ts, int(sm.key_bytes), vb)
+
+    def to_ctypes(self):
+        return _abi.Run(self.n, *[t.data_ptr() for t in self.t])
+
+
+def merge_runs_device(druns, ret, stream=None):
+    """sdb_merge_runs over DeviceRuns -> (dict of device tensors of the merged batch, MergeSummary)."""
+    import torch
+    dev = druns[0].t[0].device if druns else "cuda"
+    total = sum(r.n for r in druns)
+    kcap = sum(r.key_bytes for r in druns)
+    vcap = sum(r.val_bytes for r in druns)
+    e = lambda k, dt: torch.empty(max(k, 1), dtype=dt, device=dev)
+    o = {"key_bytes": e(kcap + 16, torch.uint8), "key_off": e(total + 1, torch.int64),
+         "val_bytes": e(vcap + 16, torch.uint8), "val_off": e(total + 1, torch.int64),
+         "kind": e(total, torch.uint8), "seq": e(total, torch.int64), "create_ts": e(total, torch.int64),
+         "expire_ts": e(total, torch.int64), "ts_mask": e(total, torch.uint8),
+         "summary": torch.zeros(C.sizeof(_abi.MergeSummary), dtype=torch.uint8, device=dev)}
+    out = _abi.MergedOut(o["key_bytes"].data_ptr(), kcap, o["key_off"].data_ptr(), o["val_bytes"].data_ptr(), vcap,
+                         o["val_off"].data_ptr(), o["kind"].data_ptr(), o["seq"].data_ptr(), o["create_ts"].data_ptr(),
+                         o["expire_ts"].data_ptr(), o["ts_mask"].data_ptr(), total, o["summary"].data_ptr())
+    cr = (_abi.Run * max(len(druns), 1))(*[r.to_ctypes() for r in druns])
+    wsb = lib().sdb_merge_runs_workspace_bytes(cr, len(druns))
+    ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
+    st = lib().sdb_merge_runs(cr, len(druns), C.byref(ret), C.byref(out), ws.data_ptr(), ws.numel(), _sp(stream))
+    if st:
+        raise SdbError(st, "sdb_merge_runs")
+    sm = _abi.MergeSummary.from_buffer_copy(o["summary"].cpu().numpy().tobytes())
+    o["_ws"] = ws
+    return o, sm
+
+
+def merged_to_host(o, sm):
+    from .batch import Batch
+    n = sm.num_out
+    v = lambda k, m, dt: o[k][:m].cpu().numpy().view(dt)
+    return Batch(v("key_bytes", sm.key_bytes, np.uint8), v("key_off", n + 1, np.uint64),
+                 v("val_bytes", sm.val_bytes, np.uint8), v("val_off", n + 1, np.uint64), v("kind", n, np.uint8),
+                 v("seq", n, np.uint64), v("create_ts", n, np.int64), v("expire_ts", n, np.int64),
+                 v("ts_mask", n, np.uint8))
+
+
+def sst_cuts_device(dbatch, prm, max_sst_size, stream=None):
+    """sdb_sst_cuts over a device batch -> list of SST start entries + [n] (synchronises)."""
+    import torch
+    n = dbatch.n
+    dev = "cuda"
+    cut = torch.zeros(n + 2, dtype=torch.int64, device=dev)
+    num = torch.zeros(1, dtype=torch.int64, device=dev)
+    wsb = lib().sdb_sst_cuts_workspace_bytes(n, C.byref(prm))
+    ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
+    kb = dbatch.to_ctypes()
+    st = lib().sdb_sst_cuts(C.byref(kb), C.byref(prm), max_sst_size, cut.data_ptr(), n + 1, num.data_ptr(),
+                            ws.data_ptr(), ws.numel(), _sp(stream))
+    if st:
+        raise SdbError(st, "sdb_sst_cuts")
+    ns = int(num.item())
+    return [int(x) for x in cut[:ns + 1].cpu().numpy()] if ns else []
+
+
+class Compactor:
+    """sdb_compactor_*: one compaction job (merge + retention + cuts + encode) per run()."""
+
+    def __init__(self, device=0):
+        require_device()
+        self.h = lib().sdb_compactor_create(device)
+        if not self.h:
+            raise SdbError(_abi.SDB_DEVICE_ERROR, "sdb_compactor_create")
+
+    def run(self, druns, ret, prm, max_sst_size, stream=None):
+        cr = (_abi.Run * max(len(druns), 1))(*[r.to_ctypes() for r in druns])
+        ns = C.c_uint32(0)
+        st = lib().sdb_compactor_run(self.h, cr, len(druns), C.byref(ret), C.byref(prm), max_sst_size, _sp(stream),
+                                     C.byref(ns))
+        self.status = st
+        return st, ns.value
+
+    def merged(self):
+        kb, sm = _abi.KvBatch(), _abi.MergeSummary()
+        st = lib().sdb_compactor_merged(self.h, C.byref(kb), C.byref(sm))
+        if st:
+            raise SdbError(st, "sdb_compactor_merged")
+        from .batch import Batch
+        n = kb.n
+        if not n:
+            return Batch(np.zeros(0, np.uint8), np.zeros(1, np.uint64), np.zeros(0, np.uint8), np.zeros(1, np.uint64),
+                         np.zeros(0, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.int64), np.zeros(0, np.int64),
+                         np.zeros(0, np.uint8)), sm
+        g = lambda p, k, dt: _d2h(p, k * np.dtype(dt).itemsize).view(dt)
+        return Batch(g(kb.key_bytes, sm.key_bytes, np.uint8), g(kb.key_off, n + 1, np.uint64),
+                     g(kb.val_bytes, sm.val_bytes, np.uint8), g(kb.val_off, n + 1, np.uint64), g(kb.kind, n, np.uint8),
+                     g(kb.seq, n, np.uint64), g(kb.create_ts, n, np.int64), g(kb.expire_ts, n, np.int64),
+                     g(kb.ts_mask, n, np.uint8)), sm
+
+    def sst(self, i):
+        """SST i of the last run as host arrays (the fields of DeviceSstOutput.to_host) + entry range."""
+        v = _abi.CompactedSst()
+        st = lib().sdb_compactor_sst(self.h, i, C.byref(v))
+        if st:
+            raise SdbError(st, "sdb_compactor_sst")
+        sm = v.summary
+        nb = sm.num_blocks
+        g = lambda p, k, dt: _d2h(p, k * np.dtype(dt).itemsize).view(dt)
+        return {"summary": sm, "entry_start": v.entry_start, "entry_end": v.entry_end,
+                "data": g(v.data, sm.data_len, np.uint8), "block_off": g(v.block_off, nb + 1, np.uint64),
+                "block_first_entry": g(v.block_first_entry, nb + 1, np.uint32),
+                "index_key_len": g(v.index_key_len, nb, np.uint32),
+                "block_stats": g(v.block_stats, 3 * nb, np.uint16).reshape(-1, 3),
+                "bloom": g(v.bloom, sm.bloom_len, np.uint8)}
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().sdb_compactor_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,259 @@
+"""GPU parity of the compaction output side (sdb_merge_runs, sdb_sst_cuts, sdb_compactor_*;
+slatedb_amd/csrc/sdb_compact.hip, sdb_compactor.cpp) against the oracle restatement (orc_merge_runs,
+orc_sst_cuts, orc_encode_sst per output SST): the merged + retained stream field by field, the cut
+list, and every output SST byte for byte — on the reference's retention table, random multi-run
+inputs (duplicate seqs, merges, expiry, tombstone filtering), multi-chunk / multi-group streams, and
+SSTs encoded then decoded on the device as the inputs."""
+import json
+import os
+import random
+import types
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from slatedb_amd import _abi
+from slatedb_amd.batch import Batch, Run
+
+from .test_compaction_oracle import GOLDEN, entries_of, rand_runs, to_entry
+from .test_gpu_parity import assert_same
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rt():
+    from slatedb_amd import runtime
+    runtime.require_device()
+    return runtime
+
+
+def assert_batch_same(got, ref, what=""):
+    assert got.n == ref.n, (what, got.n, ref.n)
+    for f in ("key_off", "val_off", "kind", "seq", "ts_mask", "create_ts", "expire_ts"):
+        assert np.array_equal(np.asarray(getattr(got, f)), np.asarray(getattr(ref, f))), (what, f)
+    assert np.array_equal(got.key_bytes, ref.key_bytes), what
+    assert np.array_equal(got.val_bytes, ref.val_bytes), what
+
+
+def merge_both(rt, runs, ret):
+    import torch
+    druns = [rt.DeviceRun.from_host(r) for r in runs]
+    o, sm = rt.merge_runs_device(druns, ret)
+    torch.cuda.synchronize()
+    ref, rsm = O.merge_runs(runs, ret)
+    assert sm.status == rsm.status, (sm.status, rsm.status)
+    assert sm.first_error_entry == rsm.first_error_entry
+    assert sm.num_in == rsm.num_in
+    if rsm.status == 0:
+        for f in ("num_out", "key_bytes", "val_bytes", "expired_values", "expired_merges"):
+            assert getattr(sm, f) == getattr(rsm, f), f
+        assert_batch_same(rt.merged_to_host(o, sm), ref)
+    return ref, rsm
+
+
+@pytest.mark.parametrize("case", GOLDEN, ids=[c["name"] for c in GOLDEN])
+def test_retention_golden_device(rt, case):
+    to = case["timeout_s"]
+    ret = O.retention(min_seq=case["retention_min_seq"], time_seq=0 if to else None,
+                      compaction_start_ts=case["compaction_start_ts"], filter_tombstone=case["filter_tombstone"],
+                      merge_operands=True)
+    run = Run.from_entries([to_entry(e) for e in case["input"]])
+    ref, _ = merge_both(rt, [run], ret)
+    assert entries_of(ref) == [to_entry(e) for e in case["expected"]]
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_merge_retention_random_device(rt, seed):
+    rng = random.Random(100 + seed)
+    runs = rand_runs(rng, rng.randrange(1, 9), 300, 5, merge=0.2, dup_seq=seed % 3 == 0)
+    ret = O.retention(min_seq=rng.choice([None, 0, 200, 700]), time_seq=rng.choice([None, 0, 400]),
+                      compaction_start_ts=rng.choice([0, 1000, 5000]), filter_tombstone=bool(seed % 2),
+                      merge_operands=True)
+    merge_both(rt, [Run.from_entries(r) for r in runs], ret)
+
+
+def test_merge_errors_device(rt):
+    runs = [[(b"a", 0, b"1", 3, None, None), (b"b", 1, b"x", 2, None, None), (b"c", 1, b"y", 1, None, None)],
+            [(b"a", 0, b"0", 1, None, None), (b"bb", 1, b"z", 5, None, None)]]
+    _, sm = merge_both(rt, [Run.from_entries(r) for r in runs], O.retention())
+    assert sm.status == _abi.SDB_MERGE_OPERATOR_MISSING and sm.first_error_entry == 2
+    bad = Run.from_entries([(b"b", 0, b"1", 3, None, None), (b"a", 0, b"0", 1, None, None)])
+    _, sm = merge_both(rt, [Run.from_entries(runs[0][:1]), bad], O.retention())
+    assert sm.status == _abi.SDB_INVALID_ARGUMENT and sm.first_error_entry == 2
+
+
+def test_merge_empty_runs(rt):
+    e = Run.from_entries([])
+    merge_both(rt, [e, e], O.retention())
+    ret = O.retention(compaction_start_ts=10 ** 9, filter_tombstone=True)  # everything expires and goes
+    merge_both(rt, [Run.from_entries([(b"k", 0, b"v", 1, None, 5)])], ret)
+
+
+def big_runs(seed, nkeys, nruns, maxver=3, vmax=120, tomb=0.1, expire=0.05):
+    """numpy-built sorted runs: 16-byte keys (8-byte BE random prefix + 8-byte BE counter), 1..maxver
+    versions each spread over the runs, unique seqs, values of 0..vmax bytes."""
+    rng = np.random.default_rng(seed)
+    pre = np.sort(rng.integers(0, 1 << 62, nkeys, dtype=np.int64).astype(np.uint64))
+    nver = rng.integers(1, maxver + 1, nkeys)
+    kidx = np.repeat(np.arange(nkeys), nver)
+    m = len(kidx)
+    seq = rng.permutation(m).astype(np.uint64) + 1
+    # within a key: seqs descending
+    order = np.lexsort((-seq.astype(np.int64), kidx))
+    seq = seq[order]
+    run = rng.integers(0, nruns, m)
+    kb = np.zeros((m, 16), np.uint8)
+    kb[:, :8] = pre[kidx].byteswap().view(np.uint8).reshape(-1, 8)
+    kb[:, 8:] = np.arange(nkeys, dtype=np.uint64)[kidx].byteswap().view(np.uint8).reshape(-1, 8)
+    vlen = rng.integers(0, vmax + 1, m)
+    kind = np.where(rng.random(m) < tomb, _abi.KIND_TOMBSTONE, _abi.KIND_VALUE).astype(np.uint8)
+    vlen[kind == _abi.KIND_TOMBSTONE] = 0
+    pool = rng.integers(0, 256, int(vlen.sum()) + 16, dtype=np.uint8)
+    ets = rng.integers(0, 2000, m).astype(np.int64)
+    mask = np.where(rng.random(m) < expire, _abi.TS_EXPIRE, 0).astype(np.uint8)
+    runs = []
+    vstart = np.concatenate([[0], np.cumsum(vlen)])
+    for r in range(nruns):
+        sel = np.nonzero(run == r)[0]
+        n = len(sel)
+        koff = np.arange(n + 1, dtype=np.uint64) * 16
+        vl = vlen[sel]
+        voff = np.concatenate([[0], np.cumsum(vl)]).astype(np.uint64)
+        vb = np.concatenate([pool[vstart[i]:vstart[i] + vlen[i]] for i in sel]) if n else np.zeros(0, np.uint8)
+        runs.append(Run.from_batch(Batch(kb[sel].reshape(-1), koff, vb, voff, kind[sel], seq[sel],
+                                         np.zeros(n, np.int64), ets[sel], mask[sel])))
+    return runs
+
+
+@pytest.mark.parametrize("nruns", [2, 7])
+def test_merge_big_device(rt, nruns):
+    runs = big_runs(nruns, 60000, nruns)
+    merge_both(rt, runs, O.retention(min_seq=50000, compaction_start_ts=1000, filter_tombstone=nruns == 7))
+
+
+def cuts_both(rt, batch, prm, max_sst):
+    got = rt.sst_cuts_device(batch.to_device(), prm, max_sst)
+    st, ref = O.sst_cuts(batch, prm, max_sst)
+    assert st == 0
+    assert got == ref, (len(got), len(ref), [(a, b) for a, b in zip(got, ref) if a != b][:4])
+    return ref
+
+
+@pytest.mark.parametrize("max_sst", [1, 5000, 300000, 10 ** 12])
+@pytest.mark.parametrize("version,bs", [(2, 4096), (2, 512), (1, 4096)])
+def test_sst_cuts_device(rt, max_sst, version, bs):
+    runs = big_runs(5, 40000, 1, maxver=1)
+    r = runs[0]
+    b = Batch(r.key_arena, r.key_off, r.val_base, np.concatenate([r.val_off, [r.val_off[-1] + r.val_len[-1]]]),
+              np.where(r.flags & 1, 2, 0).astype(np.uint8), r.seq, r.create_ts, r.expire_ts,
+              np.where(r.flags & 2, 2, 0).astype(np.uint8))
+    cuts = cuts_both(rt, b, O.params(sst_version=version, block_size=bs), max_sst)
+    if max_sst == 10 ** 12:
+        assert cuts == [0, b.n]
+
+
+def test_sst_cuts_long_blocks_device(rt):
+    """64 KiB blocks of tiny rows: the chain tables are off (serial walk mode)."""
+    n = 30000
+    ents = [(b"%08d" % i, 0, b"", 1, None, None) for i in range(n)]
+    b = Batch.from_entries(ents)
+    cuts_both(rt, b, O.params(block_size=65536), 100000)
+
+
+def sst_view(d):
+    return types.SimpleNamespace(status=d["summary"].status,
+                                 summary={f: getattr(d["summary"], f) for f, _ in _abi.SstSummary._fields_},
+                                 data=d["data"], block_off=d["block_off"], block_first_entry=d["block_first_entry"],
+                                 index_key_len=d["index_key_len"], block_stats=d["block_stats"], bloom=d["bloom"])
+
+
+def compact_both(rt, runs, ret, prm_kw, max_sst, druns=None):
+    import torch
+    druns = druns or [rt.DeviceRun.from_host(r) for r in runs]
+    comp = rt.Compactor()
+    st, ns = comp.run(druns, ret, rt.params(**prm_kw), max_sst)
+    torch.cuda.synchronize()
+    merged, msum, cuts, ssts = O.compact(runs, ret, O.params(**prm_kw), max_sst)
+    assert st == msum.status, (st, msum.status)
+    if st:
+        return comp, ssts
+    gm, gsm = comp.merged()
+    assert_batch_same(gm, merged, "merged")
+    assert ns == len(ssts), (ns, len(ssts))
+    for i, ref in enumerate(ssts):
+        d = comp.sst(i)
+        assert (d["entry_start"], d["entry_end"]) == (cuts[i], cuts[i + 1])
+        assert_same(ref, sst_view(d), "sst %d" % i)
+    return comp, ssts
+
+
+@pytest.mark.parametrize("version", [1, 2])
+def test_compactor_big(rt, version):
+    runs = big_runs(11, 80000, 5)
+    comp, ssts = compact_both(rt, runs, O.retention(min_seq=100000, compaction_start_ts=1000, filter_tombstone=True),
+                              dict(sst_version=version, block_size=4096, bloom_bits_per_key=10), 2 << 20)
+    assert len(ssts) >= 3
+    comp.close()
+
+
+def test_compactor_small_cases(rt):
+    rng = random.Random(5)
+    runs = [Run.from_entries(r) for r in rand_runs(rng, 4, 500, 4)]
+    for max_sst in (1, 700, 10 ** 9):
+        compact_both(rt, runs, O.retention(min_seq=100, compaction_start_ts=900), dict(block_size=256), max_sst)
+    # merge operands without a merge operator fail the job
+    mruns = [Run.from_entries(r) for r in rand_runs(rng, 2, 50, 3, merge=0.3)]
+    compact_both(rt, mruns, O.retention(), dict(), 10 ** 9)
+    # everything filtered: no output SST
+    compact_both(rt, [Run.from_entries([(b"k", 2, b"", 1, None, None)])], O.retention(filter_tombstone=True),
+                 dict(), 100)
+
+
+def test_compactor_from_device_decoded_ssts(rt):
+    """The whole device path: input SSTs encoded on the GPU, decoded on the GPU (sdb_decode_blocks),
+    merged / retained / cut / re-encoded on the GPU; checked against the oracle on the host runs."""
+    import torch
+    runs = big_runs(21, 30000, 3)
+    prm_kw = dict(block_size=4096, bloom_bits_per_key=10)
+    druns = []
+    keep = []
+    for r in runs:
+        n = r.n
+        b = Batch(r.key_arena, r.key_off, r.val_base, np.concatenate([r.val_off, [r.val_off[-1] + r.val_len[-1]]]),
+                  np.where(r.flags & 1, 2, 0).astype(np.uint8), r.seq, r.create_ts, r.expire_ts,
+                  np.where(r.flags & 2, 2, 0).astype(np.uint8))
+        enc = O.encode_sst(b, O.params(**prm_kw))
+        blocks = torch.from_numpy(np.concatenate([enc.data, np.zeros(64, np.uint8)])).cuda()
+        boff = torch.from_numpy(enc.block_off.view(np.int64)).cuda()
+        nb = len(enc.block_off) - 1
+        dout = rt.DeviceDecodeOutput(nb, n + 16, int(r.key_off[-1]) + 64)
+        st = rt.lib().sdb_decode_blocks(blocks.data_ptr(), boff.data_ptr(), nb, 2, __import__("ctypes").byref(dout.out),
+                                        dout.workspace.data_ptr(), dout.workspace.numel(), None)
+        assert st == 0
+        torch.cuda.synchronize()
+        assert dout.summary_host().num_entries == n
+        druns.append(rt.DeviceRun.from_decoded(dout, blocks, n))
+        keep.append((blocks, boff, dout))
+    compact_both(rt, runs, O.retention(min_seq=40000, compaction_start_ts=1000), prm_kw, 1 << 20, druns=druns)
+
+
+def test_v1_blocks_past_block_size(rt):
+    """V1 blocks may hold block_size + 2 bytes (the new entry's offset is not counted, block.rs:117-123):
+    their CRC runs through the windowed path with a 1-2 byte first window (encode and decode)."""
+    from .test_gpu_parity import assert_decode_same
+    runs = big_runs(11, 80000, 5)
+    merged, _ = O.merge_runs(runs, O.retention(min_seq=100000, compaction_start_ts=1000, filter_tombstone=True))
+    b = merged.slice(0, 30000)
+    prm = dict(sst_version=1, block_size=4096)
+    ref = O.encode_sst(b, O.params(**prm))
+    lens = np.diff(ref.block_off.astype(np.int64)) - 4
+    assert (lens > 4096).any()
+    enc = rt.Encoder(rt.params(**prm))
+    got = enc.encode(b)
+    enc.close()
+    assert_same(ref, got, "v1 oversized")
+    dref = O.decode_blocks(ref.data, ref.block_off, 1)
+    dec = rt.Decoder()
+    assert_decode_same(dref, dec.decode(ref.data, ref.block_off, 1), "v1 oversized decode")
