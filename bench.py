@@ -37,7 +37,7 @@ PMC_FILE = "r2_pmc_traffic.json"
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=1500)
+    p.add_argument("--steps", type=int, default=2000)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch", type=int, default=8, help="SSTs per GPU per step (one sdb_encode_ssts call)")
     p.add_argument("--job-ssts", type=int, default=0,
@@ -271,7 +271,7 @@ def main():
                    "ssts_per_gpu_per_step": batch, "entries_per_sst": hosts[0].n, "block_size": 4096,
                    "sst_version": 2, "bloom_bits_per_key": args.bpk, "resident_input_ssts_per_gpu": len(dbs),
                    "parallelism": "independent SSTs per GPU (no collective)"},
-        "roofline": {"bound": "hbm", "kernel": "whole encode pipeline (k_facts, k_bloom_bin_hd, k_seg, k_group, "
+        "roofline": {"bound": "hbm", "kernel": "whole encode pipeline (k_facts + fused bloom binning, k_seg, k_group, "
                                                "k_enum, k_bloom_fill_hd, k_emit: one launch sequence per step)",
                      "achieved": round(pipe_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(pipe_gbs / PEAK_HBM_GBS, 4),

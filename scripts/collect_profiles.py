@@ -50,8 +50,10 @@ def main():
     shutil.copy(one("enc/**/run_kernel_stats.csv"), os.path.join(PROF, tag + "_encode_kernel_stats.csv"))
     shutil.copy(one("dec/**/run_kernel_stats.csv"), os.path.join(PROF, tag + "_decode_kernel_stats.csv"))
     fetch, write = pmc("FETCH_SIZE"), pmc("WRITE_SIZE")
+    batch = json.load(open(one("bench.json")))["config"]["ssts_per_gpu_per_step"]
     out = {"command": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) -- "
-                      "python3 bench.py --steps 3 --warmup 1 --no-cpu --no-verify",
+                      "python3 bench.py --steps 3 --warmup 1 --no-cpu --no-verify --single-steps 0 --stage-steps 0",
+           "ssts_per_dispatch": batch,
            "correction": "read_bytes = 2 * 1024 * FETCH_SIZE (gfx950 half-count of wide reads); "
                          "write_bytes = 1024 * WRITE_SIZE",
            "per_dispatch": {}}
@@ -60,6 +62,9 @@ def main():
             continue
         rd, wr = 2048.0 * fetch.get(k, 0.0), 1024.0 * write.get(k, 0.0)
         out["per_dispatch"][k] = {"read_bytes": round(rd), "write_bytes": round(wr), "traffic_bytes": round(rd + wr)}
+    # per SST: every pipeline kernel's dispatch encodes one launch set of `batch` SSTs
+    out["per_kernel"] = {k: round(v["traffic_bytes"] / batch) for k, v in out["per_dispatch"].items()}
+    out["per_sst_bytes"] = sum(out["per_kernel"].values())
     json.dump(out, open(os.path.join(PROF, tag + "_pmc_traffic.json"), "w"), indent=1)
     for k, v in out["per_dispatch"].items():
         print("%-22s read %8.1f MB  write %8.1f MB" % (k, v["read_bytes"] / 1e6, v["write_bytes"] / 1e6))

@@ -5,7 +5,7 @@
 #   3. PMC passes FETCH_SIZE, WRITE_SIZE (one counter per pass)      -> gpurun_out/rp/pmc_*/
 #   4. scripts/bench_configs.py (configs[2], configs[3], E2E)        -> gpurun_out/rp/configs.jsonl
 #   5. rocprofv3 --kernel-trace --stats over the decode of configs[2] -> gpurun_out/rp/dec/
-# Then on the host: python3 scripts/collect_profiles.py r1
+# Then on the host: python3 scripts/collect_profiles.py r2
 # Stops at the first failing step.
 set -u
 cd "$(dirname "$0")/.."
@@ -15,11 +15,11 @@ mkdir -p $O
 timeout -k 10 300 python3 bench.py > $O/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; grep '^{' $O/bench.log > $O/bench.json; cut -c1-300 $O/bench.json
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/enc -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu --no-verify > $O/enc.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/enc -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu --no-verify --single-steps 0 --stage-steps 0 > $O/enc.log 2>&1
 rc=$?; echo "rocprof enc rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c -d $O/pmc_$c -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-verify > $O/pmc_$c.log 2>&1
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c -d $O/pmc_$c -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-verify --single-steps 0 --stage-steps 0 > $O/pmc_$c.log 2>&1
   rc=$?; echo "pmc $c rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done
