@@ -1,5 +1,5 @@
 #!/bin/bash
-# SQ counter passes (one rocprofv3 run each) over a short bench; per-kernel averages -> gpurun_out/pmc_sq/summary.txt
+# SQ counter passes (one rocprofv3 run each) over a short bench (or $PMC_CMD); per-kernel averages -> gpurun_out/pmc_sq/summary.txt
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out/pmc_sq
@@ -8,7 +8,7 @@ i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp -d gpurun_out/pmc_sq/p$i -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-verify ${BENCH_EXTRA:-} > gpurun_out/pmc_sq/p$i.log 2>&1
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp -d gpurun_out/pmc_sq/p$i -o run --output-format csv -- ${PMC_CMD:-python3 bench.py --steps 3 --warmup 1 --no-cpu --no-verify --single-steps 0 --stage-steps 0} > gpurun_out/pmc_sq/p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done <<GROUPS
