@@ -486,6 +486,13 @@ void sdb_encoder_destroy(sdb_encoder *enc);
 /* Encode a host batch; returns the first error (host-side or device-side). */
 sdb_status sdb_encoder_encode_host(sdb_encoder *enc, const sdb_kv_batch *host_batch,
                                    sdb_sst_host_result *result);
+/* Encode `count` host batches (the SSTs of one L0 flush or of a compaction's output, config.rs:
+ * 1081, 1383-1390) with their transfers overlapped: SST i+1's marshal and H2D and SST i-1's D2H run
+ * while SST i's kernels do (two slots of pinned staging, separate H2D / kernel / D2H streams).
+ * results[i] views host memory owned by the encoder, valid until the next call; returns the first
+ * SST status that is not SDB_OK (every SST is still attempted); the *_ms timings are 0. */
+sdb_status sdb_encoder_encode_host_many(sdb_encoder *enc, uint32_t count, const sdb_kv_batch *host_batches,
+                                        sdb_sst_host_result *results);
 
 /* Mirror of EncodedSsTableBuilder's per-entry surface (sst_builder.rs:224-276,370-417). */
 typedef struct sdb_sst_builder sdb_sst_builder;

@@ -241,6 +241,7 @@ SIGNATURES = {
     "sdb_encoder_create": (C.c_void_p, [C.c_int, C.POINTER(SstParams)]),
     "sdb_encoder_destroy": (None, [C.c_void_p]),
     "sdb_encoder_encode_host": (C.c_int, [C.c_void_p, C.POINTER(KvBatch), C.POINTER(SstHostResult)]),
+    "sdb_encoder_encode_host_many": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(KvBatch), C.POINTER(SstHostResult)]),
     "sdb_sst_builder_new": (C.c_void_p, [C.c_int, C.POINTER(SstParams)]),
     "sdb_sst_builder_free": (None, [C.c_void_p]),
     "sdb_sst_builder_add": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint8, C.c_void_p,

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/slatedb_amd.h"
@@ -616,14 +617,28 @@ struct PinBuf {
 
 }  // namespace
 
+// One in-flight SST of the pipelined host path (sdb_encoder_encode_host_many).
+struct EncSlot {
+    PinBuf h_in;
+    DevBuf d_in, d_out, d_ws;
+    hipEvent_t h2d_done = nullptr, comp_done = nullptr, d2h_done = nullptr;
+    bool used = false;
+};
+
 struct sdb_encoder {
     int device = 0;
     sdb_sst_params params{};
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // kernels (and the whole single-SST path)
     hipEvent_t ev[4] = {};
     // device: input, output, workspace
     DevBuf d_in, d_out, d_ws;
     PinBuf h_in, h_out;
+    // pipelined path: H2D and D2H on their own streams (the two copy directions overlap each other
+    // and the kernels), two slots of staging / device buffers, one pinned output area per SST
+    hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+    EncSlot slot[2];
+    std::vector<PinBuf> outs;
+    PinBuf sums;
 };
 
 namespace {
@@ -631,7 +646,9 @@ namespace {
 struct InLayout {  // packed input arrays inside one allocation (256-byte aligned pieces)
     uint64_t key_bytes, key_off, val_bytes, val_off, kind, seq, cts, ets, mask, plen, total;
 };
-InLayout in_layout(uint64_t n, uint64_t kb, uint64_t vb) {
+// Only the columns the batch has take space (and H2D bytes).
+InLayout in_layout(const sdb_kv_batch *hb, uint64_t kb, uint64_t vb) {
+    const uint64_t n = hb->n;
     InLayout l{};
     uint64_t off = 0;
     auto take = [&](uint64_t bytes) {
@@ -643,14 +660,81 @@ InLayout in_layout(uint64_t n, uint64_t kb, uint64_t vb) {
     l.key_off = take(8 * (n + 1));
     l.val_bytes = take(vb + 16);
     l.val_off = take(8 * (n + 1));
-    l.kind = take(n + 1);
-    l.seq = take(8 * (n + 1));
-    l.cts = take(8 * (n + 1));
-    l.ets = take(8 * (n + 1));
-    l.mask = take(n + 1);
-    l.plen = take(4 * (n + 1));
+    l.kind = take(hb->kind ? n + 1 : 0);
+    l.seq = take(hb->seq ? 8 * (n + 1) : 0);
+    l.cts = take(hb->create_ts ? 8 * (n + 1) : 0);
+    l.ets = take(hb->expire_ts ? 8 * (n + 1) : 0);
+    l.mask = take(hb->ts_mask ? n + 1 : 0);
+    l.plen = take(hb->prefix_len ? 4 * (n + 1) : 0);
     l.total = off;
     return l;
+}
+
+// The caller's (pageable) batch into pinned staging, offsets rebased to 0.  Large copies are split
+// over a few host threads: one thread's memcpy bandwidth is below the PCIe rate.
+void marshal(const sdb_kv_batch *hb, const InLayout &il, uint8_t *hi, uint64_t k0, uint64_t kb, uint64_t v0, uint64_t vb) {
+    const uint64_t n = hb->n;
+    if (!n) return;
+    std::vector<std::pair<uint8_t *, const uint8_t *>> dst_src;
+    std::vector<uint64_t> len;
+    auto add = [&](uint8_t *d, const void *s, uint64_t l) {
+        if (s && l) {
+            dst_src.push_back({d, (const uint8_t *)s});
+            len.push_back(l);
+        }
+    };
+    add(hi + il.key_bytes, hb->key_bytes + k0, kb);
+    add(hi + il.val_bytes, hb->val_bytes ? hb->val_bytes + v0 : nullptr, vb);
+    add(hi + il.kind, hb->kind, n);
+    add(hi + il.seq, hb->seq, 8 * n);
+    add(hi + il.cts, hb->create_ts, 8 * n);
+    add(hi + il.ets, hb->expire_ts, 8 * n);
+    add(hi + il.mask, hb->ts_mask, n);
+    add(hi + il.plen, hb->prefix_len, 4 * n);
+    uint64_t total = 0;
+    for (uint64_t l : len) total += l;
+    const unsigned nt = total >= (16u << 20) ? 8 : 1;
+    auto work = [&](unsigned t) {
+        // byte range [t * total / nt, (t + 1) * total / nt) of the concatenated copies
+        const uint64_t lo = total * t / nt, hi_ = total * (t + 1) / nt;
+        uint64_t base = 0;
+        for (size_t q = 0; q < len.size(); q++) {
+            const uint64_t a = std::max(lo, base), b = std::min(hi_, base + len[q]);
+            if (a < b) memcpy(dst_src[q].first + (a - base), dst_src[q].second + (a - base), b - a);
+            base += len[q];
+        }
+        // and entries [t * (n + 1) / nt, ...) of the rebased offsets
+        uint64_t *ko = (uint64_t *)(hi + il.key_off), *vo = (uint64_t *)(hi + il.val_off);
+        const uint64_t e0 = (n + 1) * t / nt, e1 = (n + 1) * (t + 1) / nt;
+        for (uint64_t i = e0; i < e1; i++) {
+            ko[i] = hb->key_off[i] - k0;
+            vo[i] = hb->val_off[i] - v0;
+        }
+    };
+    if (nt == 1) {
+        work(0);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto &x : th) x.join();
+}
+
+sdb_kv_batch dev_batch(const sdb_kv_batch *hb, const InLayout &il, uint8_t *di) {
+    sdb_kv_batch db{};
+    db.n = hb->n;
+    db.key_bytes = di + il.key_bytes;
+    db.key_off = (const uint64_t *)(di + il.key_off);
+    db.val_bytes = di + il.val_bytes;
+    db.val_off = (const uint64_t *)(di + il.val_off);
+    db.kind = hb->kind ? di + il.kind : nullptr;
+    db.seq = hb->seq ? (const uint64_t *)(di + il.seq) : nullptr;
+    db.create_ts = hb->create_ts ? (const int64_t *)(di + il.cts) : nullptr;
+    db.expire_ts = hb->expire_ts ? (const int64_t *)(di + il.ets) : nullptr;
+    db.ts_mask = hb->ts_mask ? di + il.mask : nullptr;
+    db.prefix_len = hb->prefix_len ? (const int32_t *)(di + il.plen) : nullptr;
+    return db;
 }
 struct OutLayout {
     uint64_t data, block_off, block_first, index_key_len, block_stats, bloom, summary, total;
@@ -689,15 +773,30 @@ sdb_encoder *sdb_encoder_create(int device, const sdb_sst_params *params) {
         return nullptr;
     }
     for (auto &x : e->ev) hipEventCreate(&x);
+    if (hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->s_d2h, hipStreamNonBlocking) != hipSuccess) {
+        sdb_encoder_destroy(e);
+        return nullptr;
+    }
+    for (EncSlot &sl : e->slot) {
+        hipEventCreateWithFlags(&sl.h2d_done, hipEventDisableTiming);
+        hipEventCreateWithFlags(&sl.comp_done, hipEventDisableTiming);
+        hipEventCreateWithFlags(&sl.d2h_done, hipEventDisableTiming);
+    }
     return e;
 }
 
 void sdb_encoder_destroy(sdb_encoder *e) {
     if (!e) return;
     hipSetDevice(e->device);
-    hipStreamSynchronize(e->stream);
+    for (hipStream_t st : {e->stream, e->s_h2d, e->s_d2h})
+        if (st) hipStreamSynchronize(st);
     for (auto &x : e->ev) hipEventDestroy(x);
-    hipStreamDestroy(e->stream);
+    for (EncSlot &sl : e->slot)
+        for (hipEvent_t x : {sl.h2d_done, sl.comp_done, sl.d2h_done})
+            if (x) hipEventDestroy(x);
+    for (hipStream_t st : {e->stream, e->s_h2d, e->s_d2h})
+        if (st) hipStreamDestroy(st);
     delete e;
 }
 
@@ -710,45 +809,19 @@ sdb_status sdb_encoder_encode_host(sdb_encoder *e, const sdb_kv_batch *hb, sdb_s
     uint64_t data_cap, block_cap, bloom_cap;
     sdb_encode_bounds(n, kb, vb, &e->params, &data_cap, &block_cap, &bloom_cap);
     if (data_cap >= (1ull << 32)) return SDB_LIMIT_EXCEEDED;  // u32 per-block/chunk byte counters
-    InLayout il = in_layout(n, kb, vb);
+    InLayout il = in_layout(hb, kb, vb);
     OutLayout ol = out_layout(data_cap, block_cap, bloom_cap);
     uint64_t wsb = sdb_encode_workspace_bytes(n, &e->params);
     if (e->h_in.ensure(il.total) || e->d_in.ensure(il.total) || e->h_out.ensure(ol.total) ||
         e->d_out.ensure(ol.total) || e->d_ws.ensure(wsb))
         return SDB_DEVICE_ERROR;
-    // marshal the caller's batch into pinned staging (offsets rebased to 0)
     uint8_t *hi = (uint8_t *)e->h_in.p;
-    if (n) {
-        memcpy(hi + il.key_bytes, hb->key_bytes + k0, kb);
-        memcpy(hi + il.val_bytes, hb->val_bytes ? hb->val_bytes + v0 : hi + il.val_bytes, hb->val_bytes ? vb : 0);
-        uint64_t *ko = (uint64_t *)(hi + il.key_off), *vo = (uint64_t *)(hi + il.val_off);
-        for (uint64_t i = 0; i <= n; i++) {
-            ko[i] = hb->key_off[i] - k0;
-            vo[i] = hb->val_off[i] - v0;
-        }
-        if (hb->kind) memcpy(hi + il.kind, hb->kind, n);
-        if (hb->seq) memcpy(hi + il.seq, hb->seq, 8 * n);
-        if (hb->create_ts) memcpy(hi + il.cts, hb->create_ts, 8 * n);
-        if (hb->expire_ts) memcpy(hi + il.ets, hb->expire_ts, 8 * n);
-        if (hb->ts_mask) memcpy(hi + il.mask, hb->ts_mask, n);
-        if (hb->prefix_len) memcpy(hi + il.plen, hb->prefix_len, 4 * n);
-    }
+    marshal(hb, il, hi, k0, kb, v0, vb);
     uint8_t *di = (uint8_t *)e->d_in.p, *dout = (uint8_t *)e->d_out.p;
     hipEventRecord(e->ev[0], e->stream);
     hipMemcpyAsync(di, hi, il.total, hipMemcpyHostToDevice, e->stream);
     hipEventRecord(e->ev[1], e->stream);
-    sdb_kv_batch db{};
-    db.n = n;
-    db.key_bytes = di + il.key_bytes;
-    db.key_off = (const uint64_t *)(di + il.key_off);
-    db.val_bytes = di + il.val_bytes;
-    db.val_off = (const uint64_t *)(di + il.val_off);
-    db.kind = hb->kind ? di + il.kind : nullptr;
-    db.seq = hb->seq ? (const uint64_t *)(di + il.seq) : nullptr;
-    db.create_ts = hb->create_ts ? (const int64_t *)(di + il.cts) : nullptr;
-    db.expire_ts = hb->expire_ts ? (const int64_t *)(di + il.ets) : nullptr;
-    db.ts_mask = hb->ts_mask ? di + il.mask : nullptr;
-    db.prefix_len = hb->prefix_len ? (const int32_t *)(di + il.plen) : nullptr;
+    const sdb_kv_batch db = dev_batch(hb, il, di);
     sdb_sst_out o{};
     o.data = dout + ol.data;
     o.data_cap = data_cap;
@@ -796,6 +869,117 @@ sdb_status sdb_encoder_encode_host(sdb_encoder *e, const sdb_kv_batch *hb, sdb_s
     r->kernel_ms = t12;
     r->d2h_ms = t23;
     return (sdb_status)sm.status;
+}
+
+// Several host batches, transfers overlapped: while SST i's kernels run, SST i+1 is marshalled
+// into the other slot's pinned staging and copied H2D, and SST i-1's outputs come back D2H (three
+// streams; the copy engines serve both directions at once).  The host waits only for each SST's
+// summary (to size its D2H) and for the last D2H.
+sdb_status sdb_encoder_encode_host_many(sdb_encoder *e, uint32_t count, const sdb_kv_batch *hbs,
+                                        sdb_sst_host_result *results) {
+    if (!e || (count && (!hbs || !results))) return SDB_INVALID_ARGUMENT;
+    if (hipSetDevice(e->device) != hipSuccess) return SDB_DEVICE_ERROR;
+    if (e->outs.size() < count) e->outs.resize(count);
+    if (e->sums.ensure(sizeof(sdb_sst_summary) * (count + 1))) return SDB_DEVICE_ERROR;
+    sdb_sst_summary *sums = (sdb_sst_summary *)e->sums.p;
+    struct Job {
+        InLayout il;
+        OutLayout ol;
+        uint64_t data_cap, block_cap, bloom_cap;
+    };
+    std::vector<Job> jobs(count);
+    sdb_status first = SDB_OK;
+    auto fail = [&](sdb_status st) {
+        for (hipStream_t x : {e->s_h2d, e->stream, e->s_d2h}) hipStreamSynchronize(x);
+        return st;
+    };
+    for (uint32_t i = 0; i <= count; i++) {
+        if (i < count) {
+            const sdb_kv_batch *hb = &hbs[i];
+            EncSlot &sl = e->slot[i & 1];
+            Job &jb = jobs[i];
+            const uint64_t n = hb->n;
+            const uint64_t k0 = n ? hb->key_off[0] : 0, kb = n ? hb->key_off[n] - k0 : 0;
+            const uint64_t v0 = n ? hb->val_off[0] : 0, vb = n ? hb->val_off[n] - v0 : 0;
+            if (sdb_encode_bounds(n, kb, vb, &e->params, &jb.data_cap, &jb.block_cap, &jb.bloom_cap)) return fail(SDB_INVALID_ARGUMENT);
+            if (jb.data_cap >= (1ull << 32)) return fail(SDB_LIMIT_EXCEEDED);
+            jb.il = in_layout(hb, kb, vb);
+            jb.ol = out_layout(jb.data_cap, jb.block_cap, jb.bloom_cap);
+            const uint64_t wsb = sdb_encode_workspace_bytes(n, &e->params);
+            // the slot's previous SST (i - 2) must be out of its staging (H2D) before the marshal
+            // overwrites it; buffers only grow after every use of the slot has drained
+            if (sl.used) hipEventSynchronize(sl.h2d_done);
+            const bool grow = sl.h_in.cap < jb.il.total || sl.d_in.cap < jb.il.total || sl.d_out.cap < jb.ol.total ||
+                              sl.d_ws.cap < wsb;
+            if (grow && sl.used) {
+                hipEventSynchronize(sl.comp_done);
+                hipEventSynchronize(sl.d2h_done);
+            }
+            if (sl.h_in.ensure(jb.il.total) || sl.d_in.ensure(jb.il.total) || sl.d_out.ensure(jb.ol.total) ||
+                sl.d_ws.ensure(wsb))
+                return fail(SDB_DEVICE_ERROR);
+            marshal(hb, jb.il, (uint8_t *)sl.h_in.p, k0, kb, v0, vb);
+            // H2D once the slot's previous kernels no longer read d_in
+            if (sl.used) hipStreamWaitEvent(e->s_h2d, sl.comp_done, 0);
+            hipMemcpyAsync(sl.d_in.p, sl.h_in.p, jb.il.total, hipMemcpyHostToDevice, e->s_h2d);
+            hipEventRecord(sl.h2d_done, e->s_h2d);
+            // kernels once the input is there and the slot's previous outputs are back on the host
+            hipStreamWaitEvent(e->stream, sl.h2d_done, 0);
+            if (sl.used) hipStreamWaitEvent(e->stream, sl.d2h_done, 0);
+            const sdb_kv_batch db = dev_batch(hb, jb.il, (uint8_t *)sl.d_in.p);
+            uint8_t *dout = (uint8_t *)sl.d_out.p;
+            sdb_sst_out o{};
+            o.data = dout + jb.ol.data;
+            o.data_cap = jb.data_cap;
+            o.block_off = (uint64_t *)(dout + jb.ol.block_off);
+            o.block_first_entry = (uint32_t *)(dout + jb.ol.block_first);
+            o.index_key_len = (uint32_t *)(dout + jb.ol.index_key_len);
+            o.block_stats = (uint16_t *)(dout + jb.ol.block_stats);
+            o.block_cap = jb.block_cap;
+            o.bloom = dout + jb.ol.bloom;
+            o.bloom_cap = jb.bloom_cap;
+            o.summary = (sdb_sst_summary *)(dout + jb.ol.summary);
+            const sdb_status st = sdb_encode_sst(&db, &e->params, &o, sl.d_ws.p, sl.d_ws.cap, e->stream);
+            if (st) return fail(st);
+            hipMemcpyAsync(&sums[i], o.summary, sizeof(sdb_sst_summary), hipMemcpyDeviceToHost, e->stream);
+            hipEventRecord(sl.comp_done, e->stream);
+            sl.used = true;
+        }
+        if (i >= 1) {  // SST j's outputs: sized by its summary, copied on the D2H stream
+            const uint32_t j = i - 1;
+            EncSlot &sl = e->slot[j & 1];
+            const Job &jb = jobs[j];
+            if (hipEventSynchronize(sl.comp_done) != hipSuccess) return fail(SDB_DEVICE_ERROR);
+            const sdb_sst_summary sm = sums[j];
+            PinBuf &ho = e->outs[j];
+            if (ho.ensure(jb.ol.total)) return fail(SDB_DEVICE_ERROR);
+            uint8_t *h = (uint8_t *)ho.p, *d = (uint8_t *)sl.d_out.p;
+            hipStreamWaitEvent(e->s_d2h, sl.comp_done, 0);
+            if (sm.status == SDB_OK) {
+                const uint64_t nb = sm.num_blocks;
+                hipMemcpyAsync(h + jb.ol.data, d + jb.ol.data, sm.data_len, hipMemcpyDeviceToHost, e->s_d2h);
+                hipMemcpyAsync(h + jb.ol.block_off, d + jb.ol.block_off, 8 * (nb + 1), hipMemcpyDeviceToHost, e->s_d2h);
+                hipMemcpyAsync(h + jb.ol.block_first, d + jb.ol.block_first, 4 * (nb + 1), hipMemcpyDeviceToHost, e->s_d2h);
+                hipMemcpyAsync(h + jb.ol.index_key_len, d + jb.ol.index_key_len, 4 * nb, hipMemcpyDeviceToHost, e->s_d2h);
+                hipMemcpyAsync(h + jb.ol.block_stats, d + jb.ol.block_stats, 6 * nb, hipMemcpyDeviceToHost, e->s_d2h);
+                if (sm.bloom_len)
+                    hipMemcpyAsync(h + jb.ol.bloom, d + jb.ol.bloom, sm.bloom_len, hipMemcpyDeviceToHost, e->s_d2h);
+            }
+            hipEventRecord(sl.d2h_done, e->s_d2h);
+            sdb_sst_host_result &r = results[j];
+            r.summary = sm;
+            r.data = h + jb.ol.data;
+            r.block_off = (const uint64_t *)(h + jb.ol.block_off);
+            r.block_first_entry = (const uint32_t *)(h + jb.ol.block_first);
+            r.index_key_len = (const uint32_t *)(h + jb.ol.index_key_len);
+            r.block_stats = (const uint16_t *)(h + jb.ol.block_stats);
+            r.bloom = h + jb.ol.bloom;
+            r.h2d_ms = r.kernel_ms = r.d2h_ms = 0;
+            if (!first && sm.status) first = (sdb_status)sm.status;
+        }
+    }
+    if (hipStreamSynchronize(e->s_d2h) != hipSuccess) return SDB_DEVICE_ERROR;
+    return first;
 }
 
 }  // extern "C"

@@ -237,13 +237,26 @@ class Encoder:
         if not self._h:
             raise SdbError(_abi.SDB_DEVICE_ERROR, "sdb_encoder_create")
 
-    def encode(self, batch):
+    def encode(self, batch, copy=True):
         kb = batch.to_ctypes()
         res = _abi.SstHostResult()
         st = lib().sdb_encoder_encode_host(self._h, C.byref(kb), C.byref(res))
+        if not copy:  # the raw SstHostResult view (valid until the next call)
+            return st, res
         out = EncodedSst(res, self.params)
         out.status = st
         return out
+
+    def encode_many(self, batches, copy=True):
+        """sdb_encoder_encode_host_many: several SSTs with overlapped transfers.  copy=False returns the
+        raw SstHostResult views (valid until the next call) instead of EncodedSst copies."""
+        kbs = (_abi.KvBatch * max(len(batches), 1))(*[b.to_ctypes() for b in batches])
+        res = (_abi.SstHostResult * max(len(batches), 1))()
+        st = lib().sdb_encoder_encode_host_many(self._h, len(batches), kbs, res)
+        self.last_status = st
+        if not copy:
+            return st, res
+        return [EncodedSst(res[i], self.params) for i in range(len(batches))]
 
     def close(self):
         if self._h:

@@ -245,3 +245,21 @@ def test_decode_blocks_at_scattered_ranges(rt):
     shift = np.array(starts, np.uint64)[blk] - coff[:-1][blk]
     got.val_off = np.where(got.val_len > 0, got.val_off - shift, got.val_off)
     assert_decode_same(ref, got, "scattered ranges")
+
+
+def test_encode_host_many_pipelined(rt):
+    """sdb_encoder_encode_host_many (overlapped H2D / kernels / D2H, two staging slots): every SST equals
+    the oracle's, with sizes that grow and shrink across the slots and an empty SST in the middle."""
+    from .test_gpu_parity import assert_same
+    import types
+    sizes = [3000, 40000, 0, 578524, 7, 20000, 120000]
+    hosts = [datasets.d1(sst_index=i, n=n) if n else Batch.from_entries([]) for i, n in enumerate(sizes)]
+    prm = dict(block_size=4096, sst_version=2, bloom_bits_per_key=10)
+    enc = rt.Encoder(rt.params(**prm))
+    for rep in range(2):  # the second call reuses (and partly regrows) the slots
+        got = enc.encode_many(hosts if rep == 0 else hosts[::-1])
+        src = hosts if rep == 0 else hosts[::-1]
+        for i, (b, g) in enumerate(zip(src, got)):
+            ref = O.encode_sst(b, O.params(**prm))
+            assert_same(ref, g, "many[%d] rep %d" % (i, rep))
+    enc.close()
