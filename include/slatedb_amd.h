@@ -274,6 +274,20 @@ sdb_status sdb_decode_blocks_at(const uint8_t *arena, const uint64_t *block_star
                                 uint64_t nblocks, uint16_t sst_version, const sdb_decoded_out *out,
                                 void *workspace, uint64_t workspace_bytes, void *stream);
 
+/* Decode with options.  block_end == NULL: contiguous blocks (block_start has nblocks + 1 entries),
+ * else as sdb_decode_blocks_at.  flags:
+ *   SDB_DECODE_DESCENDING  entries in descending iteration order, as SstIterator in
+ *     IterationOrder::Descending yields them (sst_iter.rs:460, 557): blocks last to first, each
+ *     through DescendingBlockIteratorV2 (block_iterator_v2.rs:318-430) / BlockIterator Descending
+ *     (block_iterator.rs:159-224).  Keys / columns are in that order; block_entry_start keeps the
+ *     ascending prefix of the per-block counts, so block k's entries are [N - bes[k+1], N - bes[k]).
+ *     A V2 block whose restart regions do not start at restarts with shared == 0 and end at the next
+ *     one reports SDB_CORRUPT_BLOCK (the reference asserts there, block_iterator_v2.rs:76). */
+enum { SDB_DECODE_DESCENDING = 1 };
+sdb_status sdb_decode_blocks_ex(const uint8_t *arena, const uint64_t *block_start, const uint64_t *block_end,
+                                uint64_t nblocks, uint16_t sst_version, uint32_t flags, const sdb_decoded_out *out,
+                                void *workspace, uint64_t workspace_bytes, void *stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Point lookups / seeks on one encoded SST (device): the read path of Db::get and of an SstIterator
  * positioned on a key:

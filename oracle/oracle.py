@@ -44,6 +44,7 @@ def _load():
         "orc_bloom_build": (C.c_int, [V, V, C.c_uint64, C.c_uint32, V, C.c_uint64]),
         "orc_bloom_might_contain": (C.c_int, [V, C.c_uint64, C.c_uint32, V, C.c_size_t]),
         "orc_decode_blocks": (C.c_int, [V, V, C.c_uint64, C.c_uint16, P(_abi.DecodedOut)]),
+        "orc_decode_blocks_desc": (C.c_int, [V, V, C.c_uint64, C.c_uint16, P(_abi.DecodedOut)]),
         "orc_sst_lookup": (C.c_int, [P(_abi.SstView), V, V, C.c_uint64, C.c_int, P(_abi.LookupOut)]),
         "orc_bloom_build_prefix": (C.c_int, [V, V, V, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, V,
                                              C.c_uint64, P(C.c_uint64)]),
@@ -245,18 +246,18 @@ class DecodeResult:
     pass
 
 
-def decode_blocks(blocks, block_off, version=2, cap_entries=None, key_cap=None):
+def decode_blocks(blocks, block_off, version=2, cap_entries=None, key_cap=None, descending=False):
     blocks = np.ascontiguousarray(blocks, np.uint8)
     total = int(np.asarray(block_off)[-1] - np.asarray(block_off)[0]) if len(block_off) > 1 else 0
     key_cap = key_cap or (total * 4 + 4096)
     while True:
-        r = _decode_blocks(blocks, block_off, version, cap_entries, key_cap)
+        r = _decode_blocks(blocks, block_off, version, cap_entries, key_cap, descending)
         if r.status != _abi.SDB_INVALID_ARGUMENT or key_cap > (total + 1) * 1024:
             return r
         key_cap *= 8
 
 
-def _decode_blocks(blocks, block_off, version, cap_entries, key_cap):
+def _decode_blocks(blocks, block_off, version, cap_entries, key_cap, descending=False):
     block_off = np.ascontiguousarray(block_off, np.uint64)
     nb = len(block_off) - 1
     total = int(block_off[-1] - block_off[0]) if nb else 0
@@ -279,8 +280,8 @@ def _decode_blocks(blocks, block_off, version, cap_entries, key_cap):
                           r.seq.ctypes.data, r.flags.ctypes.data, r.create_ts.ctypes.data,
                           r.expire_ts.ctypes.data, cap_entries, r.bad_block.ctypes.data,
                           max(nb, 1), C.addressof(sm))
-    st = lib().orc_decode_blocks(blocks.ctypes.data if blocks.size else None, block_off.ctypes.data,
-                                 nb, version, C.byref(out))
+    fn = lib().orc_decode_blocks_desc if descending else lib().orc_decode_blocks
+    st = fn(blocks.ctypes.data if blocks.size else None, block_off.ctypes.data, nb, version, C.byref(out))
     r.status = st
     r.summary = sm
     n = sm.num_entries

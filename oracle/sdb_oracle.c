@@ -1421,3 +1421,202 @@ sdb_status orc_sst_cuts(const sdb_kv_batch *batch, const sdb_sst_params *p, uint
     free(enc.p);
     return st;
 }
+
+/* ------------------------------------------------------------------------------------------- */
+/* Descending iteration over decoded blocks: SstIterator in IterationOrder::Descending visits the  */
+/* blocks last to first (sst_iter.rs:460, 557), each through DescendingBlockIteratorV2            */
+/* (block_iterator_v2.rs:318-430: restart regions last to first, each decoded ascending from its   */
+/* restart -- seek_to_restart asserts shared == 0 there, :71-93 -- then yielded in reverse) or    */
+/* BlockIterator Descending (block_iterator.rs:159-224: the entry offsets in reverse).             */
+/* Output: entries in that order; block_entry_start keeps the ascending prefix of the per-block   */
+/* counts, so block k's entries are [N - bes[k + 1], N - bes[k]).                                 */
+/* ------------------------------------------------------------------------------------------- */
+typedef struct {
+    uint64_t kstart; uint32_t klen;
+    uint64_t vpos; uint32_t vlen;
+    uint64_t seq; uint8_t flags; int64_t cts, ets;
+} desc_ent;
+
+/* One V2 row at d[pos..] restored against cur (SstRowCodecV2::decode + restore_full_key). */
+static sdb_status desc_row_v2(const uint8_t *d, size_t data_end, size_t *pos, const uint8_t *cur, size_t curlen,
+                              uint8_t **key, size_t *klen, desc_ent *e, uint64_t base) {
+    uint32_t sh, un, vl;
+    size_t p = *pos;
+    if (!rd_varint(d, data_end, &p, &sh) || !rd_varint(d, data_end, &p, &un) || !rd_varint(d, data_end, &p, &vl))
+        return SDB_CORRUPT_BLOCK;
+    if (p + (size_t)un + (size_t)vl + 9 > data_end || sh > curlen) return SDB_CORRUPT_BLOCK;
+    size_t suf = p;
+    p += un;
+    e->vpos = base + p;
+    p += vl;
+    e->seq = rd_be(d + p, 8);
+    p += 8;
+    uint8_t f = d[p++];
+    if (!flags_ok(f)) return SDB_INVALID_ROW_FLAGS;
+    size_t need = ((f & SDB_FLAG_HAS_EXPIRE_TS) ? 8 : 0) + ((f & SDB_FLAG_HAS_CREATE_TS) ? 8 : 0);
+    if (p + need > data_end) return SDB_CORRUPT_BLOCK;
+    e->ets = e->cts = 0;
+    if (f & SDB_FLAG_HAS_EXPIRE_TS) { e->ets = (int64_t)rd_be(d + p, 8); p += 8; }
+    if (f & SDB_FLAG_HAS_CREATE_TS) { e->cts = (int64_t)rd_be(d + p, 8); p += 8; }
+    e->flags = f;
+    e->vlen = (f & SDB_FLAG_TOMBSTONE) ? 0 : vl;
+    if (!e->vlen) e->vpos = 0;
+    *klen = (size_t)sh + un;
+    *key = (uint8_t *)malloc(*klen ? *klen : 1);
+    memcpy(*key, cur, sh);
+    memcpy(*key + sh, d + suf, un);
+    *pos = p;
+    return SDB_OK;
+}
+
+sdb_status orc_decode_blocks_desc(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                                  uint16_t sst_version, const sdb_decoded_out *out) {
+    sdb_decode_summary *sm = out->summary;
+    memset(sm, 0, sizeof *sm);
+    if (sst_version != 1 && sst_version != 2) { sm->status = SDB_INVALID_VERSION; return SDB_INVALID_VERSION; }
+    sdb_status first_err = SDB_OK;
+    uint64_t *cnt = (uint64_t *)calloc(nblocks + 1, sizeof(uint64_t));
+    uint64_t n = 0, kb = 0;
+    out->key_off[0] = 0;
+    int overflow = 0;
+    for (uint64_t kk = nblocks; kk-- > 0;) {
+        const uint64_t s = block_off[kk], e = block_off[kk + 1];
+        const size_t len = (size_t)(e - s);
+        sdb_status st = SDB_OK;
+        /* the block's entries in yield order; keys malloc'd */
+        desc_ent *ents = NULL;
+        uint8_t **keys = NULL;
+        size_t ne = 0, cap = 0;
+#define PUSH(E, K) do { if (ne == cap) { cap = cap ? 2 * cap : 64; ents = (desc_ent *)realloc(ents, cap * sizeof *ents); \
+                         keys = (uint8_t **)realloc(keys, cap * sizeof *keys); } ents[ne] = (E); keys[ne] = (K); ne++; } while (0)
+        if (len < 4) st = SDB_CORRUPT_BLOCK;
+        else if (orc_crc32(blocks + s, len - 4) != (uint32_t)rd_be(blocks + e - 4, 4)) st = SDB_CHECKSUM_MISMATCH;
+        else {
+            const uint8_t *d = blocks + s;
+            const size_t blen = len - 4;
+            if (blen < 2) st = SDB_CORRUPT_BLOCK;
+            else {
+                const size_t count = (size_t)rd_be(d + blen - 2, 2);
+                if (2 + 2 * count > blen) st = SDB_CORRUPT_BLOCK;
+                else {
+                    const size_t data_end = blen - 2 - 2 * count;
+                    const uint8_t *offs = d + data_end;
+                    if (sst_version == 2) {
+                        for (size_t r = count; r-- > 0 && !st;) {
+                            /* seek_to_restart(r): the restart row's key, shared == 0 asserted */
+                            size_t p = (size_t)rd_be(offs + 2 * r, 2);
+                            const size_t rend = r + 1 < count ? (size_t)rd_be(offs + 2 * r + 2, 2) : data_end;
+                            uint32_t sh, un, vl;
+                            size_t q = p;
+                            if (!rd_varint(d, data_end, &q, &sh) || !rd_varint(d, data_end, &q, &un) ||
+                                !rd_varint(d, data_end, &q, &vl) || sh != 0 || q + un > data_end) { st = SDB_CORRUPT_BLOCK; break; }
+                            uint8_t *cur = (uint8_t *)malloc(un ? un : 1);
+                            memcpy(cur, d + q, un);
+                            size_t curlen = un;
+                            size_t r0 = ne;
+                            while (p < rend) { /* load_restart_region (:359-377) */
+                                desc_ent de;
+                                uint8_t *k;
+                                size_t kl;
+                                st = desc_row_v2(d, data_end, &p, cur, curlen, &k, &kl, &de, s);
+                                if (st) break;
+                                de.klen = (uint32_t)kl;
+                                free(cur);
+                                cur = (uint8_t *)malloc(kl ? kl : 1);
+                                memcpy(cur, k, kl);
+                                curlen = kl;
+                                PUSH(de, k);
+                            }
+                            free(cur);
+                            /* the region yields in reverse */
+                            for (size_t a = r0, b = ne; a + 1 < b; a++, b--) {
+                                desc_ent te = ents[a]; ents[a] = ents[b - 1]; ents[b - 1] = te;
+                                uint8_t *tk = keys[a]; keys[a] = keys[b - 1]; keys[b - 1] = tk;
+                            }
+                        }
+                    } else if (count > 0) {
+                        /* V1: the ascending decode, then reversed */
+                        if (data_end < 4) st = SDB_CORRUPT_BLOCK;
+                        else {
+                            size_t ov = (size_t)rd_be(d, 2), fk = (size_t)rd_be(d + 2, 2);
+                            if (ov != 0 || 4 + fk > data_end) st = SDB_CORRUPT_BLOCK;
+                            const uint8_t *first = d + 4;
+                            for (size_t i = count; i-- > 0 && !st;) {
+                                size_t p = (size_t)rd_be(offs + 2 * i, 2);
+                                if (p + 4 > data_end) { st = SDB_CORRUPT_BLOCK; break; }
+                                size_t pre = (size_t)rd_be(d + p, 2), sl = (size_t)rd_be(d + p + 2, 2);
+                                p += 4;
+                                if (p + sl + 9 > data_end) { st = SDB_CORRUPT_BLOCK; break; }
+                                size_t suf = p;
+                                p += sl;
+                                desc_ent de;
+                                de.seq = rd_be(d + p, 8);
+                                p += 8;
+                                uint8_t f = d[p++];
+                                if (!flags_ok(f)) { st = SDB_INVALID_ROW_FLAGS; break; }
+                                size_t need = ((f & SDB_FLAG_HAS_EXPIRE_TS) ? 8 : 0) + ((f & SDB_FLAG_HAS_CREATE_TS) ? 8 : 0);
+                                if (p + need > data_end) { st = SDB_CORRUPT_BLOCK; break; }
+                                de.ets = de.cts = 0;
+                                if (f & SDB_FLAG_HAS_EXPIRE_TS) { de.ets = (int64_t)rd_be(d + p, 8); p += 8; }
+                                if (f & SDB_FLAG_HAS_CREATE_TS) { de.cts = (int64_t)rd_be(d + p, 8); p += 8; }
+                                de.vlen = 0;
+                                de.vpos = 0;
+                                de.flags = f;
+                                if (f & SDB_FLAG_TOMBSTONE) de.flags = (uint8_t)(f & ~SDB_FLAG_HAS_EXPIRE_TS);
+                                else {
+                                    if (p + 4 > data_end) { st = SDB_CORRUPT_BLOCK; break; }
+                                    de.vlen = (uint32_t)rd_be(d + p, 4);
+                                    p += 4;
+                                    if (p + de.vlen > data_end) { st = SDB_CORRUPT_BLOCK; break; }
+                                    de.vpos = de.vlen ? s + p : 0;  /* empty values: 0, like emit_entry */
+                                }
+                                if (pre > fk) { st = SDB_CORRUPT_BLOCK; break; }
+                                uint8_t *k = (uint8_t *)malloc(pre + sl ? pre + sl : 1);
+                                memcpy(k, first, pre);
+                                memcpy(k + pre, d + suf, sl);
+                                de.klen = (uint32_t)(pre + sl);
+                                PUSH(de, k);
+                            }
+                        }
+                    }
+                }
+            }
+        }
+#undef PUSH
+        if (st) {
+            if (sm->num_bad_blocks < out->bad_cap) out->bad_block[sm->num_bad_blocks] = (uint32_t)kk;
+            sm->num_bad_blocks++;
+            first_err = st;  /* blocks go last to first: the lowest failing index's status remains */
+        } else {
+            for (size_t i = 0; i < ne; i++) {
+                if (n >= out->cap_entries || kb + ents[i].klen > out->key_arena_cap) { overflow = 1; break; }
+                memcpy(out->key_arena + kb, keys[i], ents[i].klen);
+                out->key_off[n] = kb;
+                kb += ents[i].klen;
+                out->key_off[n + 1] = kb;
+                out->val_off[n] = ents[i].vpos;
+                out->val_len[n] = ents[i].vlen;
+                out->seq[n] = ents[i].seq;
+                out->flags[n] = ents[i].flags;
+                out->create_ts[n] = (ents[i].flags & SDB_FLAG_HAS_CREATE_TS) ? ents[i].cts : 0;
+                out->expire_ts[n] = (ents[i].flags & SDB_FLAG_HAS_EXPIRE_TS) ? ents[i].ets : 0;
+                n++;
+            }
+            cnt[kk] = ne;
+        }
+        for (size_t i = 0; i < ne; i++) free(keys[i]);
+        free(keys);
+        free(ents);
+    }
+    uint64_t acc = 0;
+    for (uint64_t k = 0; k < nblocks; k++) {
+        out->block_entry_start[k] = acc;
+        acc += cnt[k];
+    }
+    out->block_entry_start[nblocks] = acc;
+    free(cnt);
+    sm->num_entries = n;
+    sm->key_bytes = kb;
+    sm->status = overflow ? SDB_INVALID_ARGUMENT : first_err;
+    return (sdb_status)sm->status;
+}

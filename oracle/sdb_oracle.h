@@ -62,6 +62,12 @@ int orc_bloom_might_match(const uint8_t *bitmap, uint64_t bitmap_bytes, uint32_t
 sdb_status orc_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
                              uint16_t sst_version, const sdb_decoded_out *out);
 
+/* The same blocks in descending iteration order (SstIterator Descending over
+ * DescendingBlockIteratorV2 / BlockIterator Descending); block_entry_start keeps the ascending
+ * prefix of the per-block counts (block k's entries: [N - bes[k + 1], N - bes[k])). */
+sdb_status orc_decode_blocks_desc(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                                  uint16_t sst_version, const sdb_decoded_out *out);
+
 /* Point lookups on one SST (host pointers in `sst`): the same contract as sdb_sst_lookup, following
  * filter.rs:124-136, partitioned_keyspace.rs:16-110, sst_iter.rs:501-516, block_iterator_v2.rs:
  * 138-469 and block_iterator.rs:130-190 literally (materialised keys). */

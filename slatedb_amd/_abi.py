@@ -186,6 +186,8 @@ class CompactedSst(C.Structure):
     ]
 
 
+DECODE_DESCENDING = 1
+
 LOOKUP_FILTERED, LOOKUP_EXHAUSTED, LOOKUP_POSITIONED, LOOKUP_FOUND = 0, 1, 2, 3
 
 SST_COMPACTED, SST_WAL = 0, 1
@@ -220,6 +222,8 @@ SIGNATURES = {
     "sdb_decode_blocks": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint16,
                                     C.POINTER(DecodedOut), C.c_void_p, C.c_uint64, C.c_void_p]),
     "sdb_decode_blocks_at": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint16,
+                                       C.POINTER(DecodedOut), C.c_void_p, C.c_uint64, C.c_void_p]),
+    "sdb_decode_blocks_ex": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint16, C.c_uint32,
                                        C.POINTER(DecodedOut), C.c_void_p, C.c_uint64, C.c_void_p]),
     "sdb_sst_lookup_workspace_bytes": (C.c_uint64, [C.c_uint64, C.c_uint64]),
     "sdb_sst_lookup": (C.c_int, [C.POINTER(SstView), C.c_void_p, C.c_void_p, C.c_uint64, C.c_int32,

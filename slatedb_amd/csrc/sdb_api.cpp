@@ -371,7 +371,7 @@ uint64_t sdb_decode_workspace_bytes(uint64_t nblocks) { return decode_workspace_
 
 static sdb_status decode_common(const uint8_t *blocks, const uint64_t *block_off, const uint64_t *block_end,
                                 uint64_t nblocks, uint16_t sst_version, const sdb_decoded_out *out, void *workspace,
-                                uint64_t workspace_bytes, void *stream) {
+                                uint64_t workspace_bytes, void *stream, uint32_t flags = 0) {
     if (!out || !out->summary || !out->block_entry_start) return SDB_INVALID_ARGUMENT;
     if (sst_version != 1 && sst_version != 2) return SDB_INVALID_VERSION;  // block_iterator.rs:60-77
     if (nblocks && (!blocks || !block_off)) return SDB_INVALID_ARGUMENT;
@@ -384,6 +384,7 @@ static sdb_status decode_common(const uint8_t *blocks, const uint64_t *block_off
     a.block_end = block_end;
     a.nblocks = nblocks;
     a.version = sst_version;
+    a.descending = (flags & SDB_DECODE_DESCENDING) ? 1u : 0u;
     a.out = *out;
     a.cnt = carve<uint64_t>(workspace, wl.cnt);
     a.kbytes = carve<uint64_t>(workspace, wl.kbytes);
@@ -407,6 +408,15 @@ sdb_status sdb_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, u
                              uint16_t sst_version, const sdb_decoded_out *out, void *workspace,
                              uint64_t workspace_bytes, void *stream) {
     return decode_common(blocks, block_off, nullptr, nblocks, sst_version, out, workspace, workspace_bytes, stream);
+}
+
+sdb_status sdb_decode_blocks_ex(const uint8_t *arena, const uint64_t *block_start, const uint64_t *block_end,
+                                uint64_t nblocks, uint16_t sst_version, uint32_t flags, const sdb_decoded_out *out,
+                                void *workspace, uint64_t workspace_bytes, void *stream) {
+    if (flags & ~(uint32_t)SDB_DECODE_DESCENDING) return SDB_INVALID_ARGUMENT;
+    if (block_end && nblocks && !block_start) return SDB_INVALID_ARGUMENT;
+    return decode_common(arena, block_start, block_end, nblocks, sst_version, out, workspace, workspace_bytes, stream,
+                         flags);
 }
 
 sdb_status sdb_decode_blocks_at(const uint8_t *arena, const uint64_t *block_start, const uint64_t *block_end,

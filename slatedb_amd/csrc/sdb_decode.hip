@@ -603,6 +603,21 @@ SDB_DEV Tally tally_v1(const BlockViewT<P> &v) {
     return t;
 }
 
+// Descending iteration (DescendingBlockIteratorV2, block_iterator_v2.rs:318-430) decodes each restart
+// region from its restart (asserting shared == 0 there, :71-93) and yields it in reverse.  For a
+// regular block (regions that start at restarts with shared == 0 and end exactly at the next one)
+// that is the ascending decode reversed; a block without restarts yields nothing; any other layout
+// is reported as SDB_CORRUPT_BLOCK (the reference would assert or read rows across regions).
+SDB_DEV void desc_rule(uint32_t restarts, Tally &t) {
+    if (t.status) return;
+    if (restarts == 0) {
+        t.entries = t.key_bytes = 0;
+        t.sequential = false;
+    } else if (t.sequential) {
+        t.status = SDB_CORRUPT_BLOCK;
+    }
+}
+
 // D1 count.  LDS: the CRC tables at address 0 (sdb_crc.h: this kernel has no static LDS), then one
 // region of kDecWaveLds per wave.
 __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
@@ -633,6 +648,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
             if (!v.status) {
                 if (a.version == 1) t = tally_v1(v);
                 else if (!tally_v2_fast(v, t, a.rowpos + 128 * k, a.rcnt + k)) t = tally_v2(v);
+                if (a.descending && a.version == 2) desc_rule(v.count, t);
             }
             DEC_T(t2);
             DEC_ACC(0, 0, t1 - t0);
@@ -642,6 +658,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
             const BlockView v = load_block(a, k, stage, crc);
             t.status = v.status;
             if (!v.status) t = (a.version == 2) ? tally_v2(v) : tally_v1(v);
+            if (!v.status && a.descending && a.version == 2) desc_rule(v.count, t);
         }
         if (lane_id() == 0) {
             if (t.status) {
@@ -1167,6 +1184,58 @@ __global__ void k_dec_finish(DecodeArgs a) {
     if (threadIdx.x == 0) dec_finish(a);
 }
 
+// --- descending order: reverse the decoded columns in place ------------------------------------------
+// Entry i <-> N - 1 - i for the fixed-width columns; key_off'[i] = KB - key_off[N - i]; the key arena is
+// reversed byte-wise, then each key's bytes are reversed back.  N and KB come from the summary.
+constexpr uint32_t kDescGrid = 2048, kDescThreads = 256;
+SDB_DEV bool desc_sizes(const DecodeArgs &a, uint64_t *N, uint64_t *KB) {
+    const sdb_decode_summary *sm = a.out.summary;
+    if (sm->status == SDB_INVALID_ARGUMENT) return false;  // nothing was written (capacity)
+    *N = sm->num_entries;
+    *KB = sm->key_bytes;
+    return true;
+}
+template <typename T>
+SDB_DEV void swap_at(T *p, uint64_t i, uint64_t j) {
+    const T x = p[i];
+    p[i] = p[j];
+    p[j] = x;
+}
+__global__ __launch_bounds__(kDescThreads) void k_desc_cols(DecodeArgs a) {
+    uint64_t N, KB;
+    if (!desc_sizes(a, &N, &KB)) return;
+    const sdb_decoded_out &o = a.out;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; 2 * i <= N; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t j = N - i;  // key_off has N + 1 entries
+        const uint64_t ki = o.key_off[i], kj = o.key_off[j];
+        o.key_off[i] = KB - kj;
+        o.key_off[j] = KB - ki;
+        if (2 * i + 1 < N) {  // the N fixed-width entries: i <-> N - 1 - i
+            const uint64_t m = N - 1 - i;
+            swap_at(o.val_off, i, m);
+            swap_at(o.val_len, i, m);
+            swap_at(o.seq, i, m);
+            swap_at(o.flags, i, m);
+            swap_at(o.create_ts, i, m);
+            swap_at(o.expire_ts, i, m);
+        }
+    }
+}
+__global__ __launch_bounds__(kDescThreads) void k_desc_bytes(DecodeArgs a) {
+    uint64_t N, KB;
+    if (!desc_sizes(a, &N, &KB)) return;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; 2 * i + 1 < KB; i += (uint64_t)gridDim.x * blockDim.x)
+        swap_at(a.out.key_arena, i, KB - 1 - i);
+}
+__global__ __launch_bounds__(kDescThreads) void k_desc_keys(DecodeArgs a) {
+    uint64_t N, KB;
+    if (!desc_sizes(a, &N, &KB)) return;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < N; j += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t lo = a.out.key_off[j], hi = a.out.key_off[j + 1];
+        while (lo + 1 < hi) swap_at(a.out.key_arena, lo++, --hi);
+    }
+}
+
 hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
     hipLaunchKernelGGL(k_dec_init, dim3(1), dim3(64), 0, st, a);
     static bool attrs = false;
@@ -1200,6 +1269,11 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
     }
     if (a.nblocks) hipLaunchKernelGGL(k_dec_emit, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
     if (!a.small) hipLaunchKernelGGL(k_dec_finish, dim3(1), dim3(64), 0, st, a);
+    if (a.descending && a.nblocks) {
+        hipLaunchKernelGGL(k_desc_cols, dim3(kDescGrid), dim3(kDescThreads), 0, st, a);
+        hipLaunchKernelGGL(k_desc_bytes, dim3(kDescGrid), dim3(kDescThreads), 0, st, a);
+        hipLaunchKernelGGL(k_desc_keys, dim3(kDescGrid), dim3(kDescThreads), 0, st, a);
+    }
     return hipGetLastError();
 }
 

@@ -576,6 +576,16 @@ def decode_blocks_at_device(arena, block_start, block_end, nblocks, out, sst_ver
         raise SdbError(st, "sdb_decode_blocks_at")
 
 
+def decode_blocks_ex_device(arena, block_start, block_end, nblocks, out, sst_version=2, descending=False, stream=None):
+    """Enqueue sdb_decode_blocks_ex (block_end None: contiguous blocks, block_start has nblocks + 1 entries)."""
+    flags = _abi.DECODE_DESCENDING if descending else 0
+    st = lib().sdb_decode_blocks_ex(arena.data_ptr(), block_start.data_ptr(),
+                                    None if block_end is None else block_end.data_ptr(), nblocks, sst_version, flags,
+                                    C.byref(out.out), out.workspace.data_ptr(), out.workspace.numel(), _sp(stream))
+    if st:
+        raise SdbError(st, "sdb_decode_blocks_ex")
+
+
 LOOKUP_FIELDS = (("state", "uint8"), ("status", "int32"), ("block", "int32"), ("entry", "int32"),
                  ("key_len", "int32"), ("val_off", "int64"), ("val_len", "int32"), ("seq", "int64"),
                  ("flags", "uint8"), ("create_ts", "int64"), ("expire_ts", "int64"))
