@@ -236,15 +236,45 @@ def e2e_bench(reps):
     enc.close()
 
 
+def compact_bench(reps):
+    """f2: a compaction job on the device -- 4 L0 SSTs of the configs[1] shape (D1, 578,524 x 16 B key /
+    100 B value each, key ranges interleaved) merged, retention applied, cut at max_sst_size = 256 MiB
+    (config.rs:1383) and encoded (4 KiB blocks, 10 bits/key bloom); runs resident in HBM."""
+    from slatedb_amd.batch import Run
+    hosts = [datasets.d1(sst_index=j) for j in range(4)]
+    druns = [runtime.DeviceRun.from_host(Run.from_batch(h)) for h in hosts]
+    prm = runtime.params(block_size=4096, sst_version=2, bloom_bits_per_key=10)
+    ret = _abi.Retention(0, 0, 0, 1, 0, 0, 0, 0)  # retention_min_seq Some(0), compaction_clock_tick 0
+    comp = runtime.Compactor()
+    logical = sum(h.logical_bytes() for h in hosts)
+    st, ns = comp.run(druns, ret, prm, 256 << 20)
+    assert st == 0, st
+    torch.cuda.synchronize()
+    walls = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        st, ns = comp.run(druns, ret, prm, 256 << 20)
+        walls.append((time.perf_counter() - t0) * 1e3)
+        assert st == 0
+    ms = float(np.median(walls))
+    merged, msum = comp.merged()
+    print(json.dumps({"what": "compaction job (f2): 4 x configs[1] L0 SSTs -> merge + retention + cuts + encode",
+                      "entries_in": int(msum.num_in), "entries_out": int(msum.num_out), "output_ssts": ns,
+                      "logical_bytes_in": logical, "ms_wall": round(ms, 3),
+                      "GiB_per_s_logical": round(logical / (ms * 1e-3) / 2**30, 2)}), flush=True)
+    comp.close()
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--decode", action="store_true")
     p.add_argument("--bloom", action="store_true")
     p.add_argument("--e2e", action="store_true")
+    p.add_argument("--compact", action="store_true")
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--no-granular", action="store_true", help="decode: skip the 2 MiB granularity run")
     a = p.parse_args()
-    allp = not (a.decode or a.bloom or a.e2e)
+    allp = not (a.decode or a.bloom or a.e2e or a.compact)
     torch.cuda.set_device(0)
     runtime.require_device()
     if a.bloom or allp:
@@ -253,6 +283,8 @@ def main():
         decode_bench(a.reps, not a.no_granular)
     if a.e2e or allp:
         e2e_bench(a.reps)
+    if a.compact or allp:
+        compact_bench(max(3, a.reps // 4))
 
 
 if __name__ == "__main__":

@@ -283,14 +283,22 @@ __global__ __launch_bounds__(kMergeThreads) void k_mg_scan(MergeArgs a) {
     }
 }
 
+// Byte ranges at any alignment: 16-byte unaligned vector loads / stores (unaligned global access is
+// enabled on gfx9), then the tail.
+typedef uint32_t u32x4_u __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t u32x2_u __attribute__((ext_vector_type(2), aligned(1)));
+typedef uint32_t u32_u __attribute__((aligned(1)));
 SDB_DEV void copy_bytes(uint8_t *dst, const uint8_t *src, uint64_t n) {
     uint64_t o = 0;
-    // align the destination to 4 bytes, then dword stores from unaligned 8-byte loads
-    while (o < n && ((uintptr_t)(dst + o) & 3)) {
-        dst[o] = src[o];
-        o++;
+    for (; o + 16 <= n; o += 16) *(u32x4_u *)(dst + o) = *(const u32x4_u *)(src + o);
+    if (o + 8 <= n) {
+        *(u32x2_u *)(dst + o) = *(const u32x2_u *)(src + o);
+        o += 8;
     }
-    for (; o + 4 <= n; o += 4) *(uint32_t *)(dst + o) = (uint32_t)load8(src + o, 4);
+    if (o + 4 <= n) {
+        *(u32_u *)(dst + o) = *(const u32_u *)(src + o);
+        o += 4;
+    }
     for (; o < n; o++) dst[o] = src[o];
 }
 
