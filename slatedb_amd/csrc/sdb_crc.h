@@ -195,4 +195,69 @@ SDB_DEV uint32_t wave_crc_image_ra(const lu8 *img, uint32_t Lc) {
     return crc_tree_combine(c) ^ 0xFFFFFFFFu;
 }
 
+// --- bank-replicated byte table (decode count pass) ------------------------------------------------
+// The slicing-by-8 lookups above index a table by a data byte, so the 32 lanes of a ds_read_b32 group
+// hit banks byte % 32 at random: ~3.7 LDS cycles per group instead of 1 (measured: 58 % of the count
+// pass's LDS cycles were bank conflicts, and LDS was its bound).  Here table 0 (c = T[c & 0xFF] ^ c >> 8)
+// is stored once per bank: entry i of copy b at byte 128 i + 4 b, and lane l reads copy l % 32, so every
+// lookup is conflict-free.  32 KiB; one lookup and four VALU per byte.
+constexpr uint32_t kCrcRepLds = 32 * 1024;
+
+SDB_DEV void crc_rep_to_lds(lu32 *rep) {
+    for (uint32_t q = threadIdx.x; q < 256 * 32; q += blockDim.x) rep[q] = c_crc.t[0][q >> 5];
+}
+
+template <uint32_t BASE>
+SDB_DEV uint32_t crc_rep_step(uint32_t c, uint32_t lb) {
+    uint32_t a;  // 128 * (c & 0xFF) in one op
+    asm("v_lshlrev_b32_sdwa %0, 7, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(a) : "v"(c));
+    return *(const lu32 *)(uintptr_t)((a | lb) + BASE) ^ (c >> 8);
+}
+
+// Raw CRC of one 64-byte segment (16 little-endian dwords): two 32-byte byte-at-a-time chains through
+// the replicated table at LDS BASE, combined by x^256 (the k_emit layout's tables at LDS 8 KiB).
+template <uint32_t BASE>
+SDB_DEV uint32_t crc_seg64_rep(const uint32_t (&m)[16]) {
+    const uint32_t lb = ((uint32_t)lane_id() & 31) << 2;
+    uint32_t ca = 0, cb = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        ca ^= m[i];
+        cb ^= m[8 + i];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            ca = crc_rep_step<BASE>(ca, lb);
+            cb = crc_rep_step<BASE>(cb, lb);
+        }
+    }
+    return crc_mul256_lds(ca) ^ cb;
+}
+
+// wave_crc_image_ra with the per-segment CRC through the replicated table at LDS BASE.
+template <uint32_t BASE>
+SDB_DEV uint32_t wave_crc_image_rep(const lu8 *img, uint32_t Lc) {
+    const uint32_t l = (uint32_t)lane_id();
+    const int s = (int)Lc - 64 * (64 - (int)l);
+    uint32_t c = 0;
+    if (s > -64) {
+        const lu128 *w = (const lu128 *)(uintptr_t)(lds_addr((const void *)img) + (uint32_t)(s - (int)(Lc & 15)));
+        uint32_t x[20], m[16];
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            const u32x4 v = w[i];
+            x[4 * i] = v.x;
+            x[4 * i + 1] = v.y;
+            x[4 * i + 2] = v.z;
+            x[4 * i + 3] = v.w;
+        }
+        const uint32_t q = (Lc >> 2) & 3, r = Lc & 3;
+        if (q == 0) realign16<0>(x, r, m);
+        else if (q == 1) realign16<1>(x, r, m);
+        else if (q == 2) realign16<2>(x, r, m);
+        else realign16<3>(x, r, m);
+        c = crc_seg64_rep<BASE>(m);
+    }
+    return crc_tree_combine(c) ^ 0xFFFFFFFFu;
+}
+
 }  // namespace sdb

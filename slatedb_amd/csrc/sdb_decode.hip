@@ -35,6 +35,11 @@ constexpr uint32_t kDecGuard = 64;                       // zero lead-in of the 
 constexpr uint32_t kDecWaveLds = kDecGuard + kDecImg + kDecKeys;
 constexpr uint32_t kDecLds = kCrcTablesLds + (kDecThreads / 64) * kDecWaveLds;
 constexpr uint32_t kDecCap = kDecWaveLds - kDecGuard;
+// count pass: the CRC tables, the bank-replicated byte table (sdb_crc.h), then per wave a guard + image
+constexpr uint32_t kCntRep = kCrcTablesLds;
+constexpr uint32_t kCntWaveLds = kDecGuard + kDecImg;
+constexpr uint32_t kCntLds = kCrcTablesLds + kCrcRepLds + (kDecThreads / 64) * kCntWaveLds;
+static_assert(kCntLds <= 160 * 1024, "count pass LDS");
 constexpr uint32_t kRowTmp = kDecKeys - 256;  // emit: row positions of the lane-per-row path (4 x 32 u16) in kbuf
 typedef __attribute__((address_space(3))) uint16_t lu16;  // other blocks: generic staging per wave; larger ones parse from HBM
 
@@ -235,7 +240,7 @@ typedef BlockViewT<const uint8_t *> BlockView;
 typedef BlockViewT<const lu8 *> LdsBlockView;
 
 // Stage + CRC-check block k; fills the view.  Called by a whole wave.
-SDB_DEV BlockView load_block(const DecodeArgs &a, uint64_t k, uint8_t *stage, const uint32_t (*crc)[256]) {
+SDB_DEV BlockView load_block(const DecodeArgs &a, uint64_t k, uint8_t *stage, const uint32_t (*crc)[256], uint32_t cap = kDecCap) {
     BlockView v{};
     const uint64_t s = a.block_off[k], e = block_end_of(a, k);
     const uint64_t len = e - s;
@@ -247,7 +252,7 @@ SDB_DEV BlockView load_block(const DecodeArgs &a, uint64_t k, uint8_t *stage, co
     const uint32_t blen = (uint32_t)(len - 4);
     uint32_t c;
     const uint8_t *d;
-    if (len + 32 <= kDecCap) {
+    if (len + 32 <= cap) {
         // 16-byte granules covering [s, e); stage[pad + i] = g[i]
         uint64_t a0 = s & ~15ull, a1 = (e + 15) & ~15ull;
         uint32_t nchunk = (uint32_t)((a1 - a0) >> 4);
@@ -311,21 +316,51 @@ SDB_DEV bool dec_fast(uint64_t s, uint64_t e) {
     return e >= s && len >= 8 && (s & 15) + len <= kDecImg && (s & 15) + len - 4 <= 4096;
 }
 
-SDB_DEV LdsBlockView stage_lds(const DecodeArgs &a, uint64_t s, uint64_t e, lu8 *img, bool check) {
+// A block's 16-byte granules in registers (lane l holds granules l, l + 64, ...): loaded one block
+// ahead so the HBM latency overlaps the previous block's work.
+constexpr int kGranRegs = 5;  // ceil(kDecImg / 16 / 64)
+struct Granules {
+    uint4 g[kGranRegs];
+};
+SDB_DEV void gran_load(const DecodeArgs &a, uint64_t s, uint64_t e, Granules &r) {
+    const uint32_t l = (uint32_t)lane_id();
+    const uint64_t a0 = s & ~15ull;
+    const uint32_t ng = (uint32_t)((((e + 15) & ~15ull) - a0) >> 4);
+    const uint4 *src = (const uint4 *)(a.blocks + a0);
+#pragma unroll
+    for (int i = 0; i < kGranRegs; i++) {
+        const uint32_t q = l + 64 * i;
+        if (q < ng) r.g[i] = src[q];
+    }
+}
+SDB_DEV void gran_store(uint64_t s, uint64_t e, const Granules &r, lu8 *img) {
+    const uint32_t l = (uint32_t)lane_id();
+    const uint32_t ng = (uint32_t)((((e + 15) & ~15ull) - (s & ~15ull)) >> 4);
+#pragma unroll
+    for (int i = 0; i < kGranRegs; i++) {
+        const uint32_t q = l + 64 * i;
+        if (q < ng) {
+            u32x4 w;
+            w.x = r.g[i].x;
+            w.y = r.g[i].y;
+            w.z = r.g[i].z;
+            w.w = r.g[i].w;
+            ((lu128 *)img)[q] = w;
+        }
+    }
+}
+
+SDB_DEV LdsBlockView stage_lds(const DecodeArgs &a, uint64_t s, uint64_t e, lu8 *img, bool check, bool rep = false,
+                               const Granules *pre = nullptr) {
     LdsBlockView v{};
     const uint32_t l = (uint32_t)lane_id();
     const uint32_t p0 = (uint32_t)(s & 15), len = (uint32_t)(e - s), blen = len - 4, Lc = p0 + blen;
-    const uint64_t a0 = s & ~15ull;
-    const uint32_t ng = (uint32_t)((((e + 15) & ~15ull) - a0) >> 4);
-    const uint4 *src = (const uint4 *)(a.blocks + a0);  // aligned granules that hold block bytes
-    for (uint32_t q = l; q < ng; q += 64) {
-        const uint4 g = src[q];
-        u32x4 w;
-        w.x = g.x;
-        w.y = g.y;
-        w.z = g.z;
-        w.w = g.w;
-        ((lu128 *)img)[q] = w;
+    if (pre) {
+        gran_store(s, e, *pre, img);
+    } else {
+        Granules g;
+        gran_load(a, s, e, g);
+        gran_store(s, e, g, img);
     }
     wave_sync_d();
     const lu8 *d = img + p0;
@@ -336,7 +371,12 @@ SDB_DEV LdsBlockView stage_lds(const DecodeArgs &a, uint64_t s, uint64_t e, lu8 
         if (l < p0) img[l] = 0;
         if (l < 4) img[p0 + l] ^= 0xFF;
         wave_sync_d();
-        const uint32_t c = wave_crc_image_ra(img, Lc);  // zeros before img (the guard) and before p0
+        // zeros before img (the guard) and before p0
+#ifdef SDB_EXP_NO_CRC  // diagnostic: no CRC (every block accepted)
+        const uint32_t c = stored;
+#else
+        const uint32_t c = rep ? wave_crc_image_rep<kCntRep>(img, Lc) : wave_crc_image_ra(img, Lc);
+#endif
         wave_sync_d();
         if (l < 4) img[p0 + l] ^= 0xFF;
         wave_sync_d();
@@ -504,57 +544,143 @@ SDB_DEV uint32_t lds_read4(const lu8 *p) {
     return __builtin_amdgcn_alignbyte(d[1], d[0], sh);
 }
 
+SDB_DEV uint32_t lds_byte(const lu8 *p) { return *p; }
+
+// The region walks as one wave-uniform loop (no per-lane breaks: a lane that finishes or fails just
+// stops advancing), so a step is ~20 instructions instead of ~80 of exec-mask bookkeeping and branches
+// (the walk was issue-bound with 1 - 4 live lanes per wave).
 SDB_DEV bool tally_v2_fast(const LdsBlockView &v, Tally &t, uint16_t *rowpos, uint64_t *rcnt) {
-    const int l = lane_id();
+    const uint32_t l = (uint32_t)lane_id();
     const uint32_t R = v.count;
-    if (R == 0 || rd_be(v.offs, 2) != 0) return false;
-    uint32_t my_entries = 0, my_kb = 0, my_kmax = 0;
-    bool ok = true;
-    for (uint32_t q = l; q < R && ok; q += 64) {
-        const uint32_t pos = (uint32_t)rd_be(v.offs + 2 * q, 2);
-        const uint32_t end = (q + 1 < R) ? (uint32_t)rd_be(v.offs + 2 * q + 2, 2) : v.data_end;
-        if (end <= pos || end > v.data_end) {
-            ok = false;
-            break;
-        }
-        uint32_t p = pos, prevlen = 0, fl = 0, bad = 0;
-        bool first = true;
-        while (p < end) {
-            const uint32_t h = lds_read4(v.d + p);
-            // the previous row's flags (read one step earlier, off the chain): value, tombstone or merge
-            // only (no timestamps, not both kinds, no unknown bits)
-            bad |= (fl != 0 && fl != SDB_FLAG_TOMBSTONE && fl != SDB_FLAG_MERGE_OPERAND) ? 1u : 0u;
-            const uint32_t sh = h & 0xFF, un = (h >> 8) & 0xFF, vl = (h >> 16) & 0xFF;
-            if ((h & 0x808080u) || (first && sh) || (!first && sh > prevlen) || p + 12 + un + vl > end) {
-                ok = false;
-                break;
-            }
-            fl = v.d[p + 11 + un + vl];
-            first = false;
-            prevlen = sh + un;
-            if (q < 4 && my_entries < 32) rowpos[q * 32 + my_entries] = (uint16_t)p;
-            my_kmax = prevlen > my_kmax ? prevlen : my_kmax;
-            my_entries++;
-            my_kb += prevlen;
-            p += 12 + un + vl;
-        }
-        bad |= (fl != 0 && fl != SDB_FLAG_TOMBSTONE && fl != SDB_FLAG_MERGE_OPERAND) ? 1u : 0u;
-        if (p != end || bad) ok = false;
+    if (R == 0 || R > 64 || rd_be(v.offs, 2) != 0) return false;
+    uint32_t p = 0, end = 0, bad = 0;
+    if (l < R) {
+        p = (uint32_t)rd_be(v.offs + 2 * l, 2);
+        end = (l + 1 < R) ? (uint32_t)rd_be(v.offs + 2 * l + 2, 2) : v.data_end;
+        if (end <= p || end > v.data_end) bad = 1;
     }
-    if (__ballot(!ok) != 0) return false;
-    t.entries = wave_sum((uint64_t)my_entries);
-    t.key_bytes = wave_sum((uint64_t)my_kb);
+    uint32_t ne = 0, kb = 0, kmax = 0, prevlen = 0, fl = 0;
+    const uint32_t rec = (l < 4) ? 32u : 0u;  // positions recorded for regions 0..3, <= 32 rows each
+    uint16_t *rp = rowpos + 32 * l;
+    // every condition below is bit arithmetic on 0/1 values (no short-circuit), so the step compiles
+    // to straight-line selects; the only branches are the loop's and the position store's
+    constexpr uint32_t kFlagsOk = (1u << 0) | (1u << SDB_FLAG_TOMBSTONE) | (1u << SDB_FLAG_MERGE_OPERAND);
+    for (;;) {
+        const uint32_t act = (uint32_t)(p < end) & (bad ^ 1u);
+        if (__ballot(act != 0) == 0) break;
+        const uint32_t h = lds_read4(v.d + p);
+        const uint32_t sh = h & 0xFF, un = (h >> 8) & 0xFF, vl = (h >> 16) & 0xFF;
+        const uint32_t nx = p + 12 + un + vl, klen = sh + un;
+        // the previous row's flags (read one step earlier): value, tombstone or merge only
+        const uint32_t fbad = ((kFlagsOk >> (fl & 31)) & 1u) ^ 1u | (uint32_t)(fl > 31);
+        const uint32_t lim = ne ? prevlen : 0u;
+        const uint32_t rbad = (uint32_t)((h & 0x808080u) != 0) | (uint32_t)(sh > lim) | (uint32_t)(nx > end);
+        const uint32_t fpos = nx - 1 < end ? nx - 1 : end;
+        const uint32_t fnew = lds_byte(v.d + fpos);
+        if (act && ne < rec) rp[ne] = (uint16_t)p;
+        bad = act ? (fbad | rbad) : bad;
+        fl = act ? fnew : fl;
+        kmax = act && klen > kmax ? klen : kmax;
+        kb += act ? klen : 0u;
+        prevlen = act ? klen : prevlen;
+        ne += act;
+        p = act ? nx : p;
+    }
+    bad |= (fl != 0 && fl != SDB_FLAG_TOMBSTONE && fl != SDB_FLAG_MERGE_OPERAND) ? 1u : 0u;
+    if (p != end) bad = 1;
+    if (__ballot(l < R && bad) != 0) return false;
+    t.entries = wave_sum((uint64_t)ne);
+    t.key_bytes = wave_sum((uint64_t)kb);
     t.status = 0;
     t.sequential = false;
     // the emit pass parses lane = row straight from the recorded positions when the block has <= 4
     // regions of <= 32 rows, <= 64 rows and keys of <= 16 bytes
-    const uint32_t mx = wave_max((uint32_t)l < R ? my_entries : 0u), kmx = wave_max(my_kmax);
+    const uint32_t mx = wave_max(l < R ? ne : 0u), kmx = wave_max(kmax);
     uint64_t c = ~0ull;
     if (R <= 4 && mx <= 32 && t.entries <= 64 && kmx <= 16) {
         c = 0;
-        for (uint32_t q = 0; q < R; q++) c |= (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)my_entries, (int)q) << (16 * q);
+        for (uint32_t q = 0; q < R; q++) c |= (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)ne, (int)q) << (16 * q);
     }
     if (l == 0) *rcnt = c;
+    return true;
+}
+
+// Speculative lane-per-row parse of a block of <= 4 restart regions (the common 4 KiB shape: 16-row
+// restart intervals give 3 regions).  Lane group q (G = 64 / 16 / ... lanes) takes region q, lane i of
+// it row i.  Row positions are guessed from the lengths of rows 0 and 1 (c_i = p_1 + (i - 1) L_1), every
+// lane reads its header, and the guesses are checked against the previous lane's row end; the first
+// wrong guess of a group shifts the guesses after it by its error (right for a single row of another
+// length, e.g. a key-counter carry), for at most four rounds.  The fixed point is exactly the walk of
+// BlockIteratorV2::next (block_iterator_v2.rs:235-267) over regular rows; anything else (no
+// convergence, more rows than lanes, multi-byte varints, timestamps, bad flags) returns false and the
+// caller walks the block.  All lanes work, vs 1 - 4 lanes stepping row by row.
+SDB_DEV uint32_t bperm(uint32_t lane, uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lane << 2), (int)v); }
+
+SDB_DEV bool tally_v2_spec(const LdsBlockView &v, Tally &t, uint16_t *rowpos, uint64_t *rcnt) {
+    const uint32_t l = (uint32_t)lane_id();
+    const uint32_t R = v.count;
+    if (R == 0 || R > 4 || rd_be(v.offs, 2) != 0) return false;
+    const uint32_t lg = R == 1 ? 6u : (R == 2 ? 5u : 4u), G = 1u << lg;
+    const uint32_t q = l >> lg, i = l & (G - 1);
+    const bool grp = q < R;
+    const uint64_t gmask = lg == 6 ? ~0ull : (((1ull << G) - 1) << (q * G));
+    uint32_t pos = 0, end = 0;
+    if (grp) {
+        pos = (uint32_t)rd_be(v.offs + 2 * q, 2);
+        end = (q + 1 < R) ? (uint32_t)rd_be(v.offs + 2 * q + 2, 2) : v.data_end;
+    }
+    if (__ballot(grp && (end <= pos || end > v.data_end)) != 0) return false;
+    constexpr uint32_t kEnd = 0xFFFFFFFFu;
+    // initial guesses from the lengths of rows 0 and 1 (reads shared by the group's lanes)
+    const uint32_t h0 = lds_read4(v.d + (grp ? pos : 0u));
+    const uint32_t p1 = pos + 12 + ((h0 >> 8) & 0xFF) + ((h0 >> 16) & 0xFF);
+    const uint32_t h1 = lds_read4(v.d + (grp && p1 < end ? p1 : 0u));
+    const uint32_t L1 = 12 + ((h1 >> 8) & 0xFF) + ((h1 >> 16) & 0xFF);
+    uint32_t c = i == 0 ? pos : p1 + (i - 1) * L1;
+    uint32_t h = 0, n = 0, live = 0;
+    for (int round = 0;; round++) {
+        live = grp && c < end ? 1u : 0u;
+        h = lds_read4(v.d + (live ? c : 0u));
+        n = c + 12 + ((h >> 8) & 0xFF) + ((h >> 16) & 0xFF);
+        const uint32_t n_prev = bperm(l - 1, n), live_prev = bperm(l - 1, live);
+        const uint32_t exp = i == 0 ? pos : (live_prev && n_prev < end ? n_prev : kEnd);
+        const bool mism = grp && (exp == kEnd ? live != 0 : c != exp);
+        const uint64_t M = __ballot(mism);
+        if (M == 0) break;
+        if (round == 3) return false;
+        const uint64_t mg = M & gmask;
+        const uint32_t f = mg ? (uint32_t)__builtin_ctzll(mg) : 0u;
+        const uint32_t fe = bperm(f, exp), fc = bperm(f, c);
+        if (mg && l >= f) c = fe == kEnd ? kEnd : c + (fe - fc);
+    }
+    // the converged rows: fast shape and regular
+    const uint32_t sh = h & 0xFF, un = (h >> 8) & 0xFF, klen = sh + un;
+    const uint32_t kprev = bperm(l - 1, klen);
+    const uint32_t fl = lds_byte(v.d + (live ? n - 1 : 0u));
+    constexpr uint32_t kFlagsOk = (1u << 0) | (1u << SDB_FLAG_TOMBSTONE) | (1u << SDB_FLAG_MERGE_OPERAND);
+    const bool rbad = (h & 0x808080u) != 0 || n > end || (i == 0 ? sh != 0 : sh > kprev) || fl > 31 ||
+                      !((kFlagsOk >> (fl & 31)) & 1u) || (i == G - 1 && n < end);
+    if (__ballot(live && rbad) != 0) return false;
+    const uint64_t L = __ballot(live != 0);
+    t.entries = (uint64_t)__builtin_popcountll(L);
+    t.key_bytes = wave_sum((uint64_t)(live ? klen : 0u));
+    t.status = 0;
+    t.sequential = false;
+    if (live && q < 4 && i < 32) rowpos[32 * q + i] = (uint16_t)c;
+    // per-region row counts for the emit pass's lane-per-row parse (<= 64 rows, keys of <= 16 bytes)
+    const uint32_t kmx = wave_max(live ? klen : 0u);
+    uint64_t rc = ~0ull;
+    if (kmx <= 16) {
+        rc = 0;
+        for (uint32_t r = 0; r < R; r++) {
+            const uint64_t gm = lg == 6 ? ~0ull : (((1ull << G) - 1) << (r * G));
+            const uint32_t cnt = (uint32_t)__builtin_popcountll(L & gm);
+            rc |= (uint64_t)cnt << (16 * r);
+            if (cnt > 32) rc = ~0ull;  // positions are recorded for 32 rows per region
+            if (cnt > 32) break;
+        }
+    }
+    if (l == 0) *rcnt = rc;
     return true;
 }
 
@@ -627,27 +753,48 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
         return;
     }
     crc_tables_to_lds((lu32 *)smem);
+    crc_rep_to_lds((lu32 *)(smem + kCntRep));
     __syncthreads();
     const uint32_t(*crc)[256] = (const uint32_t(*)[256])smem;
     const uint32_t wave = threadIdx.x >> 6;
-    lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kDecWaveLds + kDecGuard;
+    lu8 *img = (lu8 *)smem + kCntRep + kCrcRepLds + wave * kCntWaveLds + kDecGuard;
     if (lane_id() < kDecGuard / 4) ((lu32 *)(img - kDecGuard))[lane_id()] = 0;  // never written again
     uint8_t *stage = (uint8_t *)img;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
     (void)gwave;
-    for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave; k < a.nblocks; k += nwaves) {
+    // one block ahead: its offsets and (fast path) its granules in registers
+    uint64_t k = gwave, ns = 0, ne = 0;
+    Granules pre;
+    if (k < a.nblocks) {
+        ns = a.block_off[k];
+        ne = block_end_of(a, k);
+        if (dec_fast(ns, ne)) gran_load(a, ns, ne, pre);
+    }
+    for (; k < a.nblocks; k += nwaves) {
         DEC_T(t0);
-        const uint64_t s = a.block_off[k], e = block_end_of(a, k);
+        const uint64_t s = ns, e = ne;
+        const Granules cur = pre;
+        if (k + nwaves < a.nblocks) {
+            ns = a.block_off[k + nwaves];
+            ne = block_end_of(a, k + nwaves);
+            if (dec_fast(ns, ne)) gran_load(a, ns, ne, pre);
+        }
         Tally t{0, 0, 0, false};
         if (lane_id() == 0) a.rcnt[k] = ~0ull;  // row positions not recorded (tally_v2_fast overwrites)
         if (dec_fast(s, e)) {
-            const LdsBlockView v = stage_lds(a, s, e, img, true);
+            const LdsBlockView v = stage_lds(a, s, e, img, true, true, &cur);
             DEC_T(t1);
             t.status = v.status;
             if (!v.status) {
+#ifdef SDB_EXP_NO_WALK  // diagnostic: stage + CRC only (wrong counts by design)
+                t.entries = v.count;
+#else
                 if (a.version == 1) t = tally_v1(v);
-                else if (!tally_v2_fast(v, t, a.rowpos + 128 * k, a.rcnt + k)) t = tally_v2(v);
+                else if (!tally_v2_spec(v, t, a.rowpos + 128 * k, a.rcnt + k) &&
+                         !tally_v2_fast(v, t, a.rowpos + 128 * k, a.rcnt + k))
+                    t = tally_v2(v);
+#endif
                 if (a.descending && a.version == 2) desc_rule(v.count, t);
             }
             DEC_T(t2);
@@ -655,7 +802,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
             DEC_ACC(0, 1, t2 - t1);
             DEC_ACC(0, 3, 1);
         } else {
-            const BlockView v = load_block(a, k, stage, crc);
+            const BlockView v = load_block(a, k, stage, crc, kDecImg);
             t.status = v.status;
             if (!v.status) t = (a.version == 2) ? tally_v2(v) : tally_v1(v);
             if (!v.status && a.descending && a.version == 2) desc_rule(v.count, t);
@@ -929,7 +1076,7 @@ SDB_DEV void emit_v2(const DecodeArgs &a, const BlockViewT<P> &v, bool sequentia
 // V2 emit, lane = row, for blocks whose row positions the count pass recorded (rc: rows of restart
 // regions 0..3, 16 bits each; pos: 4 x 32 positions): no walk at all.  Key byte b of row j is suffix byte
 // b of the last row r <= j with shared_r <= b (a max-scan over the lanes per byte position).
-SDB_DEV void emit_v2_rows(const DecodeArgs &a, const LdsBlockView &v, uint64_t rc, const uint16_t *pos, uint64_t ent0,
+SDB_DEV void emit_v2_rows(const DecodeArgs &a, const LdsBlockView &v, uint64_t rc, const lu16 *pos, uint64_t ent0,
                           uint64_t kb0, uint64_t gbase, lu8 *kbuf) {
     const uint32_t j = (uint32_t)lane_id();
     const uint32_t c0 = rc & 0xFFFF, c1 = (rc >> 16) & 0xFFFF, c2 = (rc >> 32) & 0xFFFF, c3 = (rc >> 48) & 0xFFFF;
@@ -1062,27 +1209,51 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
     (void)gwave;
     // capacity guard: if the counted output does not fit the caller's arrays, write nothing
     if (tot_ent > a.out.cap_entries || tot_kb > a.out.key_arena_cap) run = false;
-    for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave; run && k < a.nblocks; k += nwaves) {
-        const uint64_t ent0 = a.small ? s_ent0 : a.ent_start[k];
-        const uint64_t n_ent = (a.small ? s_ent1 : a.ent_start[k + 1]) - ent0;
+    // one block ahead: its offsets (scalar loads: these arrays are read-only here) and, fast path, its
+    // granules in registers, so the block's HBM latency overlaps the previous block's work
+    typedef const __attribute__((address_space(4))) uint64_t *cu64;
+    const bool small = a.small != 0;
+    auto off_s = [&](uint64_t kk) { return ((cu64)a.block_off)[kk]; };
+    auto off_e = [&](uint64_t kk) { return a.block_end ? ((cu64)a.block_end)[kk] : ((cu64)a.block_off)[kk + 1]; };
+    uint64_t k = gwave, ns = 0, ne = 0;
+    Granules pre;
+    if (run && k < a.nblocks) {
+        ns = off_s(k);
+        ne = off_e(k);
+        if (dec_fast(ns, ne)) gran_load(a, ns, ne, pre);
+    }
+    for (; run && k < a.nblocks; k += nwaves) {
+        const uint64_t s = ns, e = ne;
+        const Granules cur = pre;
+        if (k + nwaves < a.nblocks) {
+            ns = off_s(k + nwaves);
+            ne = off_e(k + nwaves);
+            if (dec_fast(ns, ne)) gran_load(a, ns, ne, pre);
+        }
+        const uint64_t ent0 = small ? s_ent0 : ((cu64)a.ent_start)[k];
+        const uint64_t n_ent = (small ? s_ent1 : ((cu64)a.ent_start)[k + 1]) - ent0;
         if (l == 0) a.out.block_entry_start[k] = ent0;
         if (n_ent == 0) continue;
-        const uint64_t kb0 = a.small ? s_kb0 : a.key_start[k];
-        const uint64_t kbn = (a.small ? s_kb1 : a.key_start[k + 1]) - kb0;
-        const uint64_t s = a.block_off[k], e = block_end_of(a, k);
+        const uint64_t kb0 = small ? s_kb0 : ((cu64)a.key_start)[k];
+        const uint64_t kbn = (small ? s_kb1 : ((cu64)a.key_start)[k + 1]) - kb0;
         const bool seq = a.flag[k] != 0;
         if (dec_fast(s, e)) {
             DEC_T(t0);
-            const LdsBlockView v = stage_lds(a, s, e, img, false);
+            const LdsBlockView v = stage_lds(a, s, e, img, false, false, &cur);
             if (v.status) continue;  // cannot happen: the count pass accepted it
             DEC_T(t1);
             if (a.version == 1) {
                 emit_v1(a, v, ent0, kb0, s);
             } else {
                 const bool lds_keys = kbn + 16 <= kDecKeys;
-                const uint64_t rc = seq ? ~0ull : a.rcnt[k];
-                if (rc != ~0ull && kbn + 16 <= kRowTmp) emit_v2_rows(a, v, rc, a.rowpos + 128 * k, ent0, kb0, s, kbuf);
-                else emit_v2(a, v, seq, ent0, kb0, s, lds_keys ? kbuf : nullptr);
+                const uint64_t rc = seq ? ~0ull : ((cu64)a.rcnt)[k];
+                if (rc != ~0ull && kbn + 16 <= kRowTmp) {
+                    ((lu32 *)(kbuf + kRowTmp))[l] = ((const uint32_t *)(a.rowpos + 128 * k))[l];
+                    wave_sync_d();
+                    emit_v2_rows(a, v, rc, (const lu16 *)(kbuf + kRowTmp), ent0, kb0, s, kbuf);
+                } else {
+                    emit_v2(a, v, seq, ent0, kb0, s, lds_keys ? kbuf : nullptr);
+                }
                 DEC_T(t2);
                 if (lds_keys) {
                     wave_sync_d();
@@ -1240,7 +1411,7 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
     hipLaunchKernelGGL(k_dec_init, dim3(1), dim3(64), 0, st, a);
     static bool attrs = false;
     if (!attrs) {
-        hipFuncSetAttribute((const void *)k_dec_count, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDecLds);
+        hipFuncSetAttribute((const void *)k_dec_count, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCntLds);
         hipFuncSetAttribute((const void *)k_dec_emit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDecLds);
         (void)hipGetLastError();
         attrs = true;
@@ -1252,7 +1423,7 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
     if (cus > 0 && wgs > (uint64_t)cus) wgs = (uint64_t)cus;
     if (wgs == 0) wgs = 1;
     const size_t lds = kDecLds;
-    if (a.nblocks) hipLaunchKernelGGL(k_dec_count, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
+    if (a.nblocks) hipLaunchKernelGGL(k_dec_count, dim3((uint32_t)wgs), dim3(kDecThreads), kCntLds, st, a);
     // scans: ent_start = excl(cnt), key_start = excl(kbytes); small batches scan inside k_dec_emit
     a.small = a.nblocks > 0 && a.nblocks <= kScanTile && wgs * (kDecThreads / 64) >= a.nblocks ? 1u : 0u;
     uint64_t nt = (a.nblocks + kScanTile - 1) / kScanTile;
