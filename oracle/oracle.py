@@ -42,6 +42,7 @@ def _load():
                                       C.c_uint64, P(C.c_uint64), V]),
         "orc_encode_sst": (C.c_int, [P(_abi.KvBatch), P(_abi.SstParams), P(_abi.SstOut)]),
         "orc_bloom_build": (C.c_int, [V, V, C.c_uint64, C.c_uint32, V, C.c_uint64]),
+        "orc_bloom_build_range": (C.c_int, [V, V, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, V, C.c_uint64]),
         "orc_bloom_might_contain": (C.c_int, [V, C.c_uint64, C.c_uint32, V, C.c_size_t]),
         "orc_decode_blocks": (C.c_int, [V, V, C.c_uint64, C.c_uint16, P(_abi.DecodedOut)]),
         "orc_decode_blocks_desc": (C.c_int, [V, V, C.c_uint64, C.c_uint16, P(_abi.DecodedOut)]),
@@ -233,6 +234,31 @@ def bloom_build(key_bytes, key_off, bpk):
     st = lib().orc_bloom_build(key_bytes.ctypes.data, key_off.ctypes.data, n, bpk, bm.ctypes.data, fb)
     assert st == 0
     return bm[:fb]
+
+
+def bloom_build_threads(key_bytes, key_off, bpk, threads):
+    """build_filter split by key range over `threads` threads (private bitmaps, OR-merged): the
+    multi-thread CPU baseline of configs[3].  ctypes drops the GIL inside the C call."""
+    import threading
+    n = len(key_off) - 1
+    fb = filter_size_bytes(n, bpk)
+    parts = [np.zeros(max(fb, 1), np.uint8) for _ in range(threads)]
+    cuts = [n * t // threads for t in range(threads + 1)]
+
+    def run(t):
+        st = lib().orc_bloom_build_range(key_bytes.ctypes.data, key_off.ctypes.data, n, cuts[t], cuts[t + 1],
+                                         bpk, parts[t].ctypes.data, fb)
+        assert st == 0
+
+    ths = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    out = parts[0]
+    for q in parts[1:]:
+        np.bitwise_or(out, q, out=out)
+    return out[:fb]
 
 
 def might_contain(bitmap, num_probes, key):

@@ -203,6 +203,26 @@ sdb_status orc_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, ui
     return SDB_OK;
 }
 
+/* The same build_filter loop over keys [lo, hi) of an n-key filter, OR-ing into a caller-zeroed
+ * bitmap: the CPU baseline splits configs[3] by key range over threads and ORs the partial bitmaps
+ * (set_bit commutes), test infrastructure only. */
+sdb_status orc_bloom_build_range(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n, uint64_t lo,
+                                 uint64_t hi, uint32_t bpk, uint8_t *bitmap, uint64_t bitmap_bytes) {
+    uint64_t fb = orc_filter_size_bytes(n, bpk);
+    if (bitmap_bytes < fb || lo > hi || hi > n) return SDB_INVALID_ARGUMENT;
+    if (fb == 0) return SDB_OK;
+    uint16_t k = orc_optimal_num_probes(bpk);
+    uint32_t m = (uint32_t)(fb * 8);
+    uint32_t pr[64];
+    if (k > 64) return SDB_INVALID_ARGUMENT;
+    for (uint64_t i = lo; i < hi; i++) {
+        uint64_t h = orc_filter_hash(key_bytes + key_off[i], (size_t)(key_off[i + 1] - key_off[i]));
+        orc_probes_for_key(h, k, m, pr);
+        for (uint16_t j = 0; j < k; j++) bitmap[pr[j] / 8] |= (uint8_t)(1u << (pr[j] % 8));
+    }
+    return SDB_OK;
+}
+
 /* PrefixExtractor::prefix_len for the device-supported families (prefix_extractor.rs:41-95): -1 = None */
 int64_t orc_prefix_len(uint32_t kind, uint32_t arg, const uint8_t *key, size_t klen, int64_t given) {
     if (kind == SDB_PREFIX_FIXED) return klen >= arg ? (int64_t)arg : -1;

@@ -47,6 +47,8 @@ sdb_status orc_encode_sst(const sdb_kv_batch *batch, const sdb_sst_params *param
 /* Bloom bitmap (filter.rs:71-90) over keys. */
 sdb_status orc_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,
                            uint32_t bpk, uint8_t *bitmap, uint64_t bitmap_bytes);
+sdb_status orc_bloom_build_range(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n, uint64_t lo,
+                                 uint64_t hi, uint32_t bpk, uint8_t *bitmap, uint64_t bitmap_bytes);
 int orc_bloom_might_contain(const uint8_t *bitmap, uint64_t bitmap_bytes, uint32_t num_probes,
                             const uint8_t *key, size_t klen);
 /* Prefix filters (filter.rs:40-90, 149-175; prefix_extractor.rs:41-95). */

@@ -10,6 +10,10 @@ DESIGN.md:
           counted.
   bloom   configs[3]: 10 M sorted random 16 B keys, 10 bits/key; bitmap bit-exact vs the oracle.
   e2e     configs[1] from pinned host memory: sdb_encoder_encode_host (H2D + kernels + D2H).
+  hbm     the box's measured HBM copy / read bandwidth (torch copy_ and a sum over 4 GiB), beside the
+          8.0 TB/s spec that every roofline fraction uses (BASELINE.md reporting rules).
+CPU baselines (oracle/sdb_oracle.c, a restatement — not the Rust binary) are timed beside decode and
+bloom on 1 thread and on the process's CPU share (one SST / one key range per thread).
 """
 import argparse
 import ctypes as C
@@ -28,6 +32,43 @@ from slatedb_amd import _abi, datasets, runtime  # noqa: E402
 PEAK = 8000.0
 
 
+def cpu_share():
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        return max(1, int(os.environ["OMP_NUM_THREADS"]))
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_model():
+    try:
+        return [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:
+        return "unknown"
+
+
+def threaded(fn, items, deadline_s):
+    """Run fn(item) repeatedly on one thread per item until the deadline; returns (calls, wall s)."""
+    import threading
+    counts = [0] * len(items)
+    t0 = time.perf_counter()
+
+    def run(i):
+        while True:
+            fn(items[i])
+            counts[i] += 1
+            if time.perf_counter() - t0 >= deadline_s:
+                break
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(len(items))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    return sum(counts), time.perf_counter() - t0
+
+
 def timed(fn, reps, stream):
     for _ in range(3):
         fn()
@@ -41,7 +82,7 @@ def timed(fn, reps, stream):
     return e0.elapsed_time(e1) / reps
 
 
-def decode_bench(reps, granular=True):
+def decode_bench(reps, granular=True, cpu_s=0.0):
     lib = runtime.lib()
     dev = torch.device("cuda", 0)
     s = torch.cuda.Stream(device=dev)
@@ -111,6 +152,28 @@ def decode_bench(reps, granular=True):
                       "ms": round(ms, 4), "GiB_per_s_encoded": round(enc / (ms * 1e-3) / 2**30, 2),
                       "algorithmic_bytes": alg, "achieved_GBps": round(gbs, 1), "frac": round(gbs / PEAK, 4),
                       "verified_keys": bool(ok)}), flush=True)
+    if cpu_s > 0:  # CPU baseline: the oracle decoding whole D1 SSTs (read_blocks -> DataBlockIterator)
+        from oracle import oracle as O
+        host = []
+        for j in range(16):
+            lo = int(offs[j][0])
+            hi = int(offs[j][-1]) if j == 15 else int(offs[j + 1][0])
+            bo = np.append(offs[j].cpu().numpy(), hi) if j < 15 else offs[j].cpu().numpy()
+            host.append((blocks[lo:hi].cpu().numpy(), (bo - lo).astype(np.uint64)))
+        enc_sst = host[0][0].size
+        dec = lambda hb: O.decode_blocks(hb[0], hb[1], 2, cap_entries=600000, key_cap=10 << 20)
+        r = dec(host[0])
+        assert r.status == 0 and r.n == nent // 16
+        n1, w1 = threaded(dec, host[:1], cpu_s / 4)
+        th = cpu_share()
+        nt, wt = threaded(dec, [host[i % 16] for i in range(th)], cpu_s * 3 / 4)
+        print(json.dumps({"what": "decode configs[2] CPU baseline (oracle, port)", "kind": "port",
+                          "single_thread_GiB_per_s_encoded": round(n1 * enc_sst / w1 / 2**30, 3),
+                          "threads": th, "GiB_per_s_encoded": round(nt * enc_sst / wt / 2**30, 3),
+                          "configs2_ms_at_threads": round(16 * wt / nt * 1e3, 1),
+                          "sample": "%d D1 SSTs on 1 thread (%.1f s), then %d threads x 1 SST for %.1f s (%d SSTs)"
+                                    % (n1, w1, th, wt, nt), "cpu": cpu_model(), "nproc": os.cpu_count()}),
+              flush=True)
     if not granular:
         return
     # 2 MiB ranged-GET granularity (≈ 520 blocks per call), launched back to back
@@ -188,12 +251,22 @@ def bloom_bench(reps):
     ref = O.bloom_build(kb, ko, 10)
     cpu_s = time.perf_counter() - t0
     ok = np.array_equal(got, np.frombuffer(bytes(ref), np.uint8) if not isinstance(ref, np.ndarray) else ref)
+    th = cpu_share()
+    t0 = time.perf_counter()
+    ref_t = O.bloom_build_threads(kb, ko, 10, th)
+    cpu_t = time.perf_counter() - t0
+    ok = ok and np.array_equal(ref_t, ref)
     alg = n * 16 + fb
     gbs = alg / (ms * 1e-3) / 1e9
     print(json.dumps({"what": "bloom configs[3]", "keys": n, "bitmap_bytes": fb, "ms": round(ms, 4),
                       "Mkeys_per_s": round(n / (ms * 1e-3) / 1e6, 1), "algorithmic_bytes": alg,
                       "achieved_GBps": round(gbs, 1), "frac": round(gbs / PEAK, 4), "bit_exact": bool(ok),
-                      "oracle_1thread_s": round(cpu_s, 3)}), flush=True)
+                      "cpu_baseline": {"kind": "port", "single_thread_s": round(cpu_s, 3),
+                                       "single_thread_Mkeys_per_s": round(n / cpu_s / 1e6, 2), "threads": th,
+                                       "threads_s": round(cpu_t, 3), "threads_Mkeys_per_s": round(n / cpu_t / 1e6, 2),
+                                       "sample": "the whole 10 M-key build, 1 thread then key ranges over %d "
+                                                 "threads OR-merged" % th, "cpu": cpu_model(),
+                                       "nproc": os.cpu_count()}}), flush=True)
 
 
 def e2e_bench(reps):
@@ -265,24 +338,47 @@ def compact_bench(reps):
     comp.close()
 
 
+def hbm_bench(reps):
+    """STREAM-like: torch's copy kernel over 4 GiB (read + write) and a read-only int64 sum."""
+    dev = torch.device("cuda", 0)
+    nbytes = 4 << 30
+    a = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    s = torch.cuda.current_stream()
+    ms_copy = timed(lambda: b.copy_(a), reps, s)
+    a64 = a.view(torch.int64)
+    ms_read = timed(lambda: a64.sum(), reps, s)
+    cp = 2 * nbytes / (ms_copy * 1e-3) / 1e9
+    rd = nbytes / (ms_read * 1e-3) / 1e9
+    print(json.dumps({"what": "measured HBM bandwidth (4 GiB buffers)", "copy_GBps": round(cp, 1),
+                      "read_GBps": round(rd, 1), "spec_GBps": PEAK, "copy_frac_of_spec": round(cp / PEAK, 3),
+                      "note": "roofline fractions use the 8.0 TB/s spec; this is the attainable ceiling"}),
+          flush=True)
+    del a, b, a64
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--decode", action="store_true")
     p.add_argument("--bloom", action="store_true")
     p.add_argument("--e2e", action="store_true")
     p.add_argument("--compact", action="store_true")
+    p.add_argument("--hbm", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="decode CPU baseline budget (0: skip)")
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--no-granular", action="store_true", help="decode: skip the 2 MiB granularity run")
     a = p.parse_args()
-    allp = not (a.decode or a.bloom or a.e2e or a.compact)
+    allp = not (a.decode or a.bloom or a.e2e or a.compact or a.hbm)
     torch.cuda.set_device(0)
     runtime.require_device()
     if a.bloom or allp:
         bloom_bench(a.reps)
     if a.decode or allp:
-        decode_bench(a.reps, not a.no_granular)
+        decode_bench(a.reps, not a.no_granular, a.cpu_seconds)
     if a.e2e or allp:
         e2e_bench(a.reps)
+    if a.hbm or allp:
+        hbm_bench(a.reps)
     if a.compact or allp:
         compact_bench(max(3, a.reps // 4))
 

@@ -26,6 +26,6 @@ done
 timeout -k 10 400 python3 scripts/bench_configs.py > $O/configs.log 2>&1
 rc=$?; echo "configs rc=$rc"; grep '^{' $O/configs.log > $O/configs.jsonl; cut -c1-200 $O/configs.jsonl
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/dec -o run --output-format csv -- python3 scripts/bench_configs.py --decode --no-granular --reps 5 > $O/dec.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/dec -o run --output-format csv -- python3 scripts/bench_configs.py --decode --no-granular --reps 5 --cpu-seconds 0 > $O/dec.log 2>&1
 rc=$?; echo "rocprof dec rc=$rc"
 exit $rc
