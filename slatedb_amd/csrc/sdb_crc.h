@@ -50,17 +50,18 @@ SDB_DEV uint32_t crc_slice8_lds(uint32_t c, uint32_t lo, uint32_t hi, const lu32
     return x ^ y ^ z;
 }
 
-// x^256 * c (the x^(8*32) shift of a CRC) from the 4 byte tables at LDS 8 KiB (k_emit layout)
+// x^256 * c (the x^(8*32) shift of a CRC) from the 4 byte tables at LDS MB KiB (8: the standard layout)
+template <int MB = 8>
 SDB_DEV uint32_t crc_mul256_lds(uint32_t c) {
-    return crc_tab<8>(nullptr, bytex4<0>(c)) ^ crc_tab<9>(nullptr, bytex4<1>(c)) ^ crc_tab<10>(nullptr, bytex4<2>(c)) ^
-           crc_tab<11>(nullptr, bytex4<3>(c));
+    return crc_tab<MB>(nullptr, bytex4<0>(c)) ^ crc_tab<MB + 1>(nullptr, bytex4<1>(c)) ^
+           crc_tab<MB + 2>(nullptr, bytex4<2>(c)) ^ crc_tab<MB + 3>(nullptr, bytex4<3>(c));
 }
 
-// x^(8*64*2^s) * c from the 4 byte tables of tree step s (LDS 12 KiB + s * 4 KiB, k_emit layout)
-template <int S>
+// x^(8*64*2^s) * c from the 4 byte tables of tree step s (LDS TB KiB + s * 4 KiB; 12: standard layout)
+template <int S, int TB = 12>
 SDB_DEV uint32_t crc_tree_mul(uint32_t c) {
-    return crc_tab<12 + 4 * S>(nullptr, bytex4<0>(c)) ^ crc_tab<13 + 4 * S>(nullptr, bytex4<1>(c)) ^
-           crc_tab<14 + 4 * S>(nullptr, bytex4<2>(c)) ^ crc_tab<15 + 4 * S>(nullptr, bytex4<3>(c));
+    return crc_tab<TB + 4 * S>(nullptr, bytex4<0>(c)) ^ crc_tab<TB + 1 + 4 * S>(nullptr, bytex4<1>(c)) ^
+           crc_tab<TB + 2 + 4 * S>(nullptr, bytex4<2>(c)) ^ crc_tab<TB + 3 + 4 * S>(nullptr, bytex4<3>(c));
 }
 
 constexpr uint32_t kCrcTablesLds = 36 * 1024;
@@ -70,6 +71,15 @@ SDB_DEV void crc_tables_to_lds(lu32 *crc) {
     for (uint32_t q = threadIdx.x; q < 8 * 256; q += blockDim.x) crc[q] = (&c_crc.t[0][0])[q];
     for (uint32_t q = threadIdx.x; q < 4 * 256; q += blockDim.x) crc[8 * 256 + q] = (&c_mul256.t[0][0])[q];
     for (uint32_t q = threadIdx.x; q < kTreeSteps * 4 * 256; q += blockDim.x) crc[12 * 256 + q] = (&g_tree.t[0][0][0])[q];
+}
+// Only the x^256 and tree tables, at LDS byte address `at` (28 KiB).
+SDB_DEV void crc_combine_tables_to_lds(lu32 *at) {
+    for (uint32_t q = threadIdx.x; q < 4 * 256; q += blockDim.x) at[q] = (&c_mul256.t[0][0])[q];
+    for (uint32_t q = threadIdx.x; q < kTreeSteps * 4 * 256; q += blockDim.x) at[4 * 256 + q] = (&g_tree.t[0][0][0])[q];
+}
+// The slicing-by-8 tables alone (8 KiB) at `at`.
+SDB_DEV void crc_slice_tables_to_lds(lu32 *at) {
+    for (uint32_t q = threadIdx.x; q < 8 * 256; q += blockDim.x) at[q] = (&c_crc.t[0][0])[q];
 }
 
 // crc32fast::hash of the image [0, Lc), 4 <= Lc <= 4096, in every lane.  img: 16-byte aligned LDS,
@@ -97,7 +107,7 @@ SDB_DEV uint32_t wave_crc_image(const lu8 *img, uint32_t Lc, bool fold_init) {
             cb = crc_slice8_lds(cb, v3.x, v3.y, crc);
             ca = crc_slice8_lds(ca, v1.z, v1.w, crc);
             cb = crc_slice8_lds(cb, v3.z, v3.w, crc);
-            c = crc_mul256_lds(ca) ^ cb;  // raw(seg) = raw(first 32) * x^256 + raw(last 32)
+            c = crc_mul256_lds<>(ca) ^ cb;  // raw(seg) = raw(first 32) * x^256 + raw(last 32)
         }
     }
     // partner = lane + 2^s: DPP row_shl inside a row, then permlane16 / permlane32 swaps.  Lanes l with
@@ -133,27 +143,28 @@ SDB_DEV uint32_t crc_seg64_lds(const uint32_t (&m)[16]) {
     cb = crc_slice8_lds(cb, m[12], m[13], crc);
     ca = crc_slice8_lds(ca, m[6], m[7], crc);
     cb = crc_slice8_lds(cb, m[14], m[15], crc);
-    return crc_mul256_lds(ca) ^ cb;
+    return crc_mul256_lds<>(ca) ^ cb;
 }
 
 // Combine the 64 lanes' segment CRCs (lane l's segment followed by those of lanes l+1 .. 63) into
-// lane 0 by six pairwise tree steps; returns the wave-uniform result.
+// lane 0 by six pairwise tree steps; returns the wave-uniform result.  Tree tables at LDS TB KiB.
+template <int TB = 12>
 SDB_DEV uint32_t crc_tree_combine(uint32_t c) {
     const uint32_t l = (uint32_t)lane_id();
     // partner = lane + 2^s: DPP row_shl inside a row, then permlane16 / permlane32 swaps.  Lanes l with
     // l % 2^(s+1) != 0 hold nothing the tree still needs: their table lookups are masked off.
     uint32_t p = dpp32<0x101>(c);
-    if ((l & 1) == 0) c = crc_tree_mul<0>(c) ^ p;
+    if ((l & 1) == 0) c = crc_tree_mul<0, TB>(c) ^ p;
     p = dpp32<0x102>(c);
-    if ((l & 3) == 0) c = crc_tree_mul<1>(c) ^ p;
+    if ((l & 3) == 0) c = crc_tree_mul<1, TB>(c) ^ p;
     p = dpp32<0x104>(c);
-    if ((l & 7) == 0) c = crc_tree_mul<2>(c) ^ p;
+    if ((l & 7) == 0) c = crc_tree_mul<2, TB>(c) ^ p;
     p = dpp32<0x108>(c);
-    if ((l & 15) == 0) c = crc_tree_mul<3>(c) ^ p;
+    if ((l & 15) == 0) c = crc_tree_mul<3, TB>(c) ^ p;
     p = (uint32_t)__builtin_amdgcn_permlane16_swap(c, c, false, false)[1];
-    if ((l & 31) == 0) c = crc_tree_mul<4>(c) ^ p;
+    if ((l & 31) == 0) c = crc_tree_mul<4, TB>(c) ^ p;
     p = (uint32_t)__builtin_amdgcn_permlane32_swap(c, c, false, false)[1];
-    if (l == 0) c = crc_tree_mul<5>(c) ^ p;
+    if (l == 0) c = crc_tree_mul<5, TB>(c) ^ p;
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
 }
 
@@ -192,7 +203,7 @@ SDB_DEV uint32_t wave_crc_image_ra(const lu8 *img, uint32_t Lc) {
         else realign16<3>(x, r, m);
         c = crc_seg64_lds(m);
     }
-    return crc_tree_combine(c) ^ 0xFFFFFFFFu;
+    return crc_tree_combine<>(c) ^ 0xFFFFFFFFu;
 }
 
 // --- bank-replicated byte table (decode count pass) ------------------------------------------------
@@ -215,8 +226,8 @@ SDB_DEV uint32_t crc_rep_step(uint32_t c, uint32_t lb) {
 }
 
 // Raw CRC of one 64-byte segment (16 little-endian dwords): two 32-byte byte-at-a-time chains through
-// the replicated table at LDS BASE, combined by x^256 (the k_emit layout's tables at LDS 8 KiB).
-template <uint32_t BASE>
+// the replicated table at LDS BASE, combined by x^256 (tables at LDS MB KiB; 8: the standard layout).
+template <uint32_t BASE, int MB = 8>
 SDB_DEV uint32_t crc_seg64_rep(const uint32_t (&m)[16]) {
     const uint32_t lb = ((uint32_t)lane_id() & 31) << 2;
     uint32_t ca = 0, cb = 0;
@@ -230,11 +241,12 @@ SDB_DEV uint32_t crc_seg64_rep(const uint32_t (&m)[16]) {
             cb = crc_rep_step<BASE>(cb, lb);
         }
     }
-    return crc_mul256_lds(ca) ^ cb;
+    return crc_mul256_lds<MB>(ca) ^ cb;
 }
 
-// wave_crc_image_ra with the per-segment CRC through the replicated table at LDS BASE.
-template <uint32_t BASE>
+// wave_crc_image_ra with the per-segment CRC through the replicated table at LDS BASE; the x^256 and
+// tree tables at LDS MB / TB KiB (8 / 12: the standard layout).
+template <uint32_t BASE, int MB = 8, int TB = 12>
 SDB_DEV uint32_t wave_crc_image_rep(const lu8 *img, uint32_t Lc) {
     const uint32_t l = (uint32_t)lane_id();
     const int s = (int)Lc - 64 * (64 - (int)l);
@@ -255,9 +267,9 @@ SDB_DEV uint32_t wave_crc_image_rep(const lu8 *img, uint32_t Lc) {
         else if (q == 1) realign16<1>(x, r, m);
         else if (q == 2) realign16<2>(x, r, m);
         else realign16<3>(x, r, m);
-        c = crc_seg64_rep<BASE>(m);
+        c = crc_seg64_rep<BASE, MB>(m);
     }
-    return crc_tree_combine(c) ^ 0xFFFFFFFFu;
+    return crc_tree_combine<TB>(c) ^ 0xFFFFFFFFu;
 }
 
 }  // namespace sdb

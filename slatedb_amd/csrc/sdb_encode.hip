@@ -1334,7 +1334,9 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     wave_sync();  // stages + span table written (DS instructions of one wave complete in order)
     WAVE_T(t2);
     // 2. key suffixes + values (cooperative)
+#if !defined(SDB_EXP_NO_COPY)  // diagnostic: no key / value copy (wrong bytes by design)
     copy_spans(img, rtab, ne);
+#endif
     WAVE_T(t3);
     // 3. literals: header, the key bytes sharing a dword with non-key bytes, trailer; then the
     //    restart table, count and the zero padding of the last CRC segment
@@ -1371,13 +1373,19 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     wave_sync();
     WAVE_T(t4);
     // 4. CRC32 (format/sst.rs:541-552) of the image [0, Lc)
+#if defined(SDB_EXP_NO_CRC)  // diagnostic: no CRC (wrong bytes by design)
+    const uint32_t crc32 = 0;
+#else
     const uint32_t crc32 = wave_crc_image_ra(img, Lc);
+#endif
     if (l == 0) {
         img[Lc] = (uint8_t)(crc32 >> 24);
         img[Lc + 1] = (uint8_t)(crc32 >> 16);
         img[Lc + 2] = (uint8_t)(crc32 >> 8);
         img[Lc + 3] = (uint8_t)crc32;
+#if !defined(SDB_EXP_NO_CRC)
         if (Lc + 4 != d.bb) report_error(a.err, d.s, SDB_DEVICE_ERROR);  // internal consistency
+#endif
     }
     wave_sync();
     WAVE_T(t5);
