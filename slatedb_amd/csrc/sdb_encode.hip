@@ -1129,6 +1129,42 @@ SDB_DEV void copy_spans(lu8 *img, const lSpanCopy *tab, uint32_t ne) {
     }
 }
 
+// Row-lane copy (lane = row) for blocks whose spans fit in registers: every lane first reads the
+// aligned source dwords of its span (key run from the key stage, value run from the value stage) into
+// registers, and only then does any lane write, so the in-place value stage is never overwritten
+// before it is read (rows of one block overlap each other's stage).  One v_alignbyte per image dword
+// and about one LDS read + one write per dword, against copy_spans' per-dword table walk and two
+// reads.  Returns false (nothing written) when a span is too long; the caller then uses copy_spans.
+constexpr uint32_t kRowRegs = 28, kKeyRegs = 6;
+SDB_DEV bool copy_rows(lu8 *img, bool row, const SpanCopy &sc) {
+    const uint32_t f0 = sc.a & 0xFFFF, nd = row ? sc.a >> 16 : 0;
+    const uint32_t jk = row ? (sc.jk < nd ? sc.jk : nd) : 0, nv = nd - jk;
+    const uint32_t mk = wave_max(jk), mv = wave_max(nv);
+    if (mk + 1 > kKeyRegs || mv + 1 > kRowRegs) return false;
+    const uint32_t ks = sc.kb, vs = sc.vb + 4 * jk;  // LDS byte addresses of the two runs' first bytes
+    const lu32 *kw = (const lu32 *)(uintptr_t)(ks & ~3u), *vw = (const lu32 *)(uintptr_t)(vs & ~3u);
+    uint32_t K[kKeyRegs], W[kRowRegs];
+#pragma unroll
+    for (uint32_t t = 0; t < kKeyRegs; t++) {
+        K[t] = 0;
+        if (t <= mk && jk && t <= jk) K[t] = kw[t];
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < kRowRegs; t++) {
+        W[t] = 0;
+        if (t <= mv && nv && t <= nv) W[t] = vw[t];
+    }
+    wave_sync();  // every read of the wave is issued (and, in order, done) before the first write
+    lu32 *dw = (lu32 *)img + f0;
+#pragma unroll
+    for (uint32_t t = 0; t + 1 < kKeyRegs; t++)
+        if (t < mk && t < jk) dw[t] = __builtin_amdgcn_alignbyte(K[t + 1], K[t], ks & 3);
+#pragma unroll
+    for (uint32_t t = 0; t + 1 < kRowRegs; t++)
+        if (t < mv && t < nv) dw[jk + t] = __builtin_amdgcn_alignbyte(W[t + 1], W[t], vs & 3);
+    return true;
+}
+
 template <int V>
 SDB_DEV uint32_t write_row_hdr_trailer(lu8 *dst, const RowInfo &r, uint64_t seq, int64_t ets, int64_t cts) {
     uint32_t p = 0;
@@ -1318,24 +1354,29 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     const uint32_t kstart = row_off + h, kend = kstart + r.suf;
     const uint32_t vstart = (V == 2) ? kend : row_off + size - vlen;
     const uint32_t vend = vlen ? vstart + vlen : kend;
+    SpanCopy sc{0, 0, 0, 0};
     if (row) {
         const uint32_t F0 = kstart & ~3u, F1 = (vend + 3) & ~3u;
-        SpanCopy sc;
         sc.a = (F0 >> 2) | (((F1 - F0) >> 2) << 16);
         sc.jk = (kend - F0) >> 2;
         sc.kb = kstage + (uint32_t)(ko + shared - ka) - (kstart - F0);
         sc.vb = vstage + (uint32_t)(vo - va) - (vstart - F0);
-        rtab[l].a = sc.a;
-        rtab[l].jk = sc.jk;
-        rtab[l].kb = sc.kb;
-        rtab[l].vb = sc.vb;
     }
     WAVE_T(t1);
-    wave_sync();  // stages + span table written (DS instructions of one wave complete in order)
+    wave_sync();  // stages written (DS instructions of one wave complete in order)
     WAVE_T(t2);
-    // 2. key suffixes + values (cooperative)
+    // 2. key suffixes + values: lane = row from registers, or cooperative by the span table
 #if !defined(SDB_EXP_NO_COPY)  // diagnostic: no key / value copy (wrong bytes by design)
-    copy_spans(img, rtab, ne);
+    if (!copy_rows(img, row, sc)) {
+        if (row) {
+            rtab[l].a = sc.a;
+            rtab[l].jk = sc.jk;
+            rtab[l].kb = sc.kb;
+            rtab[l].vb = sc.vb;
+        }
+        wave_sync();
+        copy_spans(img, rtab, ne);
+    }
 #endif
     WAVE_T(t3);
     // 3. literals: header, the key bytes sharing a dword with non-key bytes, trailer; then the
