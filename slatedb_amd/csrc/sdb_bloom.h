@@ -10,12 +10,21 @@
 
 namespace sdb {
 
-#define SIPROUND                                                                                   \
-    do {                                                                                           \
-        v0 += v1; v1 = __builtin_rotateleft64(v1, 13); v1 ^= v0; v0 = __builtin_rotateleft64(v0, 32); \
-        v2 += v3; v3 = __builtin_rotateleft64(v3, 16); v3 ^= v2;                                   \
-        v0 += v3; v3 = __builtin_rotateleft64(v3, 21); v3 ^= v0;                                   \
-        v2 += v1; v1 = __builtin_rotateleft64(v1, 17); v1 ^= v2; v2 = __builtin_rotateleft64(v2, 32); \
+// 64-bit rotate left by R (0 < R < 32) as two v_alignbit_b32 (the generic lowering is a 64-bit shift,
+// a 32-bit shift and an or: one VALU more per rotate, 24 per hash)
+template <int R>
+SDB_DEV uint64_t rotl64(uint64_t x) {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - R), nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - R);
+    return ((uint64_t)nhi << 32) | nlo;
+}
+SDB_DEV uint64_t swap32(uint64_t x) { return (x << 32) | (x >> 32); }
+#define SIPROUND                                                                 \
+    do {                                                                         \
+        v0 += v1; v1 = rotl64<13>(v1); v1 ^= v0; v0 = swap32(v0);               \
+        v2 += v3; v3 = rotl64<16>(v3); v3 ^= v2;                                 \
+        v0 += v3; v3 = rotl64<21>(v3); v3 ^= v0;                                 \
+        v2 += v1; v1 = rotl64<17>(v1); v1 ^= v2; v2 = swap32(v2);               \
     } while (0)
 
 // SipHash-1-3 of a 16-byte key whose bytes are the little-endian words m0, m1 (the D1 / config-4
