@@ -272,7 +272,7 @@ def main():
                    "sst_version": 2, "bloom_bits_per_key": args.bpk, "resident_input_ssts_per_gpu": len(dbs),
                    "parallelism": "independent SSTs per GPU (no collective)"},
         "roofline": {"bound": "hbm", "kernel": "whole encode pipeline (k_facts + fused bloom binning, k_seg, k_group, "
-                                               "k_enum, k_bloom_fill_hd, k_emit: one launch sequence per step)",
+                                               "k_enum, k_emit; the bloom slice fill runs in k_seg's grid: one launch sequence per step)",
                      "achieved": round(pipe_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(pipe_gbs / PEAK_HBM_GBS, 4),
                      "traffic": traffic_sst * batch if traffic_sst else None,

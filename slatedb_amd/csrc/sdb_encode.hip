@@ -332,17 +332,14 @@ SDB_DEV uint32_t walk_size_v2(const EncodeArgs &a, uint64_t j, bool rs) {
     return rs ? f.s_r : f.s_nr;
 }
 
-__global__ __launch_bounds__(kSegThreads, SDB_SEG_WAVES) void k_seg(SstSet P) {
-    const EncodeArgs a = make_args(P, blockIdx.y);
-    if (blockIdx.x >= a.nchunks) return;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+SDB_DEV void seg_chunk(const EncodeArgs &a, uint8_t *smem, uint32_t k) {
     uint32_t *s_r = (uint32_t *)smem;          // kSegSpan: true restart-row sizes (V1: row sizes)
     uint32_t *s_P = s_r + kSegSpan;            // kSegSpan + 4: prefix of clamped non-restart sizes
     uint32_t *s_R = s_P + kSegSpan + 4;        // kSegSpan: restart surcharge of each entry
     uint32_t *s_bb = s_R + kSegSpan;           // kChunk: encoded block bytes for blocks starting here
     uint16_t *s_nx = (uint16_t *)(s_bb + kChunk);  // kChunk: next(b) - cs (0xFFFF: out of range)
     __shared__ uint32_t s_len[kSegThreads / 64];
-    const uint32_t k = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
     const uint64_t cs = (uint64_t)k * kChunk;
     const uint64_t ce = cs + kChunk < a.n ? cs + kChunk : a.n;
     const uint64_t se = ce + a.seg_look < a.n ? ce + a.seg_look : a.n;
@@ -545,6 +542,20 @@ __global__ __launch_bounds__(kSegThreads, SDB_SEG_WAVES) void k_seg(SstSet P) {
     }
     PHASE_MARK(5);
     PHASE_MARK(6);
+}
+
+// k_seg: workgroups [0, max_chunks) segment chunk x; with the fused bloom, workgroups past them fill
+// bitmap slice x - max_chunks from the slots k_facts binned (independent of the segmentation: both
+// only need k_facts, and both are latency-bound, so they share the CUs in one launch).
+__global__ __launch_bounds__(kSegThreads, SDB_SEG_WAVES) void k_seg(SstSet P) {
+    const EncodeArgs a = make_args(P, blockIdx.y);
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (blockIdx.x < P.max_chunks) {
+        if (blockIdx.x < a.nchunks) seg_chunk(a, smem, blockIdx.x);
+    } else if (a.bloom_fused && blockIdx.x - P.max_chunks < a.bpl.nslices) {
+        bloom_fill_slice(blockIdx.x - P.max_chunks, a.key_bytes, a.key_off, a.n, a.bpl, a.bq, a.bloom_out,
+                         a.bloom_len, (uint32_t *)smem);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1851,7 +1862,6 @@ extern "C" int sdb_diag_phase_times(uint64_t *out, int nblocks) {
 }
 #endif
 
-__global__ void k_bloom_fill_hd(SstSet P);
 static int g_cus = 0;
 static uint32_t g_emit_threads = kEmitThreads, g_emit_wg_per_cu = kEmitWgPerCu;
 static std::once_flag g_attrs_once;
@@ -1875,26 +1885,18 @@ static void set_lds_attrs() {
         (void)hipFuncSetAttribute((const void *)k_emit<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
         (void)hipFuncSetAttribute((const void *)k_enum, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEnumLds);
         (void)hipFuncSetAttribute((const void *)k_group, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGroupLds);
-        (void)hipFuncSetAttribute((const void *)k_seg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLdsMax);
-        (void)hipFuncSetAttribute((const void *)k_bloom_fill_hd, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        (void)hipFuncSetAttribute((const void *)k_seg, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
         (void)hipFuncSetAttribute((const void *)k_facts, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLds);
         (void)hipGetLastError();  // an unsupported attribute value must not poison the next launch status
     });
 }
 
 // ------------------------------------------------------------------------------------------------
-// Bloom (fused with the encode's k_facts hashes): bin tiles of kChunk keys' probes into (tile, slice)
-// slots, then one workgroup per slice ORs them into LDS and writes the bitmap slice (sdb_bloom.h).
-// They run on a per-device side stream forked after k_facts and joined after k_emit, so they fill
-// the CUs the latency-bound k_seg / k_group / k_enum leave idle.
+// Bloom (fused with the encode): k_facts bins each chunk's probes into (tile, slice) slots, and
+// workgroups of k_seg past its chunks OR one slice's slots into LDS and write the bitmap slice
+// (sdb_bloom.h).
 // ------------------------------------------------------------------------------------------------
 static_assert(kChunk == kFactsEntries && kFactsThreads == kBinThreads, "bloom tiles are k_facts' chunks of kChunk keys");
-__global__ __launch_bounds__(kFillThreads) void k_bloom_fill_hd(SstSet P) {
-    const EncodeArgs a = make_args(P, blockIdx.y);
-    if (!a.bloom_fused || blockIdx.x >= a.bpl.nslices) return;
-    extern __shared__ __attribute__((aligned(16))) uint32_t blds[];
-    bloom_fill_slice(blockIdx.x, a.key_bytes, a.key_off, a.n, a.bpl, a.bq, a.bloom_out, a.bloom_len, blds);
-}
 
 hipError_t launch_encode_set(const SstSet &P, size_t bin_lds, size_t fill_lds, hipStream_t st) {
     set_lds_attrs();
@@ -1905,7 +1907,9 @@ hipError_t launch_encode_set(const SstSet &P, size_t bin_lds, size_t fill_lds, h
     hipLaunchKernelGGL(k_facts, dim3(P.max_facts, P.count), dim3(kFactsThreads), P.max_tiles ? bin_lds : 0, st, P);
     stage_mark(st, kStFacts, false);
     stage_mark(st, kStSeg, true);
-    hipLaunchKernelGGL(k_seg, dim3(P.max_chunks, P.count), dim3(kSegThreads), kSegLds, st, P);
+    // k_seg also fills the fused bloom's slices (workgroups past the chunks)
+    const size_t seg_lds = kSegLds > fill_lds ? kSegLds : fill_lds;
+    hipLaunchKernelGGL(k_seg, dim3(P.max_chunks + P.max_slices, P.count), dim3(kSegThreads), seg_lds, st, P);
     stage_mark(st, kStSeg, false);
     stage_mark(st, kStGroup, true);
     hipLaunchKernelGGL(k_group, dim3(P.max_groups, P.count), dim3(kGroupThreads), kGroupLds, st, P);
@@ -1913,11 +1917,6 @@ hipError_t launch_encode_set(const SstSet &P, size_t bin_lds, size_t fill_lds, h
     stage_mark(st, kStEnum, true);
     hipLaunchKernelGGL(k_enum, dim3(P.max_chunks, P.count), dim3(kEnumThreads), kEnumLds, st, P);
     stage_mark(st, kStEnum, false);
-    if (P.max_slices) {
-        stage_mark(st, kStBloomFill, true);
-        hipLaunchKernelGGL(k_bloom_fill_hd, dim3(P.max_slices, P.count), dim3(kFillThreads), fill_lds, st, P);
-        stage_mark(st, kStBloomFill, false);
-    }
     stage_mark(st, kStEmit, true);
     if (P.version == 2) hipLaunchKernelGGL(k_emit<2>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, P);
     else hipLaunchKernelGGL(k_emit<1>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, P);
