@@ -49,6 +49,10 @@ def main():
     shutil.copy(one("configs.jsonl"), os.path.join(PROF, tag + "_configs.jsonl"))
     shutil.copy(one("enc/**/run_kernel_stats.csv"), os.path.join(PROF, tag + "_encode_kernel_stats.csv"))
     shutil.copy(one("dec/**/run_kernel_stats.csv"), os.path.join(PROF, tag + "_decode_kernel_stats.csv"))
+    for what in ("enc", "dec"):
+        f = os.path.join(RP, "sq_%s" % what, "summary.txt")
+        if os.path.exists(f):
+            shutil.copy(f, os.path.join(PROF, "%s_pmc_sq_%s.txt" % (tag, {"enc": "encode", "dec": "decode"}[what])))
     fetch, write = pmc("FETCH_SIZE"), pmc("WRITE_SIZE")
     batch = json.load(open(one("bench.json")))["config"]["ssts_per_gpu_per_step"]
     out = {"command": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) -- "
