@@ -67,6 +67,7 @@ typedef enum sdb_status {
     SDB_INVALID_ARGUMENT = 8,       /* bad kind byte, capacity too small, NULL pointer, ... */
     SDB_CORRUPT_BLOCK = 9,          /* block bytes that the reference would panic on while parsing */
     SDB_MERGE_OPERATOR_MISSING = 10,/* SlateDBError::MergeOperatorMissing (merge_operator.rs:213-223) */
+    SDB_DECOMPRESSION_ERROR = 11,   /* SlateDBError::BlockDecompressionError (format/sst.rs:884-917) */
     SDB_DEVICE_ERROR = 100          /* no HIP device / launch failure */
 } sdb_status;
 
@@ -287,6 +288,35 @@ enum { SDB_DECODE_DESCENDING = 1 };
 sdb_status sdb_decode_blocks_ex(const uint8_t *arena, const uint64_t *block_start, const uint64_t *block_end,
                                 uint64_t nblocks, uint16_t sst_version, uint32_t flags, const sdb_decoded_out *out,
                                 void *workspace, uint64_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Compressed blocks (SsTableInfo.compression_format != None): the first half of decode_block
+ * (format/sst.rs:980-999) — validate_checksum over the stored bytes, then SsTableFormat::decompress
+ * (format/sst.rs:884-917) — on the device, for the LZ-family codecs:
+ *   SDB_CODEC_LZ4     lz4_flex 0.11.6 block::decompress_size_prepended (u32 LE size, then an LZ4 block;
+ *                     output shorter than the declared size is kept, as lz4_flex truncates);
+ *   SDB_CODEC_SNAPPY  snap 1.1.1 raw::Decoder::decompress_vec (varint size, then Snappy raw elements).
+ * Zlib and Zstd return SDB_UNSUPPORTED.  Two steps, so the caller can size the output:
+ *   1. sdb_decompress_plan writes out_start[0..nblocks] (device): block k's output slot starts at
+ *      out_start[k] and holds its declared length + 4; out_start[nblocks] = the bytes `out` needs.  A
+ *      header that cannot be read, or one declaring more than 64 MiB, gets an empty slot (that block
+ *      then fails in step 2).
+ *   2. sdb_decompress_blocks fills out[out_start[k] .. out_end[k]) with the uncompressed block followed
+ *      by the CRC32 (BE) of those bytes — Block::encode() ++ crc, so sdb_decode_blocks_at(out,
+ *      out_start, out_end, ...) decodes the run (value references then point into `out`).  *err
+ *      (device u64) = block << 8 | status of the first failing block in block order (~0: none):
+ *      SDB_CHECKSUM_MISMATCH, SDB_DECOMPRESSION_ERROR, SDB_CORRUPT_BLOCK (fewer than 4 bytes),
+ *      SDB_LIMIT_EXCEEDED (over 64 MiB) or SDB_INVALID_ARGUMENT (slot past out_cap); a failing block's
+ *      out_end[k] = out_start[k].
+ * blocks / block_off (nblocks + 1) as sdb_decode_blocks.  Workspace (step 1 only):
+ * sdb_decompress_workspace_bytes(nblocks). */
+enum { SDB_CODEC_NONE = 0, SDB_CODEC_SNAPPY = 1, SDB_CODEC_ZLIB = 2, SDB_CODEC_LZ4 = 3, SDB_CODEC_ZSTD = 4 };
+uint64_t sdb_decompress_workspace_bytes(uint64_t nblocks);
+sdb_status sdb_decompress_plan(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                               uint64_t *out_start, void *workspace, uint64_t workspace_bytes, void *stream);
+sdb_status sdb_decompress_blocks(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                                 uint8_t *out, uint64_t out_cap, const uint64_t *out_start, uint64_t *out_end,
+                                 uint64_t *err, void *stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Point lookups / seeks on one encoded SST (device): the read path of Db::get and of an SstIterator

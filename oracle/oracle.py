@@ -52,6 +52,9 @@ def _load():
         "orc_bloom_might_match": (C.c_int, [V, C.c_uint64, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, V,
                                             C.c_size_t, C.c_int, C.c_int64]),
         "orc_prefix_len": (C.c_int64, [C.c_uint32, C.c_uint32, V, C.c_size_t, C.c_int64]),
+        "orc_decompressed_len": (C.c_int64, [C.c_uint32, V, C.c_size_t]),
+        "orc_decompress": (C.c_int, [C.c_uint32, V, C.c_size_t, V, C.c_size_t, P(C.c_size_t)]),
+        "orc_decompress_blocks": (C.c_int, [C.c_uint32, V, V, C.c_uint64, V, C.c_uint64, V, V, P(C.c_uint64)]),
         "orc_merge_runs": (C.c_int, [P(_abi.Run), C.c_uint32, P(_abi.Retention), P(_abi.MergedOut)]),
         "orc_sst_cuts": (C.c_int, [P(_abi.KvBatch), P(_abi.SstParams), C.c_uint64, V, C.c_uint64, P(C.c_uint64)]),
     }
@@ -416,3 +419,41 @@ def compact(runs, ret, prm, max_sst_size):
     assert st == 0, st
     ssts = [encode_sst(merged.slice(cuts[i], cuts[i + 1]), prm) for i in range(len(cuts) - 1)]
     return merged, sm, cuts, ssts
+
+
+# --- f3: block decompression (format/sst.rs:884-917) -----------------------------------------------
+CODEC_SNAPPY, CODEC_LZ4 = 1, 3  # CompressionFormat (schemas/sst.fbs)
+
+
+def decompress(codec, data):
+    """SsTableFormat::decompress of one payload -> (status, bytes)."""
+    b = np.frombuffer(bytes(data), np.uint8)
+    n = lib().orc_decompressed_len(codec, b.ctypes.data if b.size else None, b.size)
+    cap = max(int(n), 0) + 1
+    out = np.zeros(cap, np.uint8)
+    ol = C.c_size_t(0)
+    st = lib().orc_decompress(codec, b.ctypes.data if b.size else None, b.size, out.ctypes.data, cap, C.byref(ol))
+    return st, out[:ol.value].tobytes() if st == 0 else b""
+
+
+class DecompressResult:
+    pass
+
+
+def decompress_blocks(codec, blocks, block_off, out_cap=None):
+    """decode_block's first half over a block run: (status, out, out_start, out_end, first_err)."""
+    blocks = np.ascontiguousarray(blocks, np.uint8)
+    block_off = np.ascontiguousarray(block_off, np.uint64)
+    nb = len(block_off) - 1
+    cap = out_cap if out_cap is not None else int(blocks.size) * 64 + 4 * nb + 64
+    r = DecompressResult()
+    r.out = np.zeros(max(cap, 1), np.uint8)
+    r.out_start = np.zeros(nb + 1, np.uint64)
+    r.out_end = np.zeros(max(nb, 1), np.uint64)
+    fe = C.c_uint64(0)
+    r.status = lib().orc_decompress_blocks(codec, blocks.ctypes.data if blocks.size else None, block_off.ctypes.data,
+                                           nb, r.out.ctypes.data, cap, r.out_start.ctypes.data, r.out_end.ctypes.data,
+                                           C.byref(fe))
+    r.first_err = fe.value
+    r.out_end = r.out_end[:nb]
+    return r

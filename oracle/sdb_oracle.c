@@ -1640,3 +1640,192 @@ sdb_status orc_decode_blocks_desc(const uint8_t *blocks, const uint64_t *block_o
     sm->status = overflow ? SDB_INVALID_ARGUMENT : first_err;
     return (sdb_status)sm->status;
 }
+
+/* ------------------------------------------------------------------------------------------- */
+/* Block decompression (f3): SsTableFormat::decompress (format/sst.rs:884-917)                 */
+/* ------------------------------------------------------------------------------------------- */
+enum { ORC_CODEC_SNAPPY = 1, ORC_CODEC_LZ4 = 3 };
+
+/* snap 1.1.1 raw::decompress_len: a little-endian base-128 varint of at most 5 bytes, < 2^32 */
+static int snappy_header(const uint8_t *in, size_t n, uint64_t *len, size_t *hdr) {
+    uint64_t v = 0;
+    for (size_t i = 0; i < 5; i++) {
+        if (i >= n) return 0;
+        v |= (uint64_t)(in[i] & 0x7F) << (7 * i);
+        if (!(in[i] & 0x80)) {
+            if (v > 0xFFFFFFFFull) return 0;
+            *len = v;
+            *hdr = i + 1;
+            return 1;
+        }
+    }
+    return 0;
+}
+
+int64_t orc_decompressed_len(uint32_t codec, const uint8_t *in, size_t n) {
+    if (codec == ORC_CODEC_LZ4) {  /* lz4_flex block::uncompressed_size: u32 little-endian prefix */
+        if (n < 4) return -1;
+        return (int64_t)((uint32_t)in[0] | (uint32_t)in[1] << 8 | (uint32_t)in[2] << 16 | (uint32_t)in[3] << 24);
+    }
+    if (codec == ORC_CODEC_SNAPPY) {
+        uint64_t len;
+        size_t h;
+        return snappy_header(in, n, &len, &h) ? (int64_t)len : -1;
+    }
+    return -1;
+}
+
+/* LZ4 block format: sequences of token (literal length << 4 | match length - 4), extension bytes of
+ * 255 for either nibble 15, literals, then (unless the input ends after the literals) a 16-bit LE
+ * offset and the match.  lz4_flex decompresses into a buffer of the declared size and truncates to
+ * what was written; writing past it, an offset of 0 or past the output start, or input that ends
+ * inside a sequence is an error. */
+static sdb_status lz4_block(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *olen) {
+    size_t ip = 0, op = 0;
+    for (;;) {
+        if (ip >= n) return SDB_DECOMPRESSION_ERROR;
+        const uint8_t tok = in[ip++];
+        size_t lit = tok >> 4;
+        if (lit == 15) {
+            uint8_t b;
+            do {
+                if (ip >= n) return SDB_DECOMPRESSION_ERROR;
+                b = in[ip++];
+                lit += b;
+            } while (b == 255);
+        }
+        if (lit > n - ip || lit > cap - op) return SDB_DECOMPRESSION_ERROR;
+        memcpy(out + op, in + ip, lit);
+        ip += lit;
+        op += lit;
+        if (ip == n) break;  /* the last sequence has literals only */
+        if (n - ip < 2) return SDB_DECOMPRESSION_ERROR;
+        const size_t off = (size_t)in[ip] | (size_t)in[ip + 1] << 8;
+        ip += 2;
+        size_t ml = (size_t)(tok & 15) + 4;
+        if ((tok & 15) == 15) {
+            uint8_t b;
+            do {
+                if (ip >= n) return SDB_DECOMPRESSION_ERROR;
+                b = in[ip++];
+                ml += b;
+            } while (b == 255);
+        }
+        if (off == 0 || off > op || ml > cap - op) return SDB_DECOMPRESSION_ERROR;
+        for (size_t i = 0; i < ml; i++) out[op + i] = out[op - off + i];  /* overlapping copies repeat */
+        op += ml;
+    }
+    *olen = op;
+    return SDB_OK;
+}
+
+/* Snappy raw format: elements tagged by the low two bits: 0 literal (length - 1 in the upper six bits,
+ * or 60..63 -> 1..4 little-endian length bytes), 1 copy of 4..11 bytes with an 11-bit offset, 2 copy of
+ * 1..64 bytes with a 16-bit offset, 3 the same with a 32-bit offset.  snap checks every element
+ * against the declared length and requires the output to end exactly there. */
+static sdb_status snappy_raw(const uint8_t *in, size_t n, uint8_t *out, size_t len) {
+    size_t ip = 0, op = 0;
+    while (ip < n) {
+        const uint8_t tag = in[ip++];
+        if ((tag & 3) == 0) {
+            size_t l = tag >> 2;
+            if (l >= 60) {
+                const size_t nb = l - 59;
+                if (n - ip < nb) return SDB_DECOMPRESSION_ERROR;
+                l = 0;
+                for (size_t i = 0; i < nb; i++) l |= (size_t)in[ip + i] << (8 * i);
+                ip += nb;
+            }
+            l += 1;
+            if (l > n - ip || l > len - op) return SDB_DECOMPRESSION_ERROR;
+            memcpy(out + op, in + ip, l);
+            ip += l;
+            op += l;
+            continue;
+        }
+        size_t l, off;
+        if ((tag & 3) == 1) {
+            if (ip >= n) return SDB_DECOMPRESSION_ERROR;
+            l = 4 + ((tag >> 2) & 7);
+            off = ((size_t)(tag >> 5) << 8) | in[ip++];
+        } else if ((tag & 3) == 2) {
+            if (n - ip < 2) return SDB_DECOMPRESSION_ERROR;
+            l = 1 + (tag >> 2);
+            off = (size_t)in[ip] | (size_t)in[ip + 1] << 8;
+            ip += 2;
+        } else {
+            if (n - ip < 4) return SDB_DECOMPRESSION_ERROR;
+            l = 1 + (tag >> 2);
+            off = (size_t)in[ip] | (size_t)in[ip + 1] << 8 | (size_t)in[ip + 2] << 16 | (size_t)in[ip + 3] << 24;
+            ip += 4;
+        }
+        if (off == 0 || off > op || l > len - op) return SDB_DECOMPRESSION_ERROR;
+        for (size_t i = 0; i < l; i++) out[op + i] = out[op - off + i];
+        op += l;
+    }
+    return op == len ? SDB_OK : SDB_DECOMPRESSION_ERROR;
+}
+
+sdb_status orc_decompress(uint32_t codec, const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len) {
+    const int64_t len = orc_decompressed_len(codec, in, n);
+    if (codec != ORC_CODEC_LZ4 && codec != ORC_CODEC_SNAPPY) return SDB_UNSUPPORTED;
+    if (len < 0) return SDB_DECOMPRESSION_ERROR;
+    if ((uint64_t)len > cap) return SDB_INVALID_ARGUMENT;
+    if (codec == ORC_CODEC_LZ4) return lz4_block(in + 4, n - 4, out, (size_t)len, out_len);
+    uint64_t l = 0;
+    size_t h = 0;
+    snappy_header(in, n, &l, &h);
+    *out_len = (size_t)len;
+    return snappy_raw(in + h, n - h, out, (size_t)len);
+}
+
+/* The output plan of sdb_decompress_plan: block k's slot holds its declared length + 4 (CRC) bytes; 0
+ * when the header is unreadable or declares more than kMaxBlockOut (documented device limit). */
+#define ORC_MAX_BLOCK_OUT (64ull << 20)
+static uint64_t dz_slot(uint32_t codec, const uint8_t *blocks, uint64_t s, uint64_t e) {
+    if (e < s || e - s < 4) return 0;
+    const int64_t len = orc_decompressed_len(codec, blocks + s, (size_t)(e - s - 4));
+    return len < 0 || (uint64_t)len > ORC_MAX_BLOCK_OUT ? 0 : (uint64_t)len + 4;
+}
+
+sdb_status orc_decompress_blocks(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                                 uint8_t *out, uint64_t out_cap, uint64_t *out_start, uint64_t *out_end,
+                                 uint64_t *first_err) {
+    if (codec != ORC_CODEC_LZ4 && codec != ORC_CODEC_SNAPPY) return SDB_UNSUPPORTED;
+    uint64_t pos = 0, ferr = ~0ull;
+    for (uint64_t k = 0; k < nblocks; k++) {
+        out_start[k] = pos;
+        pos += dz_slot(codec, blocks, block_off[k], block_off[k + 1]);
+    }
+    out_start[nblocks] = pos;
+    if (pos > out_cap) return SDB_INVALID_ARGUMENT;
+    for (uint64_t k = 0; k < nblocks; k++) {
+        const uint64_t s = block_off[k], e = block_off[k + 1], o = out_start[k];
+        const uint64_t slot = out_start[k + 1] - o;
+        out_end[k] = o;
+        int st = SDB_OK;
+        size_t ol = 0;
+        if (e < s || e - s < 4) {
+            st = SDB_CORRUPT_BLOCK;
+        } else {
+            const uint8_t *b = blocks + s;
+            const size_t bl = (size_t)(e - s - 4);
+            const uint32_t stored = (uint32_t)b[bl] << 24 | (uint32_t)b[bl + 1] << 16 | (uint32_t)b[bl + 2] << 8 | b[bl + 3];
+            if (orc_crc32(b, bl) != stored) st = SDB_CHECKSUM_MISMATCH;  /* validate_checksum (format/sst.rs:1029-1038) */
+            else if (!slot) st = orc_decompressed_len(codec, b, bl) < 0 ? SDB_DECOMPRESSION_ERROR : SDB_LIMIT_EXCEEDED;
+            else st = orc_decompress(codec, b, bl, out + o, (size_t)(slot - 4), &ol);
+        }
+        if (st) {
+            if (ferr == ~0ull) ferr = (k << 8) | (uint64_t)st;
+            continue;
+        }
+        const uint32_t c = orc_crc32(out + o, ol);  /* re-framed: Block bytes ++ CRC32 BE */
+        out[o + ol] = (uint8_t)(c >> 24);
+        out[o + ol + 1] = (uint8_t)(c >> 16);
+        out[o + ol + 2] = (uint8_t)(c >> 8);
+        out[o + ol + 3] = (uint8_t)c;
+        out_end[k] = o + ol + 4;
+    }
+    *first_err = ferr;
+    return ferr == ~0ull ? SDB_OK : (sdb_status)(ferr & 0xFF);
+}

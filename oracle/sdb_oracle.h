@@ -60,6 +60,21 @@ int orc_bloom_might_match(const uint8_t *bitmap, uint64_t bitmap_bytes, uint32_t
                           uint32_t kind, uint32_t arg, const uint8_t *q, size_t qn, int is_prefix,
                           int64_t given);
 
+/* SsTableFormat::decompress (format/sst.rs:884-917) for the two LZ-family codecs, restated from their
+ * format specifications: codec 3 = lz4_flex 0.11.6 block::decompress_size_prepended (u32 LE size, then
+ * an LZ4 block), codec 1 = snap 1.1.1 raw::Decoder::decompress_vec (varint size, then Snappy
+ * elements).  orc_decompressed_len: the declared length (-1: bad header / other codec). */
+int64_t orc_decompressed_len(uint32_t codec, const uint8_t *in, size_t n);
+sdb_status orc_decompress(uint32_t codec, const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len);
+/* decode_block's first half over a block run (format/sst.rs:980-999): validate_checksum over the stored
+ * bytes, decompress, then the block re-framed with the CRC32 of its uncompressed bytes, so that
+ * [out_start[k], out_end[k]) is a plain block for orc_decode_blocks / sdb_decode_blocks_at.  out_start
+ * (nblocks+1) is the plan: slots of declared length + 4 (0 for an unreadable header or one over 64 MiB).
+ * *first_err: (block << 8 | status) of the first failing block (~0: none); a failing block is empty. */
+sdb_status orc_decompress_blocks(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                                 uint8_t *out, uint64_t out_cap, uint64_t *out_start, uint64_t *out_end,
+                                 uint64_t *first_err);
+
 /* read_blocks/decode_block + DataBlockIterator (format/sst.rs:938-1038, block_iterator*.rs). */
 sdb_status orc_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
                              uint16_t sst_version, const sdb_decoded_out *out);

@@ -16,12 +16,14 @@ SDB_UNSUPPORTED = 7
 SDB_INVALID_ARGUMENT = 8
 SDB_CORRUPT_BLOCK = 9
 SDB_MERGE_OPERATOR_MISSING = 10
+SDB_DECOMPRESSION_ERROR = 11
 SDB_DEVICE_ERROR = 100
+CODEC_NONE, CODEC_SNAPPY, CODEC_ZLIB, CODEC_LZ4, CODEC_ZSTD = 0, 1, 2, 3, 4  # CompressionFormat
 
 STATUS_NAMES = {
     0: "OK", 1: "EMPTY_KEY", 2: "EMPTY_BLOCK", 3: "CHECKSUM_MISMATCH", 4: "INVALID_ROW_FLAGS",
     5: "INVALID_VERSION", 6: "LIMIT_EXCEEDED", 7: "UNSUPPORTED", 8: "INVALID_ARGUMENT",
-    9: "CORRUPT_BLOCK", 10: "MERGE_OPERATOR_MISSING", 100: "DEVICE_ERROR",
+    9: "CORRUPT_BLOCK", 10: "MERGE_OPERATOR_MISSING", 11: "DECOMPRESSION_ERROR", 100: "DEVICE_ERROR",
 }
 
 KIND_VALUE, KIND_MERGE, KIND_TOMBSTONE = 0, 1, 2
@@ -225,6 +227,11 @@ SIGNATURES = {
                                        C.POINTER(DecodedOut), C.c_void_p, C.c_uint64, C.c_void_p]),
     "sdb_decode_blocks_ex": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint16, C.c_uint32,
                                        C.POINTER(DecodedOut), C.c_void_p, C.c_uint64, C.c_void_p]),
+    "sdb_decompress_workspace_bytes": (C.c_uint64, [C.c_uint64]),
+    "sdb_decompress_plan": (C.c_int, [C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                      C.c_uint64, C.c_void_p]),
+    "sdb_decompress_blocks": (C.c_int, [C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "sdb_sst_lookup_workspace_bytes": (C.c_uint64, [C.c_uint64, C.c_uint64]),
     "sdb_sst_lookup": (C.c_int, [C.POINTER(SstView), C.c_void_p, C.c_void_p, C.c_uint64, C.c_int32,
                                  C.POINTER(LookupOut), C.c_void_p, C.c_uint64, C.c_void_p]),

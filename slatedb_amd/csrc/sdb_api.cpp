@@ -95,6 +95,7 @@ const char *sdb_status_name(int s) {
         case SDB_INVALID_ARGUMENT: return "INVALID_ARGUMENT";
         case SDB_CORRUPT_BLOCK: return "CORRUPT_BLOCK";
         case SDB_MERGE_OPERATOR_MISSING: return "MERGE_OPERATOR_MISSING";
+        case SDB_DECOMPRESSION_ERROR: return "DECOMPRESSION_ERROR";
         case SDB_DEVICE_ERROR: return "DEVICE_ERROR";
         default: return "UNKNOWN";
     }
@@ -424,6 +425,30 @@ sdb_status sdb_decode_blocks_at(const uint8_t *arena, const uint64_t *block_star
                                 void *workspace, uint64_t workspace_bytes, void *stream) {
     if (nblocks && !block_end) return SDB_INVALID_ARGUMENT;
     return decode_common(arena, block_start, block_end, nblocks, sst_version, out, workspace, workspace_bytes, stream);
+}
+
+uint64_t sdb_decompress_workspace_bytes(uint64_t nblocks) { return decompress_workspace_bytes(nblocks); }
+
+static bool lz_codec(uint32_t codec) { return codec == SDB_CODEC_LZ4 || codec == SDB_CODEC_SNAPPY; }
+
+sdb_status sdb_decompress_plan(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                               uint64_t *out_start, void *workspace, uint64_t workspace_bytes, void *stream) {
+    if (!lz_codec(codec)) return codec == SDB_CODEC_ZLIB || codec == SDB_CODEC_ZSTD ? SDB_UNSUPPORTED : SDB_INVALID_ARGUMENT;
+    if (!out_start || (nblocks && (!blocks || !block_off))) return SDB_INVALID_ARGUMENT;
+    if (!workspace || workspace_bytes < decompress_workspace_bytes(nblocks)) return SDB_INVALID_ARGUMENT;
+    if (!device_ok()) return SDB_DEVICE_ERROR;
+    return launch_decompress_plan(codec, blocks, block_off, nblocks, out_start, workspace, S(stream)) == hipSuccess
+               ? SDB_OK : SDB_DEVICE_ERROR;
+}
+
+sdb_status sdb_decompress_blocks(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                                 uint8_t *out, uint64_t out_cap, const uint64_t *out_start, uint64_t *out_end,
+                                 uint64_t *err, void *stream) {
+    if (!lz_codec(codec)) return codec == SDB_CODEC_ZLIB || codec == SDB_CODEC_ZSTD ? SDB_UNSUPPORTED : SDB_INVALID_ARGUMENT;
+    if (!err || !out_start || (nblocks && (!blocks || !block_off || !out_end || (out_cap && !out)))) return SDB_INVALID_ARGUMENT;
+    if (!device_ok()) return SDB_DEVICE_ERROR;
+    return launch_decompress_run(codec, blocks, block_off, nblocks, out, out_cap, out_start, out_end,
+                                 (unsigned long long *)err, S(stream)) == hipSuccess ? SDB_OK : SDB_DEVICE_ERROR;
 }
 
 uint64_t sdb_merge_runs_workspace_bytes(const sdb_run *runs, uint32_t nruns) {

@@ -58,5 +58,15 @@ inline DecodeWorkspace decode_workspace_layout(uint64_t nblocks) {
 }
 
 hipError_t launch_decode(DecodeArgs a, hipStream_t st);
+hipError_t launch_excl_scan2(const uint64_t *x, const uint64_t *y, uint64_t n, uint64_t *tx, uint64_t *ty,
+                             uint64_t *ox, uint64_t *oy, hipStream_t st);
+
+// f3: per-block decompression (sdb_codec.hip)
+uint64_t decompress_workspace_bytes(uint64_t nblocks);
+hipError_t launch_decompress_plan(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                                  uint64_t *out_start, void *ws, hipStream_t st);
+hipError_t launch_decompress_run(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                                 uint8_t *out, uint64_t out_cap, const uint64_t *out_start, uint64_t *out_end,
+                                 unsigned long long *err, hipStream_t st);
 
 }  // namespace sdb

@@ -1343,6 +1343,21 @@ __global__ __launch_bounds__(1024) void k_scan_apply(const uint64_t *x, const ui
     }
 }
 
+// Exclusive scans of x and y over n values (ox/oy: n + 1 values, the totals last); tx/ty: (n + 1023) /
+// 1024 + 1 tile sums each.  Shared with the decompression plan (sdb_codec.hip).
+hipError_t launch_excl_scan2(const uint64_t *x, const uint64_t *y, uint64_t n, uint64_t *tx, uint64_t *ty,
+                             uint64_t *ox, uint64_t *oy, hipStream_t st) {
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(ox, 0, 8, st);
+        return e != hipSuccess ? e : hipMemsetAsync(oy, 0, 8, st);
+    }
+    const uint64_t nt = (n + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(k_scan_tiles, dim3((uint32_t)nt), dim3(kScanTile), 0, st, x, y, n, tx, ty);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanTile), 0, st, tx, ty, nt);
+    hipLaunchKernelGGL(k_scan_apply, dim3((uint32_t)nt), dim3(kScanTile), 0, st, x, y, n, tx, ty, nt, ox, oy);
+    return hipGetLastError();
+}
+
 __global__ void k_dec_init(DecodeArgs a) {
     if (threadIdx.x == 0) {
         *a.err = ~0ull;

@@ -586,6 +586,37 @@ def decode_blocks_ex_device(arena, block_start, block_end, nblocks, out, sst_ver
         raise SdbError(st, "sdb_decode_blocks_ex")
 
 
+def decompress_blocks_device(codec, blocks, block_off, stream=None):
+    """Compressed blocks -> a plain block run (sdb_decompress_plan + sdb_decompress_blocks; the first half
+    of decode_block, format/sst.rs:980-999).  blocks: device u8 tensor, block_off: device int64 tensor of
+    nblocks + 1.  Synchronises once to size the output.  Returns (out, out_start, out_end, err) device
+    tensors (err: block << 8 | status of the first failing block, ~0 none) — decode them with
+    decode_blocks_at_device(out, out_start, out_end, ...)."""
+    import torch
+    dev = blocks.device
+    nb = block_off.numel() - 1
+    sp = _sp(stream)
+    ws = torch.empty(int(lib().sdb_decompress_workspace_bytes(nb)), dtype=torch.uint8, device=dev)
+    out_start = torch.empty(nb + 1, dtype=torch.int64, device=dev)
+    st = lib().sdb_decompress_plan(codec, blocks.data_ptr(), block_off.data_ptr(), nb, out_start.data_ptr(),
+                                   ws.data_ptr(), ws.numel(), sp)
+    if st:
+        raise SdbError(st, "sdb_decompress_plan")
+    if stream is not None and hasattr(stream, "synchronize"):
+        stream.synchronize()
+    else:
+        torch.cuda.synchronize(dev)
+    total = int(out_start[nb].item())
+    out = torch.empty(max(total, 1) + 16, dtype=torch.uint8, device=dev)
+    out_end = torch.empty(max(nb, 1), dtype=torch.int64, device=dev)
+    err = torch.empty(1, dtype=torch.int64, device=dev)
+    st = lib().sdb_decompress_blocks(codec, blocks.data_ptr(), block_off.data_ptr(), nb, out.data_ptr(), total,
+                                     out_start.data_ptr(), out_end.data_ptr(), err.data_ptr(), sp)
+    if st:
+        raise SdbError(st, "sdb_decompress_blocks")
+    return out, out_start, out_end[:nb], err
+
+
 LOOKUP_FIELDS = (("state", "uint8"), ("status", "int32"), ("block", "int32"), ("entry", "int32"),
                  ("key_len", "int32"), ("val_off", "int64"), ("val_len", "int32"), ("seq", "int64"),
                  ("flags", "uint8"), ("create_ts", "int64"), ("expire_ts", "int64"))

@@ -1,0 +1,107 @@
+"""f3 on the device: sdb_decompress_plan / sdb_decompress_blocks against the oracle (and through
+sdb_decode_blocks_at), bit-exact.  Compressed runs: tests/codec_util.py."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from slatedb_amd import _abi, datasets, runtime
+
+from .codec_util import compress_run, frame
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+CODECS = [O.CODEC_LZ4, O.CODEC_SNAPPY]
+
+
+def _dev(a, dt=None):
+    t = torch.from_numpy(np.ascontiguousarray(a).view(dt) if dt else np.ascontiguousarray(a))
+    return t.to("cuda")
+
+
+def _run(codec, comp, coff):
+    out, start, end, err = runtime.decompress_blocks_device(codec, _dev(comp), _dev(coff, np.int64))
+    torch.cuda.synchronize()
+    return (out.cpu().numpy(), start.cpu().numpy().view(np.uint64), end.cpu().numpy().view(np.uint64),
+            int(err.cpu().numpy().view(np.uint64)[0]))
+
+
+def _check(codec, comp, coff):
+    out, start, end, err = _run(codec, comp, coff)
+    r = O.decompress_blocks(codec, comp, coff)
+    assert err == r.first_err
+    assert np.array_equal(start, r.out_start) and np.array_equal(end, r.out_end)
+    for k in range(len(coff) - 1):
+        a, b = int(start[k]), int(end[k])
+        assert np.array_equal(out[a:b], r.out[a:b]), k
+    return out, start, end, err
+
+
+@pytest.mark.parametrize("codec", CODECS)
+@pytest.mark.parametrize("version,block_size,n", [(2, 4096, 20000), (1, 1024, 3000), (2, 65536, 6000),
+                                                  (2, 256, 3000)])
+def test_decompress_matches_oracle(codec, version, block_size, n):
+    b = datasets.d3(n=n) if version == 1 or block_size == 256 else datasets.d1(n=n, sst_index=7)
+    enc = O.encode_sst(b, O.params(block_size=block_size, sst_version=version, bloom_bits_per_key=0))
+    comp, coff = compress_run(codec, enc.data, enc.block_off)
+    out, start, end, err = _check(codec, comp, coff)
+    assert err == 2**64 - 1
+    nb = len(coff) - 1
+    assert np.array_equal(out[: int(start[nb])], enc.data)  # the uncompressed data section, bit for bit
+
+
+@pytest.mark.parametrize("codec", CODECS)
+def test_decompress_then_decode_on_device(codec):
+    b = datasets.d1(n=30000, sst_index=2)
+    enc = O.encode_sst(b, O.params(block_size=4096, bloom_bits_per_key=0))
+    comp, coff = compress_run(codec, enc.data, enc.block_off)
+    out, start, end, err = runtime.decompress_blocks_device(codec, _dev(comp), _dev(coff, np.int64))
+    nb = len(coff) - 1
+    dout = runtime.DeviceDecodeOutput(nb, b.n + 16, int(b.key_off[-1]) + 4096)
+    runtime.decode_blocks_at_device(out, start[:nb], end, nb, dout, 2)
+    torch.cuda.synchronize()
+    got = dout.to_host()
+    ref = O.decode_blocks(enc.data, enc.block_off, 2)
+    assert got.status == 0 and got.summary["num_entries"] == ref.n
+    assert np.array_equal(got.key_arena, ref.key_arena) and np.array_equal(got.seq, ref.seq)
+    assert np.array_equal(got.val_len, ref.val_len) and np.array_equal(got.val_off, ref.val_off)
+
+
+def test_big_blocks_single_lane_path():
+    # 64 KiB blocks of 2 KiB random values: payloads over the 8 KiB stage / 16 KiB image
+    rng = np.random.default_rng(4)
+    from slatedb_amd.batch import Batch
+    ents = [(b"k%08d" % i, 0, bytes(rng.integers(0, 256, 2048, dtype=np.uint8)) * (1 + (i % 3)), 100 - i, None, None)
+            for i in range(60)]
+    b = Batch.from_entries(ents)
+    enc = O.encode_sst(b, O.params(block_size=65536, bloom_bits_per_key=0))
+    for codec in CODECS:
+        comp, coff = compress_run(codec, enc.data, enc.block_off)
+        assert max(np.diff(coff)) > 8192
+        out, start, end, err = _check(codec, comp, coff)
+        assert err == 2**64 - 1
+
+
+@pytest.mark.parametrize("codec", CODECS)
+def test_device_errors_match_oracle(codec):
+    enc = O.encode_sst(datasets.d1(n=3000, sst_index=5), O.params(block_size=4096, bloom_bits_per_key=0))
+    comp, coff = compress_run(codec, enc.data, enc.block_off)
+    c2 = comp.copy()
+    c2[int(coff[5]) + 9] ^= 0x01  # CRC mismatch in block 5
+    _, _, _, err = _check(codec, c2, coff)
+    assert err == (5 << 8) | _abi.SDB_CHECKSUM_MISMATCH
+    parts = [comp[int(coff[k]):int(coff[k + 1])].tobytes() for k in range(len(coff) - 1)]
+    p = parts[1][:-4]
+    parts[1] = frame(p[: len(p) - 7])  # re-framed truncated stream: decompression error in block 1
+    c3 = np.frombuffer(b"".join(parts), np.uint8).copy()
+    o3 = np.cumsum([0] + [len(x) for x in parts]).astype(np.uint64)
+    _, _, _, err = _check(codec, c3, o3)
+    assert err == (1 << 8) | _abi.SDB_DECOMPRESSION_ERROR
+
+
+def test_unsupported_codecs():
+    lib = runtime.lib()
+    z = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    for c in (_abi.CODEC_ZLIB, _abi.CODEC_ZSTD):
+        assert lib.sdb_decompress_plan(c, z.data_ptr(), z.data_ptr(), 0, z.data_ptr(), z.data_ptr(), 64, None) == \
+            _abi.SDB_UNSUPPORTED
