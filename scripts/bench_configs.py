@@ -338,6 +338,65 @@ def compact_bench(reps):
     comp.close()
 
 
+def codec_bench(reps):
+    """f3: 4 D1 SSTs (68,064 blocks) compressed per block (LZ4 / Snappy via the canonical C++ codecs in
+    pyarrow, framed as compress_and_transform does), then on the device: sdb_decompress_blocks
+    (CRC check + decompress + re-frame) and the decode of the result.  Device-resident, HIP events."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from codec_util import compress_run
+    from oracle import oracle as O
+    lib = runtime.lib()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(device=dev)
+    prm = runtime.params(block_size=4096, sst_version=2, bloom_bits_per_key=0)
+    datas, offs, base, nent, kbytes = [], [], 0, 0, 0
+    for j in range(4):
+        h = datasets.d1(sst_index=j)
+        db = h.to_device(dev)
+        out = runtime.DeviceSstOutput(h.n, h.logical_bytes(), h.logical_bytes(), prm, device=dev)
+        runtime.encode_sst_device(db, out)
+        torch.cuda.synchronize()
+        r = out.to_host()
+        datas.append(r["data"])
+        bo = r["block_off"].astype(np.uint64)
+        offs.append((bo[:-1] if j < 3 else bo) + np.uint64(base))
+        base += int(r["data"].size)
+        nent += h.n
+        kbytes += int(h.key_off[-1])
+        del db, out
+    data, block_off = np.concatenate(datas), np.concatenate(offs)
+    nb = len(block_off) - 1
+    for codec, name in ((O.CODEC_LZ4, "lz4"), (O.CODEC_SNAPPY, "snappy")):
+        comp, coff = compress_run(codec, data, block_off)
+        dc = torch.from_numpy(comp).to(dev)
+        do = torch.from_numpy(coff.view(np.int64)).to(dev)
+        with torch.cuda.stream(s):
+            o, start, end, err = runtime.decompress_blocks_device(codec, dc, do, stream=s)
+        torch.cuda.synchronize()
+        total = int(start[nb].item())
+        ok = int(err.cpu().numpy().view(np.uint64)[0]) == 2**64 - 1 and np.array_equal(o[:total].cpu().numpy(), data)
+        fn = lib.sdb_decompress_blocks
+
+        def run():
+            if fn(codec, dc.data_ptr(), do.data_ptr(), nb, o.data_ptr(), total, start.data_ptr(), end.data_ptr(),
+                  err.data_ptr(), s.cuda_stream):
+                raise RuntimeError("sdb_decompress_blocks")
+
+        with torch.cuda.stream(s):
+            ms = timed(run, reps, s)
+        dout = runtime.DeviceDecodeOutput(nb, nent + 16, kbytes + 4096, device=dev)
+
+        def dec():
+            runtime.decode_blocks_at_device(o, start[:nb], end, nb, dout, 2, stream=s)
+
+        with torch.cuda.stream(s):
+            ms_dec = timed(dec, reps, s)
+        print(json.dumps({"what": "f3 decompress (%s) of 4 D1 SSTs" % name, "blocks": nb, "compressed_bytes": int(comp.size),
+                          "decompressed_bytes": total, "ratio": round(total / comp.size, 4), "ms": round(ms, 4),
+                          "GiB_per_s_decompressed": round(total / (ms * 1e-3) / 2**30, 2),
+                          "decode_after_ms": round(ms_dec, 4), "bit_exact": bool(ok)}), flush=True)
+
+
 def hbm_bench(reps):
     """STREAM-like: torch's copy kernel over 4 GiB (read + write) and a read-only int64 sum."""
     dev = torch.device("cuda", 0)
@@ -364,11 +423,12 @@ def main():
     p.add_argument("--e2e", action="store_true")
     p.add_argument("--compact", action="store_true")
     p.add_argument("--hbm", action="store_true")
+    p.add_argument("--codec", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="decode CPU baseline budget (0: skip)")
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--no-granular", action="store_true", help="decode: skip the 2 MiB granularity run")
     a = p.parse_args()
-    allp = not (a.decode or a.bloom or a.e2e or a.compact or a.hbm)
+    allp = not (a.decode or a.bloom or a.e2e or a.compact or a.hbm or a.codec)
     torch.cuda.set_device(0)
     runtime.require_device()
     if a.bloom or allp:
@@ -379,6 +439,8 @@ def main():
         e2e_bench(a.reps)
     if a.hbm or allp:
         hbm_bench(a.reps)
+    if a.codec or allp:
+        codec_bench(max(3, a.reps // 2))
     if a.compact or allp:
         compact_bench(max(3, a.reps // 4))
 

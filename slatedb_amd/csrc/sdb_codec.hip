@@ -27,9 +27,9 @@
 
 namespace sdb {
 
-constexpr uint32_t kDzThreads = 256;                    // 4 waves per workgroup
-constexpr uint32_t kDzIn = 8192;                        // compressed bytes staged per wave
-constexpr uint32_t kDzOut = 16384;                      // decompressed image per wave
+constexpr uint32_t kDzThreads = 1024;                   // 16 waves per workgroup, one workgroup per CU
+constexpr uint32_t kDzIn = 4096 + 256;                  // compressed bytes staged per wave (a 4 KiB block)
+constexpr uint32_t kDzOut = 4096 + 256;                 // decompressed image per wave
 constexpr uint64_t kMaxBlockOut = 64ull << 20;          // larger declared lengths: SDB_LIMIT_EXCEEDED
 constexpr uint32_t kDzWaveLds = kDzIn + 32 + kDzOut;
 constexpr uint32_t kDzLds = 8 * 1024 + (kDzThreads / 64) * kDzWaveLds;  // slicing tables, then the waves
@@ -89,6 +89,19 @@ __global__ __launch_bounds__(256) void k_dz_plan(DzArgs a) {
 // The byte of `p` every lane reads (a wave-uniform LDS broadcast, or one lane's global read), kept scalar.
 template <typename P>
 SDB_DEV uint32_t ub(P p) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)*p); }
+
+// The 8 bytes at p as one wave-uniform little-endian word: eight byte reads issued together (one LDS
+// round trip instead of one per header byte).  Wave mode only: p lies in the staged block, which has
+// slack past its end.
+template <typename P>
+SDB_DEV uint64_t win8(P p) {
+    uint32_t b[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) b[i] = p[i];
+    const uint32_t lo = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24, hi = b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24;
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)lo) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)hi) << 32;
+}
 
 // Copies of one decoder step: lanes first, first + step, ... (64-lane wave mode, or one lane: 0, 1).
 template <typename PI, typename PO>
@@ -213,13 +226,123 @@ SDB_DEV int dz_snappy(PI in, uint32_t n, PO out, uint32_t len, uint32_t first, u
     return op == len ? 0 : SDB_DECOMPRESSION_ERROR;
 }
 
+// The same LZ4 decode for the wave mode (input staged in LDS): each sequence reads its header through two
+// 8-byte windows, the second issued before the literal copy so its latency overlaps it.
+template <typename PI, typename PO>
+SDB_DEV int dz_lz4_win(PI in, uint32_t n, PO out, uint32_t cap, uint32_t *olen, uint32_t first) {
+    uint32_t ip = 0, op = 0;
+    for (;;) {
+        if (ip >= n) return SDB_DECOMPRESSION_ERROR;
+        uint64_t w = win8(in + ip);
+        const uint32_t tok = (uint32_t)w & 0xFF;
+        uint32_t c = 1, lit = tok >> 4;
+        if (lit == 15) {
+            uint32_t b;
+            do {
+                if (ip + c >= n) return SDB_DECOMPRESSION_ERROR;
+                if (c == 8) {
+                    ip += 8;
+                    c = 0;
+                    w = win8(in + ip);
+                }
+                b = (uint32_t)(w >> (8 * c)) & 0xFF;
+                c++;
+                lit += b;
+            } while (b == 255);
+        }
+        ip += c;
+        if (lit > n - ip || lit > cap - op) return SDB_DECOMPRESSION_ERROR;
+        const bool last = ip + lit == n;
+        const uint64_t w2 = last ? 0 : win8(in + ip + lit);  // offset + match extension, in flight over the copy
+        dz_literal(out, op, in, ip, lit, first, 64u);
+        ip += lit;
+        op += lit;
+        if (last) break;
+        if (n - ip < 2) return SDB_DECOMPRESSION_ERROR;
+        const uint32_t off = (uint32_t)w2 & 0xFFFF;
+        uint32_t ml = (tok & 15) + 4;
+        c = 2;
+        w = w2;
+        if ((tok & 15) == 15) {
+            uint32_t b;
+            do {
+                if (ip + c >= n) return SDB_DECOMPRESSION_ERROR;
+                if (c == 8) {
+                    ip += 8;
+                    c = 0;
+                    w = win8(in + ip);
+                }
+                b = (uint32_t)(w >> (8 * c)) & 0xFF;
+                c++;
+                ml += b;
+            } while (b == 255);
+        }
+        ip += c;
+        if (off == 0 || off > op || ml > cap - op) return SDB_DECOMPRESSION_ERROR;
+        dz_sync(true);  // the literals and earlier matches (other lanes' writes) before the match reads them
+        dz_match(out, op, off, ml, first, 64u);
+        op += ml;
+    }
+    *olen = op;
+    return 0;
+}
+
+// Snappy for the wave mode: one 8-byte window per element (tag + up to four length / offset bytes).
+template <typename PI, typename PO>
+SDB_DEV int dz_snappy_win(PI in, uint32_t n, PO out, uint32_t len, uint32_t first) {
+    uint32_t ip = 0, op = 0;
+    while (ip < n) {
+        const uint64_t w = win8(in + ip);
+        const uint32_t tag = (uint32_t)w & 0xFF;
+        const uint32_t rest = n - ip - 1;  // bytes after the tag
+        if ((tag & 3) == 0) {
+            uint32_t l = tag >> 2, nb = 0;
+            if (l >= 60) {
+                nb = l - 59;
+                if (rest < nb) return SDB_DECOMPRESSION_ERROR;
+                l = (uint32_t)(w >> 8) & (nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1));
+                if (l == 0xFFFFFFFFu) return SDB_DECOMPRESSION_ERROR;
+            }
+            l += 1;
+            ip += 1 + nb;
+            if (l > n - ip || l > len - op) return SDB_DECOMPRESSION_ERROR;
+            dz_literal(out, op, in, ip, l, first, 64u);
+            ip += l;
+            op += l;
+            continue;
+        }
+        uint32_t l, off, nb;
+        if ((tag & 3) == 1) {
+            nb = 1;
+            l = 4 + ((tag >> 2) & 7);
+            off = ((tag >> 5) << 8) | ((uint32_t)(w >> 8) & 0xFF);
+        } else if ((tag & 3) == 2) {
+            nb = 2;
+            l = 1 + (tag >> 2);
+            off = (uint32_t)(w >> 8) & 0xFFFF;
+        } else {
+            nb = 4;
+            l = 1 + (tag >> 2);
+            off = (uint32_t)(w >> 8);
+        }
+        if (rest < nb) return SDB_DECOMPRESSION_ERROR;
+        ip += 1 + nb;
+        if (off == 0 || off > op || l > len - op) return SDB_DECOMPRESSION_ERROR;
+        dz_sync(true);
+        dz_match(out, op, off, l, first, 64u);
+        op += l;
+    }
+    return op == len ? 0 : SDB_DECOMPRESSION_ERROR;
+}
+
 template <typename PI, typename PO>
 SDB_DEV int dz_payload(uint32_t codec, PI in, uint32_t n, PO out, uint32_t decl, uint32_t *olen, uint32_t first,
                        uint32_t step) {
     const uint32_t h = dz_header_len(codec, in);
-    if (codec == SDB_CODEC_LZ4) return dz_lz4(in + h, n - h, out, decl, olen, first, step);
+    if (codec == SDB_CODEC_LZ4)
+        return step > 1 ? dz_lz4_win(in + h, n - h, out, decl, olen, first) : dz_lz4(in + h, n - h, out, decl, olen, first, step);
     *olen = decl;
-    return dz_snappy(in + h, n - h, out, decl, first, step);
+    return step > 1 ? dz_snappy_win(in + h, n - h, out, decl, first) : dz_snappy(in + h, n - h, out, decl, first, step);
 }
 
 // crc32fast::hash of msg[0, n) (generic pointer: LDS or HBM), every lane; tab: slicing tables in LDS.
@@ -283,8 +406,14 @@ __global__ __launch_bounds__(kDzThreads) void k_dz_run(DzArgs a) {
                             img[ol + 3] = (uint8_t)c;
                         }
                         dz_sync(true);
+                        // 16-byte stores (unaligned in HBM, aligned in LDS), the < 16-byte tail by bytes
                         uint8_t *g = a.out + o;
-                        for (uint32_t q = l; q < ol + 4; q += 64) g[q] = img[q];
+                        const uint32_t L = ol + 4, nfull = L >> 4;
+                        for (uint32_t q = l; q < nfull; q += 64) {
+                            const uint4 v = ((const uint4 *)img)[q];
+                            __builtin_memcpy(g + 16 * q, &v, 16);
+                        }
+                        if (l < (L & 15)) g[(nfull << 4) + l] = img[(nfull << 4) + l];
                     }
                 } else {
                     // one lane, HBM to HBM (the match reads see the lane's own earlier stores)
@@ -365,8 +494,8 @@ hipError_t launch_decompress_run(uint32_t codec, const uint8_t *blocks, const ui
         int dev = 0, cus = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        uint64_t wgs = (nblocks + 3) / 4;
-        const uint64_t most = (uint64_t)(cus > 0 ? cus : 256) * 4;
+        uint64_t wgs = (nblocks + 15) / 16;
+        const uint64_t most = (uint64_t)(cus > 0 ? cus : 256) * 2;
         if (wgs > most) wgs = most;
         hipLaunchKernelGGL(k_dz_run, dim3((uint32_t)wgs), dim3(kDzThreads), kDzLds, st, a);
     }
