@@ -50,6 +50,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--bpk", type=int, default=10, help="bloom bits per key (0 = no filter; diagnostics)")
+    p.add_argument("--block-size", type=int, default=4096, help="SstBlockSize (diagnostics; the metric is 4096)")
     return p.parse_args()
 
 
@@ -143,7 +144,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     runtime.require_device()
     lib = runtime.lib()
-    prm = runtime.params(block_size=4096, sst_version=2, restart_interval=16, bloom_bits_per_key=args.bpk)
+    prm = runtime.params(block_size=args.block_size, sst_version=2, restart_interval=16, bloom_bits_per_key=args.bpk)
 
     # this rank's SSTs: the fixed job's share (configs[4]) or `batch` per step (weak scaling)
     if args.job_ssts:
@@ -180,7 +181,7 @@ def main():
         step(0)
         torch.cuda.synchronize()
         from oracle import oracle as O
-        oprm = O.params(block_size=4096, sst_version=2, bloom_bits_per_key=args.bpk)
+        oprm = O.params(block_size=args.block_size, sst_version=2, bloom_bits_per_key=args.bpk)
         verified = True
         for q in sorted({0, batch - 1}):
             got = outs[0][q].to_host()
@@ -268,7 +269,7 @@ def main():
                                 "configs[4]; each SST = configs[1]: 578,524 x 16 B key / 100 B value -> 17,016 "
                                 "V2 4 KiB blocks + CRC32 + bloom 10 bits/key), one sdb_encode_ssts launch "
                                 "sequence" % batch),
-                   "ssts_per_gpu_per_step": batch, "entries_per_sst": hosts[0].n, "block_size": 4096,
+                   "ssts_per_gpu_per_step": batch, "entries_per_sst": hosts[0].n, "block_size": args.block_size,
                    "sst_version": 2, "bloom_bits_per_key": args.bpk, "resident_input_ssts_per_gpu": len(dbs),
                    "parallelism": "independent SSTs per GPU (no collective)"},
         "roofline": {"bound": "hbm", "kernel": "whole encode pipeline (k_facts + fused bloom binning, k_seg, k_group, "

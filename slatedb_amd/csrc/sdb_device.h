@@ -157,6 +157,15 @@ static __constant__ CrcTables c_crc = make_crc_tables();
 static __constant__ CrcShift64 c_shift = make_shift64();
 static __constant__ CrcSegShift c_seg = make_seg_shift();
 static __constant__ CrcMul256 c_mul256 = make_mul256();
+struct CrcX8 {  // x^(8 r), r < 64: with c_seg.seg, the shift of a CRC past any n < 5120 bytes
+    uint32_t t[64];
+};
+constexpr CrcX8 make_x8() {
+    CrcX8 r{};
+    for (int i = 0; i < 64; i++) r.t[i] = x8n_c((uint64_t)i);
+    return r;
+}
+static __constant__ CrcX8 c_x8 = make_x8();
 static __device__ const CrcSegMul g_seg_mul = make_seg_mul();
 SDB_DEV uint32_t seg_shift_mul(uint32_t k, uint32_t c) {
     const uint32_t(*t)[256] = g_seg_mul.t[k];
@@ -172,6 +181,10 @@ SDB_DEV uint32_t gf_mul(uint32_t a, uint32_t b) {
         b = (b >> 1) ^ (kPoly & (0u - (b & 1u)));
     }
     return p;
+}
+// A raw CRC shifted past n more message bytes (n < 5120): c * x^(8 n).
+SDB_DEV uint32_t crc_shift_bytes(uint32_t c, uint32_t n) {
+    return gf_mul(gf_mul(c_seg.seg[n >> 6], c_x8.t[n & 63]), c);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -14,6 +14,8 @@ constexpr uint32_t kImgCap = 4096 + 64;      // LDS block image per wave (fast p
 constexpr uint32_t kStageCap = 4096;         // value staging per wave (LDS-DMA, 1 KiB per instruction), in place
 constexpr uint32_t kStageGuard = 64;         // LDS bytes before each image the value stage may use
 constexpr uint32_t kKeyStageCap = 1024;      // key staging per wave
+// k_emit's piece path (blocks over one image): a row it can stage with other rows' pieces
+constexpr uint32_t kPieceRowMax = 4000, kPieceKeyMax = 960, kPieceValMax = 3968;
 constexpr uint32_t kSegLook = 1024;           // k_seg: max lookahead entries staged past the chunk
 constexpr uint32_t kSegSpan = kChunk + kSegLook;
 constexpr uint32_t kSegThreads = 1024;
@@ -91,8 +93,11 @@ struct EncodeArgs {
     uint32_t *wmax;
     uint32_t *slow_count;
     uint32_t *slow_list;
+    uint32_t *big_count;    // blocks over one k_emit image whose rows fit pieces (k_emit_big)
+    uint32_t *big_list;
     BlockDesc *desc;
     uint64_t *stat_part;    // per k_facts workgroup: raw key, raw val, puts, deletes, merges
+    uint32_t *huge_part;    // per k_facts workgroup (= chunk): 1 if a row is too large for k_emit's piece path
     uint32_t *wmax_part;    // per chunk: longest candidate block (entries)
     unsigned long long *err_part;  // per k_facts workgroup: min (entry << 8 | code) of the checks (~0: none)
     uint32_t *gtab_exit;    // per group of kGroup chunks, seg_look candidates: composed transfer table
@@ -126,7 +131,9 @@ struct EncodeArgs {
 // the SST's workspace base; the bloom slots come last and are sized on the host.
 struct EncodeWorkspace {
     uint64_t lcp, szr, sznr, hd, row_scratch, next, bbytes, tab_exit, tab_cnt, tab_bytes;
-    uint64_t anchor_e, anchor_blk, anchor_byte, err, wmax, slow_count, slow_list, desc, stat_part, wmax_part, bloom_rep;
+    uint64_t anchor_e, anchor_blk, anchor_byte, err, wmax, slow_count, slow_list, big_count, big_list, desc, stat_part,
+        huge_part, wmax_part,
+        bloom_rep;
     uint64_t err_part, done, gtab_exit, gtab_cnt, gtab_bytes, mode, blen;
     uint64_t total;
 };
@@ -159,9 +166,12 @@ __host__ __device__ inline EncodeWorkspace encode_workspace_offsets(uint64_t n, 
     w.wmax = take(4);
     w.slow_count = take(4);
     w.slow_list = take(4 * (n + 1));
+    w.big_count = take(4);
+    w.big_list = take(4 * (n + 1));
     w.desc = take(sizeof(BlockDesc) * (n + 1));
     const uint64_t nf = (n + kFactsEntries - 1) / kFactsEntries;
     w.stat_part = take(8 * 5 * (nf + 1));
+    w.huge_part = take(4 * (nf + 1));
     w.wmax_part = take(4 * (nc + 1));
     w.err_part = take(8 * (nf + 1));
     w.done = take(8);
@@ -268,8 +278,11 @@ __host__ __device__ inline EncodeArgs make_args(const SstSet &P, uint32_t i) {
     a.wmax = (uint32_t *)(b + w.wmax);
     a.slow_count = (uint32_t *)(b + w.slow_count);
     a.slow_list = (uint32_t *)(b + w.slow_list);
+    a.big_count = (uint32_t *)(b + w.big_count);
+    a.big_list = (uint32_t *)(b + w.big_list);
     a.desc = (BlockDesc *)(b + w.desc);
     a.stat_part = (uint64_t *)(b + w.stat_part);
+    a.huge_part = (uint32_t *)(b + w.huge_part);
     a.wmax_part = (uint32_t *)(b + w.wmax_part);
     a.err_part = (unsigned long long *)(b + w.err_part);
     a.gtab_exit = (uint32_t *)(b + w.gtab_exit);

@@ -191,6 +191,7 @@ __global__ __launch_bounds__(kFactsThreads) void k_facts(SstSet P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t blds[];  // fused bloom binning
     __shared__ uint64_t s_part[kFactsThreads / 64][5];
     __shared__ unsigned long long s_err[kFactsThreads / 64];
+    __shared__ uint32_t s_huge[kFactsThreads / 64];
     const uint32_t tid = threadIdx.x, lane = (uint32_t)lane_id();
     const uint64_t e0 = (uint64_t)blockIdx.x * kFactsEntries + tid;  // entries e0 + r * kFactsThreads
     const uint64_t n = a.n;
@@ -241,6 +242,7 @@ __global__ __launch_bounds__(kFactsThreads) void k_facts(SstSet P) {
     }
     uint64_t rk = 0, rv = 0, c = 0;
     uint64_t err = ~0ull;
+    bool huge = false;  // a row k_emit's piece path cannot stage (the block goes to the workgroup path)
     uint32_t hh[kFactsPerT], dd[kFactsPerT];
 #pragma unroll
     for (uint32_t r = 0; r < kFactsPerT; r++) {
@@ -272,6 +274,7 @@ __global__ __launch_bounds__(kFactsThreads) void k_facts(SstSet P) {
                 const uint64_t ev = (e << 8) | (uint64_t)x.err;
                 err = ev < err ? ev : err;
             }
+            huge |= x.s_r > kPieceRowMax || x.klen > kPieceKeyMax || x.vlen > kPieceValMax;
             rk += x.klen;
             rv += x.vlen;
             c += (uint64_t)(x.kind == SDB_KIND_VALUE) | ((uint64_t)(x.kind == SDB_KIND_TOMBSTONE) << 20) |
@@ -292,6 +295,8 @@ __global__ __launch_bounds__(kFactsThreads) void k_facts(SstSet P) {
         s_part[w][4] = (c >> 40) & 0xFFFFF;
         s_err[w] = err;
     }
+    const bool wh = __ballot(huge) != 0;
+    if (lane == 0) s_huge[w] = wh ? 1u : 0u;
     __syncthreads();
     if (tid < 5) {
         uint64_t t = 0;
@@ -302,6 +307,9 @@ __global__ __launch_bounds__(kFactsThreads) void k_facts(SstSet P) {
         unsigned long long m = ~0ull;
         for (uint32_t q = 0; q < kFactsThreads / 64; q++) m = s_err[q] < m ? s_err[q] : m;
         a.err_part[blockIdx.x] = m;  // every workgroup writes its slot: no initialisation needed
+        uint32_t h = 0;
+        for (uint32_t q = 0; q < kFactsThreads / 64; q++) h |= s_huge[q];
+        a.huge_part[blockIdx.x] = h;
     }
     // the fused bloom: this workgroup's kChunk keys are one binning tile (sdb_bloom.h)
     if (a.bloom_fused) {
@@ -617,6 +625,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(SstSet P) {
         *a.wmax = W;
         *a.err = s_err;
         *a.slow_count = 0;
+        *a.big_count = 0;
         a.done[0] = 0;
         a.done[1] = 0;
         *a.mode = fast ? 1u : 0u;
@@ -1007,8 +1016,19 @@ __global__ __launch_bounds__(kEnumThreads) void k_enum(SstSet P) {
         d.ke = a.key_off[e];
         d.bb = bl_b[t];
         d.pad = 0;
+        if (!emit_fast(d)) {
+            // too big for one wave image: k_emit's piece path, unless a row is too large for a piece
+            // (then the workgroup path, marked pad = 1)
+            uint32_t h = 0;
+            for (uint64_t q = s / kChunk; q <= (e - 1) / kChunk; q++) h |= a.huge_part[q];
+            if (h) {
+                d.pad = 1;
+                a.slow_list[atomicAdd(a.slow_count, 1u)] = blk;
+            } else {
+                a.big_list[atomicAdd(a.big_count, 1u)] = blk;
+            }
+        }
         a.desc[blk] = d;
-        if (!emit_fast(d)) a.slow_list[atomicAdd(a.slow_count, 1u)] = blk;
     }
     PHASE_MARK_E(5);
 }
@@ -1480,6 +1500,199 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     wave_sync();
 }
 
+// Blocks that do not fit one wave image (over 64 rows or 4 KiB: block sizes of 8-64 KiB) but whose rows
+// each fit a piece: the wave assembles the block as consecutive pieces of <= 64 rows and <= 4 KiB, each
+// exactly like a small block's rows (metadata lane = row, staged keys / values, row-lane copies, literal
+// header / trailer), stores each piece at its offset in the block and chains the CRC32 over the pieces
+// (raw(A || B) = raw(A) x^(8 |B|) + raw(B), crc_shift_bytes).  Restart offsets go straight to their
+// trailer slots (the trailer's position, D = block bytes - 4 - 2 - 2 noffs, is known from k_seg's block
+// size); the trailer is CRC'd last, read back through the image.  No prefetch: the pieces of one block
+// keep the wave busy while other waves' loads are in flight.
+template <int V>
+SDB_DEV void emit_big(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, lu8 *img, lu8 *kst, lSpanCopy *rtab) {
+    const uint32_t l = (uint32_t)lane_id();
+    const uint32_t ne = d.e - d.s, ri = a.restart_interval;
+    const uint32_t noffs = (V == 2) ? (ne + ri - 1) / ri : ne;
+    const uint32_t Lc = d.bb - 4, D = Lc - 2 * noffs - 2;
+    uint8_t *gblk = a.out_data + d.off;
+    const uint32_t vstage = lds_addr((const void *)img) - kStageGuard, kstage = lds_addr((const void *)kst);
+    const uint32_t fkl = (uint32_t)(a.key_off[d.s + 1] - d.ks);  // V1: prefixes against the block's first key
+    uint32_t crc = 0, base = 0, pu = 0, de = 0, me = 0, ik = 0;
+    for (uint32_t r = 0; r < ne;) {
+        const uint32_t nr = ne - r < 64 ? ne - r : 64;
+        const bool row = l < nr;
+        const uint64_t j = d.s + r + (row ? l : 0);
+        const uint64_t ko = a.key_off[j], ko1 = a.key_off[j + 1], vo = a.val_off[j], vo1 = a.val_off[j + 1];
+        const uint64_t seq = a.seq ? a.seq[j] : 0;
+        const uint32_t lcp = a.lcp[j];
+        const uint8_t kind = row && a.kind ? a.kind[j] : 0, mask = row && a.ts_mask ? a.ts_mask[j] : 0;
+        const int64_t cts = (mask & SDB_TS_CREATE) ? a.create_ts[j] : 0, ets = (mask & SDB_TS_EXPIRE) ? a.expire_ts[j] : 0;
+        const uint32_t klen = row ? (uint32_t)(ko1 - ko) : 0;
+        const uint32_t vlen = (row && kind != SDB_KIND_TOMBSTONE) ? (uint32_t)(vo1 - vo) : 0;
+        uint32_t shared = 0;
+        if (V == 2 && row) shared = ((r + l) % ri == 0) ? 0 : lcp;
+        if (V == 1 && row && r + l > 0) {
+            const uint32_t mn = fkl < klen ? fkl : klen;
+            shared = lcp_bytes(a.key_bytes + d.ks, mn, a.key_bytes + ko, mn);
+        }
+        if (r == 0 && l == 0 && d.s > 0 && !a.wal) {  // compute_index_key (utils.rs:198-226)
+            const uint32_t pkl = (uint32_t)(d.ks - a.key_off[d.s - 1]);
+            ik = (lcp == pkl && pkl == klen) ? klen : lcp + 1;
+        }
+        RowInfo ri_;
+        ri_.shared = shared;
+        ri_.suf = klen - shared;
+        ri_.vlen = vlen;
+        ri_.flags = (uint8_t)((kind == SDB_KIND_MERGE ? SDB_FLAG_MERGE_OPERAND : 0) |
+                              (kind == SDB_KIND_TOMBSTONE ? SDB_FLAG_TOMBSTONE : 0) |
+                              ((mask & SDB_TS_EXPIRE) ? SDB_FLAG_HAS_EXPIRE_TS : 0) |
+                              ((mask & SDB_TS_CREATE) ? SDB_FLAG_HAS_CREATE_TS : 0));
+        const uint32_t ts8 = 8u * (((mask & SDB_TS_CREATE) != 0) + ((mask & SDB_TS_EXPIRE) != 0));
+        uint32_t size = 0, h = 0;
+        if (row) {
+            if (V == 2) {
+                h = varint_len(shared) + varint_len(ri_.suf) + varint_len(vlen);
+                size = h + ri_.suf + vlen + 9 + ts8;
+            } else {
+                h = 4;
+                size = 4 + ri_.suf + 9 + ts8 + (kind == SDB_KIND_TOMBSTONE ? 0 : 4 + vlen);
+            }
+        }
+        ri_.size = size;
+        const uint32_t inc = wave_incl_scan(size);
+        // the piece: the longest prefix of these rows whose bytes, staged values and keys fit
+        const uint64_t va = wave_readlane(vo, 0) & ~15ull, ka = wave_readlane(ko, 0) & ~15ull;
+        const bool fits = row && inc <= 4096 && (vo1 - va) <= kStageCap && (ko1 - ka) <= kKeyStageCap;
+        const uint64_t nofit = __ballot(!fits);
+        const uint32_t c = nofit ? (uint32_t)__builtin_ctzll(nofit) : 64u;
+        if (c == 0) {  // k_enum routes blocks with rows this large to the workgroup path
+            if (l == 0) report_error(a.err, d.s + r, SDB_DEVICE_ERROR);
+            return;
+        }
+        const bool prow = l < c;
+        const uint32_t Lp = wave_readlane(inc, c - 1);
+        const uint64_t ve = wave_readlane(vo1, c - 1), ke = wave_readlane(ko1, c - 1);
+        // stage the piece's values (in place below the image) and keys
+        {
+            const uint32_t nv16 = ve > va ? (uint32_t)((ve - va + 15) >> 4) : 0, nk16 = (uint32_t)((ke - ka + 15) >> 4);
+            const uint4 *vsrc = (const uint4 *)(a.val_bytes + va), *ksrc = (const uint4 *)(a.key_bytes + ka);
+            for (uint32_t q = l; q < nv16; q += 64) {
+                const uint4 g = vsrc[q];
+                u32x4 w;
+                w.x = g.x;
+                w.y = g.y;
+                w.z = g.z;
+                w.w = g.w;
+                *(lu128 *)(uintptr_t)(vstage + 16 * q) = w;
+            }
+            for (uint32_t q = l; q < nk16; q += 64) {
+                const uint4 g = ksrc[q];
+                u32x4 w;
+                w.x = g.x;
+                w.y = g.y;
+                w.z = g.z;
+                w.w = g.w;
+                *(lu128 *)(uintptr_t)(kstage + 16 * q) = w;
+            }
+        }
+        const uint32_t row_off = inc - size;
+        const uint32_t kstart = row_off + h, kend = kstart + ri_.suf;
+        const uint32_t vstart = (V == 2) ? kend : row_off + size - vlen;
+        const uint32_t vend = vlen ? vstart + vlen : kend;
+        SpanCopy sc{0, 0, 0, 0};
+        if (prow) {
+            const uint32_t F0 = kstart & ~3u, F1 = (vend + 3) & ~3u;
+            sc.a = (F0 >> 2) | (((F1 - F0) >> 2) << 16);
+            sc.jk = (kend - F0) >> 2;
+            sc.kb = kstage + (uint32_t)(ko + shared - ka) - (kstart - F0);
+            sc.vb = vstage + (uint32_t)(vo - va) - (vstart - F0);
+        }
+        wave_sync();
+        if (!copy_rows(img, prow, sc)) {
+            if (prow) {
+                rtab[l].a = sc.a;
+                rtab[l].jk = sc.jk;
+                rtab[l].kb = sc.kb;
+                rtab[l].vb = sc.vb;
+            }
+            wave_sync();
+            copy_spans(img, rtab, c);
+        }
+        if (prow) {
+            write_row_hdr_trailer<V>(img + row_off, ri_, seq, ets, cts);
+            const uint32_t kj = (kend & ~3u) > kstart ? (kend & ~3u) : kstart;
+            const lu8 *ksrc = kst + (uint32_t)(ko + shared - ka) - kstart;
+#pragma unroll
+            for (uint32_t q = 0; q < 3; q++)
+                if (kj + q < kend) img[kj + q] = ksrc[kj + q];
+            // the restart offsets go straight to their trailer slots
+            const uint32_t br = base + row_off;
+            if (V == 2) {
+                if ((r + l) % ri == 0) {
+                    if (br > 0xFFFF) report_error(a.err, d.s + r + l, SDB_LIMIT_EXCEEDED);  // block_v2.rs:195
+                    const uint32_t q = (r + l) / ri;
+                    gblk[D + 2 * q] = (uint8_t)(br >> 8);
+                    gblk[D + 2 * q + 1] = (uint8_t)br;
+                }
+            } else {
+                gblk[D + 2 * (r + l)] = (uint8_t)(br >> 8);  // `as u16` (block.rs:163)
+                gblk[D + 2 * (r + l) + 1] = (uint8_t)br;
+            }
+        }
+        wave_sync();
+        if (l < 16) ((lu32 *)(img - kStageGuard))[l] = 0;  // the zero lead-in of the right-aligned segments
+        if (r == 0 && l == 0) ((lu32 *)img)[0] = ~((const lu32 *)img)[0];  // crc32fast's init, folded in
+        wave_sync();
+        crc = crc_shift_bytes(crc, Lp) ^ wave_crc_image_ra(img, Lp) ^ 0xFFFFFFFFu;
+        uint8_t *gp = gblk + base;
+        const uint32_t nfull = Lp >> 4;
+        for (uint32_t cc = l; cc < nfull; cc += 64) {
+            u32x4 v = ((const lu128 *)img)[cc];
+            if (cc == 0 && r == 0) v.x = ~v.x;
+            __builtin_memcpy(gp + 16 * cc, &v, 16);
+        }
+        if (l < (Lp & 15)) {
+            const uint32_t x = (nfull << 4) + l;
+            gp[x] = (r == 0 && x < 4) ? (uint8_t)~img[x] : img[x];
+        }
+        pu += (uint32_t)__popcll(__ballot(prow && kind == SDB_KIND_VALUE));
+        de += (uint32_t)__popcll(__ballot(prow && kind == SDB_KIND_TOMBSTONE));
+        me += (uint32_t)__popcll(__ballot(prow && kind == SDB_KIND_MERGE));
+        base += Lp;
+        r += c;
+        wave_sync();
+    }
+    if (base != D && l == 0) report_error(a.err, d.s, SDB_DEVICE_ERROR);  // internal consistency
+    if (l == 0) {
+        gblk[D + 2 * noffs] = (uint8_t)(noffs >> 8);
+        gblk[D + 2 * noffs + 1] = (uint8_t)noffs;
+    }
+    __threadfence_block();
+    wave_sync();
+    // the trailer [D, Lc) read back through the image in <= 4 KiB windows
+    for (uint32_t t = D; t < Lc; t += 4096) {
+        const uint32_t w = Lc - t < 4096 ? Lc - t : 4096;
+        for (uint32_t q = l; q < w; q += 64) img[q] = gblk[t + q];
+        if (l < 16) ((lu32 *)(img - kStageGuard))[l] = 0;
+        for (uint32_t q = w + l; q < ((w + 63) & ~63u); q += 64) img[q] = 0;
+        wave_sync();
+        crc = crc_shift_bytes(crc, w) ^ wave_crc_image_ra(img, w) ^ 0xFFFFFFFFu;
+        wave_sync();
+    }
+    crc ^= 0xFFFFFFFFu;
+    if (l == 0) {
+        gblk[Lc] = (uint8_t)(crc >> 24);
+        gblk[Lc + 1] = (uint8_t)(crc >> 16);
+        gblk[Lc + 2] = (uint8_t)(crc >> 8);
+        gblk[Lc + 3] = (uint8_t)crc;
+        a.out_block_stats[3 * (uint64_t)blk] = (uint16_t)pu;
+        a.out_block_stats[3 * (uint64_t)blk + 1] = (uint16_t)de;
+        a.out_block_stats[3 * (uint64_t)blk + 2] = (uint16_t)me;
+        a.out_index_key_len[blk] = ik;
+    }
+    wave_sync();
+}
+
 // One wave per block, blocks strided over the grid's waves; each wave runs a two-stage software
 // pipeline: while block i is assembled, CRC'd and stored from LDS, block i + 1's granules and row
 // metadata are in flight into registers, and block i + 2's descriptor behind them.
@@ -1617,7 +1830,7 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(SstSet P) {
                     locate(nblk, nsi, nlb);
                     dv = (nblk < r1 && l < 14) ? desc_dw(nsi)[14 * (uint64_t)nlb + l] : 0;
                 }
-                if (fast) emit_block<V>(make_args(P, csi), clb, d, p, img, kst, rtab, crc, ph);  // slow blocks: done above
+                if (fast) emit_block<V>(make_args(P, csi), clb, d, p, img, kst, rtab, crc, ph);  // others: k_emit_big, slow path
             }
         }
     }
@@ -1800,6 +2013,47 @@ SDB_DEV void emit_slow_blocks(const EncodeArgs &a, uint8_t *scratch, const uint3
 template __global__ void k_emit<1>(SstSet);
 template __global__ void k_emit<2>(SstSet);
 
+// The piece path (emit_big) in a launch of its own, before k_emit (whose last workgroup writes the
+// summaries, so it sees this kernel's errors): inlined into k_emit it cost the fast path its registers.
+// Waves take the set's big blocks round-robin; a set without any returns before the table copy.
+template <int V>
+__global__ __launch_bounds__(kEmitThreads, 1) void k_emit_big(SstSet P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t pre[kMaxSsts + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kMaxSsts; i++) {
+        uint32_t nb = 0;
+        if (i < P.count) {
+            const EncodeArgs ai = make_args(P, i);
+            if (*ai.err == ~0ull) nb = *ai.big_count;
+        }
+        pre[i + 1] = pre[i] + nb;
+    }
+    const uint32_t total = pre[kMaxSsts];
+    if (!total || lds_addr((const void *)smem) != 0) return;
+    crc_tables_to_lds((lu32 *)smem);
+    __syncthreads();
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), wpb = blockDim.x >> 6;
+    lu8 *img = (lu8 *)smem + kCrcLds + 16 + wave * kEmitWaveLds + kStageGuard;
+    lu8 *kst = img + kImgCap + 16;
+    lSpanCopy *rtab = (lSpanCopy *)(kst + kKeyStageCap);
+    for (uint32_t g = blockIdx.x * wpb + wave; g < total; g += gridDim.x * wpb) {
+        uint32_t si = 0, base = 0;
+#pragma unroll
+        for (uint32_t j = 1; j < kMaxSsts; j++)
+            if (g >= pre[j] && pre[j] < total) {
+                si = j;
+                base = pre[j];
+            }
+        const EncodeArgs a = make_args(P, si);
+        const uint32_t blk = a.big_list[g - base];
+        emit_big<V>(a, blk, a.desc[blk], img, kst, rtab);
+    }
+}
+template __global__ void k_emit_big<1>(SstSet);
+template __global__ void k_emit_big<2>(SstSet);
+
 // ------------------------------------------------------------------------------------------------
 // Launcher
 // ------------------------------------------------------------------------------------------------
@@ -1821,6 +2075,7 @@ __global__ void k_init_summary(EncodeArgs a) {
         *a.err = ~0ull;
         *a.wmax = 0;
         *a.slow_count = 0;
+        *a.big_count = 0;
         if (a.n == 0 && a.block_cap + 1 > 0) {  // empty SST: BlockMeta list is empty, offsets = [0]
             a.out_block_off[0] = 0;
             a.out_block_first[0] = 0;
@@ -1883,6 +2138,8 @@ static void set_lds_attrs() {
         }
         (void)hipFuncSetAttribute((const void *)k_emit<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
         (void)hipFuncSetAttribute((const void *)k_emit<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
+        (void)hipFuncSetAttribute((const void *)k_emit_big<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
+        (void)hipFuncSetAttribute((const void *)k_emit_big<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
         (void)hipFuncSetAttribute((const void *)k_enum, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEnumLds);
         (void)hipFuncSetAttribute((const void *)k_group, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGroupLds);
         (void)hipFuncSetAttribute((const void *)k_seg, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
@@ -1918,6 +2175,8 @@ hipError_t launch_encode_set(const SstSet &P, size_t bin_lds, size_t fill_lds, h
     hipLaunchKernelGGL(k_enum, dim3(P.max_chunks, P.count), dim3(kEnumThreads), kEnumLds, st, P);
     stage_mark(st, kStEnum, false);
     stage_mark(st, kStEmit, true);
+    if (P.version == 2) hipLaunchKernelGGL(k_emit_big<2>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, P);
+    else hipLaunchKernelGGL(k_emit_big<1>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, P);
     if (P.version == 2) hipLaunchKernelGGL(k_emit<2>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, P);
     else hipLaunchKernelGGL(k_emit<1>, dim3(emit_grid()), dim3(g_emit_threads), emit_lds(), st, P);
     stage_mark(st, kStEmit, false);
