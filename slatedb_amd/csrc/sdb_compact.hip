@@ -355,7 +355,7 @@ __global__ void k_cut(SstSet P, uint64_t max_sst, uint64_t *cut, uint64_t *num) 
     if (threadIdx.x || blockIdx.x) return;
     const EncodeArgs a = make_args(P, 0);
     const uint64_t n = a.n;
-    const bool fast = *a.mode == 1;
+    const bool fast = *a.mode >= 1;  // 1 and 2: the chunk / group tables describe the chain
     const uint32_t W = *a.wmax, G = a.group, L = a.seg_look;
     uint64_t e = 0, acc = 0, ns = 0;
     bool entry_pt = true;  // reached from the previous chunk (or the stream start): the tables apply

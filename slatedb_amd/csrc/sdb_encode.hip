@@ -619,7 +619,11 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(SstSet P) {
     }
     __syncthreads();
     const uint32_t W = s_W;
-    const bool fast = W >= 1 && W <= a.seg_look && (uint64_t)W * (ngroups + G) * 16 + 64 <= kEnumTabLds;
+    // mode 1: the tables describe the chain and k_enum stages its walk in LDS; mode 2: the same walk
+    // straight from HBM (tables too large for k_enum's LDS: blocks of 16 KiB and more); mode 0: blocks
+    // longer than the staged lookahead, anchors by a serial walk of next()
+    const bool fast = W >= 1 && W <= a.seg_look;
+    const bool enum_lds = (uint64_t)W * (ngroups + G) * 16 + 64 <= kEnumTabLds;
     if (g == 0 && tid == 0) {
         // device state for k_enum / k_emit (this kernel runs alone on the stream)
         *a.wmax = W;
@@ -628,7 +632,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(SstSet P) {
         *a.big_count = 0;
         a.done[0] = 0;
         a.done[1] = 0;
-        *a.mode = fast ? 1u : 0u;
+        *a.mode = fast ? (enum_lds ? 1u : 2u) : 0u;
         sdb_sst_summary *sm = a.summary;
         uint64_t t[5];
         for (int f = 0; f < 5; f++) {
@@ -673,6 +677,31 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(SstSet P) {
     // this group's chunk tables -> LDS (exit offsets clamped into [0, W): candidates past a chunk's
     // own bound are never entry points, their stale slots only need to stay in range)
     const uint32_t k0 = g * G, k1 = k0 + G < K ? k0 + G : K, nk = k1 - k0;
+    if ((uint64_t)nk * W * 14 + 64 > kGroupLds) {
+        // too large for LDS: each candidate walks the chunk tables in HBM (the same clamping)
+        for (uint32_t o = tid; o < W; o += nt) {
+            uint32_t e = o, c = 0;
+            uint64_t b = 0;
+            for (uint32_t j = 0; j < nk; j++) {
+                const uint32_t k = k0 + j;
+                const uint64_t cs = (uint64_t)k * kChunk, ce = cs + kChunk < a.n ? cs + kChunk : a.n;
+                uint32_t x = 0;
+                if (cs + e < ce) {
+                    const uint64_t t = (uint64_t)k * a.seg_look + e;
+                    const uint32_t te = a.tab_exit[t];
+                    x = te >= ce && te - ce < W ? (uint32_t)(te - ce) : W - 1;
+                    c += a.tab_cnt[t];
+                    b += a.tab_bytes[t];
+                }
+                e = x;
+            }
+            const uint64_t t = (uint64_t)g * a.seg_look + o;
+            a.gtab_exit[t] = e;
+            a.gtab_cnt[t] = c;
+            a.gtab_bytes[t] = b;
+        }
+        return;
+    }
     uint16_t *ex = (uint16_t *)smem;                                 // nk x W
     uint32_t *cn_ = (uint32_t *)(smem + ((2 * nk * W + 15) & ~15u)); // nk x W
     uint64_t *by_ = (uint64_t *)((uint8_t *)cn_ + ((4 * nk * W + 15) & ~15u));
@@ -858,7 +887,54 @@ __global__ __launch_bounds__(kEnumThreads) void k_enum(SstSet P) {
     uint32_t *bl_b = bl_s + kChunk;
     uint64_t *bl_o = (uint64_t *)(bl_b + kChunk);
     uint16_t *lv = (uint16_t *)(bl_o + kChunk);
-    if (*a.mode) {
+    if (*a.mode == 2) {
+        // the same walk as below, one thread straight through the tables in HBM (they do not fit LDS)
+        if (tid == 0) {
+            const uint32_t W = *a.wmax, G = a.group, g = k / G, k0 = g * G;
+            uint32_t e = 0;
+            uint64_t blk = 0, by = 0;
+            for (uint32_t q = 0; q < g; q++) {
+                const uint64_t t = (uint64_t)q * a.seg_look + e;
+                blk += a.gtab_cnt[t];
+                by += a.gtab_bytes[t];
+                const uint32_t x = a.gtab_exit[t];
+                e = x < W ? x : W - 1;
+            }
+            for (uint32_t kk = k0; kk < k; kk++) {
+                const uint64_t ccs = (uint64_t)kk * kChunk, cce = ccs + kChunk < a.n ? ccs + kChunk : a.n;
+                uint32_t x = 0;
+                if (ccs + e < cce) {
+                    const uint64_t t = (uint64_t)kk * a.seg_look + e;
+                    const uint32_t te = a.tab_exit[t];
+                    x = te >= cce ? te - (uint32_t)cce : 0;
+                    blk += a.tab_cnt[t];
+                    by += a.tab_bytes[t];
+                }
+                e = x < W ? x : W - 1;
+            }
+            uint32_t cn = 0;
+            uint64_t cb = 0;
+            if (cs + e < ce) {
+                const uint64_t t = (uint64_t)k * a.seg_look + e;
+                cn = a.tab_cnt[t];
+                cb = a.tab_bytes[t];
+            }
+            s_anc[0] = cs + e;
+            s_anc[1] = blk;
+            s_anc[2] = by;
+            s_anc[3] = cn;
+            if (k + 1 == K) {
+                const uint64_t tb = blk + cn, ty = by + cb;
+                a.anchor_blk[K] = (uint32_t)tb;
+                a.anchor_byte[K] = ty;
+                a.anchor_e[K] = (uint32_t)a.n;
+                a.summary->num_blocks = tb;
+                a.summary->data_len = ty;
+                if (tb > a.block_cap || ty > a.data_cap) report_error(a.err, 0, SDB_INVALID_ARGUMENT);
+            }
+        }
+        __syncthreads();
+    } else if (*a.mode) {
         // walk the group tables of the groups before this chunk's, then this group's chunk tables
         // (k's own last: its block count), from entry 0.  Tables -> LDS first (one batch of loads).
         const uint32_t W = *a.wmax, G = a.group, g = k / G, k0 = g * G, nc = k - k0 + 1;
@@ -1517,6 +1593,11 @@ SDB_DEV void emit_big(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, lu8
     uint8_t *gblk = a.out_data + d.off;
     const uint32_t vstage = lds_addr((const void *)img) - kStageGuard, kstage = lds_addr((const void *)kst);
     const uint32_t fkl = (uint32_t)(a.key_off[d.s + 1] - d.ks);  // V1: prefixes against the block's first key
+    // a trailer of <= 64 bytes is gathered in the 64 image bytes past 4 KiB that no piece touches, and
+    // CRC'd from there; a longer one goes to HBM slot by slot and is read back
+    const uint32_t Tl = 2 * noffs + 2;
+    const bool tr_lds = Tl <= 64;
+    lu8 *tr = img + 4096;
     uint32_t crc = 0, base = 0, pu = 0, de = 0, me = 0, ik = 0;
     for (uint32_t r = 0; r < ne;) {
         const uint32_t nr = ne - r < 64 ? ne - r : 64;
@@ -1627,16 +1708,23 @@ SDB_DEV void emit_big(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, lu8
                 if (kj + q < kend) img[kj + q] = ksrc[kj + q];
             // the restart offsets go straight to their trailer slots
             const uint32_t br = base + row_off;
+            int q = -1;
             if (V == 2) {
                 if ((r + l) % ri == 0) {
                     if (br > 0xFFFF) report_error(a.err, d.s + r + l, SDB_LIMIT_EXCEEDED);  // block_v2.rs:195
-                    const uint32_t q = (r + l) / ri;
+                    q = (int)((r + l) / ri);
+                }
+            } else {
+                q = (int)(r + l);  // `as u16` (block.rs:163)
+            }
+            if (q >= 0) {
+                if (tr_lds) {
+                    tr[2 * q] = (uint8_t)(br >> 8);
+                    tr[2 * q + 1] = (uint8_t)br;
+                } else {
                     gblk[D + 2 * q] = (uint8_t)(br >> 8);
                     gblk[D + 2 * q + 1] = (uint8_t)br;
                 }
-            } else {
-                gblk[D + 2 * (r + l)] = (uint8_t)(br >> 8);  // `as u16` (block.rs:163)
-                gblk[D + 2 * (r + l) + 1] = (uint8_t)br;
             }
         }
         wave_sync();
@@ -1663,14 +1751,28 @@ SDB_DEV void emit_big(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, lu8
         wave_sync();
     }
     if (base != D && l == 0) report_error(a.err, d.s, SDB_DEVICE_ERROR);  // internal consistency
-    if (l == 0) {
-        gblk[D + 2 * noffs] = (uint8_t)(noffs >> 8);
-        gblk[D + 2 * noffs + 1] = (uint8_t)noffs;
+    if (tr_lds) {
+        if (l == 0) {
+            tr[2 * noffs] = (uint8_t)(noffs >> 8);
+            tr[2 * noffs + 1] = (uint8_t)noffs;
+        }
+        wave_sync();
+        const uint8_t v = l < Tl ? tr[l] : 0;
+        if (l < 16) ((lu32 *)(img - kStageGuard))[l] = 0;
+        img[l] = v;
+        wave_sync();
+        crc = crc_shift_bytes(crc, Tl) ^ wave_crc_image_ra(img, Tl) ^ 0xFFFFFFFFu;
+        if (l < Tl) gblk[D + l] = v;
+    } else {
+        if (l == 0) {
+            gblk[D + 2 * noffs] = (uint8_t)(noffs >> 8);
+            gblk[D + 2 * noffs + 1] = (uint8_t)noffs;
+        }
+        __threadfence_block();
+        wave_sync();
     }
-    __threadfence_block();
-    wave_sync();
-    // the trailer [D, Lc) read back through the image in <= 4 KiB windows
-    for (uint32_t t = D; t < Lc; t += 4096) {
+    // a long trailer [D, Lc) read back through the image in <= 4 KiB windows
+    for (uint32_t t = tr_lds ? Lc : D; t < Lc; t += 4096) {
         const uint32_t w = Lc - t < 4096 ? Lc - t : 4096;
         for (uint32_t q = l; q < w; q += 64) img[q] = gblk[t + q];
         if (l < 16) ((lu32 *)(img - kStageGuard))[l] = 0;
