@@ -1076,6 +1076,9 @@ __global__ __launch_bounds__(kEnumThreads) void k_enum(SstSet P) {
             carry += wave_readlane(inc, 63);
         }
     }
+    __shared__ uint32_t s_nbig, s_bigbase;
+    uint32_t *big_local = (uint32_t *)lv;  // the lifting levels are done: this chunk's piece-path blocks
+    if (tid == 0) s_nbig = 0;
     __syncthreads();
     for (uint32_t t = tid; t < nb; t += nt) {
         const uint64_t s = bl_s[t], e = t + 1 < nb ? bl_s[t + 1] : a.next[s];
@@ -1101,10 +1104,17 @@ __global__ __launch_bounds__(kEnumThreads) void k_enum(SstSet P) {
                 d.pad = 1;
                 a.slow_list[atomicAdd(a.slow_count, 1u)] = blk;
             } else {
-                a.big_list[atomicAdd(a.big_count, 1u)] = blk;
+                big_local[atomicAdd(&s_nbig, 1u)] = blk;  // LDS: one global reservation per chunk below
             }
         }
         a.desc[blk] = d;
+    }
+    __syncthreads();
+    const uint32_t nbig = s_nbig;
+    if (nbig) {  // (a global atomic per big block serialised on the counter: 65 us per SST at 8 KiB blocks)
+        if (tid == 0) s_bigbase = atomicAdd(a.big_count, nbig);
+        __syncthreads();
+        for (uint32_t i = tid; i < nbig; i += nt) a.big_list[s_bigbase + i] = big_local[i];
     }
     PHASE_MARK_E(5);
 }

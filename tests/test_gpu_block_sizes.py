@@ -1,0 +1,56 @@
+"""Every SstBlockSize (config.rs:231-267) against the oracle, bit for bit.  Blocks over one k_emit wave
+image take the piece path (k_emit_big: pieces of <= 64 rows / 4 KiB, CRC chained across pieces, short
+trailers gathered in LDS, long ones read back), chains whose chunk tables exceed k_enum's LDS take the
+HBM table walk (mode 2), and blocks with rows too large for a piece the workgroup path."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from slatedb_amd import datasets
+from slatedb_amd.batch import Batch
+
+from .test_gpu_parity import assert_same, encode_both, rt  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("block_size", [8192, 16384, 32768, 65536])
+def test_d1_large_blocks(rt, block_size):  # noqa: F811
+    b = datasets.d1(n=150000, sst_index=11)
+    ref, got = encode_both(rt, b, block_size=block_size, sst_version=2, bloom_bits_per_key=10)
+    assert_same(ref, got, "d1 bs=%d" % block_size)
+
+
+@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("block_size", [8192, 16384])
+def test_mixed_large_blocks(rt, version, block_size):  # noqa: F811
+    # tombstones, merges, timestamps, long keys, values of 0-299 bytes
+    b = datasets.d3(n=6000)
+    ref, got = encode_both(rt, b, block_size=block_size, sst_version=version, bloom_bits_per_key=10)
+    assert_same(ref, got, "d3 v%d bs=%d" % (version, block_size))
+
+
+@pytest.mark.parametrize("restart_interval", [1, 3, 16])
+def test_piece_trailer_paths(rt, restart_interval):  # noqa: F811
+    # 64 KiB blocks of ~40-byte rows: ~1600 rows per block; restart interval 1 makes a 3 KiB trailer
+    # (read back through the image), 16 a ~200-byte one
+    rng = np.random.default_rng(8)
+    ents = [(b"key%012d" % i, 0, bytes(rng.integers(0, 256, 20, dtype=np.uint8)), 5000 - i, None, None)
+            for i in range(5000)]
+    b = Batch.from_entries(ents)
+    ref, got = encode_both(rt, b, block_size=65536, sst_version=2, restart_interval=restart_interval,
+                           bloom_bits_per_key=10)
+    assert_same(ref, got, "ri=%d" % restart_interval)
+
+
+def test_blocks_with_rows_too_large_for_a_piece(rt):  # noqa: F811
+    # 16 KiB blocks where some rows carry 5 KiB values: those blocks stay on the workgroup path, the
+    # others take pieces
+    rng = np.random.default_rng(9)
+    ents = []
+    for i in range(3000):
+        vlen = 5000 if i % 97 == 5 else int(rng.integers(10, 200))
+        ents.append((b"row%08d" % i, 0, bytes(rng.integers(0, 256, vlen, dtype=np.uint8)), 1, None, None))
+    b = Batch.from_entries(ents)
+    ref, got = encode_both(rt, b, block_size=16384, sst_version=2, bloom_bits_per_key=10)
+    assert_same(ref, got, "huge rows")
