@@ -39,9 +39,31 @@ def main():
         e1.record(s)
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / reps / 8 * 1000
-        print(json.dumps({"block_size": bs, "us_per_sst": round(us, 1), "blocks": int(got["summary"].num_blocks),
-                          "GiB_per_s": round(hosts[0].logical_bytes() / (us * 1e-6) / 2**30, 1), "bit_exact": bool(ok)}),
-              flush=True)
+        # decode of SST 0 (sdb_decode_blocks over its data section)
+        nb = int(got["summary"].num_blocks)
+        dout = runtime.DeviceDecodeOutput(nb, hosts[0].n + 16, int(hosts[0].key_off[-1]) + 4096, device=dev)
+        data = outs[0].data[:int(got["summary"].data_len)]
+        boff = outs[0].block_off[:nb + 1]
+
+        def dec():
+            runtime.decode_blocks_at_device(data, boff[:nb], boff[1:], nb, dout, 2, stream=s)
+
+        with torch.cuda.stream(s):
+            dec()
+        torch.cuda.synchronize()
+        dh = dout.to_host()
+        dok = dh.status == 0 and np.array_equal(dh.key_arena, hosts[0].key_bytes)
+        d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        d0.record(s)
+        with torch.cuda.stream(s):
+            for _ in range(reps):
+                dec()
+        d1.record(s)
+        torch.cuda.synchronize()
+        dus = d0.elapsed_time(d1) / reps * 1000
+        print(json.dumps({"block_size": bs, "us_per_sst": round(us, 1), "blocks": nb,
+                          "GiB_per_s": round(hosts[0].logical_bytes() / (us * 1e-6) / 2**30, 1), "bit_exact": bool(ok),
+                          "decode_us_per_sst": round(dus, 1), "decode_keys_ok": bool(dok)}), flush=True)
         del outs, ws
 
 
