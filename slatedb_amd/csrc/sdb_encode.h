@@ -29,10 +29,10 @@ constexpr uint32_t kEmitThreads = 1024;      // 16 waves per workgroup (two bloc
 constexpr uint32_t kEmitWgPerCu = 1;
 constexpr uint32_t kEmitWaveLds = kStageGuard + kImgCap + 16 + kKeyStageCap + 64 * 16;  // guard, image, key stage, spans
 constexpr uint32_t kEmitLds = kCrcLds + 16 + (kEmitThreads / 64) * kEmitWaveLds;  // tables, ticket, waves
-constexpr uint32_t kEnumLds = kChunk * 16 + 12 * kChunk * 2;  // block list + 12 lifting levels
-constexpr uint32_t kEnumTabLds = 12 * kChunk * 2;  // k_enum's table walk (aliases the lifting levels)
+constexpr uint32_t kEnumLds = kChunk * 16 + 11 * kChunk * 2;  // block list + 11 lifting levels (nb <= kChunk = 2^11)
+constexpr uint32_t kEnumTabLds = 11 * kChunk * 2;  // k_enum's table walk (aliases the lifting levels)
 constexpr uint32_t kGroupThreads = 1024;
-constexpr uint32_t kEnumThreads = 1024;
+constexpr uint32_t kEnumThreads = 512;         // two workgroups per CU (76 KiB LDS, 85 VGPRs)
 constexpr uint32_t kGroupLds = kResolveLds;         // group tables, or the single-workgroup resolve
 
 // bloom build plan (sdb_bloom.hip): 2^sb-bit slices, T-key binning tiles
