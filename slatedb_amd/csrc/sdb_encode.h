@@ -18,11 +18,11 @@ constexpr uint32_t kKeyStageCap = 1024;      // key staging per wave
 constexpr uint32_t kPieceRowMax = 4000, kPieceKeyMax = 960, kPieceValMax = 3968;
 constexpr uint32_t kSegLook = 1024;           // k_seg: max lookahead entries staged past the chunk
 constexpr uint32_t kSegSpan = kChunk + kSegLook;
-constexpr uint32_t kSegThreads = 1024;
+constexpr uint32_t kSegThreads = 512;          // four workgroups per CU (kSegLds)
 constexpr uint32_t kFactsThreads = 1024;      // k_facts: a chunk (= a fused bloom tile) per workgroup
 constexpr uint32_t kFactsPerT = 2;            //   entries per thread
 constexpr uint32_t kFactsEntries = kFactsThreads * kFactsPerT;
-constexpr uint32_t kSegLds = (3 * kSegSpan + 4) * 4 + kChunk * 6;
+constexpr uint32_t kSegLds = (2 * kSegSpan + 4) * 4 + kChunk * 6;  // 36 KiB: four workgroups per CU
 constexpr uint32_t kSegLdsMax = 64 * 1024;          // k_seg's LDS with the fused bloom binning
 constexpr uint32_t kHashPerT = kChunk / kSegThreads;  // chunk entries (hashes) per k_seg thread
 constexpr uint32_t kEmitThreads = 1024;      // 16 waves per workgroup (two blocks in flight each), 1 per CU

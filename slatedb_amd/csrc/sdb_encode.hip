@@ -341,8 +341,7 @@ SDB_DEV uint32_t walk_size_v2(const EncodeArgs &a, uint64_t j, bool rs) {
 }
 
 SDB_DEV void seg_chunk(const EncodeArgs &a, uint8_t *smem, uint32_t k) {
-    uint32_t *s_r = (uint32_t *)smem;          // kSegSpan: true restart-row sizes (V1: row sizes)
-    uint32_t *s_P = s_r + kSegSpan;            // kSegSpan + 4: prefix of clamped non-restart sizes
+    uint32_t *s_P = (uint32_t *)smem;          // kSegSpan + 4: prefix of clamped non-restart sizes
     uint32_t *s_R = s_P + kSegSpan + 4;        // kSegSpan: restart surcharge of each entry
     uint32_t *s_bb = s_R + kSegSpan;           // kChunk: encoded block bytes for blocks starting here
     uint16_t *s_nx = (uint16_t *)(s_bb + kChunk);  // kChunk: next(b) - cs (0xFFFF: out of range)
@@ -376,7 +375,6 @@ SDB_DEV void seg_chunk(const EncodeArgs &a, uint8_t *smem, uint32_t k) {
     for (uint32_t u = 0; u < kPerT; u++) {
         const uint32_t x = tid + u * nt;
         if (x >= sn) continue;
-        s_r[x] = zr[u];
         if (v2) {
             const uint32_t cr = zr[u] < clampv ? zr[u] : clampv, cnr = znr[u] < clampv ? znr[u] : clampv;
             s_P[x] = cnr;
@@ -445,7 +443,7 @@ SDB_DEV void seg_chunk(const EncodeArgs &a, uint8_t *smem, uint32_t k) {
                 while (e > lo && size_of(e) > bs) e--;
             }
             j = cs + e;
-            if (e == lo) bytes = 2ull + s_r[x] + 2;  // single row: its true size
+            if (e == lo) bytes = 2ull + a.szr[b] + 2;  // single row: its true size (unclamped, from HBM)
             else bytes = size_of(e);
             if (e == sn && se < a.n) {
                 // the block may continue past the staged span (only for blocks longer than
@@ -488,7 +486,7 @@ SDB_DEV void seg_chunk(const EncodeArgs &a, uint8_t *smem, uint32_t k) {
                     uint64_t ko = a.key_off[j];
                     prefix = lcp_bytes(a.key_bytes + fko, fkl, a.key_bytes + ko, (uint32_t)(a.key_off[j + 1] - ko));
                 }
-                uint64_t sr = j < se ? s_r[j - cs] : entry_facts(a, j).s_r;
+                uint64_t sr = a.szr[j];
                 uint64_t sz = sr - prefix;
                 if (p > 0 && acc + sz > bs) break;  // the new entry's 2-byte offset is not counted (block.rs:117-123)
                 acc += sz + 2;
