@@ -159,6 +159,41 @@ template <uint32_t KPT>
 SDB_DEV void bloom_bin_core(uint32_t tile, const uint32_t (&hh)[KPT], const uint32_t (&dd)[KPT], uint32_t nk,
                             const BloomPlan &pl, const BloomSlots &q, uint32_t *lds) {
     const uint32_t S = pl.nslices;
+    if (pl.one_pass) {
+        // every probe takes the next place of its slice's LDS bucket (cap u16 offsets, the slot's own
+        // capacity: a longer run is an overflow either way), then each bucket is copied to its slot
+        uint32_t *cnt = lds;                           // S
+        uint16_t *bkt = (uint16_t *)(lds + S);         // S x cap
+        const uint32_t tid = threadIdx.x, nt = blockDim.x, cap = q.cap, mask = (1u << pl.sb) - 1;
+        for (uint32_t x = tid; x < S; x += nt) cnt[x] = 0;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; j++)
+            if (tid + j * nt < nk)
+                probes_hd(hh[j], dd[j], pl.k, pl.m, [&](uint32_t p) {
+                    const uint32_t sl = p >> pl.sb, pos = atomicAdd(&cnt[sl], 1u);
+                    if (pos < cap) bkt[sl * cap + pos] = (uint16_t)(p & mask);
+                });
+        __syncthreads();
+        for (uint32_t x = tid; x < S; x += nt) {
+            const uint32_t c = cnt[x];
+            q.count[(uint64_t)tile * S + x] = c <= cap ? c : kSlotOverflow;
+        }
+        // wave w copies buckets w, w + nw, ...: two offsets per lane per step (cap is a multiple of 4)
+        const uint64_t stride = (uint64_t)pl.tiles * cap;
+        uint16_t *slots = (uint16_t *)q.slot + (uint64_t)tile * cap;
+        const uint32_t w = tid >> 6, nw = nt >> 6, l = tid & 63;
+        for (uint32_t sl = w; sl < S; sl += nw) {
+            const uint32_t c0 = cnt[sl], c = c0 < cap ? c0 : cap;
+            const uint32_t *src = (const uint32_t *)(bkt + sl * cap);
+            uint32_t *dst = (uint32_t *)(slots + sl * stride);
+            for (uint32_t i = 2 * l; i < c; i += 128) {
+                if (i + 1 < c) dst[i >> 1] = src[i >> 1];
+                else ((uint16_t *)dst)[i] = (uint16_t)src[i >> 1];
+            }
+        }
+        return;
+    }
     uint32_t *hist = lds;        // S: counts, then local run starts
     uint32_t *cur = hist + S;    // S: local scatter cursors
     uint32_t *sorted = cur + S;  // nk * k probes, slice order

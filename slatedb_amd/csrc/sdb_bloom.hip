@@ -83,6 +83,10 @@ BloomPlan bloom_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes, uint32_t til
     pl.tiles = (uint32_t)((n + T - 1) / T);
     if (pl.tiles == 0) pl.tiles = 1;
     pl.mmod = pl.m ? ~0ull / pl.m + 1 : 0;
+    // one pass (probes straight into per-slice LDS buckets of the slot capacity) when the offsets are
+    // u16 and the buckets take no more LDS than the two-pass counting sort
+    const uint64_t bk = 4ull * pl.nslices + 2ull * pl.nslices * bloom_slot_cap(pl);
+    pl.one_pass = pl.sb <= 16 && bk <= 4ull * (2ull * pl.nslices + (uint64_t)pl.T * pl.k) ? 1u : 0u;
     return pl;
 }
 
@@ -121,7 +125,10 @@ BloomSlots bloom_slots(void *ws, const BloomPlan &pl) {
     return q;
 }
 
-size_t bloom_bin_lds(const BloomPlan &pl) { return 4 * (2 * (size_t)pl.nslices + (size_t)pl.T * pl.k); }
+size_t bloom_bin_lds(const BloomPlan &pl) {
+    if (pl.one_pass) return 4 * (size_t)pl.nslices + 2 * (size_t)pl.nslices * bloom_slot_cap(pl);
+    return 4 * (2 * (size_t)pl.nslices + (size_t)pl.T * pl.k);
+}
 size_t bloom_fill_lds(const BloomPlan &pl) { return 4 * ((size_t)(1u << (pl.sb - 5)) + pl.tiles); }
 
 hipError_t launch_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n,

@@ -847,7 +847,11 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
         Tally t{0, 0, 0, false};
         if (lane_id() == 0) a.rcnt[k] = ~0ull;  // row positions not recorded (tally_v2_fast overwrites)
         if (dec_fast(s, e)) {
+            #ifdef SDB_EXP_CRC8  // diagnostic: slicing-by-8 CRC in the count pass (bank conflicts, half the VALU)
+            const LdsBlockView v = stage_lds(a, s, e, img, true, false, &cur);
+#else
             const LdsBlockView v = stage_lds(a, s, e, img, true, true, &cur);
+#endif
             DEC_T(t1);
             t.status = v.status;
             if (!v.status) {

@@ -40,6 +40,8 @@ struct BloomPlan {
     uint32_t k, m;        // probes per key, bitmap bits
     uint32_t sb;          // log2 bits per slice
     uint32_t nslices, T, tiles;
+    uint32_t one_pass;    // bin straight into per-slice LDS buckets of cap u16 (bloom_bin_core)
+    uint32_t pad;
     uint64_t mmod;        // Lemire fastmod constant: floor((2^64 - 1) / m) + 1
 };
 struct BloomSlots {
