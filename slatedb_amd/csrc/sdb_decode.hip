@@ -36,9 +36,8 @@ constexpr uint32_t kDecWaveLds = kDecGuard + kDecImg + kDecKeys;
 constexpr uint32_t kDecLds = kCrcTablesLds + (kDecThreads / 64) * kDecWaveLds;
 constexpr uint32_t kDecCap = kDecWaveLds - kDecGuard;
 // count pass: the CRC tables, the bank-replicated byte table (sdb_crc.h), then per wave a guard + image
-constexpr uint32_t kCntRep = kCrcTablesLds;
 constexpr uint32_t kCntWaveLds = kDecGuard + kDecImg;
-constexpr uint32_t kCntLds = kCrcTablesLds + kCrcRepLds + (kDecThreads / 64) * kCntWaveLds;
+constexpr uint32_t kCntLds = kCrcTablesLds + (kDecThreads / 64) * kCntWaveLds;
 static_assert(kCntLds <= 160 * 1024, "count pass LDS");
 constexpr uint32_t kRowTmp = kDecKeys - 256;  // emit: row positions of the lane-per-row path (4 x 32 u16) in kbuf
 typedef __attribute__((address_space(3))) uint16_t lu16;  // other blocks: generic staging per wave; larger ones parse from HBM
@@ -414,7 +413,7 @@ SDB_DEV void gran_store(uint64_t s, uint64_t e, const Granules &r, lu8 *img) {
     }
 }
 
-SDB_DEV LdsBlockView stage_lds(const DecodeArgs &a, uint64_t s, uint64_t e, lu8 *img, bool check, bool rep = false,
+SDB_DEV LdsBlockView stage_lds(const DecodeArgs &a, uint64_t s, uint64_t e, lu8 *img, bool check,
                                const Granules *pre = nullptr) {
     LdsBlockView v{};
     const uint32_t l = (uint32_t)lane_id();
@@ -439,7 +438,7 @@ SDB_DEV LdsBlockView stage_lds(const DecodeArgs &a, uint64_t s, uint64_t e, lu8 
 #ifdef SDB_EXP_NO_CRC  // diagnostic: no CRC (every block accepted)
         const uint32_t c = stored;
 #else
-        const uint32_t c = rep ? wave_crc_image_rep<kCntRep>(img, Lc) : wave_crc_image_ra(img, Lc);
+        const uint32_t c = wave_crc_image_ra(img, Lc);
 #endif
         wave_sync_d();
         if (l < 4) img[p0 + l] ^= 0xFF;
@@ -817,11 +816,10 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
         return;
     }
     crc_tables_to_lds((lu32 *)smem);
-    crc_rep_to_lds((lu32 *)(smem + kCntRep));
     __syncthreads();
     const uint32_t(*crc)[256] = (const uint32_t(*)[256])smem;
     const uint32_t wave = threadIdx.x >> 6;
-    lu8 *img = (lu8 *)smem + kCntRep + kCrcRepLds + wave * kCntWaveLds + kDecGuard;
+    lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kCntWaveLds + kDecGuard;
     if (lane_id() < kDecGuard / 4) ((lu32 *)(img - kDecGuard))[lane_id()] = 0;  // never written again
     uint8_t *stage = (uint8_t *)img;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -847,11 +845,9 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
         Tally t{0, 0, 0, false};
         if (lane_id() == 0) a.rcnt[k] = ~0ull;  // row positions not recorded (tally_v2_fast overwrites)
         if (dec_fast(s, e)) {
-            #ifdef SDB_EXP_CRC8  // diagnostic: slicing-by-8 CRC in the count pass (bank conflicts, half the VALU)
-            const LdsBlockView v = stage_lds(a, s, e, img, true, false, &cur);
-#else
-            const LdsBlockView v = stage_lds(a, s, e, img, true, true, &cur);
-#endif
+                        // slicing-by-8 CRC: the pass is VALU-bound, and the bank-replicated byte table costs twice the
+            // VALU per byte for its conflict-free lookups (515 vs 479 us on configs[2])
+            const LdsBlockView v = stage_lds(a, s, e, img, true, &cur);
             DEC_T(t1);
             t.status = v.status;
             if (!v.status) {
@@ -1307,7 +1303,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
         const bool seq = a.flag[k] != 0;
         if (dec_fast(s, e)) {
             DEC_T(t0);
-            const LdsBlockView v = stage_lds(a, s, e, img, false, false, &cur);
+            const LdsBlockView v = stage_lds(a, s, e, img, false, &cur);
             if (v.status) continue;  // cannot happen: the count pass accepted it
             DEC_T(t1);
             if (a.version == 1) {
