@@ -12,6 +12,11 @@ timing barrier and the max / sum of scalars.  `--job-ssts 64` runs configs[4] as
 scaling); `--batch 1` is the single-SST configs[1] shape.  The single-SST latency (sdb_encode_sst,
 one SST per launch sequence) is reported beside the headline as `single_sst`.
 
+`--streams S` (default 2) runs S such builders per GPU concurrently, each on its own HIP stream with its
+own workspace and outputs (step i on stream i mod S): the flush / compaction builders of the reference
+run concurrently, and two launch sequences in flight let one's latency-bound prep kernels overlap the
+other's kernels and tails.  The same sequences back to back on ONE stream are reported as `one_stream`.
+
   python bench.py [--gpus N --steps K --warmup W --batch B]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
@@ -37,9 +42,11 @@ PMC_FILE = "r2_pmc_traffic.json"
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--steps", type=int, default=2200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch", type=int, default=8, help="SSTs per GPU per step (one sdb_encode_ssts call)")
+    p.add_argument("--streams", type=int, default=2,
+                   help="concurrent builders per GPU: step i runs on stream i mod S (its own workspace and outputs)")
     p.add_argument("--job-ssts", type=int, default=0,
                    help="configs[4] fixed job: J distinct SSTs over all ranks (SST j -> rank j mod N), one pass per step")
     p.add_argument("--ssts", type=int, default=0, help="distinct resident input SSTs per rank (0: 2 x batch)")
@@ -162,17 +169,21 @@ def main():
     logical = hosts[0].logical_bytes()
     nsets = max(1, len(dbs) // batch)
     sets = [dbs[q * batch:(q + 1) * batch] for q in range(nsets)]
+    nslot = max(2, args.streams)
     outs = [[runtime.DeviceSstOutput(hosts[0].n, logical, logical, prm, device=dev, workspace=False) for _ in range(batch)]
-            for _ in range(2)]
-    wss = [runtime.ssts_workspace(sets[0], prm, device=dev) for _ in range(2)]
-    stream = torch.cuda.Stream(device=dev)
+            for _ in range(nslot)]
+    wss = [runtime.ssts_workspace(sets[0], prm, device=dev) for _ in range(nslot)]
+    streams = [torch.cuda.Stream(device=dev) for _ in range(max(1, args.streams))]
+    stream = streams[0]
 
-    def step(i):
-        runtime.encode_ssts_device(sets[i % nsets], outs[i % 2], prm, wss[i % 2], stream)
+    def step(i, one_stream=False):
+        # with S streams, slot i mod S (workspace + outputs) only ever runs on stream i mod S
+        q = i % nslot if not one_stream else i % 2
+        st = stream if one_stream else streams[i % len(streams)]
+        runtime.encode_ssts_device(sets[i % nsets], outs[q], prm, wss[q], st)
 
-    with torch.cuda.stream(stream):
-        for i in range(args.warmup):
-            step(i)
+    for i in range(args.warmup):
+        step(i)
     torch.cuda.synchronize()
 
     # verify against the oracle (bit-exact) before timing: the first and the last SST of a set
@@ -202,8 +213,14 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
+    for st in streams[1:]:
+        st.wait_event(ev0)
     for i in range(args.steps):
         step(i)
+    for st in streams[1:]:
+        j = torch.cuda.Event()
+        j.record(st)
+        stream.wait_event(j)
     ev1.record(stream)
     torch.cuda.synchronize()
     if dist:
@@ -215,7 +232,7 @@ def main():
     # per-kernel pass: HIP events recorded around each kernel on the encode stream (sdb_diag_*)
     lib.sdb_diag_enable_stage_timing(1)
     for i in range(args.stage_steps):
-        step(i)
+        step(i, one_stream=True)
     torch.cuda.synchronize()
     lib.sdb_diag_enable_stage_timing(0)
     ms = (C.c_double * 16)()
@@ -226,6 +243,21 @@ def main():
     emit_ms = stage_ms.get("emit", 0.0)
     emit_bytes = batch * (hosts[0].algorithmic_input_bytes() + sm.data_len)  # read keys+values(+seq/flags), write data
     emit_gbs = emit_bytes / (emit_ms * 1e-3) / 1e9 if emit_ms else 0.0
+
+    # the same launch sequences back to back on one stream (no concurrent builders)
+    one_stream = None
+    if len(streams) > 1:
+        k1 = max(1, min(args.steps, 400))
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(k1):
+            step(i, one_stream=True)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        oms = e0.elapsed_time(e1) / k1 / batch
+        og = alg_sst / (oms * 1e-3) / 1e9
+        one_stream = {"device_ms_per_sst": round(oms, 5), "GiB_per_s": round(logical / (oms * 1e-3) / 2**30, 2),
+                      "achieved_GBps": round(og, 1), "frac": round(og / PEAK_HBM_GBS, 4)}
 
     # single-SST latency (configs[1] shape: sdb_encode_sst, one SST per launch sequence)
     single = None
@@ -268,7 +300,9 @@ def main():
                                ("%d distinct 64 MiB L0/compaction SSTs per GPU per step (the per-GPU share of "
                                 "configs[4]; each SST = configs[1]: 578,524 x 16 B key / 100 B value -> 17,016 "
                                 "V2 4 KiB blocks + CRC32 + bloom 10 bits/key), one sdb_encode_ssts launch "
-                                "sequence" % batch),
+                                "sequence; %d such builders in flight per GPU, one HIP stream each"
+                                % (batch, len(streams))),
+                   "builders_per_gpu": len(streams),
                    "ssts_per_gpu_per_step": batch, "entries_per_sst": hosts[0].n, "block_size": args.block_size,
                    "sst_version": 2, "bloom_bits_per_key": args.bpk, "resident_input_ssts_per_gpu": len(dbs),
                    "parallelism": "independent SSTs per GPU (no collective)"},
@@ -285,6 +319,7 @@ def main():
                                 "avg_launch_ms": round(emit_ms, 5), "algorithmic_bytes_per_launch": emit_bytes,
                                 "traffic_per_sst": traffic_kernels.get("k_emit")},
                      "stage_ms_per_step": {k: round(v, 5) for k, v in stage_ms.items()}},
+        "one_stream": one_stream,
         "single_sst": single,
         "verified_vs_oracle": verified,
     }
