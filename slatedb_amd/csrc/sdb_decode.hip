@@ -1251,10 +1251,14 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
         }
         __syncthreads();
         const uint64_t *r = sres + 4 * (threadIdx.x >> 6);
-        s_ent0 = r[0];
-        s_ent1 = r[1];
-        s_kb0 = r[2];
-        s_kb1 = r[3];
+        auto uni = [](uint64_t v) {  // wave-uniform: keep it in scalar registers
+            return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+                   ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
+        };
+        s_ent0 = uni(r[0]);
+        s_ent1 = uni(r[1]);
+        s_kb0 = uni(r[2]);
+        s_kb1 = uni(r[3]);
         __syncthreads();
     } else {
         tot_ent = a.ent_start[a.nblocks];
@@ -1279,28 +1283,56 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
     const bool small = a.small != 0;
     auto off_s = [&](uint64_t kk) { return ((cu64)a.block_off)[kk]; };
     auto off_e = [&](uint64_t kk) { return a.block_end ? ((cu64)a.block_end)[kk] : ((cu64)a.block_off)[kk + 1]; };
+    // the per-block scan results, flag and row counts (scalar loads) and the recorded row positions
+    // (one dword per lane, loaded whether or not the block recorded them) are fetched one block ahead
+    // with its granules, so no block starts on a dependent HBM round trip
+    struct Meta {
+        uint64_t ent0, ent1, kb0, kb1, rcw;
+        uint32_t fw;  // the dword of the flag array holding this block's flag
+        SDB_DEV uint64_t rc(uint64_t kk) const { return ((fw >> (8 * (kk & 3))) & 0xFF) ? ~0ull : rcw; }
+    };
+    typedef const __attribute__((address_space(4))) uint32_t *cu32;
+    auto meta_load = [&](uint64_t kk, Meta &m) {
+        if (kk >= a.nblocks) return;
+        m.ent0 = small ? s_ent0 : ((cu64)a.ent_start)[kk];
+        m.ent1 = small ? s_ent1 : ((cu64)a.ent_start)[kk + 1];
+        m.kb0 = small ? s_kb0 : ((cu64)a.key_start)[kk];
+        m.kb1 = small ? s_kb1 : ((cu64)a.key_start)[kk + 1];
+        m.fw = ((cu32)a.flag)[kk >> 2];  // the flag array is 256-byte aligned (decode_workspace_layout)
+        m.rcw = ((cu64)a.rcnt)[kk];
+    };
+    auto rowpos_load = [&](uint64_t kk) -> uint32_t { return ((const uint32_t *)(a.rowpos + 128 * kk))[l]; };
     uint64_t k = gwave, ns = 0, ne = 0;
     Granules pre;
+    Meta m1{};
+    uint32_t rp1 = 0;
     if (run && k < a.nblocks) {
         ns = off_s(k);
         ne = off_e(k);
         if (dec_fast(ns, ne)) gran_load(a, ns, ne, pre);
+        rp1 = rowpos_load(k);
+        meta_load(k, m1);
     }
     for (; run && k < a.nblocks; k += nwaves) {
         const uint64_t s = ns, e = ne;
         const Granules cur = pre;
+        const Meta m = m1;
+        const uint32_t rp = rp1;
         if (k + nwaves < a.nblocks) {
             ns = off_s(k + nwaves);
             ne = off_e(k + nwaves);
             if (dec_fast(ns, ne)) gran_load(a, ns, ne, pre);
+            rp1 = rowpos_load(k + nwaves);
+            meta_load(k + nwaves, m1);
         }
-        const uint64_t ent0 = small ? s_ent0 : ((cu64)a.ent_start)[k];
-        const uint64_t n_ent = (small ? s_ent1 : ((cu64)a.ent_start)[k + 1]) - ent0;
+        const uint64_t ent0 = m.ent0;
+        const uint64_t n_ent = m.ent1 - ent0;
         if (l == 0) a.out.block_entry_start[k] = ent0;
         if (n_ent == 0) continue;
-        const uint64_t kb0 = small ? s_kb0 : ((cu64)a.key_start)[k];
-        const uint64_t kbn = (small ? s_kb1 : ((cu64)a.key_start)[k + 1]) - kb0;
-        const bool seq = a.flag[k] != 0;
+        const uint64_t kb0 = m.kb0;
+        const uint64_t kbn = m.kb1 - kb0;
+        const uint64_t rc = m.rc(k);
+        const bool seq = rc == ~0ull && ((m.fw >> (8 * (k & 3))) & 0xFF) != 0;
         if (dec_fast(s, e)) {
             DEC_T(t0);
             const LdsBlockView v = stage_lds(a, s, e, img, false, &cur);
@@ -1310,9 +1342,8 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
                 emit_v1(a, v, ent0, kb0, s);
             } else {
                 const bool lds_keys = kbn + 16 <= kDecKeys;
-                const uint64_t rc = seq ? ~0ull : ((cu64)a.rcnt)[k];
                 if (rc != ~0ull && kbn + 16 <= kRowTmp) {
-                    ((lu32 *)(kbuf + kRowTmp))[l] = ((const uint32_t *)(a.rowpos + 128 * k))[l];
+                    ((lu32 *)(kbuf + kRowTmp))[l] = rp;
                     wave_sync_d();
                     emit_v2_rows(a, v, rc, (const lu16 *)(kbuf + kRowTmp), ent0, kb0, s, kbuf);
                 } else {
