@@ -137,6 +137,19 @@ SDB_DEV void key_hd(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t 
 // the probes of for_each_probe from (h0, d0)
 template <typename F>
 SDB_DEV void probes_hd(uint32_t h, uint32_t d, uint32_t k, uint32_t m, F f) {
+    if (m > k && m <= 0x80000000u) {
+        // h + d, d + i < 2m <= 2^32: x mod m = min(x, x - m) in u32 (x - m wraps above x when x < m)
+        for (uint32_t i = 0; i < k; i++) {
+            d += i;
+            const uint32_t dm = d - m;
+            d = dm < d ? dm : d;
+            f(h);
+            h += d;
+            const uint32_t hm = h - m;
+            h = hm < h ? hm : h;
+        }
+        return;
+    }
     const bool small = m <= k;
     for (uint32_t i = 0; i < k; i++) {
         if (small) d = (uint32_t)(((uint64_t)d + i) % m);
