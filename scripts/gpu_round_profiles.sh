@@ -1,7 +1,7 @@
 #!/bin/bash
 # Refresh every measured number committed under profiles/ in one GPU call:
 #   1. bench.py default run (oracle verify + CPU baseline)          -> gpurun_out/rp/bench.json
-#   2. rocprofv3 --kernel-trace --stats over the bench               -> gpurun_out/rp/enc/
+#   2. rocprofv3 --kernel-trace --stats over the bench, one stream   -> gpurun_out/rp/enc/
 #   3. PMC passes FETCH_SIZE, WRITE_SIZE (one counter per pass)      -> gpurun_out/rp/pmc_*/
 #   4. scripts/bench_configs.py (configs[2], configs[3], E2E)        -> gpurun_out/rp/configs.jsonl
 #   5. rocprofv3 --kernel-trace --stats over the decode of configs[2] -> gpurun_out/rp/dec/
@@ -16,7 +16,7 @@ mkdir -p $O
 timeout -k 10 300 python3 bench.py > $O/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; grep '^{' $O/bench.log > $O/bench.json; cut -c1-300 $O/bench.json
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/enc -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu --no-verify --single-steps 0 --stage-steps 0 > $O/enc.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/enc -o run --output-format csv -- python3 bench.py --streams 1 --steps 100 --warmup 10 --no-cpu --no-verify --single-steps 0 --stage-steps 0 > $O/enc.log 2>&1
 rc=$?; echo "rocprof enc rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 for c in FETCH_SIZE WRITE_SIZE; do
