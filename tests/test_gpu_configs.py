@@ -177,6 +177,26 @@ def test_encode_ssts_full_d1_set(rt):
         assert_same(ref, got, "d1 set %d" % j)
 
 
+def test_encode_ssts_concurrent_streams(rt):
+    """bench.py's default shape: two builders in flight, each a launch set on its own stream with its own
+    workspace and outputs; the sets alternate for several rounds and every SST stays bit-exact."""
+    import torch
+    sets = [[datasets.d1(n=60000 + 1000 * j, sst_index=60 + 4 * q + j) for j in range(4)] for q in range(2)]
+    prm = rt.params()
+    dsets = [[x.to_device("cuda") for x in s] for s in sets]
+    outs = [[rt.DeviceSstOutput(x.n, x.logical_bytes(), x.logical_bytes(), prm, workspace=False) for x in s]
+            for s in sets]
+    wss = [rt.ssts_workspace(d, prm) for d in dsets]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    for _ in range(5):
+        for q in range(2):
+            rt.encode_ssts_device(dsets[q], outs[q], prm, wss[q], streams[q])
+    torch.cuda.synchronize()
+    for q in range(2):
+        for x, o in zip(sets[q], outs[q]):
+            assert_same(O.encode_sst(x, O.params()), _host_view(o.to_host()), "stream %d" % q)
+
+
 def test_encode_graph_capture_replay(rt):
     """The device entry points launch only on the caller's stream: a captured encode replays."""
     import torch
