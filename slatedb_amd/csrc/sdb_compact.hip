@@ -302,47 +302,174 @@ SDB_DEV void copy_bytes(uint8_t *dst, const uint8_t *src, uint64_t n) {
     for (; o < n; o++) dst[o] = src[o];
 }
 
+// The wave copies its 64 threads' u-th entries together: eight lanes per entry, 16 bytes each per step,
+// so a load instruction reads eight contiguous 128-byte spans instead of 64 scattered 16-byte pieces
+// (a thread copying its own entries ran at one seventh of the HBM rate).
+struct CopyDesc {
+    const uint8_t *ks, *vs;
+    uint8_t *kd, *vd;
+    uint32_t kb, vb;
+};
+// <= 16 bytes as independent loads (16, or 8 / 4 / 2 / 1 pieces: never past the range), so a lane's
+// chunks of several entries are all in flight before the first store waits
+struct Chunk {
+    uint64_t lo, hi;
+    uint32_t n;
+};
+typedef uint16_t u16_u __attribute__((aligned(1)));
+typedef uint64_t u64_u __attribute__((aligned(1)));
+SDB_DEV void chunk_load(Chunk &c, const uint8_t *src, uint32_t n) {
+    c.n = n;
+    if (n >= 16) {
+        c.lo = *(const u64_u *)src;
+        c.hi = *(const u64_u *)(src + 8);
+        return;
+    }
+    const uint32_t o = n & 8, b4 = n & 4, b2 = n & 2;
+    c.lo = o ? *(const u64_u *)src : 0;
+    uint64_t t = 0;
+    if (b4) t = *(const u32_u *)(src + o);
+    if (b2) t |= (uint64_t)*(const u16_u *)(src + o + b4) << (8 * b4);
+    if (n & 1) t |= (uint64_t)src[o + b4 + b2] << (8 * (b4 + b2));
+    if (o) c.hi = t;
+    else c.lo = t;
+}
+SDB_DEV void chunk_store(const Chunk &c, uint8_t *dst) {
+    const uint32_t n = c.n;
+    if (n >= 16) {
+        *(u64_u *)dst = c.lo;
+        *(u64_u *)(dst + 8) = c.hi;
+        return;
+    }
+    const uint32_t o = n & 8, b4 = n & 4, b2 = n & 2;
+    if (o) *(u64_u *)dst = c.lo;
+    const uint64_t t = o ? c.hi : c.lo;
+    if (b4) *(u32_u *)(dst + o) = (uint32_t)t;
+    if (b2) *(u16_u *)(dst + o + b4) = (uint16_t)(t >> (8 * b4));
+    if (n & 1) dst[o + b4 + b2] = (uint8_t)(t >> (8 * (b4 + b2)));
+}
+// lane chunk x of every listed entry's key (K) or value bytes: all eight loads, then the stores
+template <bool K>
+SDB_DEV void copy_group_chunks(const CopyDesc *cd, uint32_t l, uint32_t x) {
+    Chunk ch[8];
+#pragma unroll
+    for (uint32_t q = 0; q < 8; q++) {
+        const CopyDesc &c = cd[8 * q + (l >> 3)];
+        const uint32_t len = K ? c.kb : c.vb;
+        ch[q].n = 0;
+        if (x < len) chunk_load(ch[q], (K ? c.ks : c.vs) + x, len - x < 16 ? len - x : 16);
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 8; q++) {
+        const CopyDesc &c = cd[8 * q + (l >> 3)];
+        if (ch[q].n) chunk_store(ch[q], (K ? c.kd : c.vd) + x);
+    }
+}
+
+// One merged entry's inputs, every load issued before any output store (the output may alias nothing
+// the compiler can prove, so loads after a store would wait for it).
+struct EntIn {
+    const uint8_t *ks, *vs;
+    uint64_t seq;
+    uint32_t kb, vb, run, i;  // timestamps (rare) are read at the store from (run, i)
+    uint8_t d, f;
+};
+SDB_DEV void ent_load(const MergeArgs &a, uint64_t p, EntIn &x) {
+    x.d = 0;
+    x.kb = x.vb = 0;
+    if (p >= a.total) return;
+    x.d = a.dec[p];
+    const uint64_t g = a.perm[p];
+    if (!x.d) return;
+    x.run = run_of(a, g);
+    const RunDesc &R = a.r[x.run];
+    const uint64_t i = g - R.base;
+    x.i = (uint32_t)i;
+    x.f = R.flags[i];
+    const uint64_t k0 = R.key_off[i], k1 = R.key_off[i + 1];
+    x.ks = R.key_arena + k0;
+    x.kb = (uint32_t)(k1 - k0);
+    const uint32_t vl = R.val_len[i];
+    x.vs = R.val_base + R.val_off[i];
+    x.seq = R.seq[i];
+    x.vb = (x.d == 1 && !(x.f & SDB_FLAG_TOMBSTONE)) ? vl : 0;
+}
+
+// Columns from each thread's kPerT consecutive positions; the key / value bytes then move half a tile at
+// a time: every entry's copy descriptor goes to LDS and each wave copies a contiguous run of entries, so
+// the output is written as one stream per wave (a thread's strided entries left lines half-written).
+constexpr uint32_t kCopyHalf = kMergeTile / 2;
+
 __global__ __launch_bounds__(kMergeThreads) void k_mg_emit(MergeArgs a) {
     if (a.out.summary->status != SDB_OK) return;
     __shared__ uint64_t s_w[17];
+    __shared__ CopyDesc s_cd[kCopyHalf];
     const uint64_t p0 = (uint64_t)blockIdx.x * kMergeTile + (uint64_t)threadIdx.x * kPerT;
-    OutSizes s[kPerT];
+    EntIn x[kPerT];
+#pragma unroll
+    for (uint32_t u = 0; u < kPerT; u++) ent_load(a, p0 + u, x[u]);
     uint64_t c = 0, kb = 0, vb = 0, tot;
 #pragma unroll
     for (uint32_t u = 0; u < kPerT; u++) {
-        s[u] = out_sizes(a, p0 + u);
-        c += s[u].keep;
-        kb += s[u].kb;
-        vb += s[u].vb;
+        c += x[u].d != 0;
+        kb += x[u].kb;
+        vb += x[u].vb;
     }
     uint64_t j = a.tile_sum[3 * (uint64_t)blockIdx.x + 0] + block_excl_scan_u64(c, s_w, &tot);
     uint64_t ko = a.tile_sum[3 * (uint64_t)blockIdx.x + 1] + block_excl_scan_u64(kb, s_w, &tot);
     uint64_t vo = a.tile_sum[3 * (uint64_t)blockIdx.x + 2] + block_excl_scan_u64(vb, s_w, &tot);
     const sdb_merged_out &o = a.out;
+    CopyDesc cds[kPerT];
 #pragma unroll
     for (uint32_t u = 0; u < kPerT; u++) {
-        if (!s[u].keep) continue;
-        const uint64_t p = p0 + u, g = a.perm[p];
-        const RunDesc &R = a.r[run_of(a, g)];
-        const uint64_t i = g - R.base;
-        const uint8_t d = a.dec[p], f = R.flags[i];
-        const bool tomb = d == 2 || (f & SDB_FLAG_TOMBSTONE);
+        CopyDesc &cd = cds[u];
+        cd = CopyDesc{nullptr, nullptr, nullptr, nullptr, 0, 0};
+        const EntIn &e = x[u];
+        if (!e.d) continue;
+        const bool tomb = e.d == 2 || (e.f & SDB_FLAG_TOMBSTONE);
         uint8_t mask = 0;
-        if (f & SDB_FLAG_HAS_CREATE_TS) mask |= SDB_TS_CREATE;
-        if ((f & SDB_FLAG_HAS_EXPIRE_TS) && d == 1) mask |= SDB_TS_EXPIRE;  // converted: expire_ts None
+        if (e.f & SDB_FLAG_HAS_CREATE_TS) mask |= SDB_TS_CREATE;
+        if ((e.f & SDB_FLAG_HAS_EXPIRE_TS) && e.d == 1) mask |= SDB_TS_EXPIRE;  // converted: expire_ts None
         o.key_off[j] = ko;
         o.val_off[j] = vo;
-        o.kind[j] = tomb ? SDB_KIND_TOMBSTONE : (f & SDB_FLAG_MERGE_OPERAND) ? SDB_KIND_MERGE : SDB_KIND_VALUE;
-        o.seq[j] = R.seq[i];
+        o.kind[j] = tomb ? SDB_KIND_TOMBSTONE : (e.f & SDB_FLAG_MERGE_OPERAND) ? SDB_KIND_MERGE : SDB_KIND_VALUE;
+        o.seq[j] = e.seq;
         o.ts_mask[j] = mask;
-        o.create_ts[j] = (mask & SDB_TS_CREATE) ? R.create_ts[i] : 0;
-        o.expire_ts[j] = (mask & SDB_TS_EXPIRE) ? R.expire_ts[i] : 0;
-        copy_bytes(o.key_bytes + ko, R.key_arena + R.key_off[i], s[u].kb);
-        if (s[u].vb) copy_bytes(o.val_bytes + vo, R.val_base + R.val_off[i], s[u].vb);
+        o.create_ts[j] = (mask & SDB_TS_CREATE) ? a.r[e.run].create_ts[e.i] : 0;
+        o.expire_ts[j] = (mask & SDB_TS_EXPIRE) ? a.r[e.run].expire_ts[e.i] : 0;
+        cd.ks = e.ks;
+        cd.kd = o.key_bytes + ko;
+        cd.kb = e.kb;
+        if (e.vb) {
+            cd.vs = e.vs;
+            cd.vd = o.val_bytes + vo;
+            cd.vb = e.vb;
+        }
         j++;
-        ko += s[u].kb;
-        vo += s[u].vb;
+        ko += e.kb;
+        vo += e.vb;
     }
+    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6, nw = kMergeThreads / 64;
+    constexpr uint32_t kPerWave = kCopyHalf / (kMergeThreads / 64);  // entries a wave copies per half
+#pragma unroll
+    for (uint32_t h = 0; h < kMergeTile / kCopyHalf; h++) {
+#pragma unroll
+        for (uint32_t u = 0; u < kPerT; u++) {
+            const uint32_t idx = threadIdx.x * kPerT + u;  // position in the tile
+            if (idx / kCopyHalf == h) s_cd[idx - h * kCopyHalf] = cds[u];
+        }
+        __syncthreads();
+        for (uint32_t g = 0; g < kPerWave; g += 64) {
+            // lanes 8q' .. 8q' + 7 copy entry 8q + q' of these 64; lane l's 16-byte chunks start at
+            // 16 (l & 7) and step by 128 (entries over 128 bytes take more steps, wave-uniformly)
+            const CopyDesc *cd = s_cd + w * kPerWave + g;
+            const uint32_t mk = wave_max(cd[l].kb), mv = wave_max(cd[l].vb);
+            for (uint32_t x0 = 0; x0 < mk; x0 += 128) copy_group_chunks<true>(cd, l, x0 + 16 * (l & 7));
+            for (uint32_t x0 = 0; x0 < mv; x0 += 128) copy_group_chunks<false>(cd, l, x0 + 16 * (l & 7));
+        }
+        __syncthreads();
+    }
+    (void)nw;
 }
 
 // ------------------------------------------------------------------------------------------------
