@@ -312,17 +312,16 @@ struct CopyDesc {
 };
 // <= 16 bytes as independent loads (16, or 8 / 4 / 2 / 1 pieces: never past the range), so a lane's
 // chunks of several entries are all in flight before the first store waits
-struct Chunk {
+struct Chunk {  // (its length is recomputed at the store from the descriptor: fewer live registers)
     uint64_t lo, hi;
-    uint32_t n;
 };
 typedef uint16_t u16_u __attribute__((aligned(1)));
 typedef uint64_t u64_u __attribute__((aligned(1)));
 SDB_DEV void chunk_load(Chunk &c, const uint8_t *src, uint32_t n) {
-    c.n = n;
-    if (n >= 16) {
-        c.lo = *(const u64_u *)src;
-        c.hi = *(const u64_u *)(src + 8);
+    if (n >= 16) {  // one 16-byte access
+        const u32x4_u v = *(const u32x4_u *)src;
+        c.lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        c.hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
         return;
     }
     const uint32_t o = n & 8, b4 = n & 4, b2 = n & 2;
@@ -334,11 +333,11 @@ SDB_DEV void chunk_load(Chunk &c, const uint8_t *src, uint32_t n) {
     if (o) c.hi = t;
     else c.lo = t;
 }
-SDB_DEV void chunk_store(const Chunk &c, uint8_t *dst) {
-    const uint32_t n = c.n;
+SDB_DEV void chunk_store(const Chunk &c, uint8_t *dst, uint32_t n) {
     if (n >= 16) {
-        *(u64_u *)dst = c.lo;
-        *(u64_u *)(dst + 8) = c.hi;
+        u32x4_u v;
+        v.x = (uint32_t)c.lo, v.y = (uint32_t)(c.lo >> 32), v.z = (uint32_t)c.hi, v.w = (uint32_t)(c.hi >> 32);
+        *(u32x4_u *)dst = v;
         return;
     }
     const uint32_t o = n & 8, b4 = n & 4, b2 = n & 2;
@@ -348,6 +347,23 @@ SDB_DEV void chunk_store(const Chunk &c, uint8_t *dst) {
     if (b2) *(u16_u *)(dst + o + b4) = (uint16_t)(t >> (8 * b4));
     if (n & 1) dst[o + b4 + b2] = (uint8_t)(t >> (8 * (b4 + b2)));
 }
+// lane chunk x of every listed entry's key and value bytes: all sixteen loads, then the stores
+SDB_DEV void copy_group_chunks_kv(const CopyDesc *cd, uint32_t l, uint32_t x) {
+    Chunk ck[8], cv[8];
+#pragma unroll
+    for (uint32_t q = 0; q < 8; q++) {
+        const CopyDesc &c = cd[8 * q + (l >> 3)];
+        if (x < c.kb) chunk_load(ck[q], c.ks + x, c.kb - x < 16 ? c.kb - x : 16);
+        if (x < c.vb) chunk_load(cv[q], c.vs + x, c.vb - x < 16 ? c.vb - x : 16);
+    }
+    asm volatile("" ::: "memory");  // re-read the descriptors from LDS rather than hold 8 of them
+#pragma unroll
+    for (uint32_t q = 0; q < 8; q++) {
+        const CopyDesc &c = cd[8 * q + (l >> 3)];
+        if (x < c.kb) chunk_store(ck[q], c.kd + x, c.kb - x < 16 ? c.kb - x : 16);
+        if (x < c.vb) chunk_store(cv[q], c.vd + x, c.vb - x < 16 ? c.vb - x : 16);
+    }
+}
 // lane chunk x of every listed entry's key (K) or value bytes: all eight loads, then the stores
 template <bool K>
 SDB_DEV void copy_group_chunks(const CopyDesc *cd, uint32_t l, uint32_t x) {
@@ -356,13 +372,14 @@ SDB_DEV void copy_group_chunks(const CopyDesc *cd, uint32_t l, uint32_t x) {
     for (uint32_t q = 0; q < 8; q++) {
         const CopyDesc &c = cd[8 * q + (l >> 3)];
         const uint32_t len = K ? c.kb : c.vb;
-        ch[q].n = 0;
         if (x < len) chunk_load(ch[q], (K ? c.ks : c.vs) + x, len - x < 16 ? len - x : 16);
     }
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (uint32_t q = 0; q < 8; q++) {
         const CopyDesc &c = cd[8 * q + (l >> 3)];
-        if (ch[q].n) chunk_store(ch[q], (K ? c.kd : c.vd) + x);
+        const uint32_t len = K ? c.kb : c.vb;
+        if (x < len) chunk_store(ch[q], (K ? c.kd : c.vd) + x, len - x < 16 ? len - x : 16);
     }
 }
 
@@ -430,6 +447,10 @@ __global__ __launch_bounds__(kMergeThreads) void k_mg_emit(MergeArgs a) {
         uint8_t mask = 0;
         if (e.f & SDB_FLAG_HAS_CREATE_TS) mask |= SDB_TS_CREATE;
         if ((e.f & SDB_FLAG_HAS_EXPIRE_TS) && e.d == 1) mask |= SDB_TS_EXPIRE;  // converted: expire_ts None
+#ifdef SDB_EXP_MG_NOCOLS  // diagnostic: no column stores (wrong output by design)
+        if (e.seq == 0x123456789ull)
+#endif
+        {
         o.key_off[j] = ko;
         o.val_off[j] = vo;
         o.kind[j] = tomb ? SDB_KIND_TOMBSTONE : (e.f & SDB_FLAG_MERGE_OPERAND) ? SDB_KIND_MERGE : SDB_KIND_VALUE;
@@ -437,6 +458,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_mg_emit(MergeArgs a) {
         o.ts_mask[j] = mask;
         o.create_ts[j] = (mask & SDB_TS_CREATE) ? a.r[e.run].create_ts[e.i] : 0;
         o.expire_ts[j] = (mask & SDB_TS_EXPIRE) ? a.r[e.run].expire_ts[e.i] : 0;
+        }
         cd.ks = e.ks;
         cd.kd = o.key_bytes + ko;
         cd.kb = e.kb;
@@ -459,13 +481,19 @@ __global__ __launch_bounds__(kMergeThreads) void k_mg_emit(MergeArgs a) {
             if (idx / kCopyHalf == h) s_cd[idx - h * kCopyHalf] = cds[u];
         }
         __syncthreads();
+#ifdef SDB_EXP_MG_NOCOPY  // diagnostic: no key / value byte copies (wrong output by design)
+        if (s_cd[0].kb == 0xFFFFFFFFu)
+#endif
         for (uint32_t g = 0; g < kPerWave; g += 64) {
             // lanes 8q' .. 8q' + 7 copy entry 8q + q' of these 64; lane l's 16-byte chunks start at
             // 16 (l & 7) and step by 128 (entries over 128 bytes take more steps, wave-uniformly)
             const CopyDesc *cd = s_cd + w * kPerWave + g;
             const uint32_t mk = wave_max(cd[l].kb), mv = wave_max(cd[l].vb);
-            for (uint32_t x0 = 0; x0 < mk; x0 += 128) copy_group_chunks<true>(cd, l, x0 + 16 * (l & 7));
-            for (uint32_t x0 = 0; x0 < mv; x0 += 128) copy_group_chunks<false>(cd, l, x0 + 16 * (l & 7));
+            const uint32_t mb = mk < mv ? mk : mv;  // chunk steps every entry's key and value share
+            uint32_t x0 = 0;
+            for (; x0 < mb; x0 += 128) copy_group_chunks_kv(cd, l, x0 + 16 * (l & 7));
+            for (uint32_t xk = x0; xk < mk; xk += 128) copy_group_chunks<true>(cd, l, xk + 16 * (l & 7));
+            for (uint32_t xv = x0; xv < mv; xv += 128) copy_group_chunks<false>(cd, l, xv + 16 * (l & 7));
         }
         __syncthreads();
     }
