@@ -185,7 +185,7 @@ SDB_DEV void bloom_bin_core(uint32_t tile, const uint32_t (&hh)[KPT], const uint
             if (tid + j * nt < nk)
                 probes_hd(hh[j], dd[j], pl.k, pl.m, [&](uint32_t p) {
                     const uint32_t sl = p >> pl.sb, pos = atomicAdd(&cnt[sl], 1u);
-                    if (pos < cap) bkt[sl * cap + pos] = (uint16_t)(p & mask);
+                    if (pos < cap) bkt[__umul24(sl, cap) + pos] = (uint16_t)(p & mask);  // sl < 256: full-rate mul
                 });
         __syncthreads();
         for (uint32_t x = tid; x < S; x += nt) {
