@@ -885,6 +885,16 @@ __global__ __launch_bounds__(kEnumThreads) void k_enum(SstSet P) {
     uint32_t *bl_b = bl_s + kChunk;
     uint64_t *bl_o = (uint64_t *)(bl_b + kChunk);
     uint16_t *lv = (uint16_t *)(bl_o + kChunk);
+    // next() and the block bytes of every chunk entry are independent of the entry point: their loads
+    // go out now and land while the tables are walked (bl_b holds the bytes by entry until the scan)
+    constexpr uint32_t kU = (kChunk + kEnumThreads - 1) / kEnumThreads;
+    uint32_t nx[kU], eb[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) {
+        const uint32_t x = u * nt + tid;
+        nx[u] = x < cn ? a.next[cs + x] : 0;
+        eb[u] = x < cn ? a.bbytes[cs + x] : 0;
+    }
     if (*a.mode == 2) {
         // the same walk as below, one thread straight through the tables in HBM (they do not fit LDS)
         if (tid == 0) {
@@ -1027,22 +1037,12 @@ __global__ __launch_bounds__(kEnumThreads) void k_enum(SstSet P) {
     if (!nb) return;
     uint32_t levels = 1;
     while ((1u << levels) < nb) levels++;
-    {
-        constexpr uint32_t kU = kChunk / 256;  // next() of the chunk: all loads issued first
-        uint32_t nx[kU];
 #pragma unroll
-        for (uint32_t u = 0; u < kU; u++) {
-            const uint32_t x = u * nt + tid;
-            nx[u] = x < cn ? a.next[cs + x] : 0;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++) {
-            const uint32_t x = u * nt + tid;
-            if (x < cn) lv[x] = (uint16_t)(nx[u] >= ce ? cn : (uint32_t)(nx[u] - cs));
-        }
-        for (uint32_t x = kU * nt + tid; x < cn; x += nt) {  // (blockDim < 256 only)
-            const uint64_t v = a.next[cs + x];
-            lv[x] = (uint16_t)(v >= ce ? cn : (uint32_t)(v - cs));
+    for (uint32_t u = 0; u < kU; u++) {
+        const uint32_t x = u * nt + tid;
+        if (x < cn) {
+            lv[x] = (uint16_t)(nx[u] >= ce ? cn : (uint32_t)(nx[u] - cs));
+            bl_b[x] = eb[u];  // by entry for now
         }
     }
     __syncthreads();
@@ -1055,12 +1055,24 @@ __global__ __launch_bounds__(kEnumThreads) void k_enum(SstSet P) {
         }
         __syncthreads();
     }
-    for (uint32_t t = tid; t < nb; t += nt) {
-        uint32_t x = (uint32_t)(e0 - cs);
-        for (uint32_t j = 0; j < levels; j++)
-            if ((t >> j) & 1) x = lv[(uint64_t)j * kChunk + x];
-        bl_s[t] = (uint32_t)cs + x;
-        bl_b[t] = a.bbytes[cs + x];
+    uint32_t bx[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) {
+        const uint32_t t = u * nt + tid;
+        bx[u] = 0;
+        if (t < nb) {
+            uint32_t x = (uint32_t)(e0 - cs);
+            for (uint32_t j = 0; j < levels; j++)
+                if ((t >> j) & 1) x = lv[(uint64_t)j * kChunk + x];
+            bl_s[t] = (uint32_t)cs + x;
+            bx[u] = bl_b[x];
+        }
+    }
+    __syncthreads();  // every by-entry read of bl_b is done: it becomes by block
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) {
+        const uint32_t t = u * nt + tid;
+        if (t < nb) bl_b[t] = bx[u];
     }
     __syncthreads();
     PHASE_MARK_E(4);
