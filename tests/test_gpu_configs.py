@@ -114,6 +114,20 @@ def test_bloom_slot_overflow_rebuild(rt):
     assert std[2:] == ref.bloom.tobytes()
 
 
+def test_fused_bloom_u32_slots_two_pass(rt):
+    """The fused bloom's other binning mode: a filter of > 256 x 2^16 bits has slices of 2^17 bits, so
+    the slots hold u32 bit positions and k_facts bins by the two-pass counting sort (the one-pass LDS
+    buckets take u16 offsets only)."""
+    n = 1_000_000
+    keys = np.arange(n, dtype=">u8").view(np.uint8).copy()
+    b = Batch(keys, np.arange(n + 1, dtype=np.uint64) * np.uint64(8), np.zeros(0, np.uint8),
+              np.zeros(n + 1, np.uint64), np.zeros(n, np.uint8), np.arange(n, dtype=np.uint64))
+    ref, got = encode_both(rt, b, bloom_bits_per_key=20)
+    assert ref.status == 0 and ref.summary.num_probes == 13
+    assert ref.summary.bloom_len * 8 > 256 * (1 << 16)  # slices of 2^17 bits: u32 slots
+    assert_same(ref, got, "fused bloom, u32 slots")
+
+
 # ------------------------------------------------------------------------------------------------
 # long blocks: k_seg's HBM continuation, k_group's serial walk, the emit slow path
 # ------------------------------------------------------------------------------------------------
