@@ -78,7 +78,7 @@ hipError_t launch_cuts(const SstSet &P, uint64_t max_sst_size, uint64_t *cut, ui
                        hipStream_t st);
 
 // out[2i], out[2i+1] = key_off[cut[i]], val_off[cut[i]] for i <= ns
-hipError_t launch_cut_offsets(const uint64_t *cut, uint64_t ns, const uint64_t *key_off, const uint64_t *val_off,
+hipError_t launch_cut_offsets(const uint64_t *cut, const uint64_t *num, const uint64_t *key_off, const uint64_t *val_off,
                               uint64_t *out, hipStream_t st);
 
 }  // namespace sdb

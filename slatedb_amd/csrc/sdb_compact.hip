@@ -555,20 +555,23 @@ __global__ void k_cut(SstSet P, uint64_t max_sst, uint64_t *cut, uint64_t *num) 
     *num = ns;
 }
 
-__global__ void k_cut_offsets(const uint64_t *cut, uint64_t ns, const uint64_t *key_off, const uint64_t *val_off,
+// The key / value byte offset of every cut; the cut count is read on the device (the host learns it
+// with the offsets, in one synchronisation).
+__global__ void k_cut_offsets(const uint64_t *cut, const uint64_t *num, const uint64_t *key_off, const uint64_t *val_off,
                               uint64_t *out) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > ns) return;
-    const uint64_t c = cut[i];
-    out[2 * i] = key_off[c];
-    out[2 * i + 1] = val_off[c];
+    const uint64_t ns = *num;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= ns; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = cut[i];
+        out[2 * i] = key_off[c];
+        out[2 * i + 1] = val_off[c];
+    }
 }
 
 }  // namespace
 
-hipError_t launch_cut_offsets(const uint64_t *cut, uint64_t ns, const uint64_t *key_off, const uint64_t *val_off,
+hipError_t launch_cut_offsets(const uint64_t *cut, const uint64_t *num, const uint64_t *key_off, const uint64_t *val_off,
                               uint64_t *out, hipStream_t st) {
-    hipLaunchKernelGGL(k_cut_offsets, dim3((uint32_t)((ns + 256) / 256)), dim3(256), 0, st, cut, ns, key_off, val_off, out);
+    hipLaunchKernelGGL(k_cut_offsets, dim3(64), dim3(256), 0, st, cut, num, key_off, val_off, out);
     return hipGetLastError();
 }
 

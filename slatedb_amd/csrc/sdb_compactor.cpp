@@ -143,16 +143,27 @@ sdb_status sdb_compactor_run(sdb_compactor *c, const sdb_run *runs, uint32_t nru
     uint64_t *d_off = c->cuts.at<uint64_t>(o_off);
     st = sdb_sst_cuts(&m, params, max_sst_size, d_cut, n + 1, d_num, c->cut_ws.p, c->cut_ws.cap, stream);
     if (st) return st;
+    // the cut count, the cuts and their byte offsets in one synchronisation: every SST but the last holds
+    // more than max_sst_size bytes of blocks, and a block costs at most its keys, values and 64 bytes
+    // per row, so g bounds the count (a larger one takes a second copy)
+    const uint64_t g = max_sst_size ? std::min<uint64_t>(n, 2 + (c->msum.key_bytes + c->msum.val_bytes + 64 * n) / max_sst_size) : n;
     uint64_t ns = 0;
-    if (hipMemcpyAsync(&ns, d_num, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
-        return SDB_DEVICE_ERROR;
-    if (ns == 0 || ns > n) return SDB_DEVICE_ERROR;
-    std::vector<uint64_t> cut(ns + 1), off(2 * (ns + 1));
-    if (launch_cut_offsets(d_cut, ns, m.key_off, m.val_off, d_off, s) != hipSuccess ||
-        hipMemcpyAsync(cut.data(), d_cut, 8 * (ns + 1), hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(off.data(), d_off, 16 * (ns + 1), hipMemcpyDeviceToHost, s) != hipSuccess ||
+    std::vector<uint64_t> cut(g + 1), off(2 * (g + 1));
+    if (launch_cut_offsets(d_cut, d_num, m.key_off, m.val_off, d_off, s) != hipSuccess ||
+        hipMemcpyAsync(&ns, d_num, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(cut.data(), d_cut, 8 * (g + 1), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(off.data(), d_off, 16 * (g + 1), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return SDB_DEVICE_ERROR;
+    if (ns == 0 || ns > n) return SDB_DEVICE_ERROR;
+    if (ns > g) {
+        cut.resize(ns + 1);
+        off.resize(2 * (ns + 1));
+        if (hipMemcpyAsync(cut.data(), d_cut, 8 * (ns + 1), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(off.data(), d_off, 16 * (ns + 1), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return SDB_DEVICE_ERROR;
+    }
 
     // 3. encode every output SST (sets of up to 8 per launch sequence)
     std::vector<sdb_kv_batch> batches(ns);
