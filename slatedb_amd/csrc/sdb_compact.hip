@@ -506,53 +506,130 @@ __global__ __launch_bounds__(kMergeThreads) void k_mg_emit(MergeArgs a) {
 // entry points, so whole chunks / groups whose bytes keep the SST at or under max_sst_size are
 // skipped with one lookup; near a cut the walk steps block by block through next() / bbytes.
 // ------------------------------------------------------------------------------------------------
-__global__ void k_cut(SstSet P, uint64_t max_sst, uint64_t *cut, uint64_t *num) {
-    if (threadIdx.x || blockIdx.x) return;
+constexpr uint32_t kCutThreads = 256, kCutTab = 2048;
+constexpr uint64_t kCutDone = ~1ull, kCutTables = 1ull << 62;  // staging requests: chunk k, or kCutTables | group g
+__global__ __launch_bounds__(kCutThreads) void k_cut(SstSet P, uint64_t max_sst, uint64_t *cut, uint64_t *num) {
+    // Thread 0 walks; the workgroup stages what the next steps read into LDS first: the group tables
+    // (once), the chunk tables of the group the walk is in, and a chunk's next() / block bytes before
+    // thread 0 steps block by block through it (one HBM round trip per table set or chunk instead of one
+    // per step).  Tables larger than kCutTab entries stay in HBM.
+    __shared__ uint32_t s_next[kChunk], s_bb[kChunk];
+    __shared__ uint32_t s_gx[kCutTab], s_cx[kCutTab];
+    __shared__ uint64_t s_gb[kCutTab], s_cb[kCutTab];
+    __shared__ uint64_t s_stage;  // the next staging request (kCutDone: the walk is done)
     const EncodeArgs a = make_args(P, 0);
     const uint64_t n = a.n;
     const bool fast = *a.mode >= 1;  // 1 and 2: the chunk / group tables describe the chain
     const uint32_t W = *a.wmax, G = a.group, L = a.seg_look;
+    const uint32_t K = a.nchunks, ngroups = (K + G - 1) / G;
+    const bool glds = fast && (uint64_t)ngroups * W <= kCutTab, clds = fast && (uint64_t)G * W <= kCutTab;
+    const uint32_t tid = threadIdx.x;
+    if (glds)
+        for (uint32_t x = tid; x < ngroups * W; x += kCutThreads) {
+            const uint32_t g = x / W, o = x - g * W;
+            s_gx[x] = a.gtab_exit[(uint64_t)g * L + o];
+            s_gb[x] = a.gtab_bytes[(uint64_t)g * L + o];
+        }
+    __syncthreads();
     uint64_t e = 0, acc = 0, ns = 0;
     bool entry_pt = true;  // reached from the previous chunk (or the stream start): the tables apply
-    cut[0] = 0;
-    while (e < n) {
-        const uint64_t k = e / kChunk, o = e - k * kChunk;
-        if (fast && entry_pt && o < W) {
-            if (k % G == 0) {
-                const uint64_t t = (k / G) * L + o, b = a.gtab_bytes[t];
-                if (acc + b <= max_sst) {
-                    acc += b;
-                    e = (k + G) * kChunk + a.gtab_exit[t];
+    uint64_t staged = ~0ull, gstaged = ~0ull;
+    if (tid == 0) cut[0] = 0;
+    for (;;) {
+        if (tid == 0) {
+            uint64_t want = kCutDone;
+            while (e < n) {
+                const uint64_t k = e / kChunk, o = e - k * kChunk;
+                if (fast && entry_pt && o < W) {
+                    const uint64_t g = k / G;
+                    if (k % G == 0) {
+                        uint64_t b;
+                        uint32_t gx;
+                        if (glds) {
+                            b = s_gb[g * W + o];
+                            gx = s_gx[g * W + o];
+                        } else {
+                            b = a.gtab_bytes[g * L + o];
+                            gx = a.gtab_exit[g * L + o];
+                        }
+                        if (acc + b <= max_sst) {
+                            acc += b;
+                            e = (k + G) * kChunk + gx;
+                            continue;
+                        }
+                    }
+                    if (clds && gstaged != g) {  // the group is entered chunk by chunk: its tables to LDS
+                        want = kCutTables | g;
+                        break;
+                    }
+                    uint32_t ex;
+                    uint64_t cb;
+                    if (clds) {
+                        ex = s_cx[(k - g * G) * W + o];
+                        cb = s_cb[(k - g * G) * W + o];
+                    } else {
+                        ex = a.tab_exit[k * L + o];
+                        cb = a.tab_bytes[k * L + o];
+                    }
+                    if (ex != 0xFFFFFFFFu && acc + cb <= max_sst) {
+                        acc += cb;
+                        e = ex;
+                        continue;
+                    }
+                }
+                if (staged != k) {  // the block steps of this chunk come from LDS
+                    want = k;
+                    break;
+                }
+                const uint64_t j = s_next[o];
+                if (j >= n) {  // the tail block: built by close(), never counted
+                    e = n;
+                    break;
+                }
+                acc += s_bb[o];
+                if (acc > max_sst) {
+                    // entry j's add finished the block: the writer closes with j as its one-entry tail
+                    if (j + 1 < n) cut[++ns] = j + 1;
+                    acc = 0;
+                    e = j + 1;
+                    entry_pt = (e % kChunk) == 0;
                     continue;
                 }
+                entry_pt = j / kChunk != k;
+                e = j;
             }
-            const uint64_t t = k * L + o;
-            const uint32_t ex = a.tab_exit[t];
-            if (ex != 0xFFFFFFFFu) {
-                const uint64_t b = a.tab_bytes[t];
-                if (acc + b <= max_sst) {
-                    acc += b;
-                    e = ex;
-                    continue;
-                }
+            s_stage = want;
+        }
+        __syncthreads();
+        // the loop around the barriers exits on a scalar (wave-uniform) value
+        const uint64_t sv = s_stage;
+        const uint64_t want = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sv) |
+                              ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(sv >> 32)) << 32);
+        if (want == kCutDone) break;
+        if (want & kCutTables) {
+            const uint64_t g = want & ~kCutTables, k0 = g * G, nk = k0 + G < K ? G : K - k0;
+            for (uint32_t x = tid; x < nk * W; x += kCutThreads) {
+                const uint32_t q = x / W, o = x - q * W;
+                const uint64_t kk = k0 + q, ccs = kk * kChunk, cce = ccs + kChunk < n ? ccs + kChunk : n;
+                // candidates past a short last chunk were never written: no table entry
+                s_cx[x] = ccs + o < cce ? a.tab_exit[kk * L + o] : 0xFFFFFFFFu;
+                s_cb[x] = ccs + o < cce ? a.tab_bytes[kk * L + o] : 0;
             }
+            gstaged = g;
+        } else {
+            const uint64_t cs = want * kChunk, ce = cs + kChunk < n ? cs + kChunk : n;
+            for (uint64_t x = cs + tid; x < ce; x += kCutThreads) {
+                s_next[x - cs] = a.next[x];
+                s_bb[x - cs] = a.bbytes[x];
+            }
+            staged = want;
         }
-        const uint64_t j = a.next[e];
-        if (j >= n) break;  // the tail block: built by close(), never counted
-        acc += a.bbytes[e];
-        if (acc > max_sst) {
-            // entry j's add finished the block: the writer closes with j as its one-entry tail
-            if (j + 1 < n) cut[++ns] = j + 1;
-            acc = 0;
-            e = j + 1;
-            entry_pt = (e % kChunk) == 0;
-            continue;
-        }
-        entry_pt = j / kChunk != k;
-        e = j;
+        __syncthreads();
     }
-    if (n) cut[++ns] = n;
-    *num = ns;
+    if (tid == 0) {
+        if (n) cut[++ns] = n;
+        *num = ns;
+    }
 }
 
 // The key / value byte offset of every cut; the cut count is read on the device (the host learns it
@@ -651,7 +728,7 @@ hipError_t launch_cuts(const SstSet &P, uint64_t max_sst_size, uint64_t *cut, ui
     (void)cap;  // the host checks cap >= n + 1
     hipError_t e = launch_encode_prep(P, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_cut, dim3(1), dim3(64), 0, st, P, max_sst_size, cut, num);
+    hipLaunchKernelGGL(k_cut, dim3(1), dim3(kCutThreads), 0, st, P, max_sst_size, cut, num);
     return hipGetLastError();
 }
 
