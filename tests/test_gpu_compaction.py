@@ -162,6 +162,16 @@ def test_sst_cuts_long_blocks_device(rt):
     cuts_both(rt, b, O.params(block_size=65536), 100000)
 
 
+@pytest.mark.parametrize("max_sst", [3000, 100000, 10 ** 12])
+def test_sst_cuts_tables_in_hbm_device(rt, max_sst):
+    """~315 tiny rows per 4 KiB block: ~316 candidate entry points per chunk, so a group's chunk tables
+    (and, with 123 chunks, the group tables) outgrow k_cut's LDS and the walk reads them from HBM."""
+    n = 250000
+    ents = [(b"%08d" % i, 0, b"", 1, None, None) for i in range(n)]
+    b = Batch.from_entries(ents)
+    cuts_both(rt, b, O.params(block_size=4096), max_sst)
+
+
 def sst_view(d):
     return types.SimpleNamespace(status=d["summary"].status,
                                  summary={f: getattr(d["summary"], f) for f, _ in _abi.SstSummary._fields_},
