@@ -31,7 +31,8 @@ struct MergeArgs {
     sdb_retention ret;
     sdb_merged_out out;
     // workspace
-    uint64_t *pfx;               // per global entry: first 8 key bytes, big-endian, zero padded
+    uint64_t *pfx;               // per global entry: key bytes [L0, L0 + 8), big-endian, zero padded
+    uint32_t *lcp0;              // L0: the prefix every key of the (sorted) runs shares
     uint64_t *perm;              // merged position -> global entry
     uint8_t *start;              // merged position: first version of its key
     uint8_t *dec;                // merged position: 0 drop, 1 keep, 2 keep as a tombstone
@@ -44,7 +45,7 @@ struct MergeArgs {
 static_assert(sizeof(MergeArgs) < 4000, "MergeArgs is passed as kernel arguments");
 
 struct MergeWorkspace {
-    uint64_t pfx, perm, start, dec, tile_sum, err, err_merge, metric, total;
+    uint64_t pfx, perm, start, dec, tile_sum, err, err_merge, metric, lcp0, total;
 };
 inline MergeWorkspace merge_workspace_layout(uint64_t total) {
     MergeWorkspace w{};
@@ -63,6 +64,7 @@ inline MergeWorkspace merge_workspace_layout(uint64_t total) {
     w.err = take(8);
     w.err_merge = take(8);
     w.metric = take(16);
+    w.lcp0 = take(8);
     w.total = off;
     return w;
 }

@@ -41,16 +41,6 @@ SDB_DEV uint64_t key_prefix(const uint8_t *p, uint32_t n) {  // first 8 bytes, b
     return bswap64(v);
 }
 
-// <[u8] as Ord>::cmp given the prefixes: -1, 0, 1
-SDB_DEV int cmp_key(uint64_t pa, const uint8_t *a, uint32_t na, uint64_t pb, const uint8_t *b, uint32_t nb) {
-    if (pa != pb) return pa < pb ? -1 : 1;
-    if (na > 8 && nb > 8) {
-        const uint32_t l = lcp_bytes(a + 8, na - 8, b + 8, nb - 8), m = (na < nb ? na : nb) - 8;
-        if (l < m) return a[8 + l] < b[8 + l] ? -1 : 1;
-    }
-    return na < nb ? -1 : (na > nb ? 1 : 0);
-}
-
 struct KeyAt {
     const uint8_t *p;
     uint32_t n;
@@ -60,6 +50,46 @@ SDB_DEV KeyAt key_at(const RunDesc &R, uint64_t i) {
     return {R.key_arena + o, (uint32_t)(R.key_off[i + 1] - o)};
 }
 
+// <[u8] as Ord>::cmp given the prefixes of bytes [s, s + 8) of two keys whose bytes [0, s) are equal:
+// -1, 0, 1
+SDB_DEV int cmp_key(uint64_t pa, const uint8_t *a, uint32_t na, uint64_t pb, const uint8_t *b, uint32_t nb,
+                    uint32_t s = 0) {
+    if (pa != pb) return pa < pb ? -1 : 1;
+    const uint32_t t = s + 8;
+    if (na > t && nb > t) {
+        const uint32_t l = lcp_bytes(a + t, na - t, b + t, nb - t), m = (na < nb ? na : nb) - t;
+        if (l < m) return a[t + l] < b[t + l] ? -1 : 1;
+    }
+    return na < nb ? -1 : (na > nb ? 1 : 0);
+}
+
+// L0 = the common prefix of the first and last keys of every run, with run 0's first key: every key of
+// sorted runs lies between its run's first and last, so it shares L0 bytes with them.  The merge's
+// 8-byte prefixes start there (keys with a long common prefix, e.g. big-endian counters, would otherwise
+// tie on every prefix and compare their bytes from HBM).  Checked by k_mg_prefix's full run-order test:
+// the rank and group kernels only run when every run is sorted.
+__global__ void k_mg_lcp0(MergeArgs a) {
+    if (threadIdx.x) return;
+    uint32_t L = ~0u;
+    const uint8_t *e0 = nullptr;
+    uint32_t n0 = 0;
+    for (uint32_t r = 0; r < a.nruns; r++) {
+        const RunDesc &R = a.r[r];
+        if (!R.n) continue;
+        const KeyAt f = key_at(R, 0), l = key_at(R, R.n - 1);
+        if (!e0) {
+            e0 = f.p;
+            n0 = f.n;
+            L = n0;
+        }
+        const uint32_t x = lcp_bytes(e0, n0, f.p, f.n), y = lcp_bytes(e0, n0, l.p, l.n);
+        L = x < L ? x : L;
+        L = y < L ? y : L;
+    }
+    *a.lcp0 = e0 ? L : 0;
+}
+
+
 __global__ __launch_bounds__(kPfxThreads) void k_mg_prefix(MergeArgs a) {
     const uint64_t g = (uint64_t)blockIdx.x * kPfxThreads + threadIdx.x;
     if (g >= a.total) return;
@@ -68,42 +98,69 @@ __global__ __launch_bounds__(kPfxThreads) void k_mg_prefix(MergeArgs a) {
     const uint64_t i = g - R.base;
     const KeyAt k = key_at(R, i);
     const uint64_t pk = key_prefix(k.p, k.n);
-    a.pfx[g] = pk;
-    if (i > 0) {  // sorted-run precondition: key asc, seq desc
+    const uint32_t L0 = *a.lcp0;
+    a.pfx[g] = k.n >= L0 ? key_prefix(k.p + L0, k.n - L0) : 0;  // n >= L0 whenever the runs are sorted
+    if (i > 0) {  // sorted-run precondition: key asc, seq desc (full keys)
         const KeyAt q = key_at(R, i - 1);
         const int c = cmp_key(key_prefix(q.p, q.n), q.p, q.n, pk, k.p, k.n);
         if (c > 0 || (c == 0 && R.seq[i - 1] < R.seq[i])) report_error(a.err, g, SDB_INVALID_ARGUMENT);
     }
 }
 
+// Entries of run Q (= run r2) in [lo, hi) that come before (key k, seq sq, run r): key less, or equal
+// with a larger seq, or an equal seq in an earlier run; the count is known to lie in [lo, hi].
+SDB_DEV uint64_t rank_in(const MergeArgs &a, uint32_t r2, uint32_t r, uint64_t pk, const KeyAt &k, uint64_t sq,
+                         uint32_t L0, uint64_t lo, uint64_t hi) {
+    const RunDesc &Q = a.r[r2];
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        const KeyAt f = key_at(Q, mid);
+        const int c = cmp_key(a.pfx[Q.base + mid], f.p, f.n, pk, k.p, k.n, L0);
+        bool before = c < 0;
+        if (c == 0) {
+            const uint64_t s2 = Q.seq[mid];
+            before = s2 > sq || (s2 == sq && r2 < r);
+        }
+        if (before) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// Merged position = own index + the entries of every other run that come before.  A workgroup's
+// entries are consecutive in one run, so their counts in run r2 lie between those of its first and
+// last entry: two full binary searches per workgroup and run, then each entry searches that window.
 __global__ __launch_bounds__(kPfxThreads) void k_mg_rank(MergeArgs a) {
-    const uint64_t g = (uint64_t)blockIdx.x * kPfxThreads + threadIdx.x;
-    if (g >= a.total || *a.err != ~0ull) return;
-    const uint32_t r = run_of(a, g);
-    const RunDesc &R = a.r[r];
+    __shared__ uint64_t s_win[2][kMaxRuns];
+    if (*a.err != ~0ull) return;
+    const uint64_t g0 = (uint64_t)blockIdx.x * kPfxThreads;
+    const uint64_t gl = (g0 + kPfxThreads < a.total ? g0 + kPfxThreads : a.total) - 1;
+    const uint32_t r = run_of(a, g0), tid = threadIdx.x;
+    const bool one_run = run_of(a, gl) == r;  // uniform
+    const uint32_t L0 = *a.lcp0;
+    if (one_run) {
+        // thread t < nruns: the first entry's count in run t; thread 64 + t: the last entry's
+        const uint32_t side = tid >> 6, r2 = tid & 63;
+        if (side < 2 && r2 < a.nruns && r2 != r) {
+            const uint64_t ge = side ? gl : g0;
+            const RunDesc &R = a.r[r];
+            const uint64_t i = ge - R.base;
+            s_win[side][r2] = rank_in(a, r2, r, a.pfx[ge], key_at(R, i), R.seq[i], L0, 0, a.r[r2].n);
+        }
+        __syncthreads();
+    }
+    const uint64_t g = g0 + tid;
+    if (g >= a.total) return;
+    const uint32_t rg = one_run ? r : run_of(a, g);
+    const RunDesc &R = a.r[rg];
     const uint64_t i = g - R.base;
     const KeyAt k = key_at(R, i);
     const uint64_t pk = a.pfx[g], sq = R.seq[i];
     uint64_t pos = i;
     for (uint32_t r2 = 0; r2 < a.nruns; r2++) {
-        if (r2 == r) continue;
-        const RunDesc &Q = a.r[r2];
-        // entries of run r2 that come before (key, seq, r): key less, or equal with a larger seq, or
-        // an equal seq in an earlier run
-        uint64_t lo = 0, hi = Q.n;
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi) >> 1;
-            const KeyAt f = key_at(Q, mid);
-            const int c = cmp_key(a.pfx[Q.base + mid], f.p, f.n, pk, k.p, k.n);
-            bool before = c < 0;
-            if (c == 0) {
-                const uint64_t s2 = Q.seq[mid];
-                before = s2 > sq || (s2 == sq && r2 < r);
-            }
-            if (before) lo = mid + 1;
-            else hi = mid;
-        }
-        pos += lo;
+        if (r2 == rg) continue;
+        const uint64_t lo = one_run ? s_win[0][r2] : 0, hi = one_run ? s_win[1][r2] : a.r[r2].n;
+        pos += rank_in(a, r2, rg, pk, k, sq, L0, lo, hi);
     }
     a.perm[pos] = g;
 }
@@ -120,7 +177,7 @@ __global__ __launch_bounds__(kPfxThreads) void k_mg_group(MergeArgs a) {
         const uint64_t h = a.perm[p - 1];
         const RunDesc &Q = a.r[run_of(a, h)];
         const KeyAt x = key_at(Q, h - Q.base), y = key_at(R, i);
-        st = cmp_key(a.pfx[h], x.p, x.n, a.pfx[g], y.p, y.n) != 0;
+        st = cmp_key(a.pfx[h], x.p, x.n, a.pfx[g], y.p, y.n, *a.lcp0) != 0;
     }
     a.start[p] = st;
     if (!a.ret.merge_operands && (R.flags[i] & SDB_FLAG_MERGE_OPERAND))
@@ -696,6 +753,7 @@ sdb_status build_merge_args(const sdb_run *runs, uint32_t nruns, const sdb_reten
     a.err = (unsigned long long *)(ws + w.err);
     a.err_merge = (unsigned long long *)(ws + w.err_merge);
     a.metric = (unsigned long long *)(ws + w.metric);
+    a.lcp0 = (uint32_t *)(ws + w.lcp0);
     return SDB_OK;
 }
 
@@ -705,6 +763,7 @@ hipError_t launch_merge(const MergeArgs &a, bool emit, hipStream_t st) {
         return hipErrorUnknown;
     const uint32_t gb = (uint32_t)((a.total + kPfxThreads - 1) / kPfxThreads);
     if (gb) {
+        hipLaunchKernelGGL(k_mg_lcp0, dim3(1), dim3(64), 0, st, a);
         hipLaunchKernelGGL(k_mg_prefix, dim3(gb), dim3(kPfxThreads), 0, st, a);
         hipLaunchKernelGGL(k_mg_rank, dim3(gb), dim3(kPfxThreads), 0, st, a);
         hipLaunchKernelGGL(k_mg_group, dim3(gb), dim3(kPfxThreads), 0, st, a);

@@ -635,7 +635,7 @@ SDB_DEV bool tally_v2_fast(const LdsBlockView &v, Tally &t, uint16_t *rowpos, ui
         const uint32_t sh = h & 0xFF, un = (h >> 8) & 0xFF, vl = (h >> 16) & 0xFF;
         const uint32_t nx = p + 12 + un + vl, klen = sh + un;
         // the previous row's flags (read one step earlier): value, tombstone or merge only
-        const uint32_t fbad = ((kFlagsOk >> (fl & 31)) & 1u) ^ 1u | (uint32_t)(fl > 31);
+        const uint32_t fbad = (((kFlagsOk >> (fl & 31)) & 1u) ^ 1u) | (uint32_t)(fl > 31);
         const uint32_t lim = ne ? prevlen : 0u;
         const uint32_t rbad = (uint32_t)((h & 0x808080u) != 0) | (uint32_t)(sh > lim) | (uint32_t)(nx > end);
         const uint32_t fpos = nx - 1 < end ? nx - 1 : end;
