@@ -1352,6 +1352,9 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
                 DEC_T(t2);
                 if (lds_keys) {
                     wave_sync_d();
+#ifdef SDB_EXP_NO_KEYSTORE  // diagnostic: no key arena stores (wrong output by design)
+                    if (kbn == 0x7FFFFFFFull)
+#endif
                     wave_store_bytes(a.out.key_arena + kb0, kbuf, kbn);
                 }
                 DEC_T(t3);
