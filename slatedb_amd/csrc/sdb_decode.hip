@@ -1264,7 +1264,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
         tot_ent = a.ent_start[a.nblocks];
         tot_kb = a.key_start[a.nblocks];
     }
-    if (run) crc_tables_to_lds((lu32 *)smem);  // the generic path of oversized blocks still checks windows
+    // no CRC tables: every block was checked by the count pass (load_block / stage_lds run unchecked here)
     __syncthreads();
     const uint32_t(*crc)[256] = (const uint32_t(*)[256])smem;
     const uint32_t wave = threadIdx.x >> 6;
