@@ -493,8 +493,28 @@ SDB_DEV void wave_store_bytes(uint8_t *g, const lu8 *kbuf, uint64_t n) {
             o.w = w.w;
             *(uint4 *)ga = o;
         } else {
-            for (int q = 0; q < 16; q++)
-                if (ga + q >= d0 && ga + q < d1) ((uint8_t *)ga)[q] = li[q];
+            // an edge granule (shared with the neighbouring block's keys): bytes [s, e) of it as at most
+            // four unaligned 8 / 4 / 2 / 1-byte stores instead of a store per byte
+            const u32x4 w = *(const lu128 *)li;
+            const uint32_t s = ga >= d0 ? 0u : (uint32_t)(d0 - ga), e = ga + 16 <= d1 ? 16u : (uint32_t)(d1 - ga);
+            uint64_t lo = (uint64_t)w.x | ((uint64_t)w.y << 32), hi = (uint64_t)w.z | ((uint64_t)w.w << 32);
+            if (s >= 8) {
+                lo = hi >> (8 * (s - 8));
+                hi = 0;
+            } else if (s) {
+                lo = (lo >> (8 * s)) | (hi << (64 - 8 * s));
+                hi >>= 8 * s;
+            }
+            uint8_t *dst = (uint8_t *)ga + s;
+            const uint32_t n = e - s, b8 = n & 8, b4 = n & 4, b2 = n & 2;
+            typedef uint64_t u64u __attribute__((aligned(1)));
+            typedef uint32_t u32u __attribute__((aligned(1)));
+            typedef uint16_t u16u __attribute__((aligned(1)));
+            if (b8) *(u64u *)dst = lo;
+            const uint64_t t = b8 ? hi : lo;
+            if (b4) *(u32u *)(dst + b8) = (uint32_t)t;
+            if (b2) *(u16u *)(dst + b8 + b4) = (uint16_t)(t >> (8 * b4));
+            if (n & 1) dst[b8 + b4 + b2] = (uint8_t)(t >> (8 * (b4 + b2)));
         }
     }
 }
