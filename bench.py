@@ -17,8 +17,9 @@ own workspace and outputs (step i on stream i mod S): the flush / compaction bui
 run concurrently, and two launch sequences in flight let one's latency-bound prep kernels overlap the
 other's kernels and tails.  The same sequences back to back on ONE stream are reported as `one_stream`.
 
-  python bench.py [--gpus N --steps K --warmup W --batch B]
+  python bench.py [--gpus N --steps K --warmup W --batch B]   (N > 1: spawns N ranks itself)
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+  python bench.py --gpus 2 --dry-run                          (rank plumbing on the CPU, gloo)
 """
 import argparse
 import ctypes as C
@@ -58,7 +59,59 @@ def parse():
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--bpk", type=int, default=10, help="bloom bits per key (0 = no filter; diagnostics)")
     p.add_argument("--block-size", type=int, default=4096, help="SstBlockSize (diagnostics; the metric is 4096)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="rank plumbing only, no GPU: gloo, the SST assignment, barrier and max/sum aggregation")
     return p.parse_args()
+
+
+def launch_ranks(args):
+    """`--gpus N` without a launcher (WORLD_SIZE unset, N > 1): start N child processes of this script,
+    one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), exactly as
+    `torch.distributed.run --nproc-per-node N` would, and wait for them.  Runs before anything touches
+    the GPU; the children are started as new processes (never exec).  Returns the exit code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
+def dry_run(args, world, rank):
+    """The multi-rank path without a GPU (gloo): every rank takes its share of the job, meets the
+    timing barriers and the max/sum aggregation bench.py uses, and rank 0 prints the plumbing line."""
+    import torch.distributed as tdist
+    if world > 1:
+        tdist.init_process_group("gloo")
+    dist = tdist if world > 1 else None
+    ids = job.share(args.job_ssts, world, rank) if args.job_ssts else \
+        [rank + world * q for q in range(args.ssts or 2 * args.batch)]
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    logical = len(ids) * datasets.D1_N * (16 + 100)  # D1: 16 B keys, 100 B values
+    elapsed = time.perf_counter() - t0 + 1e-6
+    if dist:
+        dist.barrier()
+    total, tmax = job.aggregate(dist, logical, elapsed, "cpu")
+    everything = [None] * world
+    if dist:
+        dist.all_gather_object(everything, ids)
+    else:
+        everything = [ids]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ssts_per_rank": everything,
+                          "total_logical_bytes": total, "max_elapsed_s": tmax}), flush=True)
+    if dist:
+        dist.destroy_process_group()
 
 
 def cpu_share():
@@ -137,9 +190,15 @@ def pmc_traffic():
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d (launch one rank per GPU)" % (args.gpus, world))
+    if args.dry_run:
+        return dry_run(args, world, rank)
     dist = world > 1
     tdist = None
     if dist:

@@ -628,6 +628,23 @@ struct DevBuf {
         if (e == hipSuccess) cap = want;
         return e;
     }
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    DevBuf(DevBuf &&o) noexcept : p(o.p), cap(o.cap) {
+        o.p = nullptr;
+        o.cap = 0;
+    }
+    DevBuf &operator=(DevBuf &&o) noexcept {
+        if (this != &o) {
+            if (p) hipFree(p);
+            p = o.p;
+            cap = o.cap;
+            o.p = nullptr;
+            o.cap = 0;
+        }
+        return *this;
+    }
     ~DevBuf() {
         if (p) hipFree(p);
     }
@@ -644,6 +661,23 @@ struct PinBuf {
         hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
         if (e == hipSuccess) cap = want;
         return e;
+    }
+    PinBuf() = default;
+    PinBuf(const PinBuf &) = delete;
+    PinBuf &operator=(const PinBuf &) = delete;
+    PinBuf(PinBuf &&o) noexcept : p(o.p), cap(o.cap) {
+        o.p = nullptr;
+        o.cap = 0;
+    }
+    PinBuf &operator=(PinBuf &&o) noexcept {
+        if (this != &o) {
+            if (p) hipHostFree(p);
+            p = o.p;
+            cap = o.cap;
+            o.p = nullptr;
+            o.cap = 0;
+        }
+        return *this;
     }
     ~PinBuf() {
         if (p) hipHostFree(p);

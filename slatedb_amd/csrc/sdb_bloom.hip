@@ -65,6 +65,274 @@ __global__ __launch_bounds__(256) void k_bloom_query(const uint8_t *bitmap, uint
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Standalone build, dense records (configs[3]: 10 M keys, 100 M bits).  The bitmap is cut into
+// slices of 2^16 bits, so a probe is stored as its u16 offset inside its slice.
+//   k_bloom_sort  one 1024-thread workgroup per tile of T keys: SipHash-1-3 and the k probes of every
+//                 key held in registers; an LDS counting sort by slice (one returning LDS add per
+//                 probe gives its rank in the slice, so the scatter needs no second atomic); the
+//                 tile's T*k u16 offsets are written as ONE dense, slice-ordered array with 16-B
+//                 stores, and the tile's run starts (S + 1 u16, T*k < 2^16) as its table row.
+//   k_bloom_or    one workgroup per run of consecutive slices (<= 8, so that the workgroups fill the
+//                 chip): its slices' table entries of every tile staged in LDS, then every tile's
+//                 contiguous run of records for those slices (dword loads, several tiles in flight per
+//                 wave) ORed into an LDS copy of the slices, written with plain stores.
+// No per-slot capacity, hence no overflow case.  Records cost 2 B written + 2 B read per probe, the
+// half of u32 records; the dense array makes every store and load a full coalesced line.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kDenseThreads = 512, kDenseSliceBits = 16, kDenseMaxSlices = 4096, kDenseMaxRun = 7;
+constexpr uint32_t kOrThreads = 1024;
+constexpr uint32_t kOrLds = 150 * 1024;
+
+struct DensePlan {
+    uint32_t k, m, S;        // probes per key, bits, slices of 2^16 bits
+    uint32_t kpt, T, tiles;  // keys per thread, keys per tile, tiles
+    uint32_t tab_stride;     // u16 per table row (>= S + 1, multiple of 8)
+    uint32_t ns, W;          // slices per k_bloom_or workgroup, workgroups
+    uint64_t rec_stride;     // u16 records per tile (T * k rounded to 8)
+    uint64_t mmod;
+    uint16_t *rec;           // tiles x rec_stride
+    uint16_t *tab;           // tiles x tab_stride
+};
+
+static DensePlan dense_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes) {
+    DensePlan d{};
+    d.k = k;
+    d.m = (uint32_t)(bitmap_bytes * 8);
+    d.S = (uint32_t)(((uint64_t)d.m + (1u << kDenseSliceBits) - 1) >> kDenseSliceBits);
+    d.kpt = k <= 7 ? 8 : 4;
+    d.T = kDenseThreads * d.kpt;
+    d.tiles = (uint32_t)((n + d.T - 1) / d.T);
+    d.tab_stride = (d.S + 1 + 7) & ~7u;
+    d.rec_stride = ((uint64_t)d.T * k + 7) & ~7ull;
+    d.ns = (d.S + 255) / 256;
+    if (d.ns > kDenseMaxRun) d.ns = kDenseMaxRun;
+    if (d.ns == 0) d.ns = 1;
+    d.W = (d.S + d.ns - 1) / d.ns;
+    d.mmod = d.m ? ~0ull / d.m + 1 : 0;
+    return d;
+}
+static size_t dense_sort_lds(const DensePlan &d) { return 4 * (size_t)d.S + 2 * (size_t)d.rec_stride; }
+static size_t dense_or_lds(const DensePlan &d) {  // the slices' bits, then 16 B of run starts per tile
+    return 4 * (size_t)d.ns * (1u << (kDenseSliceBits - 5)) + 16 * (size_t)d.tiles;
+}
+static bool dense_fits(const DensePlan &d) {
+    return d.k >= 1 && d.k <= 15 && d.m >= 2 && d.S <= kDenseMaxSlices && (uint64_t)d.T * d.k < 65536 &&
+           dense_sort_lds(d) <= kBinLds && dense_or_lds(d) <= kOrLds;
+}
+static uint64_t dense_ws_bytes(const DensePlan &d) {
+    return 256 + (((uint64_t)d.tiles * d.rec_stride * 2 + 255) & ~255ull) + (uint64_t)d.tiles * d.tab_stride * 2;
+}
+static void dense_carve(DensePlan &d, void *ws) {
+    uint8_t *w = (uint8_t *)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
+    d.rec = (uint16_t *)w;
+    d.tab = (uint16_t *)(w + (((uint64_t)d.tiles * d.rec_stride * 2 + 255) & ~255ull));
+}
+
+// KMAX: probes per key the registers hold (k <= KMAX); KPT keys per thread.
+template <uint32_t KMAX, uint32_t KPT>
+__global__ __launch_bounds__(kDenseThreads) void k_bloom_sort(const uint8_t *__restrict__ key_bytes,
+                                                              const uint64_t *__restrict__ key_off, uint64_t n,
+                                                              DensePlan d) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t *hist = lds;                          // S: counts, then run starts
+    uint16_t *sorted = (uint16_t *)(lds + d.S);    // T * k offsets, slice order
+    __shared__ uint64_t s_w[17];
+    const uint32_t tid = threadIdx.x, tile = blockIdx.x, S = d.S, k = d.k;
+    const uint64_t k0 = (uint64_t)tile * d.T;
+    const uint32_t nk = (uint32_t)((k0 + d.T < n ? k0 + d.T : n) - k0);
+    for (uint32_t x = tid; x < S; x += kDenseThreads) hist[x] = 0;
+    // hash: key tid + j * 1024 of the tile (consecutive lanes read consecutive keys)
+    BloomPlan pl{};
+    pl.m = d.m;
+    pl.mmod = d.mmod;
+    uint32_t hh[KPT], dd[KPT];
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; j++) {
+        hh[j] = dd[j] = 0;
+        if (tid + j * kDenseThreads < nk) key_hd(key_bytes, key_off, k0 + tid + j * kDenseThreads, pl, hh[j], dd[j]);
+    }
+    __syncthreads();
+    // rank of every probe inside its slice (u16: T * k < 2^16), two per register
+    uint32_t rk[(KPT * KMAX + 1) / 2];
+#pragma unroll
+    for (uint32_t x = 0; x < (KPT * KMAX + 1) / 2; x++) rk[x] = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; j++) {
+        if (tid + j * kDenseThreads < nk) {
+            uint32_t h = hh[j], dl = dd[j];
+            const uint32_t m = d.m;
+#pragma unroll
+            for (uint32_t i = 0; i < KMAX; i++) {
+                if (i < k) {
+                    dl += i;
+                    const uint32_t dm = dl - m;
+                    dl = dm < dl ? dm : dl;
+                    const uint32_t r = atomicAdd(&hist[h >> kDenseSliceBits], 1u);
+                    rk[(j * KMAX + i) / 2] |= r << (16 * ((j * KMAX + i) & 1));
+                    h += dl;
+                    const uint32_t hm = h - m;
+                    h = hm < h ? hm : h;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // run starts: exclusive scan of the counts; the table row gets S + 1 of them
+    uint64_t carry = 0;
+    uint16_t *trow = d.tab + (uint64_t)tile * d.tab_stride;
+    for (uint32_t x0 = 0; x0 < S; x0 += kDenseThreads) {
+        const uint32_t x = x0 + tid;
+        const uint32_t c = x < S ? hist[x] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_excl_scan_u64(c, s_w, &tot);
+        if (x < S) {
+            hist[x] = (uint32_t)(carry + ex);
+            trow[x] = (uint16_t)(carry + ex);
+        }
+        carry += tot;
+    }
+    if (tid == 0) trow[S] = (uint16_t)carry;
+    __syncthreads();
+    // scatter: the probes again from (h0, d0), each to its slice's run start + its rank
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; j++) {
+        if (tid + j * kDenseThreads < nk) {
+            uint32_t h = hh[j], dl = dd[j];
+            const uint32_t m = d.m;
+#pragma unroll
+            for (uint32_t i = 0; i < KMAX; i++) {
+                if (i < k) {
+                    dl += i;
+                    const uint32_t dm = dl - m;
+                    dl = dm < dl ? dm : dl;
+                    const uint32_t r = (rk[(j * KMAX + i) / 2] >> (16 * ((j * KMAX + i) & 1))) & 0xFFFFu;
+                    sorted[hist[h >> kDenseSliceBits] + r] = (uint16_t)h;
+                    h += dl;
+                    const uint32_t hm = h - m;
+                    h = hm < h ? hm : h;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // the dense record array of the tile: 16-B stores (rec_stride is a multiple of 8 u16)
+    const uint32_t n16 = (uint32_t)((carry + 7) >> 3);
+    const uint4 *src = (const uint4 *)sorted;
+    uint4 *dst = (uint4 *)(d.rec + (uint64_t)tile * d.rec_stride);
+    for (uint32_t x = tid; x < n16; x += kDenseThreads) dst[x] = src[x];
+}
+
+// Workgroup b -> its run of slices, XCD-aware: the dispatcher places workgroup b on XCD b mod 8, so
+// the runs are dealt out so that each XCD holds consecutive slices (neighbouring runs share the edge
+// lines of every tile's records in that XCD's L2).
+SDB_DEV uint32_t dense_run_of(uint32_t b, uint32_t W) {
+    const uint32_t x = b & 7, q = b >> 3;
+    uint32_t start = 0;  // runs of XCDs 0 .. x - 1: XCD y holds ceil((W - y) / 8) workgroups
+    for (uint32_t y = 0; y < x; y++) start += (W - y + 7) / 8;
+    return start + q;
+}
+
+// u16 entry j (< 8) of a row held in a uint4, without indexing a register array
+SDB_DEV uint32_t row_entry(const uint4 &r, uint32_t j) {
+    const uint64_t lo = (uint64_t)r.x | (uint64_t)r.y << 32, hi = (uint64_t)r.z | (uint64_t)r.w << 32;
+    return (uint32_t)(((j < 4 ? lo : hi) >> (16 * (j & 3))) & 0xFFFFu);
+}
+
+__global__ __launch_bounds__(kOrThreads) void k_bloom_or(DensePlan d, uint8_t *bitmap, uint64_t bytes) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    constexpr uint32_t kWords = 1u << (kDenseSliceBits - 5);
+    const uint32_t run = dense_run_of(blockIdx.x, d.W);
+    const uint32_t s0 = run * d.ns, s1 = s0 + d.ns < d.S ? s0 + d.ns : d.S, ns = s1 - s0;
+    uint32_t *bits = lds;                          // ns x 2^16 bits
+    uint4 *tabs = (uint4 *)(lds + d.ns * kWords);  // per tile: its ns + 1 (<= 8) run starts, u16
+    const uint32_t tid = threadIdx.x, T = d.tiles;
+    for (uint32_t x = tid; x < ns * kWords; x += kOrThreads) bits[x] = 0;
+    for (uint32_t t = tid; t < T; t += kOrThreads) {
+        const uint16_t *row = d.tab + (uint64_t)t * d.tab_stride + s0;
+        uint32_t e[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) e[j] = row[j <= ns ? j : ns];
+        tabs[t] = make_uint4(e[0] | e[1] << 16, e[2] | e[3] << 16, e[4] | e[5] << 16, e[6] | e[7] << 16);
+    }
+    __syncthreads();
+    // wave w: tiles w, w + nw, ...; eight tiles in flight, one dword (two records) per lane per tile.
+    // A record's slice within the run: the number of the tile's inner run starts at or below it
+    // (the row is held in registers: one 16-B LDS read per tile).
+    const uint32_t w = tid >> 6, nw = kOrThreads >> 6, l = tid & 63;
+    constexpr uint32_t U = 8;
+    for (uint32_t t0 = w; t0 < T; t0 += U * nw) {
+        uint4 row[U];
+        uint32_t v[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t t = t0 + u * nw;
+            row[u] = t < T ? tabs[t] : make_uint4(0, 0, 0, 0);
+            const uint32_t a = row[u].x & 0xFFFFu, b = row_entry(row[u], ns);
+            const uint32_t *rw = (const uint32_t *)(d.rec + (uint64_t)(t < T ? t : 0) * d.rec_stride);
+            const uint32_t i = (a >> 1) + l;
+            v[u] = i < ((b + 1) >> 1) ? rw[i] : 0;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t t = t0 + u * nw;
+            if (t >= T) continue;
+            uint32_t e[8];
+            e[0] = row[u].x & 0xFFFFu; e[1] = row[u].x >> 16; e[2] = row[u].y & 0xFFFFu; e[3] = row[u].y >> 16;
+            e[4] = row[u].z & 0xFFFFu; e[5] = row[u].z >> 16; e[6] = row[u].w & 0xFFFFu; e[7] = row[u].w >> 16;
+            const uint32_t a = e[0], b = row_entry(row[u], ns);
+            auto put = [&](uint32_t x, uint32_t o) {
+                uint32_t sub = 0;
+#pragma unroll
+                for (uint32_t j = 1; j < kDenseMaxRun; j++) sub += (j < ns && x >= e[j]) ? 1u : 0u;
+                atomicOr(&bits[sub * kWords + (o >> 5)], 1u << (o & 31));
+            };
+            const uint32_t w0 = a >> 1, w1 = (b + 1) >> 1;
+            const uint32_t *rw = (const uint32_t *)(d.rec + (uint64_t)t * d.rec_stride);
+            for (uint32_t i = w0 + l, r = 0; i < w1; i += 64, r++) {
+                const uint32_t x = r ? rw[i] : v[u];  // runs over 128 records: further dwords
+                if (2 * i >= a) put(2 * i, x & 0xFFFFu);
+                if (2 * i + 1 < b) put(2 * i + 1, x >> 16);
+            }
+        }
+    }
+    __syncthreads();
+    // bitmap bytes [s0 * 8 KiB, s1 * 8 KiB) clipped to the filter (bitmap 4-byte aligned)
+    const uint64_t b0 = (uint64_t)s0 << (kDenseSliceBits - 3);
+    const uint64_t b1 = ((uint64_t)s1 << (kDenseSliceBits - 3)) < bytes ? ((uint64_t)s1 << (kDenseSliceBits - 3)) : bytes;
+    const uint64_t nfull = (b1 - b0) >> 2;
+    for (uint64_t x = tid; x < nfull; x += kOrThreads) ((uint32_t *)(bitmap + b0))[x] = bits[x];
+    for (uint64_t x = b0 + 4 * nfull + tid; x < b1; x += kOrThreads) {
+        const uint64_t r = x - b0;
+        bitmap[x] = (uint8_t)(bits[r >> 2] >> (8 * (r & 3)));
+    }
+}
+
+static hipError_t launch_bloom_dense(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n, DensePlan d,
+                                     uint8_t *bitmap, uint64_t bitmap_bytes, void *ws, hipStream_t st) {
+    static std::once_flag attrs;
+    static hipError_t attr_err = hipSuccess;
+    std::call_once(attrs, [] {
+        const void *f[] = {(const void *)k_bloom_sort<7, 8>, (const void *)k_bloom_sort<15, 4>};
+        for (const void *x : f)
+            if (attr_err == hipSuccess)
+                attr_err = hipFuncSetAttribute(x, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLds);
+        if (attr_err == hipSuccess)
+            attr_err = hipFuncSetAttribute((const void *)k_bloom_or, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)kOrLds);
+    });
+    if (attr_err != hipSuccess) return attr_err;
+    dense_carve(d, ws);
+    if (d.k <= 7)
+        hipLaunchKernelGGL((k_bloom_sort<7, 8>), dim3(d.tiles), dim3(kDenseThreads), dense_sort_lds(d), st, key_bytes,
+                           key_off, n, d);
+    else
+        hipLaunchKernelGGL((k_bloom_sort<15, 4>), dim3(d.tiles), dim3(kDenseThreads), dense_sort_lds(d), st, key_bytes,
+                           key_off, n, d);
+    hipLaunchKernelGGL(k_bloom_or, dim3(d.W), dim3(kOrThreads), dense_or_lds(d), st, d, bitmap, bitmap_bytes);
+    return hipGetLastError();
+}
+
 BloomPlan bloom_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes, uint32_t tile_keys) {
     BloomPlan pl{};
     pl.k = k ? k : 1;
@@ -113,7 +381,10 @@ uint64_t bloom_slots_bytes(const BloomPlan &pl) {
 }
 
 uint64_t bloom_workspace_bytes(uint64_t n, uint32_t k, uint64_t bitmap_bytes) {
-    return bloom_slots_bytes(bloom_plan(n, k, bitmap_bytes));
+    const DensePlan d = dense_plan(n, k, bitmap_bytes);
+    const uint64_t a = bloom_slots_bytes(bloom_plan(n, k, bitmap_bytes));
+    const uint64_t b = dense_fits(d) ? dense_ws_bytes(d) : 0;
+    return a > b ? a : b;
 }
 
 BloomSlots bloom_slots(void *ws, const BloomPlan &pl) {
@@ -136,6 +407,10 @@ hipError_t launch_bloom_build(const uint8_t *key_bytes, const uint64_t *key_off,
                               hipStream_t st) {
     if (bitmap_bytes == 0) return hipSuccess;
     if (n == 0 || num_probes == 0) return hipMemsetAsync(bitmap, 0, bitmap_bytes, st);
+    if (ws) {
+        const DensePlan d = dense_plan(n, num_probes, bitmap_bytes);
+        if (dense_fits(d) && !((uintptr_t)bitmap & 3)) return launch_bloom_dense(key_bytes, key_off, n, d, bitmap, bitmap_bytes, ws, st);
+    }
     BloomPlan pl = bloom_plan(n, num_probes, bitmap_bytes);
     if (!ws || !bloom_plan_fits(pl)) {
         // no workspace (or a plan the binning cannot hold): device-scope atomics into the bitmap

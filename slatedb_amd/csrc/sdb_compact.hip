@@ -491,9 +491,6 @@ __global__ __launch_bounds__(kMergeThreads) void k_mg_emit(MergeArgs a) {
         uint8_t mask = 0;
         if (e.f & SDB_FLAG_HAS_CREATE_TS) mask |= SDB_TS_CREATE;
         if ((e.f & SDB_FLAG_HAS_EXPIRE_TS) && e.d == 1) mask |= SDB_TS_EXPIRE;  // converted: expire_ts None
-#ifdef SDB_EXP_MG_NOCOLS  // diagnostic: no column stores (wrong output by design)
-        if (e.seq == 0x123456789ull)
-#endif
         {
         o.key_off[j] = ko;
         o.val_off[j] = vo;
@@ -525,9 +522,6 @@ __global__ __launch_bounds__(kMergeThreads) void k_mg_emit(MergeArgs a) {
             if (idx / kCopyHalf == h) s_cd[idx - h * kCopyHalf] = cds[u];
         }
         __syncthreads();
-#ifdef SDB_EXP_MG_NOCOPY  // diagnostic: no key / value byte copies (wrong output by design)
-        if (s_cd[0].kb == 0xFFFFFFFFu)
-#endif
         for (uint32_t g = 0; g < kPerWave; g += 64) {
             // lanes 8q' .. 8q' + 7 copy entry 8q + q' of these 64; lane l's 16-byte chunks start at
             // 16 (l & 7) and step by 128 (entries over 128 bytes take more steps, wave-uniformly)

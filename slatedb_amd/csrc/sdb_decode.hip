@@ -11,6 +11,7 @@
 // D2 scan    exclusive scans over blocks (tile sums -> tile scan -> apply).
 // D3 emit    one wave per block: parse again and write keys (restored against the previous key),
 //            value references into `blocks`, seq, flags and timestamps.
+#include <mutex>
 #include <type_traits>
 
 #include "sdb_decode.h"
@@ -435,11 +436,7 @@ SDB_DEV LdsBlockView stage_lds(const DecodeArgs &a, uint64_t s, uint64_t e, lu8 
         if (l < 4) img[p0 + l] ^= 0xFF;
         wave_sync_d();
         // zeros before img (the guard) and before p0
-#ifdef SDB_EXP_NO_CRC  // diagnostic: no CRC (every block accepted)
-        const uint32_t c = stored;
-#else
         const uint32_t c = wave_crc_image_ra(img, Lc);
-#endif
         wave_sync_d();
         if (l < 4) img[p0 + l] ^= 0xFF;
         wave_sync_d();
@@ -871,14 +868,10 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
             DEC_T(t1);
             t.status = v.status;
             if (!v.status) {
-#ifdef SDB_EXP_NO_WALK  // diagnostic: stage + CRC only (wrong counts by design)
-                t.entries = v.count;
-#else
                 if (a.version == 1) t = tally_v1(v);
                 else if (!tally_v2_spec(v, t, a.rowpos + 128 * k, a.rcnt + k) &&
                          !tally_v2_fast(v, t, a.rowpos + 128 * k, a.rcnt + k))
                     t = tally_v2(v);
-#endif
                 if (a.descending && a.version == 2) desc_rule(v.count, t);
             }
             DEC_T(t2);
@@ -914,10 +907,6 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
 // create_ts / expire_ts are valid iff the flag is set).
 SDB_DEV void put_entry(const DecodeArgs &a, uint64_t idx, uint64_t kpos, uint64_t vref, uint32_t vlen, uint64_t seq,
                        uint8_t flags, int64_t cts, int64_t ets) {
-#ifdef SDB_EXP_NO_PUT
-    if (seq == 0x123456789ull) a.out.key_off[idx] = kpos;  // experiment: no column stores
-    return;
-#endif
     a.out.key_off[idx] = kpos;
     a.out.val_off[idx] = vlen ? vref : 0;
     a.out.val_len[idx] = vlen;
@@ -1372,9 +1361,6 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
                 DEC_T(t2);
                 if (lds_keys) {
                     wave_sync_d();
-#ifdef SDB_EXP_NO_KEYSTORE  // diagnostic: no key arena stores (wrong output by design)
-                    if (kbn == 0x7FFFFFFFull)
-#endif
                     wave_store_bytes(a.out.key_arena + kb0, kbuf, kbn);
                 }
                 DEC_T(t3);
@@ -1494,7 +1480,9 @@ __global__ void k_dec_finish(DecodeArgs a) {
 constexpr uint32_t kDescGrid = 2048, kDescThreads = 256;
 SDB_DEV bool desc_sizes(const DecodeArgs &a, uint64_t *N, uint64_t *KB) {
     const sdb_decode_summary *sm = a.out.summary;
-    if (sm->status == SDB_INVALID_ARGUMENT) return false;  // nothing was written (capacity)
+    // only when the emit pass ran: OK, or a per-block corruption status (the counts stay consistent);
+    // SDB_INVALID_ARGUMENT (capacity) and SDB_DEVICE_ERROR leave key_off unwritten
+    if (sm->status == SDB_INVALID_ARGUMENT || sm->status == SDB_DEVICE_ERROR) return false;
     *N = sm->num_entries;
     *KB = sm->key_bytes;
     return true;
@@ -1541,14 +1529,17 @@ __global__ __launch_bounds__(kDescThreads) void k_desc_keys(DecodeArgs a) {
 }
 
 hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
+    static std::once_flag attrs;
+    static hipError_t attr_err = hipSuccess;
+    std::call_once(attrs, [] {
+        attr_err = hipFuncSetAttribute((const void *)k_dec_count, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)kCntLds);
+        if (attr_err == hipSuccess)
+            attr_err = hipFuncSetAttribute((const void *)k_dec_emit, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)kDecLds);
+    });
+    if (attr_err != hipSuccess) return attr_err;
     hipLaunchKernelGGL(k_dec_init, dim3(1), dim3(64), 0, st, a);
-    static bool attrs = false;
-    if (!attrs) {
-        hipFuncSetAttribute((const void *)k_dec_count, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCntLds);
-        hipFuncSetAttribute((const void *)k_dec_emit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDecLds);
-        (void)hipGetLastError();
-        attrs = true;
-    }
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

@@ -1382,11 +1382,9 @@ SDB_DEV void emit_prefetch(const EncodeArgs &a, const BlockDesc &d, EmitPre &p) 
     const uint32_t nv16 = d.ve > d.vs ? (uint32_t)((d.ve - va + 15) >> 4) : 0;
     const uint32_t nk16 = (uint32_t)((d.ke - ka + 15) >> 4);
     const uint4 *vsrc = (const uint4 *)(a.val_bytes + va), *ksrc = (const uint4 *)(a.key_bytes + ka);
-#if !defined(SDB_EXP_NO_VALUE_LOAD)
 #pragma unroll
     for (uint32_t q = 0; q < kStageCap / 1024; q++)
         if (64 * q + l < nv16) p.vg[q] = vsrc[64 * q + l];
-#endif
 #pragma unroll
     for (uint32_t q = 0; q < kKeyStageCap / 1024; q++)
         if (64 * q + l < nk16) p.kg[q] = ksrc[64 * q + l];
@@ -1493,7 +1491,6 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     wave_sync();  // stages written (DS instructions of one wave complete in order)
     WAVE_T(t2);
     // 2. key suffixes + values: lane = row from registers, or cooperative by the span table
-#if !defined(SDB_EXP_NO_COPY)  // diagnostic: no key / value copy (wrong bytes by design)
     if (!copy_rows(img, row, sc)) {
         if (row) {
             rtab[l].a = sc.a;
@@ -1504,7 +1501,6 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
         wave_sync();
         copy_spans(img, rtab, ne);
     }
-#endif
     WAVE_T(t3);
     // 3. literals: header, the key bytes sharing a dword with non-key bytes, trailer; then the
     //    restart table, count and the zero padding of the last CRC segment
@@ -1541,36 +1537,25 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     wave_sync();
     WAVE_T(t4);
     // 4. CRC32 (format/sst.rs:541-552) of the image [0, Lc)
-#if defined(SDB_EXP_NO_CRC)  // diagnostic: no CRC (wrong bytes by design)
-    const uint32_t crc32 = 0;
-#else
     const uint32_t crc32 = wave_crc_image_ra(img, Lc);
-#endif
     if (l == 0) {
         img[Lc] = (uint8_t)(crc32 >> 24);
         img[Lc + 1] = (uint8_t)(crc32 >> 16);
         img[Lc + 2] = (uint8_t)(crc32 >> 8);
         img[Lc + 3] = (uint8_t)crc32;
-#if !defined(SDB_EXP_NO_CRC)
         if (Lc + 4 != d.bb) report_error(a.err, d.s, SDB_DEVICE_ERROR);  // internal consistency
-#endif
     }
     wave_sync();
     WAVE_T(t5);
     // 5. store [0, Lc + 4) -> out_data + off
     uint8_t *gdst = a.out_data + d.off;
-#if defined(SDB_EXP_ALIGNED_STORE)
-    gdst = (uint8_t *)((uintptr_t)gdst & ~(uintptr_t)15);  // experiment: wrong bytes, aligned stores
-#endif
     const uint32_t L = Lc + 4, nfull = L >> 4;
-#if !defined(SDB_EXP_NO_STORE)
     for (uint32_t cc = l; cc < nfull; cc += 64) {
         u32x4 v = ((const lu128 *)img)[cc];
         if (cc == 0) v.x = ~v.x;  // the CRC's init fold
         __builtin_memcpy(gdst + 16 * cc, &v, 16);
     }
     if (l < (L & 15)) gdst[(nfull << 4) + l] = img[(nfull << 4) + l];  // L >= 16: never image bytes [0, 4)
-#endif
     WAVE_T(t6);
 #ifdef SDB_PHASE_TIMING
     ph[0] += t1 - t0;

@@ -653,6 +653,15 @@ def sst_lookup_device(view_tensors, key_bytes, key_off, nkeys, descending=False,
 # ------------------------------------------------------------------------------------------------
 # Compaction (sdb_merge_runs / sdb_sst_cuts / sdb_compactor_*)
 # ------------------------------------------------------------------------------------------------
+def _sync(stream, dev):
+    """Wait for work queued on `stream` (a torch stream, a raw handle or None) before a host read."""
+    import torch
+    if stream is not None and hasattr(stream, "synchronize"):
+        stream.synchronize()
+    else:
+        torch.cuda.synchronize(dev)  # device-wide: covers a raw stream handle too
+
+
 def _sp(stream):
     if stream is None:
         return None
@@ -729,6 +738,7 @@ def merge_runs_device(druns, ret, stream=None):
     st = lib().sdb_merge_runs(cr, len(druns), C.byref(ret), C.byref(out), ws.data_ptr(), ws.numel(), _sp(stream))
     if st:
         raise SdbError(st, "sdb_merge_runs")
+    _sync(stream, dev)
     sm = _abi.MergeSummary.from_buffer_copy(o["summary"].cpu().numpy().tobytes())
     o["_ws"] = ws
     return o, sm
@@ -748,7 +758,7 @@ def sst_cuts_device(dbatch, prm, max_sst_size, stream=None):
     """sdb_sst_cuts over a device batch -> list of SST start entries + [n] (synchronises)."""
     import torch
     n = dbatch.n
-    dev = "cuda"
+    dev = dbatch.key_bytes.device if hasattr(dbatch, "key_bytes") else "cuda"
     cut = torch.zeros(n + 2, dtype=torch.int64, device=dev)
     num = torch.zeros(1, dtype=torch.int64, device=dev)
     wsb = lib().sdb_sst_cuts_workspace_bytes(n, C.byref(prm))
@@ -758,6 +768,7 @@ def sst_cuts_device(dbatch, prm, max_sst_size, stream=None):
                             ws.data_ptr(), ws.numel(), _sp(stream))
     if st:
         raise SdbError(st, "sdb_sst_cuts")
+    _sync(stream, dev)
     ns = int(num.item())
     return [int(x) for x in cut[:ns + 1].cpu().numpy()] if ns else []
 

@@ -297,3 +297,16 @@ def test_encode_host_many_pipelined(rt):
             ref = O.encode_sst(b, O.params(**prm))
             assert_same(ref, g, "many[%d] rep %d" % (i, rep))
     enc.close()
+
+
+def test_encode_host_many_grows_output_slots(rt):
+    """A call with more SSTs than any earlier one grows the encoder's pinned output buffers; the buffers
+    of the earlier SSTs must survive the growth (they are moved, not copied and freed)."""
+    prm = dict(block_size=4096, sst_version=2, bloom_bits_per_key=10)
+    enc = rt.Encoder(rt.params(**prm))
+    for sizes in ([5000, 9000], [5000, 9000, 300, 7000, 12000, 1, 4000], [800, 700]):
+        hosts = [datasets.d1(sst_index=i, n=n) for i, n in enumerate(sizes)]
+        got = enc.encode_many(hosts)
+        for i, (b, g) in enumerate(zip(hosts, got)):
+            assert_same(O.encode_sst(b, O.params(**prm)), g, "grow %d/%d" % (i, len(sizes)))
+    enc.close()

@@ -188,12 +188,27 @@ def test_builder_mirror(rt):
 # ------------------------------------------------------------------------------------------------
 # bloom
 # ------------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("n,bpk", [(1, 10), (7, 10), (1000, 10), (200000, 10), (100000, 7), (5, 1)])
+# (n, bpk): tiny filters (one slice), the dense build at k <= 7 (8 keys per thread) and k 8..15 (4 per
+# thread), several slices per k_bloom_or workgroup (2 M keys: 306 slices), and k = 16 (no binned plan:
+# the atomic build)
+@pytest.mark.parametrize("n,bpk", [(1, 10), (7, 10), (1000, 10), (200000, 10), (100000, 7), (5, 1), (300000, 12),
+                                   (50000, 21), (20000, 24), (2000000, 10), (8193, 10)])
 def test_bloom_bitmap(rt, n, bpk):
     kb, ko = datasets.c4_keys(n=n, seed=11 + n)
     ref = O.bloom_build(kb, ko, bpk)
     got = rt.BloomFilterPolicy(bpk).build(Batch(kb, ko, np.zeros(0, np.uint8), np.zeros(len(ko), np.uint64)))
     assert got[:2] == struct.pack(">H", O.optimal_num_probes(bpk))
+    assert got[2:] == ref.tobytes()
+
+
+def test_bloom_bitmap_ragged_keys(rt):
+    """Keys of 0..40 bytes at unaligned offsets (the generic SipHash path of the dense build)."""
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 41, 150000).astype(np.uint64)
+    ko = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    kb = rng.integers(0, 256, int(ko[-1]), dtype=np.uint8)
+    ref = O.bloom_build(kb, ko, 10)
+    got = rt.BloomFilterPolicy(10).build(Batch(kb, ko, np.zeros(0, np.uint8), np.zeros(len(ko), np.uint64)))
     assert got[2:] == ref.tobytes()
 
 

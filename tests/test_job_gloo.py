@@ -91,3 +91,25 @@ def test_job_sharding_gloo_world2():
     assert merged == single                               # sharding changes no byte
     assert total == sum(v[0] for v in single.values())   # Σ bytes over ranks
     assert tmax > 0 and job.job_rate_gibs(total, tmax) > 0
+
+
+def test_bench_spawns_gpus_ranks_dry_run():
+    """`python bench.py --gpus 2` without a launcher starts two ranks itself (before any GPU call); in
+    --dry-run they meet over gloo, take their share of the job and aggregate, and n_gpus == --gpus."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run",
+                        "--job-ssts", "64"], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2
+    assert line["ssts_per_rank"] == [job.share(64, 2, 0), job.share(64, 2, 1)]
+    assert line["total_logical_bytes"] == 64 * (578524 * 116)
+    # a launcher world that disagrees with --gpus is refused
+    env["WORLD_SIZE"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
