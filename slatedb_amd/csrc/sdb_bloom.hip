@@ -68,27 +68,32 @@ __global__ __launch_bounds__(256) void k_bloom_query(const uint8_t *bitmap, uint
 // ------------------------------------------------------------------------------------------------
 // Standalone build, dense records (configs[3]: 10 M keys, 100 M bits).  The bitmap is cut into
 // slices of 2^16 bits, so a probe is stored as its u16 offset inside its slice.
-//   k_bloom_sort  one 1024-thread workgroup per tile of T keys: SipHash-1-3 and the k probes of every
-//                 key held in registers; an LDS counting sort by slice (one returning LDS add per
-//                 probe gives its rank in the slice, so the scatter needs no second atomic); the
-//                 tile's T*k u16 offsets are written as ONE dense, slice-ordered array with 16-B
-//                 stores, and the tile's run starts (S + 1 u16, T*k < 2^16) as its table row.
-//   k_bloom_or    one workgroup per run of consecutive slices (<= 8, so that the workgroups fill the
-//                 chip): its slices' table entries of every tile staged in LDS, then every tile's
-//                 contiguous run of records for those slices (dword loads, several tiles in flight per
-//                 wave) ORed into an LDS copy of the slices, written with plain stores.
+//   k_bloom_sort  one 512-thread workgroup per tile of T = 4096 keys (two per CU): the key offsets,
+//                 then the 16-byte key words, all loads in flight before the first use; SipHash-1-3
+//                 and the k probes of every key held in registers; an LDS counting sort by slice (one
+//                 returning LDS add per probe gives its rank in the slice, so the scatter needs no
+//                 second atomic); the tile's T*k u16 offsets are written as ONE dense, slice-ordered
+//                 array with 16-byte stores, and the tile's run starts (S + 1 u16, T*k < 2^16) as its
+//                 table row.
+//   k_bloom_or    one 512-thread workgroup per pair of slices (kOrNs): the pair's run starts in every
+//                 tile staged in LDS, then every tile's contiguous run of the pair's records (a wave
+//                 reads eight tiles' runs per load instruction, 16 bytes per lane, eight such loads in
+//                 flight) ORed into an LDS copy of the pair, written with plain stores.
 // No per-slot capacity, hence no overflow case.  Records cost 2 B written + 2 B read per probe, the
-// half of u32 records; the dense array makes every store and load a full coalesced line.
+// half of u32 records.  Measured (configs[3]): sort ~115 us, or ~70 us; one workgroup per
+// slice or per four slices, 256- or 1024-thread sort workgroups were all slower.
 // ------------------------------------------------------------------------------------------------
-constexpr uint32_t kDenseThreads = 512, kDenseSliceBits = 16, kDenseMaxSlices = 4096, kDenseMaxRun = 7;
-constexpr uint32_t kOrThreads = 1024;
+constexpr uint32_t kDenseThreads = 512, kDenseSliceBits = 16, kDenseMaxSlices = 4096;
+constexpr uint32_t kOrThreads = 512;
+constexpr uint32_t kOrNs = 2, kOrLanes = 8, kOrSeg = 64 / kOrLanes, kOrUnroll = 8;
+static_assert(kOrNs >= 1 && kOrNs <= 7, "a tile row of kOrNs + 1 u16 run starts fits 16 bytes");
 constexpr uint32_t kOrLds = 150 * 1024;
 
 struct DensePlan {
     uint32_t k, m, S;        // probes per key, bits, slices of 2^16 bits
     uint32_t kpt, T, tiles;  // keys per thread, keys per tile, tiles
     uint32_t tab_stride;     // u16 per table row (>= S + 1, multiple of 8)
-    uint32_t ns, W;          // slices per k_bloom_or workgroup, workgroups
+    uint32_t W;              // k_bloom_or workgroups
     uint64_t rec_stride;     // u16 records per tile (T * k rounded to 8)
     uint64_t mmod;
     uint16_t *rec;           // tiles x rec_stride
@@ -105,17 +110,12 @@ static DensePlan dense_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes) {
     d.tiles = (uint32_t)((n + d.T - 1) / d.T);
     d.tab_stride = (d.S + 1 + 7) & ~7u;
     d.rec_stride = ((uint64_t)d.T * k + 7) & ~7ull;
-    d.ns = (d.S + 255) / 256;
-    if (d.ns > kDenseMaxRun) d.ns = kDenseMaxRun;
-    if (d.ns == 0) d.ns = 1;
-    d.W = (d.S + d.ns - 1) / d.ns;
+    d.W = (d.S + kOrNs - 1) / kOrNs;  // k_bloom_or: kOrNs slices per workgroup
     d.mmod = d.m ? ~0ull / d.m + 1 : 0;
     return d;
 }
 static size_t dense_sort_lds(const DensePlan &d) { return 4 * (size_t)d.S + 2 * (size_t)d.rec_stride; }
-static size_t dense_or_lds(const DensePlan &d) {  // the slices' bits, then 16 B of run starts per tile
-    return 4 * (size_t)d.ns * (1u << (kDenseSliceBits - 5)) + 16 * (size_t)d.tiles;
-}
+static size_t dense_or_lds(const DensePlan &d);
 static bool dense_fits(const DensePlan &d) {
     return d.k >= 1 && d.k <= 15 && d.m >= 2 && d.S <= kDenseMaxSlices && (uint64_t)d.T * d.k < 65536 &&
            dense_sort_lds(d) <= kBinLds && dense_or_lds(d) <= kOrLds;
@@ -127,6 +127,41 @@ static void dense_carve(DensePlan &d, void *ws) {
     uint8_t *w = (uint8_t *)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
     d.rec = (uint16_t *)w;
     d.tab = (uint16_t *)(w + (((uint64_t)d.tiles * d.rec_stride * 2 + 255) & ~255ull));
+}
+
+// (h0, d0) of keys k0 + tid + j * kDenseThreads (j < KPT, only those < nk are meaningful).  Every load
+// is unconditional, so all of them are in flight before the first use: the KPT offset pairs, then
+// the KPT 16-byte key words (a key that is not 16 bytes at an 8-byte aligned offset reads the 16
+// in-bounds bytes of its own offset pair instead, and is hashed by the generic path afterwards).
+template <uint32_t KPT>
+SDB_DEV void dense_hash_keys(const uint8_t *__restrict__ key_bytes, const uint64_t *__restrict__ key_off, uint64_t k0,
+                             uint32_t nk, const BloomPlan &pl, uint32_t (&hh)[KPT], uint32_t (&dd)[KPT]) {
+    const uint32_t tid = threadIdx.x;
+    uint64_t ko[KPT], ke[KPT];
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; j++) {
+        const uint32_t x = tid + j * kDenseThreads;
+        const uint64_t i = k0 + (x < nk ? x : nk - 1);
+        ko[j] = key_off[i];
+        ke[j] = key_off[i + 1];
+    }
+    uint4 w[KPT];
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; j++) {
+        const uint32_t x = tid + j * kDenseThreads;
+        const uint64_t i = k0 + (x < nk ? x : nk - 1);
+        const bool fast = ke[j] - ko[j] == 16 && (ko[j] & 7) == 0;
+        w[j] = *(const uint4 *)(fast ? key_bytes + ko[j] : (const uint8_t *)(key_off + i));
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; j++) {
+        const bool fast = ke[j] - ko[j] == 16 && (ko[j] & 7) == 0;
+        uint64_t h;
+        if (fast) h = siphash13_16((uint64_t)w[j].x | (uint64_t)w[j].y << 32, (uint64_t)w[j].z | (uint64_t)w[j].w << 32);
+        else h = siphash13(key_bytes + ko[j], ke[j] - ko[j]);
+        hh[j] = fastmod_u32((uint32_t)h, pl.mmod, pl.m);
+        dd[j] = fastmod_u32((uint32_t)(h >> 32), pl.mmod, pl.m);
+    }
 }
 
 // KMAX: probes per key the registers hold (k <= KMAX); KPT keys per thread.
@@ -147,77 +182,68 @@ __global__ __launch_bounds__(kDenseThreads) void k_bloom_sort(const uint8_t *__r
     pl.m = d.m;
     pl.mmod = d.mmod;
     uint32_t hh[KPT], dd[KPT];
-#pragma unroll
-    for (uint32_t j = 0; j < KPT; j++) {
-        hh[j] = dd[j] = 0;
-        if (tid + j * kDenseThreads < nk) key_hd(key_bytes, key_off, k0 + tid + j * kDenseThreads, pl, hh[j], dd[j]);
-    }
+    dense_hash_keys<KPT>(key_bytes, key_off, k0, nk, pl, hh, dd);
     __syncthreads();
-    // rank of every probe inside its slice (u16: T * k < 2^16), two per register
-    uint32_t rk[(KPT * KMAX + 1) / 2];
+    // every probe (u32) and its rank inside its slice (u16: T * k < 2^16, two per register) stay in
+    // registers from the counting pass to the scatter
+    uint32_t pr[KPT * KMAX], rk[(KPT * KMAX + 1) / 2];
 #pragma unroll
     for (uint32_t x = 0; x < (KPT * KMAX + 1) / 2; x++) rk[x] = 0;
 #pragma unroll
     for (uint32_t j = 0; j < KPT; j++) {
-        if (tid + j * kDenseThreads < nk) {
-            uint32_t h = hh[j], dl = dd[j];
-            const uint32_t m = d.m;
+        const bool live = tid + j * kDenseThreads < nk;
+        uint32_t h = hh[j], dl = dd[j];
+        const uint32_t m = d.m;
 #pragma unroll
-            for (uint32_t i = 0; i < KMAX; i++) {
-                if (i < k) {
-                    dl += i;
-                    const uint32_t dm = dl - m;
-                    dl = dm < dl ? dm : dl;
-                    const uint32_t r = atomicAdd(&hist[h >> kDenseSliceBits], 1u);
-                    rk[(j * KMAX + i) / 2] |= r << (16 * ((j * KMAX + i) & 1));
-                    h += dl;
-                    const uint32_t hm = h - m;
-                    h = hm < h ? hm : h;
-                }
+        for (uint32_t i = 0; i < KMAX; i++) {
+            pr[j * KMAX + i] = h;
+            if (live && i < k) {
+                dl += i;
+                const uint32_t dm = dl - m;
+                dl = dm < dl ? dm : dl;
+                const uint32_t r = atomicAdd(&hist[h >> kDenseSliceBits], 1u);
+                rk[(j * KMAX + i) / 2] |= r << (16 * ((j * KMAX + i) & 1));
+                h += dl;
+                const uint32_t hm = h - m;
+                h = hm < h ? hm : h;
             }
         }
     }
     __syncthreads();
-    // run starts: exclusive scan of the counts; the table row gets S + 1 of them
-    uint64_t carry = 0;
+    // run starts: exclusive scan of the counts (each thread sums its consecutive ceil(S / 512) counts,
+    // one block scan); the table row gets S + 1 of them
+    const uint32_t per = (S + kDenseThreads - 1) / kDenseThreads, x0 = tid * per;
+    uint32_t mine = 0;
+    for (uint32_t x = x0; x < x0 + per && x < S; x++) mine += hist[x];
+    uint64_t tot;
+    uint32_t run = (uint32_t)block_excl_scan_u64(mine, s_w, &tot);
     uint16_t *trow = d.tab + (uint64_t)tile * d.tab_stride;
-    for (uint32_t x0 = 0; x0 < S; x0 += kDenseThreads) {
-        const uint32_t x = x0 + tid;
-        const uint32_t c = x < S ? hist[x] : 0;
-        uint64_t tot;
-        const uint64_t ex = block_excl_scan_u64(c, s_w, &tot);
-        if (x < S) {
-            hist[x] = (uint32_t)(carry + ex);
-            trow[x] = (uint16_t)(carry + ex);
-        }
-        carry += tot;
+    for (uint32_t x = x0; x < x0 + per && x < S; x++) {
+        const uint32_t c = hist[x];
+        hist[x] = run;
+        trow[x] = (uint16_t)run;
+        run += c;
     }
+    const uint32_t carry = (uint32_t)tot;
     if (tid == 0) trow[S] = (uint16_t)carry;
     __syncthreads();
-    // scatter: the probes again from (h0, d0), each to its slice's run start + its rank
+    // scatter: each probe's offset to its slice's run start + its rank
 #pragma unroll
     for (uint32_t j = 0; j < KPT; j++) {
         if (tid + j * kDenseThreads < nk) {
-            uint32_t h = hh[j], dl = dd[j];
-            const uint32_t m = d.m;
 #pragma unroll
             for (uint32_t i = 0; i < KMAX; i++) {
                 if (i < k) {
-                    dl += i;
-                    const uint32_t dm = dl - m;
-                    dl = dm < dl ? dm : dl;
+                    const uint32_t p = pr[j * KMAX + i];
                     const uint32_t r = (rk[(j * KMAX + i) / 2] >> (16 * ((j * KMAX + i) & 1))) & 0xFFFFu;
-                    sorted[hist[h >> kDenseSliceBits] + r] = (uint16_t)h;
-                    h += dl;
-                    const uint32_t hm = h - m;
-                    h = hm < h ? hm : h;
+                    sorted[hist[p >> kDenseSliceBits] + r] = (uint16_t)p;
                 }
             }
         }
     }
     __syncthreads();
     // the dense record array of the tile: 16-B stores (rec_stride is a multiple of 8 u16)
-    const uint32_t n16 = (uint32_t)((carry + 7) >> 3);
+    const uint32_t n16 = (carry + 7) >> 3;
     const uint4 *src = (const uint4 *)sorted;
     uint4 *dst = (uint4 *)(d.rec + (uint64_t)tile * d.rec_stride);
     for (uint32_t x = tid; x < n16; x += kDenseThreads) dst[x] = src[x];
@@ -233,66 +259,79 @@ SDB_DEV uint32_t dense_run_of(uint32_t b, uint32_t W) {
     return start + q;
 }
 
-// u16 entry j (< 8) of a row held in a uint4, without indexing a register array
-SDB_DEV uint32_t row_entry(const uint4 &r, uint32_t j) {
-    const uint64_t lo = (uint64_t)r.x | (uint64_t)r.y << 32, hi = (uint64_t)r.z | (uint64_t)r.w << 32;
-    return (uint32_t)(((j < 4 ? lo : hi) >> (16 * (j & 3))) & 0xFFFFu);
-}
-
+// kOrNs consecutive 2^16-bit slices per workgroup.  Every tile holds one run of those slices'
+// records (run starts row[s0 .. s0 + kOrNs], u16), staged in LDS first.  A wave reads kOrSeg tiles'
+// runs per load instruction: lane group q (kOrLanes lanes) reads tile t0 + q, 16 bytes (eight
+// records) per lane, kOrUnroll such loads in flight per lane before the first OR; runs over
+// 8 * kOrLanes records loop on.  A record's slice is the number of the row's inner starts at or below
+// its position.
 __global__ __launch_bounds__(kOrThreads) void k_bloom_or(DensePlan d, uint8_t *bitmap, uint64_t bytes) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     constexpr uint32_t kWords = 1u << (kDenseSliceBits - 5);
+    constexpr uint32_t kRowU16 = kOrNs + 1 <= 2 ? 2 : kOrNs + 1 <= 4 ? 4 : 8;  // u16 per staged row
     const uint32_t run = dense_run_of(blockIdx.x, d.W);
-    const uint32_t s0 = run * d.ns, s1 = s0 + d.ns < d.S ? s0 + d.ns : d.S, ns = s1 - s0;
-    uint32_t *bits = lds;                          // ns x 2^16 bits
-    uint4 *tabs = (uint4 *)(lds + d.ns * kWords);  // per tile: its ns + 1 (<= 8) run starts, u16
+    const uint32_t s0 = run * kOrNs, s1 = s0 + kOrNs < d.S ? s0 + kOrNs : d.S, ns = s1 - s0;
+    uint32_t *bits = lds;                                // kOrNs x 2^16 bits
+    uint16_t *rows = (uint16_t *)(lds + kOrNs * kWords);  // per tile: run starts s0 .. s0 + kOrNs
     const uint32_t tid = threadIdx.x, T = d.tiles;
-    for (uint32_t x = tid; x < ns * kWords; x += kOrThreads) bits[x] = 0;
-    for (uint32_t t = tid; t < T; t += kOrThreads) {
-        const uint16_t *row = d.tab + (uint64_t)t * d.tab_stride + s0;
-        uint32_t e[8];
+    for (uint32_t x = tid; x < kOrNs * kWords; x += kOrThreads) bits[x] = 0;
+    for (uint32_t t0 = tid; t0 < T; t0 += 4 * kOrThreads) {  // four rows' loads in flight per thread
+        uint32_t e[4][kOrNs + 1];
 #pragma unroll
-        for (uint32_t j = 0; j < 8; j++) e[j] = row[j <= ns ? j : ns];
-        tabs[t] = make_uint4(e[0] | e[1] << 16, e[2] | e[3] << 16, e[4] | e[5] << 16, e[6] | e[7] << 16);
-    }
-    __syncthreads();
-    // wave w: tiles w, w + nw, ...; eight tiles in flight, one dword (two records) per lane per tile.
-    // A record's slice within the run: the number of the tile's inner run starts at or below it
-    // (the row is held in registers: one 16-B LDS read per tile).
-    const uint32_t w = tid >> 6, nw = kOrThreads >> 6, l = tid & 63;
-    constexpr uint32_t U = 8;
-    for (uint32_t t0 = w; t0 < T; t0 += U * nw) {
-        uint4 row[U];
-        uint32_t v[U];
+        for (uint32_t u = 0; u < 4; u++) {
+            const uint32_t t = t0 + u * kOrThreads;
+            const uint16_t *row = d.tab + (uint64_t)(t < T ? t : 0) * d.tab_stride + s0;
 #pragma unroll
-        for (uint32_t u = 0; u < U; u++) {
-            const uint32_t t = t0 + u * nw;
-            row[u] = t < T ? tabs[t] : make_uint4(0, 0, 0, 0);
-            const uint32_t a = row[u].x & 0xFFFFu, b = row_entry(row[u], ns);
-            const uint32_t *rw = (const uint32_t *)(d.rec + (uint64_t)(t < T ? t : 0) * d.rec_stride);
-            const uint32_t i = (a >> 1) + l;
-            v[u] = i < ((b + 1) >> 1) ? rw[i] : 0;
+            for (uint32_t j = 0; j <= kOrNs; j++) e[u][j] = row[j <= ns ? j : ns];
         }
 #pragma unroll
-        for (uint32_t u = 0; u < U; u++) {
-            const uint32_t t = t0 + u * nw;
-            if (t >= T) continue;
-            uint32_t e[8];
-            e[0] = row[u].x & 0xFFFFu; e[1] = row[u].x >> 16; e[2] = row[u].y & 0xFFFFu; e[3] = row[u].y >> 16;
-            e[4] = row[u].z & 0xFFFFu; e[5] = row[u].z >> 16; e[6] = row[u].w & 0xFFFFu; e[7] = row[u].w >> 16;
-            const uint32_t a = e[0], b = row_entry(row[u], ns);
-            auto put = [&](uint32_t x, uint32_t o) {
+        for (uint32_t u = 0; u < 4; u++)
+            if (t0 + u * kOrThreads < T)
+#pragma unroll
+                for (uint32_t j = 0; j <= kOrNs; j++) rows[(t0 + u * kOrThreads) * kRowU16 + j] = (uint16_t)e[u][j];
+    }
+    __syncthreads();
+    const uint32_t w = tid >> 6, nw = kOrThreads >> 6, l = tid & 63, q = l / kOrLanes, sl = l % kOrLanes;
+    // lane sl of a group covers records [a8 + 8 sl, a8 + 8 sl + 8) of its tile, a8 = a & ~7 (16-byte
+    // aligned: rec_stride is a multiple of 8 records); records outside [a, b) are skipped
+    const uint64_t rlim = (uint64_t)T * d.rec_stride;  // u16 records in the workspace
+    for (uint32_t t0 = w * kOrSeg; t0 < T; t0 += nw * kOrSeg * kOrUnroll) {
+        uint4 v[kOrUnroll];
+        uint32_t rb[kOrUnroll][kOrNs + 1];
+        // unconditional loads (lanes past their run read an in-bounds clamped address, masked at use):
+        // a load under a branch makes the compiler wait for every earlier load at the join
+#pragma unroll
+        for (uint32_t u = 0; u < kOrUnroll; u++) {
+            const uint32_t t = t0 + u * nw * kOrSeg + q, tc = t < T ? t : T - 1;
+#pragma unroll
+            for (uint32_t j = 0; j <= kOrNs; j++) rb[u][j] = t < T ? rows[tc * kRowU16 + j] : 0;
+            uint64_t x = (uint64_t)tc * d.rec_stride + (rb[u][0] & ~7u) + 8 * sl;
+            x = x + 8 <= rlim ? x : 0;
+            v[u] = *(const uint4 *)(d.rec + x);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kOrUnroll; u++) {
+            const uint32_t t = t0 + u * nw * kOrSeg + q;
+            const uint32_t a = rb[u][0], b = rb[u][kOrNs];
+            auto put = [&](uint32_t i, uint32_t o) {  // record i of the tile, offset o in its slice
                 uint32_t sub = 0;
 #pragma unroll
-                for (uint32_t j = 1; j < kDenseMaxRun; j++) sub += (j < ns && x >= e[j]) ? 1u : 0u;
+                for (uint32_t j = 1; j < kOrNs; j++) sub += i >= rb[u][j] ? 1u : 0u;
                 atomicOr(&bits[sub * kWords + (o >> 5)], 1u << (o & 31));
             };
-            const uint32_t w0 = a >> 1, w1 = (b + 1) >> 1;
-            const uint32_t *rw = (const uint32_t *)(d.rec + (uint64_t)t * d.rec_stride);
-            for (uint32_t i = w0 + l, r = 0; i < w1; i += 64, r++) {
-                const uint32_t x = r ? rw[i] : v[u];  // runs over 128 records: further dwords
-                if (2 * i >= a) put(2 * i, x & 0xFFFFu);
-                if (2 * i + 1 < b) put(2 * i + 1, x >> 16);
+            uint32_t i = (a & ~7u) + 8 * sl;  // first record of this lane's 16 bytes
+            const uint32_t wv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+            for (uint32_t j = 0; j < 8; j++)
+                if (i + j >= a && i + j < b) put(i + j, (wv[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
+            if (t < T) {
+                for (i += 8 * kOrLanes; i < b; i += 8 * kOrLanes) {  // runs over 8 * kOrLanes records
+                    const uint4 y = *(const uint4 *)(d.rec + (uint64_t)t * d.rec_stride + i);
+                    const uint32_t yw[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+                    for (uint32_t j = 0; j < 8; j++)
+                        if (i + j < b) put(i + j, (yw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
+                }
             }
         }
     }
@@ -306,6 +345,11 @@ __global__ __launch_bounds__(kOrThreads) void k_bloom_or(DensePlan d, uint8_t *b
         const uint64_t r = x - b0;
         bitmap[x] = (uint8_t)(bits[r >> 2] >> (8 * (r & 3)));
     }
+}
+
+static size_t dense_or_lds(const DensePlan &d) {  // the slices' bits, then one row of run starts per tile
+    constexpr uint32_t kRowU16 = kOrNs + 1 <= 2 ? 2 : kOrNs + 1 <= 4 ? 4 : 8;
+    return 4 * (size_t)kOrNs * (1u << (kDenseSliceBits - 5)) + 2 * (size_t)kRowU16 * d.tiles;
 }
 
 static hipError_t launch_bloom_dense(const uint8_t *key_bytes, const uint64_t *key_off, uint64_t n, DensePlan d,

@@ -185,7 +185,7 @@ SDB_DEV EntryFacts entry_facts(const EncodeArgs &a, uint64_t i) {
 // first probe and step.  Lanes hold consecutive entries: the next entry's offsets and the previous
 // key's first 16 bytes come from the neighbour lane by DPP (lane 63 / lane 0 load their own).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kFactsThreads) void k_facts(SstSet P) {
+__global__ __launch_bounds__(kFactsThreads, 8) void k_facts(SstSet P) {
     const EncodeArgs a = make_args(P, blockIdx.y);
     if (blockIdx.x >= a.nfacts) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t blds[];  // fused bloom binning
@@ -217,6 +217,11 @@ __global__ __launch_bounds__(kFactsThreads) void k_facts(SstSet P) {
             }
         }
     }
+    // the first 16 bytes of every key (and lane 0's previous key): one unconditional 16-byte load per
+    // entry, all in flight together (a load under a branch would make the compiler wait for every
+    // earlier one at the join).  A window that would run past the key bytes (a short key at the end
+    // of the batch) reads 16 in-bounds bytes of key_off instead and is re-read byte-exactly below.
+    const uint64_t ktot = a.key_off[n];
 #pragma unroll
     for (uint32_t r = 0; r < kFactsPerT; r++) {
         FactsIn &f = in[r];
@@ -226,18 +231,44 @@ __global__ __launch_bounds__(kFactsThreads) void k_facts(SstSet P) {
             f.vo1 = nv;
         }
         const uint64_t e = e0 + r * kFactsThreads;
-        f.ck0 = f.ck1 = f.pk0 = f.pk1 = 0;
-        if (e < n) {
+        const bool live = e < n;
+        const uint8_t *safe = (const uint8_t *)a.key_off;  // >= 16 bytes (n + 1 >= 2 offsets)
+        const uint8_t *cs = live && f.ko0 + 16 <= ktot ? a.key_bytes + f.ko0 : safe;
+        uint4 cw;
+        __builtin_memcpy(&cw, cs, 16);
+        f.ck0 = (uint64_t)cw.x | (uint64_t)cw.y << 32;
+        f.ck1 = (uint64_t)cw.z | (uint64_t)cw.w << 32;
+        f.pk0 = f.pk1 = 0;
+    }
+    // lane 0's previous keys last: their branch joins after every other load is already in flight
+#pragma unroll
+    for (uint32_t r = 0; r < kFactsPerT; r++) {
+        FactsIn &f = in[r];
+        const uint64_t e = e0 + r * kFactsThreads;
+        if (lane == 0 && e > 0 && e < n && f.pko + 16 <= ktot) {
+            uint4 pw;
+            __builtin_memcpy(&pw, a.key_bytes + f.pko, 16);
+            f.pk0 = (uint64_t)pw.x | (uint64_t)pw.y << 32;
+            f.pk1 = (uint64_t)pw.z | (uint64_t)pw.w << 32;
+        }
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kFactsPerT; r++) {  // short keys at the very end of the batch
+        FactsIn &f = in[r];
+        const uint64_t e = e0 + r * kFactsThreads;
+        if (e < n && f.ko0 + 16 > ktot) {
             const uint64_t kl = f.ko1 - f.ko0;
             const uint32_t kn = (uint32_t)(kl < 16 ? kl : 16);
+            f.ck0 = f.ck1 = 0;
             if (kn) f.ck0 = load8(a.key_bytes + f.ko0, kn < 8 ? kn : 8);
             if (kn > 8) f.ck1 = load8(a.key_bytes + f.ko0 + 8, kn - 8);
-            if (lane == 0 && e > 0) {
-                const uint64_t pl = f.ko0 - f.pko;
-                const uint32_t pn = (uint32_t)(pl < 16 ? pl : 16);
-                if (pn) f.pk0 = load8(a.key_bytes + f.pko, pn < 8 ? pn : 8);
-                if (pn > 8) f.pk1 = load8(a.key_bytes + f.pko + 8, pn - 8);
-            }
+        }
+        if (lane == 0 && e > 0 && e < n && f.pko + 16 > ktot) {
+            const uint64_t pl = f.ko0 - f.pko;
+            const uint32_t pn = (uint32_t)(pl < 16 ? pl : 16);
+            f.pk0 = f.pk1 = 0;
+            if (pn) f.pk0 = load8(a.key_bytes + f.pko, pn < 8 ? pn : 8);
+            if (pn > 8) f.pk1 = load8(a.key_bytes + f.pko + 8, pn - 8);
         }
     }
     uint64_t rk = 0, rv = 0, c = 0;
