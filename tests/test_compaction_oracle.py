@@ -193,3 +193,14 @@ def test_compact_end_to_end_oracle():
                                             oracle.params(block_size=512), 1024)
     assert sm.status == 0 and len(ssts) == len(cuts) - 1 >= 2
     assert sum(s.summary.num_entries for s in ssts) == merged.n
+
+
+@pytest.mark.skipif(not os.path.exists("/root/reference/slatedb/src/retention_iterator.rs"),
+                    reason="reference sources not present (GPU box)")
+def test_retention_fixture_reproducible():
+    """tests/golden/retention_cases.json is what make_retention_cases.py extracts from the reference."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(HERE, "golden", "make_retention_cases.py"), "--check"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr + r.stdout
