@@ -292,15 +292,19 @@ sdb_status sdb_decode_blocks_ex(const uint8_t *arena, const uint64_t *block_star
 /* ---------------------------------------------------------------------------------------------
  * Compressed blocks (SsTableInfo.compression_format != None): the first half of decode_block
  * (format/sst.rs:980-999) — validate_checksum over the stored bytes, then SsTableFormat::decompress
- * (format/sst.rs:884-917) — on the device, for the LZ-family codecs:
+ * (format/sst.rs:884-917) — on the device, for every codec:
  *   SDB_CODEC_LZ4     lz4_flex 0.11.6 block::decompress_size_prepended (u32 LE size, then an LZ4 block;
  *                     output shorter than the declared size is kept, as lz4_flex truncates);
- *   SDB_CODEC_SNAPPY  snap 1.1.1 raw::Decoder::decompress_vec (varint size, then Snappy raw elements).
- * Zlib and Zstd return SDB_UNSUPPORTED.  Two steps, so the caller can size the output:
+ *   SDB_CODEC_SNAPPY  snap 1.1.1 raw::Decoder::decompress_vec (varint size, then Snappy raw elements);
+ *   SDB_CODEC_ZLIB    flate2 1.1.9 read::ZlibDecoder::read_to_end (zlib header, deflate, Adler-32; input
+ *                     that ends inside the stream yields the bytes decoded so far, as flate2's read does);
+ *   SDB_CODEC_ZSTD    zstd 0.13.3 stream::decode_all (zstd frames and skippable frames in sequence).
+ * Two steps, so the caller can size the output:
  *   1. sdb_decompress_plan writes out_start[0..nblocks] (device): block k's output slot starts at
- *      out_start[k] and holds its declared length + 4; out_start[nblocks] = the bytes `out` needs.  A
- *      header that cannot be read, or one declaring more than 64 MiB, gets an empty slot (that block
- *      then fails in step 2).
+ *      out_start[k] and holds its decompressed length + 4 (the declared length for Lz4 / Snappy; Zlib /
+ *      Zstd are decoded to count it, their Adler-32 / XXH64 checksums are verified in step 2);
+ *      out_start[nblocks] = the bytes `out` needs.  A header that cannot be read, a Zlib / Zstd stream
+ *      that fails to decode, or more than 64 MiB gets an empty slot (that block then fails in step 2).
  *   2. sdb_decompress_blocks fills out[out_start[k] .. out_end[k]) with the uncompressed block followed
  *      by the CRC32 (BE) of those bytes — Block::encode() ++ crc, so sdb_decode_blocks_at(out,
  *      out_start, out_end, ...) decodes the run (value references then point into `out`).  *err

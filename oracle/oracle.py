@@ -53,6 +53,7 @@ def _load():
                                             C.c_size_t, C.c_int, C.c_int64]),
         "orc_prefix_len": (C.c_int64, [C.c_uint32, C.c_uint32, V, C.c_size_t, C.c_int64]),
         "orc_decompressed_len": (C.c_int64, [C.c_uint32, V, C.c_size_t]),
+        "orc_xxh64": (C.c_uint64, [V, C.c_size_t, C.c_uint64]),
         "orc_decompress": (C.c_int, [C.c_uint32, V, C.c_size_t, V, C.c_size_t, P(C.c_size_t)]),
         "orc_decompress_blocks": (C.c_int, [C.c_uint32, V, V, C.c_uint64, V, C.c_uint64, V, V, P(C.c_uint64)]),
         "orc_merge_runs": (C.c_int, [P(_abi.Run), C.c_uint32, P(_abi.Retention), P(_abi.MergedOut)]),
@@ -422,13 +423,15 @@ def compact(runs, ret, prm, max_sst_size):
 
 
 # --- f3: block decompression (format/sst.rs:884-917) -----------------------------------------------
-CODEC_SNAPPY, CODEC_LZ4 = 1, 3  # CompressionFormat (schemas/sst.fbs)
+CODEC_SNAPPY, CODEC_ZLIB, CODEC_LZ4, CODEC_ZSTD = 1, 2, 3, 4  # CompressionFormat (schemas/sst.fbs)
 
 
 def decompress(codec, data):
     """SsTableFormat::decompress of one payload -> (status, bytes)."""
     b = np.frombuffer(bytes(data), np.uint8)
     n = lib().orc_decompressed_len(codec, b.ctypes.data if b.size else None, b.size)
+    if n < 0 and codec in (CODEC_ZLIB, CODEC_ZSTD):  # the length comes from decoding: it failed
+        return _abi.SDB_DECOMPRESSION_ERROR, b""
     cap = max(int(n), 0) + 1
     out = np.zeros(cap, np.uint8)
     ol = C.c_size_t(0)

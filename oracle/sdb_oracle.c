@@ -1662,7 +1662,13 @@ static int snappy_header(const uint8_t *in, size_t n, uint64_t *len, size_t *hdr
     return 0;
 }
 
+int64_t orc_entropy_len(uint32_t codec, const uint8_t *in, size_t n);
+sdb_status orc_entropy_decompress(uint32_t codec, const uint8_t *in, size_t n, uint8_t *out, size_t cap,
+                                  size_t *out_len);
+enum { ORC_CODEC_ZLIB = 2, ORC_CODEC_ZSTD = 4 };
+
 int64_t orc_decompressed_len(uint32_t codec, const uint8_t *in, size_t n) {
+    if (codec == ORC_CODEC_ZLIB || codec == ORC_CODEC_ZSTD) return orc_entropy_len(codec, in, n);  /* by decoding */
     if (codec == ORC_CODEC_LZ4) {  /* lz4_flex block::uncompressed_size: u32 little-endian prefix */
         if (n < 4) return -1;
         return (int64_t)((uint32_t)in[0] | (uint32_t)in[1] << 8 | (uint32_t)in[2] << 16 | (uint32_t)in[3] << 24);
@@ -1767,6 +1773,7 @@ static sdb_status snappy_raw(const uint8_t *in, size_t n, uint8_t *out, size_t l
 }
 
 sdb_status orc_decompress(uint32_t codec, const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len) {
+    if (codec == ORC_CODEC_ZLIB || codec == ORC_CODEC_ZSTD) return orc_entropy_decompress(codec, in, n, out, cap, out_len);
     const int64_t len = orc_decompressed_len(codec, in, n);
     if (codec != ORC_CODEC_LZ4 && codec != ORC_CODEC_SNAPPY) return SDB_UNSUPPORTED;
     if (len < 0) return SDB_DECOMPRESSION_ERROR;
@@ -1791,7 +1798,7 @@ static uint64_t dz_slot(uint32_t codec, const uint8_t *blocks, uint64_t s, uint6
 sdb_status orc_decompress_blocks(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
                                  uint8_t *out, uint64_t out_cap, uint64_t *out_start, uint64_t *out_end,
                                  uint64_t *first_err) {
-    if (codec != ORC_CODEC_LZ4 && codec != ORC_CODEC_SNAPPY) return SDB_UNSUPPORTED;
+    if (codec < ORC_CODEC_SNAPPY || codec > ORC_CODEC_ZSTD) return SDB_UNSUPPORTED;
     uint64_t pos = 0, ferr = ~0ull;
     for (uint64_t k = 0; k < nblocks; k++) {
         out_start[k] = pos;

@@ -366,7 +366,7 @@ def codec_bench(reps):
         del db, out
     data, block_off = np.concatenate(datas), np.concatenate(offs)
     nb = len(block_off) - 1
-    for codec, name in ((O.CODEC_LZ4, "lz4"), (O.CODEC_SNAPPY, "snappy")):
+    for codec, name in ((O.CODEC_LZ4, "lz4"), (O.CODEC_SNAPPY, "snappy"), (O.CODEC_ZLIB, "zlib"), (O.CODEC_ZSTD, "zstd")):
         comp, coff = compress_run(codec, data, block_off)
         dc = torch.from_numpy(comp).to(dev)
         do = torch.from_numpy(coff.view(np.int64)).to(dev)
@@ -384,6 +384,34 @@ def codec_bench(reps):
 
         with torch.cuda.stream(s):
             ms = timed(run, reps, s)
+        plan_ws = torch.empty(lib.sdb_decompress_workspace_bytes(nb), dtype=torch.uint8, device=dev)
+
+        def plan():  # the output plan (zlib / zstd decode to count)
+            if lib.sdb_decompress_plan(codec, dc.data_ptr(), do.data_ptr(), nb, start.data_ptr(), plan_ws.data_ptr(),
+                                       plan_ws.numel(), s.cuda_stream):
+                raise RuntimeError("sdb_decompress_plan")
+
+        with torch.cuda.stream(s):
+            ms_plan = timed(plan, max(3, reps // 4), s)
+        # CPU baselines on a bounded sample of the same blocks: the oracle (one thread), and for zlib /
+        # zstd the canonical C decoders of this image (Python's zlib, pyarrow's zstd) per block
+        ns = min(nb, 4000)
+        t0 = time.perf_counter()
+        rs = O.decompress_blocks(codec, comp[: int(coff[ns])], coff[: ns + 1])
+        cpu_s = time.perf_counter() - t0
+        cpu_bytes = int(rs.out_start[ns])
+        canon = None
+        if codec in (O.CODEC_ZLIB, O.CODEC_ZSTD):
+            import pyarrow as pa
+            zc = pa.Codec("zstd")
+            blk = [comp[int(coff[k]):int(coff[k + 1]) - 4].tobytes() for k in range(ns)]
+            t0 = time.perf_counter()
+            for k, x in enumerate(blk):
+                if codec == O.CODEC_ZLIB:
+                    __import__("zlib").decompress(x)
+                else:
+                    zc.decompress(x, decompressed_size=int(rs.out_start[k + 1] - rs.out_start[k]) - 4, asbytes=True)
+            canon = round(cpu_bytes / (time.perf_counter() - t0) / 2**30, 3)
         dout = runtime.DeviceDecodeOutput(nb, nent + 16, kbytes + 4096, device=dev)
 
         def dec():
@@ -394,7 +422,10 @@ def codec_bench(reps):
         print(json.dumps({"what": "f3 decompress (%s) of 4 D1 SSTs" % name, "blocks": nb, "compressed_bytes": int(comp.size),
                           "decompressed_bytes": total, "ratio": round(total / comp.size, 4), "ms": round(ms, 4),
                           "GiB_per_s_decompressed": round(total / (ms * 1e-3) / 2**30, 2),
-                          "decode_after_ms": round(ms_dec, 4), "bit_exact": bool(ok)}), flush=True)
+                          "plan_ms": round(ms_plan, 4), "decode_after_ms": round(ms_dec, 4), "bit_exact": bool(ok),
+                          "cpu_baseline": {"kind": "port", "GiB_per_s": round(cpu_bytes / cpu_s / 2**30, 3),
+                                           "cores": 1, "sample": "first %d blocks, oracle orc_decompress_blocks" % ns,
+                                           "canonical_lib_GiB_per_s_1_thread": canon}}), flush=True)
 
 
 def hbm_bench(reps):

@@ -429,11 +429,13 @@ sdb_status sdb_decode_blocks_at(const uint8_t *arena, const uint64_t *block_star
 
 uint64_t sdb_decompress_workspace_bytes(uint64_t nblocks) { return decompress_workspace_bytes(nblocks); }
 
-static bool lz_codec(uint32_t codec) { return codec == SDB_CODEC_LZ4 || codec == SDB_CODEC_SNAPPY; }
+static bool lz_codec(uint32_t codec) {  // every compressing codec of CompressionCodec (format/sst.rs:884-917)
+    return codec == SDB_CODEC_LZ4 || codec == SDB_CODEC_SNAPPY || codec == SDB_CODEC_ZLIB || codec == SDB_CODEC_ZSTD;
+}
 
 sdb_status sdb_decompress_plan(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
                                uint64_t *out_start, void *workspace, uint64_t workspace_bytes, void *stream) {
-    if (!lz_codec(codec)) return codec == SDB_CODEC_ZLIB || codec == SDB_CODEC_ZSTD ? SDB_UNSUPPORTED : SDB_INVALID_ARGUMENT;
+    if (!lz_codec(codec)) return SDB_INVALID_ARGUMENT;
     if (!out_start || (nblocks && (!blocks || !block_off))) return SDB_INVALID_ARGUMENT;
     if (!workspace || workspace_bytes < decompress_workspace_bytes(nblocks)) return SDB_INVALID_ARGUMENT;
     if (!device_ok()) return SDB_DEVICE_ERROR;
@@ -444,7 +446,7 @@ sdb_status sdb_decompress_plan(uint32_t codec, const uint8_t *blocks, const uint
 sdb_status sdb_decompress_blocks(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
                                  uint8_t *out, uint64_t out_cap, const uint64_t *out_start, uint64_t *out_end,
                                  uint64_t *err, void *stream) {
-    if (!lz_codec(codec)) return codec == SDB_CODEC_ZLIB || codec == SDB_CODEC_ZSTD ? SDB_UNSUPPORTED : SDB_INVALID_ARGUMENT;
+    if (!lz_codec(codec)) return SDB_INVALID_ARGUMENT;
     if (!err || !out_start || (nblocks && (!blocks || !block_off || !out_end || (out_cap && !out)))) return SDB_INVALID_ARGUMENT;
     if (!device_ok()) return SDB_DEVICE_ERROR;
     return launch_decompress_run(codec, blocks, block_off, nblocks, out, out_cap, out_start, out_end,

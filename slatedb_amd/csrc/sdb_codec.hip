@@ -7,7 +7,7 @@
 //                               u32 little-endian uncompressed size, then one LZ4 block;
 //   CompressionFormat::Snappy = snap 1.1.1 raw::Decoder::decompress_vec (Cargo.lock:3406): varint
 //                               uncompressed size, then Snappy raw elements.
-// Zlib / Zstd (entropy-coded) return SDB_UNSUPPORTED.  Every output block is re-framed as
+// Zlib / Zstd (entropy-coded) run in sdb_codec_ent.hip.  Every output block is re-framed as
 // Block::encode() ++ CRC32 BE of those bytes, so the output is a plain uncompressed block run that
 // sdb_decode_blocks_at decodes unchanged (values then reference the decompressed arena).
 //
@@ -456,6 +456,14 @@ uint64_t decompress_workspace_bytes(uint64_t nblocks) {
 
 static std::once_flag g_dz_once;
 
+// entropy-coded codecs (sdb_codec_ent.hip)
+hipError_t launch_ent_slots(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                            uint64_t *slot, hipStream_t st);
+hipError_t launch_ent_run(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks, uint8_t *out,
+                          uint64_t out_cap, const uint64_t *out_start, uint64_t *out_end, unsigned long long *err,
+                          hipStream_t st);
+static bool ent_codec(uint32_t codec) { return codec == SDB_CODEC_ZLIB || codec == SDB_CODEC_ZSTD; }
+
 hipError_t launch_decompress_plan(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
                                   uint64_t *out_start, void *ws, hipStream_t st) {
     uint8_t *w = (uint8_t *)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
@@ -468,7 +476,12 @@ hipError_t launch_decompress_plan(uint32_t codec, const uint8_t *blocks, const u
     a.slot = (uint64_t *)w;
     uint64_t *scratch = a.slot + (nblocks + 2);
     uint64_t *tx = scratch + (nblocks + 2), *ty = tx + (nt + 1);
-    hipLaunchKernelGGL(k_dz_plan, dim3((uint32_t)((nblocks + 256) / 256)), dim3(256), 0, st, a);
+    if (ent_codec(codec)) {
+        const hipError_t e = launch_ent_slots(codec, blocks, block_off, nblocks, a.slot, st);
+        if (e != hipSuccess) return e;
+    } else {
+        hipLaunchKernelGGL(k_dz_plan, dim3((uint32_t)((nblocks + 256) / 256)), dim3(256), 0, st, a);
+    }
     return launch_excl_scan2(a.slot, a.slot, nblocks, tx, ty, out_start, scratch, st);
 }
 
@@ -490,6 +503,7 @@ hipError_t launch_decompress_run(uint32_t codec, const uint8_t *blocks, const ui
     a.out_end = out_end;
     a.err = err;
     hipLaunchKernelGGL(k_dz_init, dim3(1), dim3(64), 0, st, err);
+    if (ent_codec(codec)) return launch_ent_run(codec, blocks, block_off, nblocks, out, out_cap, out_start, out_end, err, st);
     if (nblocks) {
         int dev = 0, cus = 0;
         (void)hipGetDevice(&dev);

@@ -11,7 +11,7 @@ from .codec_util import compress_run, frame
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
-CODECS = [O.CODEC_LZ4, O.CODEC_SNAPPY]
+CODECS = [O.CODEC_LZ4, O.CODEC_SNAPPY, O.CODEC_ZLIB, O.CODEC_ZSTD]
 
 
 def _dev(a, dt=None):
@@ -96,12 +96,60 @@ def test_device_errors_match_oracle(codec):
     c3 = np.frombuffer(b"".join(parts), np.uint8).copy()
     o3 = np.cumsum([0] + [len(x) for x in parts]).astype(np.uint64)
     _, _, _, err = _check(codec, c3, o3)
-    assert err == (1 << 8) | _abi.SDB_DECOMPRESSION_ERROR
+    if codec == O.CODEC_ZLIB:  # flate2's read_to_end keeps what a cut stream decodes to (no error)
+        assert err == 2**64 - 1
+    else:
+        assert err == (1 << 8) | _abi.SDB_DECOMPRESSION_ERROR
 
 
-def test_unsupported_codecs():
+def test_unknown_codec():
     lib = runtime.lib()
     z = torch.zeros(64, dtype=torch.uint8, device="cuda")
-    for c in (_abi.CODEC_ZLIB, _abi.CODEC_ZSTD):
+    for c in (0, 5):
         assert lib.sdb_decompress_plan(c, z.data_ptr(), z.data_ptr(), 0, z.data_ptr(), z.data_ptr(), 64, None) == \
-            _abi.SDB_UNSUPPORTED
+            _abi.SDB_INVALID_ARGUMENT
+
+
+def _raw_run(codec, payloads):
+    """Arbitrary payloads (not SST blocks) framed with the CRC, as a block run."""
+    parts = [frame(p) for p in payloads]
+    return (np.frombuffer(b"".join(parts), np.uint8).copy(),
+            np.cumsum([0] + [len(x) for x in parts]).astype(np.uint64))
+
+
+def test_entropy_codecs_levels_and_frames():
+    """zlib at every level / window and strategy, zstd at negative to high levels, multi-block zstd frames
+    (repeat tables, treeless literals), hand-built frames (raw / RLE blocks, checksum, skippable and
+    concatenated frames) and error streams: device == oracle, and the decoded bytes == the input."""
+    import struct
+    import zlib
+    from .test_codec_entropy import frame as zframe, payloads, zstd_compress
+    ps = payloads()
+    rng = np.random.default_rng(3)
+    words = [bytes(rng.integers(97, 123, rng.integers(2, 9), dtype=np.uint8)) for _ in range(300)]
+    big = b" ".join(words[i] for i in rng.integers(0, 300, 60000))  # ~300 KiB: three zstd blocks
+    zl = []
+    for i, p in enumerate(ps + [big]):
+        c = zlib.compressobj([0, 1, 6, 9][i % 4], zlib.DEFLATED, [9, 12, 15][i % 3], 8,
+                             [zlib.Z_DEFAULT_STRATEGY, zlib.Z_FIXED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE][i % 4])
+        zl.append(c.compress(p) + c.flush())
+    zl.append(zlib.compress(ps[8])[:-9])                # cut stream: the bytes decoded so far
+    bad = bytearray(zlib.compress(ps[8]))
+    bad[-1] ^= 1
+    zl.append(bytes(bad))                               # Adler-32 mismatch
+    comp, coff = _raw_run(O.CODEC_ZLIB, zl)
+    out, start, end, err = _check(O.CODEC_ZLIB, comp, coff)
+    assert err == ((len(zl) - 1) << 8) | _abi.SDB_DECOMPRESSION_ERROR
+    for k, p in enumerate(ps + [big]):
+        assert out[int(start[k]):int(end[k]) - 4].tobytes() == p, k
+    zs = [zstd_compress(p, [-5, 1, 3, 9, 19][i % 5]) for i, p in enumerate(ps)]
+    zs += [zstd_compress(big, 1), zstd_compress(big, 12)]
+    f = zframe([(0, b"hello world", b"hello world"), (1, bytes([0x41, 200]), b"A" * 200)], checksum=True)
+    skip = struct.pack("<II", 0x184D2A53, 5) + b"12345"
+    zs += [f, skip + zs[8] + f + skip, zs[8][:-3]]
+    comp, coff = _raw_run(O.CODEC_ZSTD, zs)
+    out, start, end, err = _check(O.CODEC_ZSTD, comp, coff)
+    assert err == ((len(zs) - 1) << 8) | _abi.SDB_DECOMPRESSION_ERROR
+    want = ps + [big, big, b"hello world" + b"A" * 200, ps[8] + b"hello world" + b"A" * 200]
+    for k, p in enumerate(want):
+        assert out[int(start[k]):int(end[k]) - 4].tobytes() == p, k
