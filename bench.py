@@ -37,7 +37,8 @@ sys.path.insert(0, ROOT)
 from slatedb_amd import _abi, datasets, job, runtime  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s); the box's STREAM copy: DESIGN.md §5
-PMC_FILE = "r2_pmc_traffic.json"
+PMC_FILES = ("r3_pmc_traffic.json", "r2_pmc_traffic.json")  # newest first
+PMC_FILE = PMC_FILES[0]
 
 
 def parse():
@@ -178,14 +179,18 @@ def cpu_baseline(budget_s, threads):
 
 def pmc_traffic():
     """HBM bytes per SST of the encode from the committed PMC passes over this same bench command
-    (profiles/r2_pmc_traffic.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes, corrected per
+    (profiles/r3_pmc_traffic.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes, corrected per
     MI355X_MICROARCH.md, written by scripts/collect_profiles.py).  PMC counters are collected in
     their own rocprofv3 runs, never inside the timed region."""
-    try:
-        d = json.load(open(os.path.join(ROOT, "profiles", PMC_FILE)))
-        return d.get("per_sst_bytes"), d.get("per_kernel", {})
-    except (OSError, KeyError, ValueError):
-        return None, {}
+    global PMC_FILE
+    for f in PMC_FILES:
+        try:
+            d = json.load(open(os.path.join(ROOT, "profiles", f)))
+            PMC_FILE = f
+            return d.get("per_sst_bytes"), d.get("per_kernel", {})
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, {}
 
 
 def main():

@@ -330,11 +330,24 @@ def compact_bench(reps):
         walls.append((time.perf_counter() - t0) * 1e3)
         assert st == 0
     ms = float(np.median(walls))
+    # CPU baseline: the oracle's merge + retention + cuts + encode of the same job, one thread
+    from oracle import oracle as O
+    runs = [Run.from_batch(hh) for hh in hosts]
+    oret = O.retention(min_seq=0)
+    t0 = time.perf_counter()
+    _, osm, ocuts, ossts = O.compact(runs, oret, O.params(block_size=4096, sst_version=2, bloom_bits_per_key=10),
+                                     256 << 20)
+    cpu_s = time.perf_counter() - t0
     merged, msum = comp.merged()
+    same = len(ossts) == ns and all(np.array_equal(comp.sst(i)["data"], ossts[i].data) for i in range(ns))
     print(json.dumps({"what": "compaction job (f2): 4 x configs[1] L0 SSTs -> merge + retention + cuts + encode",
                       "entries_in": int(msum.num_in), "entries_out": int(msum.num_out), "output_ssts": ns,
                       "logical_bytes_in": logical, "ms_wall": round(ms, 3),
-                      "GiB_per_s_logical": round(logical / (ms * 1e-3) / 2**30, 2)}), flush=True)
+                      "GiB_per_s_logical": round(logical / (ms * 1e-3) / 2**30, 2), "bit_exact_vs_oracle": bool(same),
+                      "cpu_baseline": {"kind": "port", "cores": 1, "s": round(cpu_s, 3),
+                                       "GiB_per_s_logical": round(logical / cpu_s / 2**30, 3),
+                                       "sample": "the whole job, oracle compact (merge + retention + cuts + encode)"}}),
+          flush=True)
     comp.close()
 
 
@@ -428,6 +441,53 @@ def codec_bench(reps):
                                            "canonical_lib_GiB_per_s_1_thread": canon}}), flush=True)
 
 
+def lookup_bench(reps):
+    """Point lookups (sdb_sst_lookup: bloom -> index partition -> block CRC -> restart search -> seek) of
+    1 M keys into one D1 SST (configs[1] shape): half present, half absent (bloom-filtered or seeking past),
+    device-resident, HIP events; the oracle on a bounded sample as the CPU baseline."""
+    from oracle import oracle as O
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(device=dev)
+    h = datasets.d1(sst_index=5)
+    enc = O.encode_sst(h, O.params(block_size=4096, sst_version=2, bloom_bits_per_key=10))
+    ik, iko = O.sst_index_keys(h, enc)
+    rng = np.random.default_rng(17)
+    nq = 1 << 20
+    pick = rng.integers(0, h.n, nq)
+    kb = np.empty(nq * 16, np.uint8)
+    for q in range(nq):  # present keys, and the same keys with the last byte flipped (absent)
+        k0 = int(h.key_off[pick[q]])
+        kb[16 * q:16 * q + 16] = h.key_bytes[k0:k0 + 16]
+    kb[16 * np.arange(1, nq, 2) + 15] ^= 0xA5
+    koff = (np.arange(nq + 1, dtype=np.uint64) * np.uint64(16))
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64) if a.dtype == np.uint64 else a).to(dev)
+    vt = {"data": t(enc.data), "block_off": t(enc.block_off), "num_blocks": len(enc.block_off) - 1,
+          "index_keys": t(ik), "index_key_off": t(iko), "sst_version": 2, "bloom": t(enc.bloom),
+          "bloom_len": len(enc.bloom), "num_probes": O.optimal_num_probes(10)}
+    dk, do = t(kb), t(koff)
+    with torch.cuda.stream(s):
+        res = runtime.sst_lookup_device(vt, dk, do, nq, stream=s)
+    torch.cuda.synchronize()
+    ns = 20000
+    keys = [kb[16 * q:16 * q + 16].tobytes() for q in range(ns)]
+    t0 = time.perf_counter()
+    ref = O.sst_lookup(enc.data, enc.block_off, ik, iko, keys, bloom=enc.bloom, num_probes=O.optimal_num_probes(10))
+    cpu_s = time.perf_counter() - t0
+    ok = all(np.array_equal(res[f][:ns].cpu().numpy().astype(np.int64), getattr(ref, f).astype(np.int64))
+             for f in ("state", "block", "entry", "val_off", "seq"))
+
+    def run():
+        runtime.sst_lookup_device(vt, dk, do, nq, stream=s)
+
+    with torch.cuda.stream(s):
+        ms = timed(run, reps, s)
+    print(json.dumps({"what": "point lookups into one D1 SST (bloom, index, CRC, restart search, seek)",
+                      "keys": nq, "present_fraction": 0.5, "ms": round(ms, 4),
+                      "Mlookups_per_s": round(nq / (ms * 1e-3) / 1e6, 1), "matches_oracle_on_sample": bool(ok),
+                      "cpu_baseline": {"kind": "port", "cores": 1, "Mlookups_per_s": round(ns / cpu_s / 1e6, 3),
+                                       "sample": "first %d of the same keys, oracle orc_sst_lookup" % ns}}), flush=True)
+
+
 def hbm_bench(reps):
     """STREAM-like: torch's copy kernel over 4 GiB (read + write) and a read-only int64 sum."""
     dev = torch.device("cuda", 0)
@@ -455,11 +515,12 @@ def main():
     p.add_argument("--compact", action="store_true")
     p.add_argument("--hbm", action="store_true")
     p.add_argument("--codec", action="store_true")
+    p.add_argument("--lookup", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="decode CPU baseline budget (0: skip)")
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--no-granular", action="store_true", help="decode: skip the 2 MiB granularity run")
     a = p.parse_args()
-    allp = not (a.decode or a.bloom or a.e2e or a.compact or a.hbm or a.codec)
+    allp = not (a.decode or a.bloom or a.e2e or a.compact or a.hbm or a.codec or a.lookup)
     torch.cuda.set_device(0)
     runtime.require_device()
     if a.bloom or allp:
@@ -474,6 +535,8 @@ def main():
         codec_bench(max(3, a.reps // 2))
     if a.compact or allp:
         compact_bench(max(3, a.reps // 4))
+    if a.lookup or allp:
+        lookup_bench(a.reps)
 
 
 if __name__ == "__main__":

@@ -35,9 +35,11 @@ def one(pattern):
     return m[0]
 
 
-def pmc(counter):
+def pmc(pass_name):
+    """Per-kernel mean of the counter of pass rp/pmc_<pass_name> (FETCH_SIZE or WRITE_SIZE)."""
+    counter = pass_name.split("_", 1)[1] if pass_name.startswith(("bloom_", "compact_", "dec_")) else pass_name
     acc = collections.defaultdict(list)
-    for r in csv.DictReader(open(one("pmc_%s/**/run_counter_collection.csv" % counter))):
+    for r in csv.DictReader(open(one("pmc_%s/**/run_counter_collection.csv" % pass_name))):
         if r["Counter_Name"] == counter:
             acc[kname(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}
@@ -47,12 +49,25 @@ def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
     shutil.copy(one("bench.json"), os.path.join(PROF, tag + "_bench.json"))
     shutil.copy(one("configs.jsonl"), os.path.join(PROF, tag + "_configs.jsonl"))
-    shutil.copy(one("enc/**/run_kernel_stats.csv"), os.path.join(PROF, tag + "_encode_kernel_stats.csv"))
-    shutil.copy(one("dec/**/run_kernel_stats.csv"), os.path.join(PROF, tag + "_decode_kernel_stats.csv"))
-    for what in ("enc", "dec"):
-        f = os.path.join(RP, "sq_%s" % what, "summary.txt")
+    for d, name in (("enc", "encode"), ("dec", "decode"), ("bloom", "bloom"), ("compact", "compact"),
+                    ("codec", "codec"), ("lookup", "lookup")):
+        m = glob.glob(os.path.join(RP, d, "**", "run_kernel_stats.csv"), recursive=True)
+        if m:
+            shutil.copy(m[0], os.path.join(PROF, "%s_%s_kernel_stats.csv" % (tag, name)))
+    for what, name in (("enc", "encode"), ("dec", "decode")):
+        f = os.path.join(RP, "sq_%s_summary.txt" % what)
         if os.path.exists(f):
-            shutil.copy(f, os.path.join(PROF, "%s_pmc_sq_%s.txt" % (tag, {"enc": "encode", "dec": "decode"}[what])))
+            shutil.copy(f, os.path.join(PROF, "%s_pmc_sq_%s.txt" % (tag, name)))
+    # HBM bytes per dispatch of the bloom, compaction and decode kernels (same corrections)
+    extra = {}
+    for n in ("bloom", "compact", "dec"):
+        fe, wr = pmc(n + "_FETCH_SIZE"), pmc(n + "_WRITE_SIZE")
+        extra[n] = {k: {"read_bytes": round(2048.0 * fe.get(k, 0.0)), "write_bytes": round(1024.0 * wr.get(k, 0.0))}
+                    for k in sorted(set(fe) | set(wr)) if k.startswith("k_")}
+    json.dump({"correction": "read_bytes = 2 * 1024 * FETCH_SIZE; write_bytes = 1024 * WRITE_SIZE (per dispatch)",
+               "commands": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) -- "
+                           "python3 scripts/bench_configs.py --bloom | --compact | --decode --reps 3",
+               "per_dispatch": extra}, open(os.path.join(PROF, tag + "_pmc_traffic_configs.json"), "w"), indent=1)
     fetch, write = pmc("FETCH_SIZE"), pmc("WRITE_SIZE")
     batch = json.load(open(one("bench.json")))["config"]["ssts_per_gpu_per_step"]
     out = {"command": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes) -- "

@@ -59,6 +59,7 @@ struct EntLds {  // one wave's tables (zlib uses the first three Canon, aliasing
         struct {
             Canon lit, dist, clc;
             uint8_t lens[320];
+            uint16_t fast_lit[512], fast_dist[512];  // 9-bit lookup: sym | len << 12 (len 0: longer code)
         } z;
         struct {
             FseCell ll[512], of[256], ml[512], wt[64];  // wt: the Huffman weights' table (accuracy <= 6)
@@ -98,12 +99,22 @@ struct LsbBits {
     uint64_t n, pos;
     uint64_t buf;
     int cnt;
-    SDB_DEV bool get(int k, uint32_t &v) {  // k <= 16; false when the input ends first
-        while (cnt < k) {
-            if (pos >= n) return false;
+    SDB_DEV void refill() {  // up to 32 more bits: one unaligned dword load when 4 bytes remain
+        if (cnt <= 32 && pos + 4 <= n) {
+            uint32_t w;
+            __builtin_memcpy(&w, p + pos, 4);
+            buf |= (uint64_t)w << cnt;
+            cnt += 32;
+            pos += 4;
+        }
+        while (cnt <= 56 && pos < n) {
             buf |= (uint64_t)p[pos++] << cnt;
             cnt += 8;
         }
+    }
+    SDB_DEV bool get(int k, uint32_t &v) {  // k <= 16; false when the input ends first
+        if (cnt < k) refill();
+        if (cnt < k) return false;
         v = (uint32_t)(buf & ((1ull << k) - 1));
         buf >>= k;
         cnt -= k;
@@ -132,6 +143,22 @@ SDB_DEV int canon_build(Canon &h, const uint8_t *len, int n) {
     for (int s = 0; s < n; s++)
         if (len[s]) h.sym[offs[len[s]]++] = (uint16_t)s;
     return 0;
+}
+
+// the 9-bit fast table of a usable code: every code of <= 9 bits, bit-reversed (deflate sends a code's
+// bits most significant first into an LSB-first stream), replicated over the bits that follow it
+SDB_DEV void canon_fast(const Canon &h, uint16_t *fast) {
+    for (int i = 0; i < 512; i++) fast[i] = 0;
+    int code = 0, index = 0;
+    for (int l = 1; l <= 9; l++) {
+        for (int c = 0; c < h.count[l]; c++, code++, index++) {
+            int r = 0;
+            for (int b = 0; b < l; b++) r |= ((code >> b) & 1) << (l - 1 - b);
+            const uint16_t e = (uint16_t)(h.sym[index] | l << 12);
+            for (int j = r; j < 512; j += 1 << l) fast[j] = e;
+        }
+        code <<= 1;
+    }
 }
 
 // -1 input ended, -2 invalid code
@@ -230,8 +257,22 @@ SDB_DEV int inflate_raw(LsbBits &s, EntOut &o, EntLds &t) {
             for (int q = ndist - 1; q >= 0; q--) lens[288 + q] = lens[nlen + q];
         }
         if (canon_build(t.z.lit, lens, nlen) || canon_build(t.z.dist, lens + 288, ndist)) return kZErr;
+        canon_fast(t.z.lit, t.z.fast_lit);
+        canon_fast(t.z.dist, t.z.fast_dist);
+        // a symbol through the fast table when its code is <= 9 bits and the bits are there
+        auto fast_decode = [&](const uint16_t *fast, const Canon &h) -> int {
+            if (s.cnt < 9) s.refill();
+            const uint16_t e = fast[s.buf & 511];
+            const int L = e >> 12;
+            if (L && L <= s.cnt) {
+                s.buf >>= L;
+                s.cnt -= L;
+                return e & 0xFFF;
+            }
+            return canon_decode(s, h);
+        };
         for (;;) {
-            int sym = canon_decode(s, t.z.lit);
+            int sym = fast_decode(t.z.fast_lit, t.z.lit);
             if (sym == -1) return kZTrunc;
             if (sym < 0) return kZErr;
             if (sym < 256) {
@@ -244,7 +285,7 @@ SDB_DEV int inflate_raw(LsbBits &s, EntOut &o, EntLds &t) {
             uint32_t v;
             if (!s.get(c_len_extra[sym], v)) return kZTrunc;
             const uint32_t len = c_len_base[sym] + v;
-            const int ds = canon_decode(s, t.z.dist);
+            const int ds = fast_decode(t.z.fast_dist, t.z.dist);
             if (ds == -1) return kZTrunc;
             if (ds < 0 || ds >= 30) return kZErr;
             if (!s.get(c_dist_extra[ds], v)) return kZTrunc;

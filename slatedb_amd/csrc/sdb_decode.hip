@@ -333,10 +333,16 @@ SDB_DEV BlockView load_block(const DecodeArgs &a, uint64_t k, uint8_t *stage, co
         for (uint64_t w = 0; w < nwin; w++) {
             uint64_t wbeg = (w == 0) ? 0 : first + ((w - 1) << 12);
             uint32_t wlen = (uint32_t)((w == 0) ? first : 4096);
-            // the init fold inverts message bytes [0, 4), which may straddle the first two windows
-            for (uint32_t q = lane_id(); q < wlen; q += 64) stage[16 + q] = g[wbeg + q] ^ (wbeg + q < 4 ? 0xFF : 0);
+            // the window's 16-byte granules (one load each, all in flight), window byte 0 at stage[gp]
+            const uint64_t ga = (s + wbeg) & ~15ull;
+            const uint32_t gp = (uint32_t)((s + wbeg) & 15), ng = (gp + wlen + 15) >> 4;
+            const uint4 *src = (const uint4 *)(a.blocks + ga);
+            for (uint32_t q = lane_id(); q < ng; q += 64) ((uint4 *)stage)[q] = src[q];
             wave_sync_d();
-            uint32_t raw = wave_crc_raw_lds(stage + 16, wlen, crc, false);
+            // crc32fast's init folded into message bytes [0, 4), which may straddle the first two windows
+            if (lane_id() < 4 && wbeg + lane_id() < 4 && lane_id() < wlen) stage[gp + lane_id()] ^= 0xFF;
+            wave_sync_d();
+            uint32_t raw = wave_crc_raw_lds(stage + gp, wlen, crc, false);
             acc = (w == 0) ? raw : (gf_mul(c_shift.window, acc) ^ raw);
             wave_sync_d();
         }
@@ -824,6 +830,88 @@ SDB_DEV void desc_rule(uint32_t restarts, Tally &t) {
     }
 }
 
+// --- blocks over one wave image (SstBlockSize 8 - 64 KiB): restart-region pieces --------------------
+// A regular V2 block is cut into pieces of consecutive restart regions (<= 64 regions, <= kPieceBytes
+// bytes): each piece is staged in the wave's LDS image (16-byte granules) with its region offsets
+// rebased into a small big-endian table after the data, and parsed there by the same LDS walks as a
+// small block.  Region boundaries reset the key prefix (shared == 0), so pieces are independent.  Not
+// applicable (nothing staged, false): the first region does not start at 0, or a region is longer than
+// a piece; the caller then walks the block from HBM as before.
+constexpr uint32_t kPieceBytes = 3968, kPieceOffs = 4000;  // piece data in img[0, 3999], offsets at 4000
+static_assert(kPieceOffs + 128 <= kDecImg && 15 + kPieceBytes + 16 <= kPieceOffs, "piece layout");
+SDB_DEV uint32_t region_off(const BlockView &v, uint32_t q) { return (uint32_t)rd_be(v.offs + 2 * q, 2); }
+template <typename F>
+SDB_DEV bool for_each_piece(const DecodeArgs &a, uint64_t s, const BlockView &v, lu8 *img, F f) {
+    const uint32_t l = (uint32_t)lane_id(), R = v.count;
+    if (R == 0 || region_off(v, 0) != 0) return false;
+    for (uint32_t q0 = 0; q0 < R; q0 += 64) {
+        const uint32_t q = q0 + l;
+        const uint32_t lo = q < R ? region_off(v, q) : 0, hi = q < R ? (q + 1 < R ? region_off(v, q + 1) : v.data_end) : 0;
+        if (__ballot(q < R && (hi < lo || hi - lo > kPieceBytes)) != 0) return false;
+    }
+    for (uint32_t qa = 0; qa < R;) {
+        const uint32_t q = qa + l;
+        const uint32_t base = region_off(v, qa);
+        const uint32_t lo = q < R ? region_off(v, q) : 0, hi = q < R ? (q + 1 < R ? region_off(v, q + 1) : v.data_end) : 0;
+        const uint64_t fit = __ballot(q < R && hi >= base && hi - base <= kPieceBytes);
+        const uint32_t m = fit == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~fit);  // regions qa .. qa + m - 1
+        const uint32_t pb = (uint32_t)__builtin_amdgcn_readlane((int)hi, (int)(m - 1));
+        const uint64_t g0 = s + base, ga = g0 & ~15ull;
+        const uint32_t p0 = (uint32_t)(g0 & 15), ng = (p0 + (pb - base) + 15) >> 4;
+        const uint4 *src = (const uint4 *)(a.blocks + ga);
+        for (uint32_t x = l; x < ng; x += 64) {
+            const uint4 w4 = src[x];
+            u32x4 w;
+            w.x = w4.x;
+            w.y = w4.y;
+            w.z = w4.z;
+            w.w = w4.w;
+            ((lu128 *)img)[x] = w;
+        }
+        if (l < m) {
+            const uint32_t r = lo - base;
+            img[kPieceOffs + 2 * l] = (uint8_t)(r >> 8);
+            img[kPieceOffs + 2 * l + 1] = (uint8_t)r;
+        }
+        wave_sync_d();
+        LdsBlockView pv{};
+        pv.d = img + p0;
+        pv.data_end = pb - base;
+        pv.count = m;
+        pv.offs = img + kPieceOffs;
+        pv.status = 0;
+        if (!f(pv, base)) return true;  // the callback stops the walk
+        wave_sync_d();
+        qa += m;
+    }
+    return true;
+}
+
+// Count pass of a big V2 block by pieces: false when not applicable or when a piece is irregular (the
+// whole-block walk then decides, exactly as before).
+SDB_DEV bool tally_v2_pieces(const DecodeArgs &a, uint64_t s, const BlockView &v, lu8 *img, Tally &t) {
+    Tally acc{0, 0, 0, false};
+    bool irregular = false;
+    const bool ok = for_each_piece(a, s, v, img, [&](const LdsBlockView &pv, uint32_t) {
+        const Tally pt = tally_v2(pv);
+        if (pt.sequential) {
+            irregular = true;
+            return false;
+        }
+        if (pt.status) {  // the first failing region in block order; later pieces must still be regular
+            if (!acc.status) acc.status = pt.status;
+        } else if (!acc.status) {
+            acc.entries += pt.entries;
+            acc.key_bytes += pt.key_bytes;
+        }
+        return true;
+    });
+    if (!ok || irregular) return false;
+    t = acc;
+    if (t.status) t.entries = t.key_bytes = 0;
+    return true;
+}
+
 // D1 count.  LDS: the CRC tables at address 0 (sdb_crc.h: this kernel has no static LDS), then one
 // region of kDecWaveLds per wave.
 __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
@@ -881,7 +969,10 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
         } else {
             const BlockView v = load_block(a, k, stage, crc, kDecImg);
             t.status = v.status;
-            if (!v.status) t = (a.version == 2) ? tally_v2(v) : tally_v1(v);
+            if (!v.status) {
+                if (a.version == 1) t = tally_v1(v);
+                else if (!tally_v2_pieces(a, s, v, img, t)) t = tally_v2(v);
+            }
             if (!v.status && a.descending && a.version == 2) desc_rule(v.count, t);
         }
         if (lane_id() == 0) {
@@ -1209,6 +1300,25 @@ SDB_DEV void emit_v1(const DecodeArgs &a, const BlockViewT<P> &v, uint64_t ent0,
     }
 }
 
+// Emit pass of a regular big V2 block by pieces (the count pass accepted it as regular): keys restored
+// in LDS when a piece's keys fit, else straight into the arena.
+SDB_DEV bool emit_v2_pieces(const DecodeArgs &a, uint64_t s, const BlockView &v, lu8 *img, lu8 *kbuf, uint64_t ent0,
+                            uint64_t kb0) {
+    uint64_t ent = ent0, kb = kb0;
+    return for_each_piece(a, s, v, img, [&](const LdsBlockView &pv, uint32_t base) {
+        const Tally pt = tally_v2(pv);
+        const bool lds_keys = pt.key_bytes + 16 <= kDecKeys;
+        emit_v2(a, pv, false, ent, kb, s + base, lds_keys ? kbuf : nullptr);
+        if (lds_keys) {
+            wave_sync_d();
+            wave_store_bytes(a.out.key_arena + kb, kbuf, pt.key_bytes);
+        }
+        ent += pt.entries;
+        kb += pt.key_bytes;
+        return true;
+    });
+}
+
 SDB_DEV void dec_finish(const DecodeArgs &a) {
     sdb_decode_summary *s = a.out.summary;
     const uint64_t ne = a.ent_start[a.nblocks], kb = a.key_start[a.nblocks];
@@ -1373,7 +1483,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
             const BlockView v = load_block(a, k, stage, crc, kDecCap, false);
             if (v.status) continue;
             if (a.version == 1) emit_v1(a, v, ent0, kb0, s);
-            else emit_v2(a, v, seq, ent0, kb0, s, nullptr);
+            else if (seq || !emit_v2_pieces(a, s, v, img, kbuf, ent0, kb0)) emit_v2(a, v, seq, ent0, kb0, s, nullptr);
         }
         wave_sync_d();
     }

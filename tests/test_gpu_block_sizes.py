@@ -54,3 +54,56 @@ def test_blocks_with_rows_too_large_for_a_piece(rt):  # noqa: F811
     b = Batch.from_entries(ents)
     ref, got = encode_both(rt, b, block_size=16384, sst_version=2, bloom_bits_per_key=10)
     assert_same(ref, got, "huge rows")
+
+
+# ------------------------------------------------------------------------------------------------
+# decode of blocks over one wave image: restart-region pieces staged in LDS (sdb_decode.hip
+# for_each_piece), and the HBM walk for blocks a piece cannot hold
+# ------------------------------------------------------------------------------------------------
+def _decode_cases():
+    rng = np.random.default_rng(21)
+    small_rows = Batch.from_entries([(b"key%012d" % i, 0, bytes(rng.integers(0, 256, 20, dtype=np.uint8)), 9000 - i,
+                                      None, None) for i in range(9000)])
+    big_rows = Batch.from_entries([(b"row%08d" % i, 0, bytes(rng.integers(0, 256, 5000 if i % 97 == 5 else
+                                                                      int(rng.integers(10, 200)), dtype=np.uint8)),
+                                    1, None, None) for i in range(3000)])
+    return [("d1", datasets.d1(n=120000, sst_index=3), {}), ("d3", datasets.d3(n=6000), {}),
+            ("tiny-ri1", small_rows, {"restart_interval": 1}), ("tiny-ri3", small_rows, {"restart_interval": 3}),
+            ("huge-rows", big_rows, {})]
+
+
+@pytest.mark.parametrize("block_size", [8192, 16384, 65536])
+def test_decode_large_blocks(rt, block_size):  # noqa: F811
+    from .test_descending import device_desc
+    from .test_gpu_parity import assert_decode_same
+    for name, b, kw in _decode_cases():
+        e = O.encode_sst(b, O.params(block_size=block_size, **kw))
+        ref = O.decode_blocks(e.data, e.block_off, 2)
+        assert ref.status == 0
+        got = rt.Decoder().decode(e.data, e.block_off, 2)
+        assert_decode_same(ref, got, "%s bs=%d" % (name, block_size))
+        assert np.array_equal(got.key_arena, b.key_bytes)
+        desc = O.decode_blocks(e.data, e.block_off, 2, descending=True)
+        assert_decode_same(desc, device_desc(rt, e.data, e.block_off, 2), "%s desc bs=%d" % (name, block_size))
+
+
+def test_decode_large_blocks_corrupt(rt):  # noqa: F811
+    """Corruption inside big blocks: a CRC mismatch, and a row whose varint header runs past its region
+    with the CRC recomputed (the piece walk must report what the whole-block walk reports)."""
+    import struct
+    import zlib
+    from .test_gpu_parity import assert_decode_same
+    b = datasets.d1(n=40000, sst_index=4)
+    e = O.encode_sst(b, O.params(block_size=16384))
+    data = e.data.copy()
+    data[int(e.block_off[3]) + 1000] ^= 0x10  # CRC mismatch in block 3
+    k = 7
+    s, t = int(e.block_off[k]), int(e.block_off[k + 1])
+    blk = bytearray(data[s:t - 4].tobytes())
+    blk[200] = 0xFF  # a byte inside the first region's rows
+    data[s:t - 4] = np.frombuffer(bytes(blk), np.uint8)
+    data[t - 4:t] = np.frombuffer(struct.pack(">I", zlib.crc32(bytes(blk))), np.uint8)
+    ref = O.decode_blocks(data, e.block_off, 2)
+    got = rt.Decoder().decode(data, e.block_off, 2)
+    assert ref.status != 0
+    assert_decode_same(ref, got, "corrupt big blocks")
