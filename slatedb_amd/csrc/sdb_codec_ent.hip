@@ -89,6 +89,63 @@ struct EntOut {
         return true;
     }
     SDB_DEV uint8_t back(uint64_t d) const { return p ? p[len - d] : 0; }
+    // n bytes from src (not overlapping the output still to be written), 16 at a time
+    SDB_DEV bool copy(const uint8_t *src, uint64_t n) {
+        if (n > cap - len) {
+            bad = true;
+            return false;
+        }
+        if (p) {
+            uint64_t i = 0;
+            for (; i + 16 <= n; i += 16) {
+                uint4 w;
+                __builtin_memcpy(&w, src + i, 16);
+                __builtin_memcpy(p + len + i, &w, 16);
+            }
+            for (; i < n; i++) p[len + i] = src[i];
+        }
+        len += n;
+        return true;
+    }
+    // n bytes from src >= the write position (zstd's literal stage in the slot): forward, 16 at a time
+    // while the source is at least 16 bytes ahead
+    SDB_DEV bool copy_fwd(const uint8_t *src, uint64_t n) {
+        if (n > cap - len) {
+            bad = true;
+            return false;
+        }
+        uint8_t *dst = p + len;
+        uint64_t i = 0;
+        if (src - dst >= 16)
+            for (; i + 16 <= n; i += 16) {
+                uint4 w;
+                __builtin_memcpy(&w, src + i, 16);
+                __builtin_memcpy(dst + i, &w, 16);
+            }
+        if (src != dst)
+            for (; i < n; i++) dst[i] = src[i];
+        len += n;
+        return true;
+    }
+    // a match of n bytes at distance d: 16 at a time when d >= 16 (chunks never overlap their source)
+    SDB_DEV bool match(uint64_t d, uint64_t n) {
+        if (n > cap - len) {
+            bad = true;
+            return false;
+        }
+        if (p) {
+            uint64_t i = 0;
+            if (d >= 16)
+                for (; i + 16 <= n; i += 16) {
+                    uint4 w;
+                    __builtin_memcpy(&w, p + len - d + i, 16);
+                    __builtin_memcpy(p + len + i, &w, 16);
+                }
+            for (; i < n; i++) p[len + i] = p[len + i - d];
+        }
+        len += n;
+        return true;
+    }
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -291,8 +348,7 @@ SDB_DEV int inflate_raw(LsbBits &s, EntOut &o, EntLds &t) {
             if (!s.get(c_dist_extra[ds], v)) return kZTrunc;
             const uint32_t d = c_dist_base[ds] + v;
             if (d > o.len) return kZErr;
-            for (uint32_t i = 0; i < len; i++)
-                if (!o.put(o.back(d))) return kZErr;
+            if (!o.match(d, len)) return kZErr;
         }
     } while (!last);
     return kZOk;
@@ -646,8 +702,15 @@ SDB_DEV int zstd_block(EntLds &t, ZstdState &z, const uint8_t *in, uint64_t n, E
     uint64_t ip = hdr;
     if (ltype == 0) {
         if (ip + regen > n) return -1;
-        if (lit)
-            for (uint64_t i = 0; i < regen; i++) lit[i] = in[ip + i];
+        if (lit) {  // the stage sits past every byte still to be written: a plain 16-byte copy
+            uint64_t i = 0;
+            for (; i + 16 <= regen; i += 16) {
+                uint4 w;
+                __builtin_memcpy(&w, in + ip + i, 16);
+                __builtin_memcpy(lit + i, &w, 16);
+            }
+            for (; i < regen; i++) lit[i] = in[ip + i];
+        }
         ip += regen;
     } else if (ltype == 1) {
         if (ip + 1 > n) return -1;
@@ -743,19 +806,17 @@ SDB_DEV int zstd_block(EntLds &t, ZstdState &z, const uint8_t *in, uint64_t n, E
                 }
             }
             if (ll > regen - lp) return -1;
-            for (uint32_t i = 0; i < ll; i++)
-                if (!o.put(lit ? lit[lp + i] : 0)) return -1;
+            // literals: the stage is at or past the write position (o <= end - R + lp), a forward copy is safe
+            if (lit ? !o.copy_fwd(lit + lp, ll) : !o.copy(nullptr, ll)) return -1;
             lp += ll;
             if (off == 0 || off > o.len - fstart || off > window) return -1;
-            for (uint32_t i = 0; i < ml; i++)
-                if (!o.put(o.back(off))) return -1;
+            if (!o.match(off, ml)) return -1;
         }
         if (b.pos != 0) return -1;
     } else if (ip != n) {
         return -1;
     }
-    for (; lp < regen; lp++)
-        if (!o.put(lit ? lit[lp] : 0)) return -1;
+    if (lit ? !o.copy_fwd(lit + lp, regen - lp) : !o.copy(nullptr, regen - lp)) return -1;
     if (o.len - block_start > 128 * 1024) return -1;
     return 0;
 }
