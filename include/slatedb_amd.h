@@ -386,7 +386,7 @@ sdb_status sdb_sst_lookup(const sdb_sst_view *sst, const uint8_t *key_bytes, con
  *      entry whose add finished that block closes the SST as its one-entry tail block
  *      (compactor_executor.rs:833-858, sst_builder.rs:224-325); every SST then encodes as above.
  * sdb_merge_runs and sdb_sst_cuts are asynchronous on the caller's stream; sdb_compactor_run
- * orchestrates the whole job (two host synchronisations: the merged entry count, the cut list).
+ * orchestrates the whole job over decoded runs, sdb_compactor_run_ssts over encoded input SSTs.
  * ------------------------------------------------------------------------------------------- */
 /* One sorted input run in the layout sdb_decode_blocks produces (a decoded SST, or a sorted run's
  * SSTs decoded into one output): value i = val_base[val_off[i] .. val_off[i] + val_len[i]). */
@@ -472,6 +472,30 @@ sdb_compactor *sdb_compactor_create(int device);
 void sdb_compactor_destroy(sdb_compactor *c);
 sdb_status sdb_compactor_run(sdb_compactor *c, const sdb_run *runs, uint32_t nruns, const sdb_retention *retention,
                              const sdb_sst_params *params, uint64_t max_sst_size, void *stream, uint32_t *num_ssts);
+/* The same job from the encoded input SSTs, decode included (compactor_executor.rs:327-390, load_iterators:
+ * each input SST is read block by block and decoded; an L0 SST is a sorted run, a sorted run of several
+ * SSTs is their concatenation).  Every input's blocks are decoded by one launch sequence (CRC check,
+ * V1/V2 rows, key restore; values stay in place, like Bytes::slice), straight into the merge's runs; the
+ * merged stream is sized from the inputs' SstStats, so the job synchronises with the host twice: for the
+ * merged count with the cut list, and for the output SSTs' summaries.  Input i: an uncompressed data
+ * section on the device and the counts its footer holds.  Runs: inputs [run_start[r], run_start[r+1]),
+ * run_start == NULL: one run per input.  A failing input block fails the job with its status (lowest
+ * block first; the merged summary's first_error_entry = that block's index among all inputs' blocks);
+ * counts that disagree with the decoded blocks fail it with SDB_INVALID_ARGUMENT. */
+typedef struct sdb_compaction_input {
+    const uint8_t *data;            /* device: the data section (encoded blocks, each ++ crc32) */
+    const uint64_t *block_off;      /* device: num_blocks + 1 (BlockMeta.offset of each block, then the
+                                       data section length) */
+    uint64_t num_blocks;
+    uint64_t num_entries;           /* SstStats::num_rows() (num_puts + num_deletes + num_merges) */
+    uint64_t key_bytes;             /* SstStats.raw_key_size */
+    uint64_t val_bytes;             /* SstStats.raw_val_size */
+} sdb_compaction_input;
+enum { SDB_MAX_COMPACTION_INPUTS = 64 };
+sdb_status sdb_compactor_run_ssts(sdb_compactor *c, const sdb_compaction_input *inputs, uint32_t ninputs,
+                                  const uint32_t *run_start, uint32_t nruns, uint16_t input_sst_version,
+                                  const sdb_retention *retention, const sdb_sst_params *params,
+                                  uint64_t max_sst_size, void *stream, uint32_t *num_ssts);
 sdb_status sdb_compactor_sst(const sdb_compactor *c, uint32_t i, sdb_compacted_sst *out);
 /* The merged stream of the last run (device batch view) and its summary (host copy). */
 sdb_status sdb_compactor_merged(const sdb_compactor *c, sdb_kv_batch *batch, sdb_merge_summary *summary);

@@ -188,6 +188,15 @@ class CompactedSst(C.Structure):
     ]
 
 
+class CompactionInput(C.Structure):
+    _fields_ = [
+        ("data", C.c_void_p), ("block_off", C.c_void_p), ("num_blocks", C.c_uint64), ("num_entries", C.c_uint64),
+        ("key_bytes", C.c_uint64), ("val_bytes", C.c_uint64),
+    ]
+
+
+MAX_COMPACTION_INPUTS = 64
+
 DECODE_DESCENDING = 1
 
 LOOKUP_FILTERED, LOOKUP_EXHAUSTED, LOOKUP_POSITIONED, LOOKUP_FOUND = 0, 1, 2, 3
@@ -245,6 +254,9 @@ SIGNATURES = {
     "sdb_compactor_destroy": (None, [C.c_void_p]),
     "sdb_compactor_run": (C.c_int, [C.c_void_p, C.POINTER(Run), C.c_uint32, C.POINTER(Retention),
                                     C.POINTER(SstParams), C.c_uint64, C.c_void_p, u32p]),
+    "sdb_compactor_run_ssts": (C.c_int, [C.c_void_p, C.POINTER(CompactionInput), C.c_uint32, u32p, C.c_uint32,
+                                         C.c_uint16, C.POINTER(Retention), C.POINTER(SstParams), C.c_uint64,
+                                         C.c_void_p, u32p]),
     "sdb_compactor_sst": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(CompactedSst)]),
     "sdb_compactor_merged": (C.c_int, [C.c_void_p, C.POINTER(KvBatch), C.POINTER(MergeSummary)]),
     "sdb_sst_footer": (C.c_int, [C.POINTER(FooterIn), C.c_void_p, C.c_uint64, u64p]),

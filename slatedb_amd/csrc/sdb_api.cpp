@@ -482,6 +482,16 @@ uint64_t sdb_sst_cuts_workspace_bytes(uint64_t n, const sdb_sst_params *params) 
 sdb_status sdb_sst_cuts(const sdb_kv_batch *batch, const sdb_sst_params *params, uint64_t max_sst_size,
                         uint64_t *cut_start, uint64_t cut_cap, uint64_t *num_ssts, void *workspace,
                         uint64_t workspace_bytes, void *stream) {
+    return sst_cuts_padded(batch, params, max_sst_size, cut_start, cut_cap, num_ssts, workspace, workspace_bytes,
+                           S(stream), nullptr);
+}
+
+}  // extern "C"
+
+namespace sdb {
+sdb_status sst_cuts_padded(const sdb_kv_batch *batch, const sdb_sst_params *params, uint64_t max_sst_size,
+                           uint64_t *cut_start, uint64_t cut_cap, uint64_t *num_ssts, void *workspace,
+                           uint64_t workspace_bytes, hipStream_t s, const uint64_t *n_real) {
     if (!batch || !params || !cut_start || !num_ssts) return SDB_INVALID_ARGUMENT;
     sdb_sst_params p = *params;  // the chain only: no filter
     p.bloom_bits_per_key = 0;
@@ -494,7 +504,6 @@ sdb_status sdb_sst_cuts(const sdb_kv_batch *batch, const sdb_sst_params *params,
     if (cut_cap < n + 1 || (n && (!batch->key_bytes || !batch->key_off || !batch->val_off))) return SDB_INVALID_ARGUMENT;
     if (!device_ok()) return SDB_DEVICE_ERROR;
     if (!workspace || workspace_bytes < sdb_sst_cuts_workspace_bytes(n, params)) return SDB_INVALID_ARGUMENT;
-    hipStream_t s = S(stream);
     uint8_t *ws = (uint8_t *)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
     if (!n) {
         if (hipMemsetAsync(cut_start, 0, 8, s) != hipSuccess || hipMemsetAsync(num_ssts, 0, 8, s) != hipSuccess)
@@ -514,9 +523,12 @@ sdb_status sdb_sst_cuts(const sdb_kv_batch *batch, const sdb_sst_params *params,
     P.max_facts = P.s[0].nfacts;
     P.max_chunks = P.s[0].nchunks;
     P.max_groups = (P.s[0].nchunks + P.s[0].group - 1) / P.s[0].group;
-    if (launch_cuts(P, max_sst_size, cut_start, cut_cap, num_ssts, s) != hipSuccess) return SDB_DEVICE_ERROR;
+    if (launch_cuts(P, max_sst_size, cut_start, cut_cap, num_ssts, s, n_real) != hipSuccess) return SDB_DEVICE_ERROR;
     return SDB_OK;
 }
+}  // namespace sdb
+
+extern "C" {
 
 uint64_t sdb_sst_lookup_workspace_bytes(uint64_t num_blocks, uint64_t nkeys) {
     return lookup_workspace_bytes(num_blocks, nkeys) + 256;

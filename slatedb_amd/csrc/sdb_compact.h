@@ -40,6 +40,7 @@ struct MergeArgs {
     unsigned long long *err;     // run order violations: min (global entry << 8 | code)
     unsigned long long *err_merge;  // merge operands (MergeOperatorRequiredIterator): min merged position << 8 | code
     unsigned long long *metric;  // expired values, expired merges
+    const unsigned long long *gate;  // NULL, or (entry << 8 | status) of a failed input (~0: none): no merge
     RunDesc r[kMaxRuns];
 };
 static_assert(sizeof(MergeArgs) < 4000, "MergeArgs is passed as kernel arguments");
@@ -75,9 +76,37 @@ sdb_status build_merge_args(const sdb_run *runs, uint32_t nruns, const sdb_reten
 hipError_t launch_merge(const MergeArgs &a, bool emit, hipStream_t st);
 hipError_t launch_merge_emit(const MergeArgs &a, hipStream_t st);
 
-// SST cuts over the chain tables of a prep-only encode set of one slot (launch_encode_prep)
+// SST cuts over the chain tables of a prep-only encode set of one slot (launch_encode_prep).  n_real
+// (device, or NULL = the slot's n): the stream's true length when the slot covers a padded stream; the
+// walk stops there (a block before it is the same in both streams) and cuts past it are not recorded.
 hipError_t launch_cuts(const SstSet &P, uint64_t max_sst_size, uint64_t *cut, uint64_t cap, uint64_t *num,
-                       hipStream_t st);
+                       hipStream_t st, const uint64_t *n_real = nullptr);
+
+// ---- sdb_compactor_run_ssts (decode inside the job) ----
+constexpr uint32_t kMaxCxInputs = SDB_MAX_COMPACTION_INPUTS;
+struct CxInputs {  // kernel arguments: the input SSTs' blocks, in input order
+    uint32_t n, nruns;
+    uint64_t base;                          // the decoder's arena: block k = base + start[k] (mod 2^64)
+    const uint8_t *data[kMaxCxInputs];
+    const uint64_t *block_off[kMaxCxInputs];
+    uint64_t first_block[kMaxCxInputs + 1];  // prefix of num_blocks
+    uint64_t run_block[kMaxRuns + 1];        // first block of each run, then the total
+    uint64_t run_entry[kMaxRuns + 1];        // declared first entry of each run, then the total
+    uint64_t key_bytes;                      // declared total key bytes
+};
+static_assert(sizeof(CxInputs) < 4000, "CxInputs is passed as kernel arguments");
+// block k of the job -> arena offsets [start, end)
+hipError_t launch_cx_blocks(const CxInputs &in, uint64_t *start, uint64_t *end, hipStream_t st);
+// the decode's summary and run boundaries against the declared counts -> *gate (~0: the merge may run)
+hipError_t launch_cx_gate(const CxInputs &in, const sdb_decode_summary *dsum, const unsigned long long *dec_err,
+                          const uint64_t *block_entry_start, unsigned long long *gate, hipStream_t st);
+// sdb_sst_cuts over a padded stream whose true length is *n_real (device)
+sdb_status sst_cuts_padded(const sdb_kv_batch *batch, const sdb_sst_params *params, uint64_t max_sst_size,
+                           uint64_t *cut_start, uint64_t cut_cap, uint64_t *num_ssts, void *workspace,
+                           uint64_t workspace_bytes, hipStream_t stream, const uint64_t *n_real);
+// merged positions [summary.num_out + 1, cap]: empty entries (offsets = the totals), so a prep over the
+// padded stream reads defined bytes
+hipError_t launch_merge_pad(const sdb_merged_out &out, uint64_t cap, hipStream_t st);
 
 // out[2i], out[2i+1] = key_off[cut[i]], val_off[cut[i]] for i <= ns
 hipError_t launch_cut_offsets(const uint64_t *cut, const uint64_t *num, const uint64_t *key_off, const uint64_t *val_off,

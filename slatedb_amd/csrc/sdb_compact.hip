@@ -70,6 +70,11 @@ SDB_DEV int cmp_key(uint64_t pa, const uint8_t *a, uint32_t na, uint64_t pb, con
 // the rank and group kernels only run when every run is sorted.
 __global__ void k_mg_lcp0(MergeArgs a) {
     if (threadIdx.x) return;
+    if (a.gate && *a.gate != ~0ull) {  // a failed input: the job fails with its status, nothing is merged
+        *a.err = *a.gate;
+        *a.lcp0 = 0;
+        return;
+    }
     uint32_t L = ~0u;
     const uint8_t *e0 = nullptr;
     uint32_t n0 = 0;
@@ -92,7 +97,7 @@ __global__ void k_mg_lcp0(MergeArgs a) {
 
 __global__ __launch_bounds__(kPfxThreads) void k_mg_prefix(MergeArgs a) {
     const uint64_t g = (uint64_t)blockIdx.x * kPfxThreads + threadIdx.x;
-    if (g >= a.total) return;
+    if (g >= a.total || (a.gate && *a.gate != ~0ull)) return;
     const uint32_t r = run_of(a, g);
     const RunDesc &R = a.r[r];
     const uint64_t i = g - R.base;
@@ -297,7 +302,9 @@ __global__ __launch_bounds__(kMergeThreads) void k_mg_tiles(MergeArgs a) {
 __global__ __launch_bounds__(kMergeThreads) void k_mg_scan(MergeArgs a) {
     __shared__ uint64_t s_w[17];
     sdb_merge_summary *sm = a.out.summary;
-    const unsigned long long e1 = *a.err, e2 = *a.err_merge;
+    unsigned long long e1 = *a.err;
+    const unsigned long long e2 = *a.err_merge;
+    if (e1 == ~0ull && a.gate && *a.gate != ~0ull) e1 = *a.gate;  // (no entries: k_mg_lcp0 did not run)
     uint64_t carry[3] = {0, 0, 0};
     if (e1 == ~0ull && e2 == ~0ull) {
         for (uint32_t base = 0; base < a.ntiles; base += kMergeThreads) {
@@ -545,7 +552,8 @@ __global__ __launch_bounds__(kMergeThreads) void k_mg_emit(MergeArgs a) {
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t kCutThreads = 256, kCutTab = 2048;
 constexpr uint64_t kCutDone = ~1ull, kCutTables = 1ull << 62;  // staging requests: chunk k, or kCutTables | group g
-__global__ __launch_bounds__(kCutThreads) void k_cut(SstSet P, uint64_t max_sst, uint64_t *cut, uint64_t *num) {
+__global__ __launch_bounds__(kCutThreads) void k_cut(SstSet P, uint64_t max_sst, uint64_t *cut, uint64_t *num,
+                                                      const uint64_t *n_real) {
     // Thread 0 walks; the workgroup stages what the next steps read into LDS first: the group tables
     // (once), the chunk tables of the group the walk is in, and a chunk's next() / block bytes before
     // thread 0 steps block by block through it (one HBM round trip per table set or chunk instead of one
@@ -555,7 +563,10 @@ __global__ __launch_bounds__(kCutThreads) void k_cut(SstSet P, uint64_t max_sst,
     __shared__ uint64_t s_gb[kCutTab], s_cb[kCutTab];
     __shared__ uint64_t s_stage;  // the next staging request (kCutDone: the walk is done)
     const EncodeArgs a = make_args(P, 0);
-    const uint64_t n = a.n;
+    // the walk ends at the stream's true length: every block that ends before it is the same in a padded
+    // stream, the one that reaches it is the tail block (never counted), and a chunk / group skip past it
+    // adds no cut in either stream
+    const uint64_t n = n_real ? *n_real : a.n;
     const bool fast = *a.mode >= 1;  // 1 and 2: the chunk / group tables describe the chain
     const uint32_t W = *a.wmax, G = a.group, L = a.seg_look;
     const uint32_t K = a.nchunks, ngroups = (K + G - 1) / G;
@@ -681,7 +692,83 @@ __global__ void k_cut_offsets(const uint64_t *cut, const uint64_t *num, const ui
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// sdb_compactor_run_ssts: the input SSTs' blocks as one decode, the gate between decode and merge, and
+// the padding of the merged stream for the cut walk.
+// ------------------------------------------------------------------------------------------------
+__global__ void k_cx_blocks(CxInputs in, uint64_t *start, uint64_t *end) {
+    const uint64_t nb = in.first_block[in.n];
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nb; k += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t lo = 0, hi = in.n - 1;  // the input holding block k: last first_block <= k
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (in.first_block[mid] <= k) lo = mid;
+            else hi = mid - 1;
+        }
+        const uint64_t j = k - in.first_block[lo], d = (uint64_t)(uintptr_t)in.data[lo] - in.base;
+        start[k] = d + in.block_off[lo][j];
+        end[k] = d + in.block_off[lo][j + 1];
+    }
+}
+
+// ~0 when the decode succeeded and agrees with the declared counts; else the decode's first failure
+// (block << 8 | status), or SDB_INVALID_ARGUMENT at the first run whose boundary disagrees
+__global__ void k_cx_gate(CxInputs in, const sdb_decode_summary *dsum, const unsigned long long *dec_err,
+                          const uint64_t *bes, unsigned long long *gate) {
+    if (threadIdx.x) return;
+    unsigned long long g = ~0ull;
+    if (dsum->status != SDB_OK) {
+        g = *dec_err != ~0ull ? *dec_err : (unsigned long long)(uint32_t)dsum->status;
+    } else if (dsum->num_entries != in.run_entry[in.nruns] || dsum->key_bytes != in.key_bytes) {
+        g = SDB_INVALID_ARGUMENT;
+    } else {
+        for (uint32_t r = 0; r < in.nruns; r++)
+            if (bes[in.run_block[r]] != in.run_entry[r]) {
+                g = ((unsigned long long)in.run_block[r] << 8) | SDB_INVALID_ARGUMENT;
+                break;
+            }
+    }
+    *gate = g;
+}
+
+__global__ void k_mg_pad(sdb_merged_out o, uint64_t cap) {
+    const sdb_merge_summary *sm = o.summary;
+    const bool ok = sm->status == SDB_OK;
+    const uint64_t from = ok ? sm->num_out + 1 : 0;  // a failed merge: the whole stream is empty entries
+    const uint64_t kt = ok ? sm->key_bytes : 0, vt = ok ? sm->val_bytes : 0;
+    for (uint64_t i = from + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= cap;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        o.key_off[i] = kt;
+        o.val_off[i] = vt;
+        if (i < cap) {
+            o.kind[i] = SDB_KIND_VALUE;
+            o.seq[i] = 0;
+            o.ts_mask[i] = 0;
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_cx_blocks(const CxInputs &in, uint64_t *start, uint64_t *end, hipStream_t st) {
+    const uint64_t nb = in.first_block[in.n];
+    if (nb) {
+        uint64_t g = (nb + 255) / 256;
+        hipLaunchKernelGGL(k_cx_blocks, dim3((uint32_t)(g < 2048 ? g : 2048)), dim3(256), 0, st, in, start, end);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_cx_gate(const CxInputs &in, const sdb_decode_summary *dsum, const unsigned long long *dec_err,
+                          const uint64_t *block_entry_start, unsigned long long *gate, hipStream_t st) {
+    hipLaunchKernelGGL(k_cx_gate, dim3(1), dim3(64), 0, st, in, dsum, dec_err, block_entry_start, gate);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_pad(const sdb_merged_out &out, uint64_t cap, hipStream_t st) {
+    hipLaunchKernelGGL(k_mg_pad, dim3(256), dim3(256), 0, st, out, cap);
+    return hipGetLastError();
+}
 
 hipError_t launch_cut_offsets(const uint64_t *cut, const uint64_t *num, const uint64_t *key_off, const uint64_t *val_off,
                               uint64_t *out, hipStream_t st) {
@@ -763,11 +850,11 @@ hipError_t launch_merge_emit(const MergeArgs &a, hipStream_t st) {
 }
 
 hipError_t launch_cuts(const SstSet &P, uint64_t max_sst_size, uint64_t *cut, uint64_t cap, uint64_t *num,
-                       hipStream_t st) {
+                       hipStream_t st, const uint64_t *n_real) {
     (void)cap;  // the host checks cap >= n + 1
     hipError_t e = launch_encode_prep(P, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_cut, dim3(1), dim3(kCutThreads), 0, st, P, max_sst_size, cut, num);
+    hipLaunchKernelGGL(k_cut, dim3(1), dim3(kCutThreads), 0, st, P, max_sst_size, cut, num, n_real);
     return hipGetLastError();
 }
 

@@ -790,6 +790,24 @@ class Compactor:
         self.status = st
         return st, ns.value
 
+    def run_ssts(self, inputs, ret, prm, max_sst_size, input_version=2, run_start=None, stream=None):
+        """sdb_compactor_run_ssts: the job from encoded input SSTs (decode included).  inputs: objects with
+        .data / .block_off (device tensors: the data section, block_off u64[num_blocks + 1]) and the
+        SstStats counts .num_entries / .key_bytes / .val_bytes; run_start: inputs of each sorted run."""
+        ci = (_abi.CompactionInput * max(len(inputs), 1))(*[
+            _abi.CompactionInput(x.data.data_ptr(), x.block_off.data_ptr(), x.block_off.numel() - 1, x.num_entries,
+                                 x.key_bytes, x.val_bytes) for x in inputs])
+        rs = None
+        nruns = len(inputs)
+        if run_start is not None:
+            rs = (C.c_uint32 * len(run_start))(*run_start)
+            nruns = len(run_start) - 1
+        ns = C.c_uint32(0)
+        st = lib().sdb_compactor_run_ssts(self.h, ci, len(inputs), rs, nruns, input_version, C.byref(ret), C.byref(prm),
+                                          max_sst_size, _sp(stream), C.byref(ns))
+        self.status = st
+        return st, ns.value
+
     def merged(self):
         kb, sm = _abi.KvBatch(), _abi.MergeSummary()
         st = lib().sdb_compactor_merged(self.h, C.byref(kb), C.byref(sm))

@@ -155,7 +155,7 @@ def test_integration_rust_structs_match_header():
     want = ["sdb_kv_batch", "sdb_sst_params", "sdb_sst_summary", "sdb_sst_out", "sdb_sst_host_result",
             "sdb_footer_in", "sdb_decode_summary", "sdb_decoded_out", "sdb_decode_host_result", "sdb_sst_view",
             "sdb_lookup_out", "sdb_run", "sdb_retention", "sdb_merge_summary", "sdb_merged_out",
-            "sdb_compacted_sst"]
+            "sdb_compacted_sst", "sdb_compaction_input"]
     missing = [w for w in want if w not in structs]
     assert not missing, missing
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "%s"' % HDR, "int main(void){"]

@@ -267,3 +267,117 @@ def test_v1_blocks_past_block_size(rt):
     dref = O.decode_blocks(ref.data, ref.block_off, 1)
     dec = rt.Decoder()
     assert_decode_same(dref, dec.decode(ref.data, ref.block_off, 1), "v1 oversized decode")
+
+
+def encoded_inputs(rt, runs, prm_kw, split=1):
+    """Each run encoded by the oracle as `split` consecutive SSTs, uploaded: (inputs, run_start, ref_runs) with
+    ref_runs = the runs as the reference reads them back (the oracle's decode of each run's SSTs: V0 rows
+    drop a tombstone's expire_ts)."""
+    import torch
+    inputs, run_start, ref_runs = [], [0], []
+    for r in runs:
+        datas, offs, base = [], [], 0
+        b = Batch(r.key_arena, r.key_off, r.val_base, np.concatenate([r.val_off, [r.val_off[-1] + r.val_len[-1]]]),
+                  np.where(r.flags & 1, 2, 0).astype(np.uint8), r.seq, r.create_ts, r.expire_ts,
+                  np.where(r.flags & 2, 2, 0).astype(np.uint8))
+        cuts = np.linspace(0, b.n, split + 1).astype(int)
+        for i in range(split):
+            enc = O.encode_sst(b.slice(cuts[i], cuts[i + 1]), O.params(**prm_kw))
+            sm = enc.summary
+            inputs.append(types.SimpleNamespace(
+                data=torch.from_numpy(np.concatenate([enc.data, np.zeros(16, np.uint8)])).cuda(),
+                block_off=torch.from_numpy(enc.block_off.view(np.int64)).cuda(),
+                num_entries=int(sm.num_entries), key_bytes=int(sm.raw_key_size), val_bytes=int(sm.raw_val_size)))
+            bo = enc.block_off.astype(np.uint64)
+            datas.append(enc.data[:int(bo[-1])])
+            offs.append((bo if i == split - 1 else bo[:-1]) + np.uint64(base))
+            base += int(bo[-1])
+        run_start.append(len(inputs))
+        blocks = np.concatenate(datas) if datas else np.zeros(0, np.uint8)
+        d = O.decode_blocks(blocks, np.concatenate(offs), prm_kw.get("sst_version", 2))
+        assert d.status == 0 and d.n == r.n
+        ref_runs.append(Run(d.key_arena, d.key_off, blocks, d.val_off, d.val_len, d.seq, d.flags, d.create_ts,
+                            d.expire_ts))
+    return inputs, run_start, ref_runs
+
+
+def compact_ssts_both(rt, runs, ret, prm_kw, max_sst, split=1, version=2, out_kw=None):
+    """sdb_compactor_run_ssts on the runs' encoded SSTs vs O.compact on the runs."""
+    import torch
+    inputs, run_start, runs = encoded_inputs(rt, runs, dict(prm_kw, sst_version=version), split)
+    out_kw = out_kw or prm_kw
+    comp = rt.Compactor()
+    st, ns = comp.run_ssts(inputs, ret, rt.params(**out_kw), max_sst, input_version=version,
+                           run_start=run_start if split > 1 else None)
+    torch.cuda.synchronize()
+    merged, msum, cuts, ssts = O.compact(runs, ret, O.params(**out_kw), max_sst)
+    assert st == msum.status, (st, msum.status)
+    if not st:
+        gm, _ = comp.merged()
+        assert_batch_same(gm, merged, "merged")
+        assert ns == len(ssts), (ns, len(ssts))
+        for i, ref in enumerate(ssts):
+            d = comp.sst(i)
+            assert (d["entry_start"], d["entry_end"]) == (cuts[i], cuts[i + 1])
+            assert_same(ref, sst_view(d), "sst %d" % i)
+    comp.close()
+    return st, ns, inputs
+
+
+@pytest.mark.parametrize("version", [1, 2])
+def test_compactor_run_ssts(rt, version):
+    """Decode inside the job: L0 SSTs encoded by the oracle, decoded + merged + retained + cut + encoded on
+    the device, compared with the oracle's compaction of the same runs."""
+    runs = big_runs(31, 40000, 4)
+    _, ns, _ = compact_ssts_both(rt, runs, O.retention(min_seq=50000, compaction_start_ts=1000, filter_tombstone=True),
+                                 dict(block_size=4096, bloom_bits_per_key=10), 1 << 20, version=version)
+    assert ns >= 3
+
+
+def test_compactor_run_ssts_sorted_runs(rt):
+    """Sorted runs of three SSTs each (run_start), small blocks, several output SSTs."""
+    runs = big_runs(32, 20000, 3)
+    compact_ssts_both(rt, runs, O.retention(min_seq=10000, compaction_start_ts=500), dict(block_size=1024), 300000,
+                      split=3)
+
+
+def test_compactor_run_ssts_edges(rt):
+    rng = random.Random(9)
+    small = [Run.from_entries(r) for r in rand_runs(rng, 3, 400, 4)]
+    for max_sst in (1, 10 ** 9):  # one SST per block / one SST
+        compact_ssts_both(rt, small, O.retention(min_seq=100, compaction_start_ts=900), dict(block_size=256), max_sst)
+    # everything dropped: no output SST
+    compact_ssts_both(rt, [Run.from_entries([(b"k", 2, b"", 1, None, None)])], O.retention(filter_tombstone=True),
+                      dict(), 100)
+    # merge operands without a merge operator
+    mruns = [Run.from_entries(r) for r in rand_runs(rng, 2, 50, 3, merge=0.3)]
+    compact_ssts_both(rt, mruns, O.retention(), dict(), 10 ** 9)
+
+
+def test_compactor_run_ssts_bad_inputs(rt):
+    """A corrupt input block fails the job with its read error (lowest block first); counts that
+    disagree with the blocks fail it with SDB_INVALID_ARGUMENT; nothing is merged either way."""
+    import torch
+    runs = big_runs(33, 8000, 3)
+    prm_kw = dict(block_size=4096, bloom_bits_per_key=10)
+    inputs, _, _ = encoded_inputs(rt, runs, prm_kw)
+    prm, ret = rt.params(**prm_kw), O.retention()
+    comp = rt.Compactor()
+    # flip a byte inside block 3 of input 1 (job block index = input 0's blocks + 3)
+    bo = inputs[1].block_off.cpu().numpy()
+    inputs[1].data[int(bo[3]) + 10] ^= 0x5A
+    st, ns = comp.run_ssts(inputs, ret, prm, 1 << 30)
+    torch.cuda.synchronize()
+    assert st == _abi.SDB_CHECKSUM_MISMATCH and ns == 0
+    _, sm = comp.merged()
+    assert sm.first_error_entry == inputs[0].block_off.numel() - 1 + 3
+    inputs[1].data[int(bo[3]) + 10] ^= 0x5A
+    st, ns = comp.run_ssts(inputs, ret, prm, 1 << 30)
+    assert st == 0 and ns == 1
+    for f, d in (("num_entries", 1), ("key_bytes", -1)):
+        setattr(inputs[2], f, getattr(inputs[2], f) + d)
+        st, ns = comp.run_ssts(inputs, ret, prm, 1 << 30)
+        torch.cuda.synchronize()
+        assert st == _abi.SDB_INVALID_ARGUMENT and ns == 0, (f, st)
+        setattr(inputs[2], f, getattr(inputs[2], f) - d)
+    comp.close()
