@@ -348,6 +348,53 @@ def compact_bench(reps):
                                        "GiB_per_s_logical": round(logical / cpu_s / 2**30, 3),
                                        "sample": "the whole job, oracle compact (merge + retention + cuts + encode)"}}),
           flush=True)
+    # the same job from the encoded input SSTs (sdb_compactor_run_ssts: decode inside the job), the four
+    # SSTs encoded on the device and resident; CPU baseline: the oracle's decode of the four SSTs + compact
+    import types
+    dev = torch.device("cuda", 0)
+    inputs, enc_host = [], []
+    for h in hosts:
+        db = h.to_device(dev)
+        out = runtime.DeviceSstOutput(h.n, h.logical_bytes(), h.logical_bytes(), prm, device=dev)
+        runtime.encode_sst_device(db, out)
+        torch.cuda.synchronize()
+        sm = out.summary_host()
+        nb = int(sm.num_blocks)
+        inputs.append(types.SimpleNamespace(data=out.data, block_off=out.block_off[:nb + 1],
+                                            num_entries=int(sm.num_entries), key_bytes=int(sm.raw_key_size),
+                                            val_bytes=int(sm.raw_val_size), keep=out))
+        r = out.to_host()
+        enc_host.append((r["data"], r["block_off"].astype(np.uint64)))
+        del db
+    encoded = sum(int(x.block_off[-1].item()) for x in inputs)
+    comp2 = runtime.Compactor()
+    st2, ns2 = comp2.run_ssts(inputs, ret, prm, 256 << 20)
+    assert st2 == 0, st2
+    torch.cuda.synchronize()
+    walls2 = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        st2, ns2 = comp2.run_ssts(inputs, ret, prm, 256 << 20)
+        walls2.append((time.perf_counter() - t0) * 1e3)
+        assert st2 == 0
+    ms2 = float(np.median(walls2))
+    t0 = time.perf_counter()
+    druns_o = []
+    for data, bo in enc_host:
+        d = O.decode_blocks(data, bo, 2)
+        druns_o.append(Run(d.key_arena, d.key_off, data, d.val_off, d.val_len, d.seq, d.flags, d.create_ts, d.expire_ts))
+    _, osm2, ocuts2, ossts2 = O.compact(druns_o, oret, O.params(block_size=4096, sst_version=2, bloom_bits_per_key=10),
+                                        256 << 20)
+    cpu2_s = time.perf_counter() - t0
+    same2 = len(ossts2) == ns2 and all(np.array_equal(comp2.sst(i)["data"], ossts2[i].data) for i in range(ns2))
+    print(json.dumps({"what": "compaction job (f2) from encoded SSTs: 4 x configs[1] L0 SSTs -> decode + merge + "
+                              "retention + cuts + encode (sdb_compactor_run_ssts, two host synchronisations)",
+                      "encoded_bytes_in": encoded, "logical_bytes_in": logical, "output_ssts": ns2, "ms_wall": round(ms2, 3),
+                      "GiB_per_s_logical": round(logical / (ms2 * 1e-3) / 2**30, 2), "bit_exact_vs_oracle": bool(same2),
+                      "cpu_baseline": {"kind": "port", "cores": 1, "s": round(cpu2_s, 3),
+                                       "GiB_per_s_logical": round(logical / cpu2_s / 2**30, 3),
+                                       "sample": "the whole job, oracle decode of the 4 SSTs + compact"}}), flush=True)
+    comp2.close()
     comp.close()
 
 

@@ -9,8 +9,14 @@
 namespace sdb {
 
 constexpr uint32_t kMaxRuns = SDB_MAX_RUNS;
-constexpr uint32_t kMergeTile = 4096;      // merged positions per k_mg_tiles / k_mg_emit workgroup
-constexpr uint32_t kMergeThreads = 1024;
+#ifndef SDB_MERGE_TILE
+#define SDB_MERGE_TILE 1024
+#endif
+#ifndef SDB_MERGE_THREADS
+#define SDB_MERGE_THREADS 512
+#endif
+constexpr uint32_t kMergeTile = SDB_MERGE_TILE;  // merged positions per k_mg_tiles / k_mg_emit workgroup
+constexpr uint32_t kMergeThreads = SDB_MERGE_THREADS;
 
 struct RunDesc {  // sdb_run + the run's first global entry index
     uint64_t n, base;

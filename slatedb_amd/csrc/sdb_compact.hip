@@ -8,9 +8,9 @@
 //                 (MergeOperatorRequiredIterator, merge_operator.rs:213-223)
 //   k_mg_retain   per key: apply_retention_filter (retention_iterator.rs:91-204) -> keep / drop /
 //                 keep as a tombstone per version
-//   k_mg_tiles    per 4096 positions: kept entries, key bytes, value bytes
+//   k_mg_tiles    per kMergeTile positions: kept entries, key bytes, value bytes
 //   k_mg_scan     one workgroup: tile offsets, the summary
-//   k_mg_emit     per 4096 positions: the output batch (metadata + key / value bytes)
+//   k_mg_emit     per kMergeTile positions: the output batch (metadata + key / value bytes)
 //   k_cut         one lane: the compactor's max_sst_size walk (compactor_executor.rs:833-858) over
 //                 the chain tables of the encoder's k_seg / k_group (group, chunk, then block steps)
 //
