@@ -152,6 +152,25 @@ def decode_bench(reps, granular=True, cpu_s=0.0):
                       "ms": round(ms, 4), "GiB_per_s_encoded": round(enc / (ms * 1e-3) / 2**30, 2),
                       "algorithmic_bytes": alg, "achieved_GBps": round(gbs, 1), "frac": round(gbs / PEAK, 4),
                       "verified_keys": bool(ok)}), flush=True)
+    # descending iteration order (SDB_DECODE_DESCENDING): written mirrored by the emit pass
+    asc_keys = ka[:kbytes].cpu().numpy().copy()
+    asc_seq = sq[:nent].cpu().numpy().copy()
+
+    def run_desc():
+        st = lib.sdb_decode_blocks_ex(blocks.data_ptr(), block_off.data_ptr(), None, nb, 2, _abi.DECODE_DESCENDING,
+                                      C.byref(dout), ws.data_ptr(), wsb, s.cuda_stream)
+        assert st == 0, st
+
+    with torch.cuda.stream(s):
+        ms_d = timed(run_desc, reps, s)
+    torch.cuda.synchronize()
+    smd = _abi.DecodeSummary.from_buffer_copy(smy.cpu().numpy().tobytes()[:C.sizeof(_abi.DecodeSummary)])
+    okd = smd.status == 0 and smd.num_entries == nent and np.array_equal(
+        ka[:kbytes].cpu().numpy().reshape(-1, 16), asc_keys.reshape(-1, 16)[::-1]) and np.array_equal(
+        sq[:nent].cpu().numpy(), asc_seq[::-1])
+    print(json.dumps({"what": "decode configs[2], descending order", "ms": round(ms_d, 4),
+                      "GiB_per_s_encoded": round(enc / (ms_d * 1e-3) / 2**30, 2),
+                      "verified_keys_seq_reversed": bool(okd)}), flush=True)
     if cpu_s > 0:  # CPU baseline: the oracle decoding whole D1 SSTs (read_blocks -> DataBlockIterator)
         from oracle import oracle as O
         host = []

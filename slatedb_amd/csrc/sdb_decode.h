@@ -24,9 +24,10 @@ struct DecodeArgs {
     unsigned long long *err, *nbad;
     uint32_t *done;                    // k_dec_emit workgroups finished (small batches: the last one finishes)
     uint32_t small;                    // 1: nblocks <= 1024 and one block per wave: k_dec_emit scans the counts itself
-    uint32_t descending;               // 1: output in descending iteration order (reversed after the decode)
+    uint32_t descending;               // 1: output in descending iteration order (written mirrored by k_dec_emit)
     uint32_t *bad_block;
     uint64_t bad_cap;
+    uint64_t dn, dkb;                  // descending: entries and key bytes of the whole output (k_dec_emit)
 };
 
 struct DecodeWorkspace {

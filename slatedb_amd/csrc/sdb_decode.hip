@@ -995,9 +995,16 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
 
 // --- emit -----------------------------------------------------------------------------------------
 // Columns of one entry.  Timestamps are written only when the row carries them (the contract:
-// create_ts / expire_ts are valid iff the flag is set).
-SDB_DEV void put_entry(const DecodeArgs &a, uint64_t idx, uint64_t kpos, uint64_t vref, uint32_t vlen, uint64_t seq,
-                       uint8_t flags, int64_t cts, int64_t ets) {
+// create_ts / expire_ts are valid iff the flag is set).  Descending order (DescendingBlockIteratorV2 /
+// BlockIterator Descending yield a block's entries last to first, sst_iter.rs:557 the blocks last to
+// first): entry idx of the ascending order is entry N - 1 - idx, and the key at ascending arena position
+// kpos lands at KB - kpos - klen, so the arena holds the keys in descending order, each one forward.
+SDB_DEV void put_entry(const DecodeArgs &a, uint64_t idx, uint64_t kpos, uint32_t klen, uint64_t vref, uint32_t vlen,
+                       uint64_t seq, uint8_t flags, int64_t cts, int64_t ets) {
+    if (a.descending) {
+        idx = a.dn - 1 - idx;
+        kpos = a.dkb - kpos - klen;
+    }
     a.out.key_off[idx] = kpos;
     a.out.val_off[idx] = vlen ? vref : 0;
     a.out.val_len[idx] = vlen;
@@ -1005,6 +1012,22 @@ SDB_DEV void put_entry(const DecodeArgs &a, uint64_t idx, uint64_t kpos, uint64_
     a.out.flags[idx] = flags;
     if (flags & SDB_FLAG_HAS_CREATE_TS) a.out.create_ts[idx] = cts;
     if (flags & SDB_FLAG_HAS_EXPIRE_TS) a.out.expire_ts[idx] = ets;
+}
+
+// The arena address of the key at ascending position kp (kl bytes): mirrored in descending order.
+SDB_DEV uint8_t *key_dst(const DecodeArgs &a, uint64_t kp, uint32_t kl) {
+    return a.out.key_arena + (a.descending ? a.dkb - kp - kl : kp);
+}
+// Descending order: a key its lane just restored in LDS, stored by that lane to its mirrored place (the
+// block's keys are not one ascending range there, so no wave_store_bytes).
+SDB_DEV void key_store_desc(const DecodeArgs &a, uint64_t kp, const lu8 *src, uint32_t kl) {
+    typedef uint32_t u32u __attribute__((aligned(1)));
+    uint8_t *g = key_dst(a, kp, kl);
+    uint32_t i = 0;
+    for (; i + 4 <= kl; i += 4)
+        *(u32u *)(g + i) = (uint32_t)src[i] | ((uint32_t)src[i + 1] << 8) | ((uint32_t)src[i + 2] << 16) |
+                           ((uint32_t)src[i + 3] << 24);
+    for (; i < kl; i++) g[i] = src[i];
 }
 
 // Keys of <= 16 bytes as two little-endian u64 (byte x at bits 8x): key = cur[:shared] ++ suffix, the
@@ -1043,7 +1066,6 @@ SDB_DEV void emit_v2(const DecodeArgs &a, const BlockViewT<P> &v, bool sequentia
                      uint64_t gbase, lu8 *kbuf) {
     const uint32_t l = (uint32_t)lane_id();
     const uint32_t ko = (uint32_t)(kb0 & 15);
-    auto key_at = [&](uint64_t kp) -> uint8_t * { return a.out.key_arena + kp; };
     if (!sequential) {
         const uint32_t R = v.count;
         uint64_t ecarry = ent0, kcarry = kb0;
@@ -1130,9 +1152,10 @@ SDB_DEV void emit_v2(const DecodeArgs &a, const BlockViewT<P> &v, bool sequentia
                             if (b < klen) dst[b] = v.d[sa + b];
                         }
                         if (live) {
+                            if (a.descending) key_store_desc(a, kb0 + krel, dst, klen);
                             const uint8_t f = (uint8_t)x[2];
-                            put_entry(a, ecarry + j, kb0 + krel, gbase + (pj + 3 + un), (f & SDB_FLAG_TOMBSTONE) ? 0 : vl,
-                                      be64_at(x[0], x[1]), f, 0, 0);
+                            put_entry(a, ecarry + j, kb0 + krel, klen, gbase + (pj + 3 + un),
+                                      (f & SDB_FLAG_TOMBSTONE) ? 0 : vl, be64_at(x[0], x[1]), f, 0, 0);
                         }
                         done_fast = true;
                     }
@@ -1166,9 +1189,10 @@ SDB_DEV void emit_v2(const DecodeArgs &a, const BlockViewT<P> &v, bool sequentia
                                 lds_copy_small(dst, kbuf + ko + (uint32_t)(prev_kp - kb0), sh);
                                 for (uint32_t b = 0; b < un; b++) dst[sh + b] = v.d[p + 3 + b];
                             }
+                            if (a.descending) key_store_desc(a, kp, dst, klen);
                             const uint8_t f = (uint8_t)x[2];
-                            put_entry(a, idx, kp, gbase + (p + 3 + un), (f & SDB_FLAG_TOMBSTONE) ? 0 : vl, be64_at(x[0], x[1]), f,
-                                      0, 0);
+                            put_entry(a, idx, kp, klen, gbase + (p + 3 + un), (f & SDB_FLAG_TOMBSTONE) ? 0 : vl,
+                                      be64_at(x[0], x[1]), f, 0, 0);
                             prev_kp = kp;
                             kp += klen;
                             idx++;
@@ -1179,24 +1203,28 @@ SDB_DEV void emit_v2(const DecodeArgs &a, const BlockViewT<P> &v, bool sequentia
             }
             if (!done_fast && q < R) {
                 uint64_t prev_kp = 0;
+                uint32_t prev_kl = 0;
                 uint32_t p = pos;
                 while (p < end) {
                     RowV2 r;
                     parse_v2(v.d, v.data_end, p, &r);
+                    const uint32_t kl = r.shared + r.unshared;
                     if (kbuf) {
                         lu8 *dst = kbuf + ko + (uint32_t)(kp - kb0);
                         lds_copy_small(dst, kbuf + ko + (uint32_t)(prev_kp - kb0), r.shared);
                         for (uint32_t x = 0; x < r.unshared; x++) dst[r.shared + x] = v.d[r.suf_pos + x];
+                        if (a.descending) key_store_desc(a, kp, dst, kl);
                     } else {
-                        uint8_t *dst = key_at(kp);
-                        const uint8_t *pk = key_at(prev_kp);
+                        uint8_t *dst = key_dst(a, kp, kl);
+                        const uint8_t *pk = key_dst(a, prev_kp, prev_kl);
                         for (uint32_t x = 0; x < r.shared; x++) dst[x] = pk[x];
                         for (uint32_t x = 0; x < r.unshared; x++) dst[r.shared + x] = v.d[r.suf_pos + x];
                     }
                     const uint32_t vl = (r.flags & SDB_FLAG_TOMBSTONE) ? 0 : r.vlen;
-                    put_entry(a, idx, kp, gbase + r.val_pos, vl, r.seq, r.flags, r.cts, r.ets);
+                    put_entry(a, idx, kp, kl, gbase + r.val_pos, vl, r.seq, r.flags, r.cts, r.ets);
                     prev_kp = kp;
-                    kp += r.shared + r.unshared;
+                    prev_kl = kl;
+                    kp += kl;
                     idx++;
                     p = r.next;
                 }
@@ -1207,7 +1235,7 @@ SDB_DEV void emit_v2(const DecodeArgs &a, const BlockViewT<P> &v, bool sequentia
     } else if (l == 0) {
         // sequential walk (BlockIteratorV2 ascending); the initial current_key is the key at restart 0
         uint64_t idx = ent0, kp = kb0, prev_kp = 0;
-        uint32_t pos = 0;
+        uint32_t pos = 0, prev_kl = 0;
         uint32_t p0 = (uint32_t)rd_be(v.offs, 2), sh = 0, un = 0, vl0 = 0;
         rd_varint(v.d, v.data_end, &p0, &sh);
         rd_varint(v.d, v.data_end, &p0, &un);
@@ -1217,19 +1245,23 @@ SDB_DEV void emit_v2(const DecodeArgs &a, const BlockViewT<P> &v, bool sequentia
         while (pos < v.data_end) {
             RowV2 r;
             parse_v2(v.d, v.data_end, pos, &r);
+            const uint32_t kl = r.shared + r.unshared;
             if (kbuf) {
                 lu8 *dst = kbuf + ko + (uint32_t)(kp - kb0);
                 for (uint32_t x = 0; x < r.shared; x++) dst[x] = first ? v.d[init_key + x] : kbuf[ko + (uint32_t)(prev_kp - kb0) + x];
                 for (uint32_t x = 0; x < r.unshared; x++) dst[r.shared + x] = v.d[r.suf_pos + x];
+                if (a.descending) key_store_desc(a, kp, dst, kl);
             } else {
-                uint8_t *dst = key_at(kp);
-                for (uint32_t x = 0; x < r.shared; x++) dst[x] = first ? v.d[init_key + x] : a.out.key_arena[prev_kp + x];
+                uint8_t *dst = key_dst(a, kp, kl);
+                const uint8_t *pk = key_dst(a, prev_kp, prev_kl);
+                for (uint32_t x = 0; x < r.shared; x++) dst[x] = first ? v.d[init_key + x] : pk[x];
                 for (uint32_t x = 0; x < r.unshared; x++) dst[r.shared + x] = v.d[r.suf_pos + x];
             }
             const uint32_t vl = (r.flags & SDB_FLAG_TOMBSTONE) ? 0 : r.vlen;
-            put_entry(a, idx, kp, gbase + r.val_pos, vl, r.seq, r.flags, r.cts, r.ets);
+            put_entry(a, idx, kp, kl, gbase + r.val_pos, vl, r.seq, r.flags, r.cts, r.ets);
             prev_kp = kp;
-            kp += r.shared + r.unshared;
+            prev_kl = kl;
+            kp += kl;
             idx++;
             first = false;
             pos = r.next;
@@ -1268,9 +1300,10 @@ SDB_DEV void emit_v2_rows(const DecodeArgs &a, const LdsBlockView &v, uint64_t r
         if (b < klen) dst[b] = v.d[sa + b];
     }
     if (live) {
+        if (a.descending) key_store_desc(a, kb0 + krel, dst, klen);
         const uint8_t f = (uint8_t)x[2];
-        put_entry(a, ent0 + j, kb0 + krel, gbase + (pj + 3 + un), (f & SDB_FLAG_TOMBSTONE) ? 0 : vl, be64_at(x[0], x[1]), f, 0,
-                  0);
+        put_entry(a, ent0 + j, kb0 + krel, klen, gbase + (pj + 3 + un), (f & SDB_FLAG_TOMBSTONE) ? 0 : vl,
+                  be64_at(x[0], x[1]), f, 0, 0);
     }
 }
 
@@ -1291,10 +1324,10 @@ SDB_DEV void emit_v1(const DecodeArgs &a, const BlockViewT<P> &v, uint64_t ent0,
         const uint64_t inc = wave_incl_scan((uint64_t)kl);
         if (i < R) {
             const uint64_t kp = carry + inc - kl;
-            uint8_t *dst = a.out.key_arena + kp;
+            uint8_t *dst = key_dst(a, kp, kl);
             for (uint32_t q = 0; q < r.prefix; q++) dst[q] = v.d[4 + q];
             for (uint32_t q = 0; q < r.suf; q++) dst[r.prefix + q] = v.d[r.suf_pos + q];
-            put_entry(a, ent0 + i, kp, gbase + r.val_pos, r.vlen, r.seq, r.flags, r.cts, r.ets);
+            put_entry(a, ent0 + i, kp, kl, gbase + r.val_pos, r.vlen, r.seq, r.flags, r.cts, r.ets);
         }
         carry += wave_readlane(inc, 63);
     }
@@ -1309,7 +1342,7 @@ SDB_DEV bool emit_v2_pieces(const DecodeArgs &a, uint64_t s, const BlockView &v,
         const Tally pt = tally_v2(pv);
         const bool lds_keys = pt.key_bytes + 16 <= kDecKeys;
         emit_v2(a, pv, false, ent, kb, s + base, lds_keys ? kbuf : nullptr);
-        if (lds_keys) {
+        if (lds_keys && !a.descending) {  // (descending: each lane stored its keys)
             wave_sync_d();
             wave_store_bytes(a.out.key_arena + kb, kbuf, pt.key_bytes);
         }
@@ -1337,8 +1370,13 @@ SDB_DEV void dec_finish(const DecodeArgs &a) {
 // Small batches (a.small: <= 1024 blocks, one per wave — a 2 MiB read_blocks range is ~520) skip the
 // three scan kernels: every workgroup scans the per-block counts itself (one 1024-thread scan), and
 // the last workgroup to finish writes the summary (no k_dec_finish launch).
-__global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
+// DESC: the order as a compile-time constant of the local copy, so the ascending instance carries none
+// of the mirroring
+template <bool DESC>
+__global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    DecodeArgs a = a0;  // + the output totals (descending order mirrors every entry and key against them)
+    a.descending = DESC ? 1u : 0u;
     bool run = true;
     if (lds_addr((const void *)smem) != 0) {  // sdb_crc.h's lookups assume the tables at LDS address 0
         if (threadIdx.x == 0) atomicMin(a.err, (unsigned long long)SDB_DEVICE_ERROR);
@@ -1396,6 +1434,8 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
     (void)gwave;
     // capacity guard: if the counted output does not fit the caller's arrays, write nothing
     if (tot_ent > a.out.cap_entries || tot_kb > a.out.key_arena_cap) run = false;
+    a.dn = tot_ent;
+    a.dkb = tot_kb;
     // one block ahead: its offsets (scalar loads: these arrays are read-only here) and, fast path, its
     // granules in registers, so the block's HBM latency overlaps the previous block's work
     typedef const __attribute__((address_space(4))) uint64_t *cu64;
@@ -1469,7 +1509,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a) {
                     emit_v2(a, v, seq, ent0, kb0, s, lds_keys ? kbuf : nullptr);
                 }
                 DEC_T(t2);
-                if (lds_keys) {
+                if (lds_keys && !a.descending) {  // (descending: each lane stored its keys)
                     wave_sync_d();
                     wave_store_bytes(a.out.key_arena + kb0, kbuf, kbn);
                 }
@@ -1584,60 +1624,6 @@ __global__ void k_dec_finish(DecodeArgs a) {
     if (threadIdx.x == 0) dec_finish(a);
 }
 
-// --- descending order: reverse the decoded columns in place ------------------------------------------
-// Entry i <-> N - 1 - i for the fixed-width columns; key_off'[i] = KB - key_off[N - i]; the key arena is
-// reversed byte-wise, then each key's bytes are reversed back.  N and KB come from the summary.
-constexpr uint32_t kDescGrid = 2048, kDescThreads = 256;
-SDB_DEV bool desc_sizes(const DecodeArgs &a, uint64_t *N, uint64_t *KB) {
-    const sdb_decode_summary *sm = a.out.summary;
-    // only when the emit pass ran: OK, or a per-block corruption status (the counts stay consistent);
-    // SDB_INVALID_ARGUMENT (capacity) and SDB_DEVICE_ERROR leave key_off unwritten
-    if (sm->status == SDB_INVALID_ARGUMENT || sm->status == SDB_DEVICE_ERROR) return false;
-    *N = sm->num_entries;
-    *KB = sm->key_bytes;
-    return true;
-}
-template <typename T>
-SDB_DEV void swap_at(T *p, uint64_t i, uint64_t j) {
-    const T x = p[i];
-    p[i] = p[j];
-    p[j] = x;
-}
-__global__ __launch_bounds__(kDescThreads) void k_desc_cols(DecodeArgs a) {
-    uint64_t N, KB;
-    if (!desc_sizes(a, &N, &KB)) return;
-    const sdb_decoded_out &o = a.out;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; 2 * i <= N; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t j = N - i;  // key_off has N + 1 entries
-        const uint64_t ki = o.key_off[i], kj = o.key_off[j];
-        o.key_off[i] = KB - kj;
-        o.key_off[j] = KB - ki;
-        if (2 * i + 1 < N) {  // the N fixed-width entries: i <-> N - 1 - i
-            const uint64_t m = N - 1 - i;
-            swap_at(o.val_off, i, m);
-            swap_at(o.val_len, i, m);
-            swap_at(o.seq, i, m);
-            swap_at(o.flags, i, m);
-            swap_at(o.create_ts, i, m);
-            swap_at(o.expire_ts, i, m);
-        }
-    }
-}
-__global__ __launch_bounds__(kDescThreads) void k_desc_bytes(DecodeArgs a) {
-    uint64_t N, KB;
-    if (!desc_sizes(a, &N, &KB)) return;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; 2 * i + 1 < KB; i += (uint64_t)gridDim.x * blockDim.x)
-        swap_at(a.out.key_arena, i, KB - 1 - i);
-}
-__global__ __launch_bounds__(kDescThreads) void k_desc_keys(DecodeArgs a) {
-    uint64_t N, KB;
-    if (!desc_sizes(a, &N, &KB)) return;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < N; j += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t lo = a.out.key_off[j], hi = a.out.key_off[j + 1];
-        while (lo + 1 < hi) swap_at(a.out.key_arena, lo++, --hi);
-    }
-}
-
 hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
     static std::once_flag attrs;
     static hipError_t attr_err = hipSuccess;
@@ -1645,7 +1631,10 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
         attr_err = hipFuncSetAttribute((const void *)k_dec_count, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)kCntLds);
         if (attr_err == hipSuccess)
-            attr_err = hipFuncSetAttribute((const void *)k_dec_emit, hipFuncAttributeMaxDynamicSharedMemorySize,
+            attr_err = hipFuncSetAttribute((const void *)k_dec_emit<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)kDecLds);
+        if (attr_err == hipSuccess)
+            attr_err = hipFuncSetAttribute((const void *)k_dec_emit<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)kDecLds);
     });
     if (attr_err != hipSuccess) return attr_err;
@@ -1672,13 +1661,11 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
         hipMemsetAsync(a.ent_start, 0, 8, st);
         hipMemsetAsync(a.key_start, 0, 8, st);
     }
-    if (a.nblocks) hipLaunchKernelGGL(k_dec_emit, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
-    if (!a.small) hipLaunchKernelGGL(k_dec_finish, dim3(1), dim3(64), 0, st, a);
-    if (a.descending && a.nblocks) {
-        hipLaunchKernelGGL(k_desc_cols, dim3(kDescGrid), dim3(kDescThreads), 0, st, a);
-        hipLaunchKernelGGL(k_desc_bytes, dim3(kDescGrid), dim3(kDescThreads), 0, st, a);
-        hipLaunchKernelGGL(k_desc_keys, dim3(kDescGrid), dim3(kDescThreads), 0, st, a);
+    if (a.nblocks) {
+        if (a.descending) hipLaunchKernelGGL(k_dec_emit<true>, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
+        else hipLaunchKernelGGL(k_dec_emit<false>, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
     }
+    if (!a.small) hipLaunchKernelGGL(k_dec_finish, dim3(1), dim3(64), 0, st, a);
     return hipGetLastError();
 }
 

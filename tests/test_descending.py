@@ -87,7 +87,7 @@ def device_desc(rt, data, block_off, version):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("version", [1, 2])
-@pytest.mark.parametrize("bs", [256, 4096])
+@pytest.mark.parametrize("bs", [256, 4096, 16384])
 def test_descending_device(rt, version, bs):
     from .test_gpu_parity import assert_decode_same
     for b in (datasets.d3(n=3000), dup_batch(), datasets.d1(n=60000)):
