@@ -8,17 +8,20 @@
 #   6. PMC FETCH / WRITE of the bloom, the compaction and the decode      -> rp/pmc_{bloom,compact,dec}_*/
 #   7. SQ counter passes over the encode and the decode                   -> rp/sq_{enc,dec}/
 # Then on the host: python3 scripts/collect_profiles.py $TAG
-# Stops at the first failing step.
+# Stops at the first failing step.  PART=1: steps 1-4, PART=2: steps 5-7 (two gpurun calls), default both.
 set -u
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 O=gpurun_out/rp
-rm -rf $O; mkdir -p $O
+PART=${PART:-all}
+[ "$PART" = 2 ] || { rm -rf $O; }
+mkdir -p $O
 step() {  # name timeout command...
   local n=$1 t=$2; shift 2
   timeout -k 10 $t "$@" > $O/$n.log 2>&1 < /dev/null
   local rc=$?; echo "$n rc=$rc"; [ $rc -eq 0 ] || exit $rc
 }
+if [ "$PART" != 2 ]; then
 step bench 400 python3 bench.py
 grep '^{' $O/bench.log > $O/bench.json; cut -c1-300 $O/bench.json
 step enc 300 rocprofv3 --kernel-trace --stats -d $O/enc -o run --output-format csv -- python3 bench.py --streams 1 --steps 100 --warmup 10 --no-cpu --no-verify --single-steps 0 --stage-steps 0
@@ -27,6 +30,8 @@ for c in FETCH_SIZE WRITE_SIZE; do
 done
 step configs 600 python3 scripts/bench_configs.py
 grep '^{' $O/configs.log > $O/configs.jsonl; cut -c1-200 $O/configs.jsonl
+fi
+[ "$PART" = 1 ] && { echo done; exit 0; }
 step dec 300 rocprofv3 --kernel-trace --stats -d $O/dec -o run --output-format csv -- python3 scripts/bench_configs.py --decode --no-granular --reps 5 --cpu-seconds 0
 step bloom 200 rocprofv3 --kernel-trace --stats -d $O/bloom -o run --output-format csv -- python3 scripts/bench_configs.py --bloom --reps 20
 step compact 300 rocprofv3 --kernel-trace --stats -d $O/compact -o run --output-format csv -- python3 scripts/bench_configs.py --compact --reps 8
