@@ -24,7 +24,7 @@ PROF = os.path.join(ROOT, "profiles")
 
 
 def kname(s):
-    s = re.sub(r"\(.*", "", s).replace("void ", "").replace("sdb::", "")
+    s = re.sub(r"\(.*", "", s.replace("(anonymous namespace)::", "")).replace("void ", "").replace("sdb::", "")
     return re.sub(r"<.*", "", s).strip()
 
 

@@ -13,7 +13,7 @@ import sys
 
 
 def kname(s):
-    s = re.sub(r"\(.*", "", s).replace("void ", "").replace("sdb::", "")
+    s = re.sub(r"\(.*", "", s.replace("(anonymous namespace)::", "")).replace("void ", "").replace("sdb::", "")
     return re.sub(r"<.*", "", s).strip()
 
 
