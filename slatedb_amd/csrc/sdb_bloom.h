@@ -296,31 +296,32 @@ SDB_DEV void bloom_fill_slice(uint32_t s, const uint8_t *__restrict__ key_bytes,
     const uint32_t lo = s << pl.sb;
     auto set = [&](uint32_t p) { atomicOr(&bits[(p - lo) >> 5], 1u << (p & 31)); };
     if (!s_over && pl.sb <= 16) {
-        // u16 offsets: wave w takes tiles w, w + nw, ...; lane l reads offsets l, l + 64, ...; four
-        // slots in flight per wave
-        const uint32_t w = tid >> 6, nw = nt >> 6, l = tid & 63;
+        // u16 offsets, 16 bytes (eight offsets) per lane: a wave reads four tiles' slots per load
+        // instruction (lane group g = l / 16 takes a tile, lane gl its offsets 8 gl .. 8 gl + 7), four such
+        // loads in flight per lane; a slot holds a run of ~T*k/S offsets (under 128 but for the tail of
+        // the distribution: longer runs loop on).  Slots start 16-byte aligned (cap is a multiple of 8).
+        const uint32_t w = tid >> 6, nw = nt >> 6, l = tid & 63, g = l >> 4, gl = l & 15;
         const uint16_t *base = (const uint16_t *)q.slot + (uint64_t)s * T * q.cap;
         auto set16 = [&](uint32_t o) { atomicOr(&bits[o >> 5], 1u << (o & 31)); };
-        for (uint32_t t0 = w; t0 < T; t0 += 4 * nw) {
-            uint32_t v[4][4];
+        constexpr uint32_t kU = 4;
+        for (uint32_t t0 = 4 * w; t0 < T; t0 += 4 * nw * kU) {
+            uint4 v[kU];
+            uint32_t c[kU];
 #pragma unroll
-            for (uint32_t u = 0; u < 4; u++) {
-                const uint32_t t = t0 + u * nw;
-                const uint32_t c = t < T ? cnt[t] : 0;
-#pragma unroll
-                for (uint32_t r = 0; r < 4; r++) {
-                    const uint32_t i = l + 64 * r;
-                    v[u][r] = i < c ? base[(uint64_t)t * q.cap + i] : kNoProbe;
-                }
+            for (uint32_t u = 0; u < kU; u++) {  // unconditional loads (a clamped in-bounds slot when idle)
+                const uint32_t t = t0 + u * 4 * nw + g;
+                c[u] = t < T ? cnt[t] : 0;
+                const uint32_t tc = t < T ? t : 0, o = 8 * gl < q.cap ? 8 * gl : 0;  // inside the slot
+                v[u] = *(const uint4 *)(base + (uint64_t)tc * q.cap + o);
             }
 #pragma unroll
-            for (uint32_t u = 0; u < 4; u++) {
+            for (uint32_t u = 0; u < kU; u++) {
+                const uint32_t wv[4] = {v[u].x, v[u].y, v[u].z, v[u].w}, i0 = 8 * gl;
 #pragma unroll
-                for (uint32_t r = 0; r < 4; r++)
-                    if (v[u][r] != kNoProbe) set16(v[u][r]);
-                const uint32_t t = t0 + u * nw;  // runs longer than 256 probes (q.cap > 256)
-                const uint32_t c = t < T ? cnt[t] : 0;
-                for (uint32_t i = 256 + l; i < c; i += 64) set16(base[(uint64_t)t * q.cap + i]);
+                for (uint32_t j = 0; j < 8; j++)
+                    if (i0 + j < c[u]) set16((wv[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
+                const uint32_t t = t0 + u * 4 * nw + g;
+                for (uint32_t i = 128 + gl; i < c[u]; i += 16) set16(base[(uint64_t)t * q.cap + i]);
             }
         }
     } else if (!s_over) {

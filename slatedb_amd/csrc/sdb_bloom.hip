@@ -408,9 +408,9 @@ uint32_t bloom_slot_cap(const BloomPlan &pl) {
     const double frac = pl.m ? (double)(1ull << pl.sb) / pl.m : 1.0;
     const double mean = (double)pl.T * pl.k * (frac < 1.0 ? frac : 1.0);
     uint64_t cap = (uint64_t)(mean + 6.0 * __builtin_sqrt(mean + 1.0)) + 16;
-    cap = (cap + 3) & ~3ull;
+    cap = (cap + 7) & ~7ull;  // a multiple of 8: u16 slots start 16-byte aligned (bloom_fill_slice)
     const uint64_t most = (uint64_t)pl.T * pl.k;  // a slot never holds more than the tile's probes
-    if (cap > most) cap = (most + 3) & ~3ull;
+    if (cap > most) cap = (most + 7) & ~7ull;
     return (uint32_t)cap;
 }
 
