@@ -18,7 +18,8 @@ def main():
     hosts = [datasets.d1(sst_index=j) for j in range(8)]
     dbs = [h.to_device(dev) for h in hosts]
     s = torch.cuda.Stream(device=dev)
-    for bs in (1024, 2048, 4096, 8192, 16384, 32768, 65536):
+    sizes = [int(x) for x in os.environ.get("SDB_BLOCK_SIZES", "1024,2048,4096,8192,16384,32768,65536").split(",")]
+    for bs in sizes:
         prm = runtime.params(block_size=bs, sst_version=2, bloom_bits_per_key=10)
         outs = [runtime.DeviceSstOutput(h.n, h.logical_bytes(), h.logical_bytes(), prm, device=dev, workspace=False)
                 for h in hosts]
