@@ -85,7 +85,13 @@ __global__ __launch_bounds__(256) void k_bloom_query(const uint8_t *bitmap, uint
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t kDenseThreads = 512, kDenseSliceBits = 16, kDenseMaxSlices = 4096;
 constexpr uint32_t kOrThreads = 512;
-constexpr uint32_t kOrNs = 2, kOrLanes = 8, kOrSeg = 64 / kOrLanes, kOrUnroll = 8;
+#ifndef SDB_OR_NS
+#define SDB_OR_NS 2
+#endif
+#ifndef SDB_OR_LANES
+#define SDB_OR_LANES 8
+#endif
+constexpr uint32_t kOrNs = SDB_OR_NS, kOrLanes = SDB_OR_LANES, kOrSeg = 64 / kOrLanes, kOrUnroll = 8;
 static_assert(kOrNs >= 1 && kOrNs <= 7, "a tile row of kOrNs + 1 u16 run starts fits 16 bytes");
 constexpr uint32_t kOrLds = 150 * 1024;
 
