@@ -4,11 +4,11 @@
 //   k_mg_prefix   per input entry: 8-byte big-endian key prefix; run order check
 //   k_mg_rank     per input entry: its merged position = own index + one binary search per other run
 //                 (MergeIterator order, merge_iterator.rs:55-69: key asc, seq desc, then run)
-//   k_mg_group    per merged position: first version of its key?; merge operand check
-//                 (MergeOperatorRequiredIterator, merge_operator.rs:213-223)
-//   k_mg_retain   per key: apply_retention_filter (retention_iterator.rs:91-204) -> keep / drop /
-//                 keep as a tombstone per version
-//   k_mg_tiles    per kMergeTile positions: kept entries, key bytes, value bytes
+//   k_mg_keys     per merged position: first version of its key?; merge operand check
+//                 (MergeOperatorRequiredIterator, merge_operator.rs:213-223); per key, on its first
+//                 version's thread: apply_retention_filter (retention_iterator.rs:91-204) -> keep / drop /
+//                 keep as a tombstone per version, and the kept entries / key / value bytes per
+//                 kMergeTile positions
 //   k_mg_scan     one workgroup: tile offsets, the summary
 //   k_mg_emit     per kMergeTile positions: the output batch (metadata + key / value bytes)
 //   k_cut         one lane: the compactor's max_sst_size walk (compactor_executor.rs:833-858) over
@@ -27,9 +27,12 @@ namespace {
 
 constexpr uint32_t kPfxThreads = 256;
 
+// The run holding global entry g: the number of runs after the first that start at or below g (bases
+// ascend; an empty run shares its successor's base).  The loop index is uniform, so the bases are
+// scalar loads of the kernel arguments and no load waits on g.
 SDB_DEV uint32_t run_of(const MergeArgs &a, uint64_t g) {
     uint32_t r = 0;
-    while (r + 1 < a.nruns && g >= a.r[r + 1].base) r++;
+    for (uint32_t k = 1; k < a.nruns; k++) r += g >= a.r[k].base ? 1u : 0u;
     return r;
 }
 
@@ -69,6 +72,7 @@ SDB_DEV int cmp_key(uint64_t pa, const uint8_t *a, uint32_t na, uint64_t pb, con
 // tie on every prefix and compare their bytes from HBM).  Checked by k_mg_prefix's full run-order test:
 // the rank and group kernels only run when every run is sorted.
 __global__ void k_mg_lcp0(MergeArgs a) {
+    for (uint64_t x = threadIdx.x; x < 3 * (uint64_t)a.ntiles; x += blockDim.x) a.tile_sum[x] = 0;  // k_mg_keys adds
     if (threadIdx.x) return;
     if (a.gate && *a.gate != ~0ull) {  // a failed input: the job fails with its status, nothing is merged
         *a.err = *a.gate;
@@ -170,25 +174,6 @@ __global__ __launch_bounds__(kPfxThreads) void k_mg_rank(MergeArgs a) {
     a.perm[pos] = g;
 }
 
-__global__ __launch_bounds__(kPfxThreads) void k_mg_group(MergeArgs a) {
-    const uint64_t p = (uint64_t)blockIdx.x * kPfxThreads + threadIdx.x;
-    if (p >= a.total || *a.err != ~0ull) return;
-    const uint64_t g = a.perm[p];
-    const uint32_t r = run_of(a, g);
-    const RunDesc &R = a.r[r];
-    const uint64_t i = g - R.base;
-    uint8_t st = 1;
-    if (p > 0) {
-        const uint64_t h = a.perm[p - 1];
-        const RunDesc &Q = a.r[run_of(a, h)];
-        const KeyAt x = key_at(Q, h - Q.base), y = key_at(R, i);
-        st = cmp_key(a.pfx[h], x.p, x.n, a.pfx[g], y.p, y.n, *a.lcp0) != 0;
-    }
-    a.start[p] = st;
-    if (!a.ret.merge_operands && (R.flags[i] & SDB_FLAG_MERGE_OPERAND))
-        report_error(a.err_merge, p, SDB_MERGE_OPERATOR_MISSING);
-}
-
 struct Ver {
     uint64_t seq;
     int64_t ets;
@@ -205,98 +190,178 @@ SDB_DEV Ver ver_at(const MergeArgs &a, uint64_t p) {
     return v;
 }
 
-// One thread per key (the thread of its first version): the versions newest first
-// (retention_iterator.rs:91-204 over the RetentionBuffer's BTreeMap, :381-398).
-__global__ __launch_bounds__(kPfxThreads) void k_mg_retain(MergeArgs a) {
-    const uint64_t p = (uint64_t)blockIdx.x * kPfxThreads + threadIdx.x;
-    if (p >= a.total || !a.start[p] || *a.err != ~0ull || *a.err_merge != ~0ull) return;
-    uint64_t end = p + 1;
-    while (end < a.total && !a.start[end]) end++;
-    const sdb_retention &rt = a.ret;
-    uint64_t nv = 0, nm = 0;
-    bool broken = false;
-    Ver cur = ver_at(a, p);
-    for (uint64_t q = p; q < end; q++) {
-        Ver nxt{};
-        if (q + 1 < end) nxt = ver_at(a, q + 1);
-        uint8_t d = 0;
-        // a later version with the same seq replaces this one (BTreeMap::insert)
-        if (!broken && !(q + 1 < end && nxt.seq == cur.seq)) {
-            const bool is_merge = (cur.flags & SDB_FLAG_MERGE_OPERAND) != 0;
-            bool skip = false;
-            d = 1;
-            if ((cur.flags & SDB_FLAG_HAS_EXPIRE_TS) && cur.ets <= rt.compaction_start_ts) {
-                if (is_merge) {  // expired merge operands are skipped
-                    nm++;
-                    skip = true;
-                    d = 0;
-                } else {         // expired values / tombstones become tombstones
-                    nv++;
-                    d = 2;
-                }
-            }
-            if (!skip) {
-                const bool cont = (rt.has_time_window && cur.seq >= rt.time_seq) ||
-                                  (rt.has_min_seq && cur.seq > rt.min_seq) || is_merge;
-                if (!cont) broken = true;
-            }
-        }
-        a.dec[q] = d;
-        cur = nxt;
-    }
-    if (rt.filter_tombstone) {  // pop the tombstones in the tail
-        for (uint64_t q = end; q-- > p;) {
-            const uint8_t d = a.dec[q];
-            if (!d) continue;
-            if (d == 2 || (ver_at(a, q).flags & SDB_FLAG_TOMBSTONE)) a.dec[q] = 0;
-            else break;
-        }
-    }
-    if (nv) atomicAdd(&a.metric[0], (unsigned long long)nv);
-    if (nm) atomicAdd(&a.metric[1], (unsigned long long)nm);
-}
+static_assert(kMergeTile % kPfxThreads == 0, "a k_mg_keys workgroup lies in one tile");
 
-struct OutSizes {
-    uint64_t keep, kb, vb;
+// What k_mg_keys needs of the entry at merged position q: one level of gathers after perm[q].
+struct PosInfo {
+    uint64_t pf, seq;
+    const uint8_t *kp;
+    const int64_t *ets_src;
+    uint32_t kn, vlen;
+    uint8_t flags;
 };
-SDB_DEV OutSizes out_sizes(const MergeArgs &a, uint64_t p) {
-    OutSizes s{0, 0, 0};
-    if (p >= a.total) return s;
-    const uint8_t d = a.dec[p];
-    if (!d) return s;
-    const uint64_t g = a.perm[p];
+SDB_DEV PosInfo pos_info(const MergeArgs &a, uint64_t q) {
+    const uint64_t g = a.perm[q];
     const RunDesc &R = a.r[run_of(a, g)];
     const uint64_t i = g - R.base;
-    s.keep = 1;
-    s.kb = R.key_off[i + 1] - R.key_off[i];
-    s.vb = (d == 1 && !(R.flags[i] & SDB_FLAG_TOMBSTONE)) ? R.val_len[i] : 0;
-    return s;
+    PosInfo x;
+    const uint64_t k0 = R.key_off[i], k1 = R.key_off[i + 1];
+    x.pf = a.pfx[g];
+    x.seq = R.seq[i];
+    x.flags = R.flags[i];
+    x.vlen = R.val_len[i];
+    x.ets_src = R.expire_ts ? R.expire_ts + i : nullptr;  // read only when the flags carry one (rare)
+    x.kp = R.key_arena + k0;
+    x.kn = (uint32_t)(k1 - k0);
+    return x;
+}
+
+// Per merged position p: is it the first version of its key (its key differs from position p - 1's,
+// MergeIterator order)?  The merge operand check (MergeOperatorRequiredIterator, merge_operator.rs:
+// 213-223).  The thread of a key's first version then runs retention over the key's versions, newest
+// first (retention_iterator.rs:91-204 over the RetentionBuffer's BTreeMap, :381-398), writes dec[] per
+// version and sums the kept entries / key bytes / value bytes into the tile of kMergeTile positions
+// each version lies in (k_mg_lcp0 zeroed the tile sums; one atomic per workgroup and field, a version
+// past the workgroup's tile adds on its own).  Lanes hold consecutive positions: the neighbours' keys
+// come by DPP (lanes 0 / 63 gather theirs alongside their own), and a key with one version (the common
+// case) is decided from the lane's own gathers.
+__global__ __launch_bounds__(kPfxThreads) void k_mg_keys(MergeArgs a) {
+    __shared__ unsigned long long s_sum[3];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    if (tid < 3) s_sum[tid] = 0;
+    __syncthreads();
+    const uint64_t p0 = (uint64_t)blockIdx.x * kPfxThreads, p = p0 + tid, T0 = p0 / kMergeTile;
+    unsigned long long *ts = (unsigned long long *)a.tile_sum;
+    uint64_t c = 0, kb = 0, vb = 0;  // this workgroup's tile
+    if (*a.err == ~0ull) {  // (uniform: the DPP exchanges below run on every lane)
+        const uint32_t L0 = *a.lcp0;
+        const uint64_t n = a.total;
+        const bool live = p < n;
+        // lane 0 also gathers position p - 1, lane 63 position p + 1 (the others re-read their own)
+        const uint64_t qo = lane == 0 ? (p > 0 ? p - 1 : p) : lane == 63 ? (p + 1 < n ? p + 1 : p) : p;
+        PosInfo me{}, ot{};
+        if (live) {
+            me = pos_info(a, p);
+            ot = pos_info(a, qo);
+        }
+        uint64_t ppf = wave_prev_lane(me.pf), pkp = wave_prev_lane((uint64_t)me.kp);
+        uint32_t pkn = wave_prev_lane(me.kn);
+        uint64_t npf = wave_next_lane(me.pf), nkp = wave_next_lane((uint64_t)me.kp);
+        uint32_t nkn = wave_next_lane(me.kn);
+        if (lane == 0) {
+            ppf = ot.pf;
+            pkp = (uint64_t)ot.kp;
+            pkn = ot.kn;
+        } else if (lane == 63) {
+            npf = ot.pf;
+            nkp = (uint64_t)ot.kp;
+            nkn = ot.kn;
+        }
+        if (live) {
+            if (!a.ret.merge_operands && (me.flags & SDB_FLAG_MERGE_OPERAND))
+                report_error(a.err_merge, p, SDB_MERGE_OPERATOR_MISSING);
+            const bool first = p == 0 || cmp_key(ppf, (const uint8_t *)pkp, pkn, me.pf, me.kp, me.kn, L0) != 0;
+            const bool more = p + 1 < n && cmp_key(npf, (const uint8_t *)nkp, nkn, me.pf, me.kp, me.kn, L0) == 0;
+            const sdb_retention &rt = a.ret;
+            if (first && !more) {  // one version: it is the newest, so only expiry and the tombstone filter apply
+                uint8_t d = 1;
+                if ((me.flags & SDB_FLAG_HAS_EXPIRE_TS) && (me.ets_src ? *me.ets_src : 0) <= rt.compaction_start_ts) {
+                    const bool is_merge = (me.flags & SDB_FLAG_MERGE_OPERAND) != 0;
+                    atomicAdd(&a.metric[is_merge ? 1 : 0], 1ull);
+                    d = is_merge ? 0 : 2;
+                }
+                if (rt.filter_tombstone && (d == 2 || (d && (me.flags & SDB_FLAG_TOMBSTONE)))) d = 0;
+                a.dec[p] = d;
+                if (d) {
+                    c = 1;
+                    kb = me.kn;
+                    vb = (d == 1 && !(me.flags & SDB_FLAG_TOMBSTONE)) ? me.vlen : 0;
+                }
+            } else if (first) {  // several versions: walk them from HBM
+                auto same = [&](uint64_t q) {  // position q holds this key
+                    const uint64_t h = a.perm[q];
+                    const RunDesc &Q = a.r[run_of(a, h)];
+                    const KeyAt x = key_at(Q, h - Q.base);
+                    return cmp_key(a.pfx[h], x.p, x.n, me.pf, me.kp, me.kn, L0) == 0;
+                };
+                uint64_t end = p + 2;
+                while (end < n && same(end)) end++;
+                uint64_t nv = 0, nm = 0;
+                bool broken = false;
+                Ver cur = ver_at(a, p);
+                for (uint64_t q = p; q < end; q++) {
+                    Ver nxt{};
+                    if (q + 1 < end) nxt = ver_at(a, q + 1);
+                    uint8_t d = 0;
+                    // a later version with the same seq replaces this one (BTreeMap::insert)
+                    if (!broken && !(q + 1 < end && nxt.seq == cur.seq)) {
+                        const bool is_merge = (cur.flags & SDB_FLAG_MERGE_OPERAND) != 0;
+                        bool skip = false;
+                        d = 1;
+                        if ((cur.flags & SDB_FLAG_HAS_EXPIRE_TS) && cur.ets <= rt.compaction_start_ts) {
+                            if (is_merge) {  // expired merge operands are skipped
+                                nm++;
+                                skip = true;
+                                d = 0;
+                            } else {         // expired values / tombstones become tombstones
+                                nv++;
+                                d = 2;
+                            }
+                        }
+                        if (!skip) {
+                            const bool cont = (rt.has_time_window && cur.seq >= rt.time_seq) ||
+                                              (rt.has_min_seq && cur.seq > rt.min_seq) || is_merge;
+                            if (!cont) broken = true;
+                        }
+                    }
+                    a.dec[q] = d;
+                    cur = nxt;
+                }
+                if (rt.filter_tombstone) {  // pop the tombstones in the tail
+                    for (uint64_t q = end; q-- > p;) {
+                        const uint8_t d = a.dec[q];
+                        if (!d) continue;
+                        if (d == 2 || (ver_at(a, q).flags & SDB_FLAG_TOMBSTONE)) a.dec[q] = 0;
+                        else break;
+                    }
+                }
+                if (nv) atomicAdd(&a.metric[0], (unsigned long long)nv);
+                if (nm) atomicAdd(&a.metric[1], (unsigned long long)nm);
+                // output sizes of the kept versions (all of them carry this key)
+                for (uint64_t q = p; q < end; q++) {
+                    const uint8_t d = a.dec[q];
+                    if (!d) continue;
+                    const uint64_t h = a.perm[q];
+                    const RunDesc &Q = a.r[run_of(a, h)];
+                    const uint64_t qi = h - Q.base;
+                    const uint64_t v = (d == 1 && !(Q.flags[qi] & SDB_FLAG_TOMBSTONE)) ? Q.val_len[qi] : 0;
+                    const uint64_t T = q / kMergeTile;
+                    if (T == T0) {
+                        c++;
+                        kb += me.kn;
+                        vb += v;
+                    } else {
+                        atomicAdd(&ts[3 * T + 0], 1ull);
+                        atomicAdd(&ts[3 * T + 1], (unsigned long long)me.kn);
+                        if (v) atomicAdd(&ts[3 * T + 2], (unsigned long long)v);
+                    }
+                }
+            }
+        }
+    }
+    c = wave_sum(c);
+    kb = wave_sum(kb);
+    vb = wave_sum(vb);
+    if (lane == 0) {
+        if (c) atomicAdd(&s_sum[0], (unsigned long long)c);
+        if (kb) atomicAdd(&s_sum[1], (unsigned long long)kb);
+        if (vb) atomicAdd(&s_sum[2], (unsigned long long)vb);
+    }
+    __syncthreads();
+    if (tid < 3 && s_sum[tid]) atomicAdd(&ts[3 * T0 + tid], s_sum[tid]);
 }
 
 constexpr uint32_t kPerT = kMergeTile / kMergeThreads;
-
-__global__ __launch_bounds__(kMergeThreads) void k_mg_tiles(MergeArgs a) {
-    if (*a.err != ~0ull || *a.err_merge != ~0ull) return;
-    __shared__ uint64_t s_w[17];
-    const uint64_t p0 = (uint64_t)blockIdx.x * kMergeTile + (uint64_t)threadIdx.x * kPerT;
-    uint64_t c = 0, kb = 0, vb = 0, t;
-    for (uint32_t u = 0; u < kPerT; u++) {
-        const OutSizes s = out_sizes(a, p0 + u);
-        c += s.keep;
-        kb += s.kb;
-        vb += s.vb;
-    }
-    uint64_t tc, tk, tv;
-    block_excl_scan_u64(c, s_w, &tc);
-    block_excl_scan_u64(kb, s_w, &tk);
-    block_excl_scan_u64(vb, s_w, &tv);
-    (void)t;
-    if (threadIdx.x == 0) {
-        a.tile_sum[3 * (uint64_t)blockIdx.x + 0] = tc;
-        a.tile_sum[3 * (uint64_t)blockIdx.x + 1] = tk;
-        a.tile_sum[3 * (uint64_t)blockIdx.x + 2] = tv;
-    }
-}
 
 // One workgroup: exclusive tile offsets, the totals and the summary.
 __global__ __launch_bounds__(kMergeThreads) void k_mg_scan(MergeArgs a) {
@@ -320,9 +385,11 @@ __global__ __launch_bounds__(kMergeThreads) void k_mg_scan(MergeArgs a) {
         }
     }
     if (threadIdx.x) return;
+    // (a job that fails reports no retention counts: k_mg_keys ran its walks before the errors were known)
+    const bool clean = e1 == ~0ull && e2 == ~0ull;
     sm->num_in = a.total;
-    sm->expired_values = a.metric[0];
-    sm->expired_merges = a.metric[1];
+    sm->expired_values = clean ? a.metric[0] : 0;
+    sm->expired_merges = clean ? a.metric[1] : 0;
     sm->pad = 0;
     sm->first_error_entry = ~0ull;
     int32_t st = SDB_OK;
@@ -830,13 +897,11 @@ hipError_t launch_merge(const MergeArgs &a, bool emit, hipStream_t st) {
         return hipErrorUnknown;
     const uint32_t gb = (uint32_t)((a.total + kPfxThreads - 1) / kPfxThreads);
     if (gb) {
-        hipLaunchKernelGGL(k_mg_lcp0, dim3(1), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(k_mg_lcp0, dim3(1), dim3(256), 0, st, a);
         hipLaunchKernelGGL(k_mg_prefix, dim3(gb), dim3(kPfxThreads), 0, st, a);
         hipLaunchKernelGGL(k_mg_rank, dim3(gb), dim3(kPfxThreads), 0, st, a);
-        hipLaunchKernelGGL(k_mg_group, dim3(gb), dim3(kPfxThreads), 0, st, a);
-        hipLaunchKernelGGL(k_mg_retain, dim3(gb), dim3(kPfxThreads), 0, st, a);
+        hipLaunchKernelGGL(k_mg_keys, dim3(gb), dim3(kPfxThreads), 0, st, a);
     }
-    if (a.ntiles) hipLaunchKernelGGL(k_mg_tiles, dim3(a.ntiles), dim3(kMergeThreads), 0, st, a);
     hipLaunchKernelGGL(k_mg_scan, dim3(1), dim3(kMergeThreads), 0, st, a);
     if (emit && a.ntiles) hipLaunchKernelGGL(k_mg_emit, dim3(a.ntiles), dim3(kMergeThreads), 0, st, a);
     return hipGetLastError();
