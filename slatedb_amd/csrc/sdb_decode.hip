@@ -646,7 +646,7 @@ SDB_DEV bool tally_v2_fast(const LdsBlockView &v, Tally &t, uint16_t *rowpos, ui
         if (end <= p || end > v.data_end) bad = 1;
     }
     uint32_t ne = 0, kb = 0, kmax = 0, prevlen = 0, fl = 0;
-    const uint32_t rec = (l < 4) ? 32u : 0u;  // positions recorded for regions 0..3, <= 32 rows each
+    const uint32_t rec = (rowpos && l < 4) ? 32u : 0u;  // positions recorded for regions 0..3, <= 32 rows each
     uint16_t *rp = rowpos + 32 * l;
     // every condition below is bit arithmetic on 0/1 values (no short-circuit), so the step compiles
     // to straight-line selects; the only branches are the loop's and the position store's
@@ -687,7 +687,7 @@ SDB_DEV bool tally_v2_fast(const LdsBlockView &v, Tally &t, uint16_t *rowpos, ui
         c = 0;
         for (uint32_t q = 0; q < R; q++) c |= (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)ne, (int)q) << (16 * q);
     }
-    if (l == 0) *rcnt = c;
+    if (l == 0 && rcnt) *rcnt = c;
     return true;
 }
 
@@ -752,7 +752,7 @@ SDB_DEV bool tally_v2_spec(const LdsBlockView &v, Tally &t, uint16_t *rowpos, ui
     t.key_bytes = wave_sum((uint64_t)(live ? klen : 0u));
     t.status = 0;
     t.sequential = false;
-    if (live && q < 4 && i < 32) rowpos[32 * q + i] = (uint16_t)c;
+    if (rowpos && live && q < 4 && i < 32) rowpos[32 * q + i] = (uint16_t)c;
     // per-region row counts for the emit pass's lane-per-row parse (<= 64 rows, keys of <= 16 bytes)
     const uint32_t kmx = wave_max(live ? klen : 0u);
     uint64_t rc = ~0ull;
@@ -766,7 +766,7 @@ SDB_DEV bool tally_v2_spec(const LdsBlockView &v, Tally &t, uint16_t *rowpos, ui
             if (cnt > 32) break;
         }
     }
-    if (l == 0) *rcnt = rc;
+    if (l == 0 && rcnt) *rcnt = rc;
     return true;
 }
 
@@ -893,7 +893,9 @@ SDB_DEV bool tally_v2_pieces(const DecodeArgs &a, uint64_t s, const BlockView &v
     Tally acc{0, 0, 0, false};
     bool irregular = false;
     const bool ok = for_each_piece(a, s, v, img, [&](const LdsBlockView &pv, uint32_t) {
-        const Tally pt = tally_v2(pv);
+        // the small-block walks first (regular rows; no positions recorded), the general one decides the rest
+        Tally pt{0, 0, 0, false};
+        if (!tally_v2_spec(pv, pt, nullptr, nullptr) && !tally_v2_fast(pv, pt, nullptr, nullptr)) pt = tally_v2(pv);
         if (pt.sequential) {
             irregular = true;
             return false;
@@ -1339,9 +1341,27 @@ SDB_DEV bool emit_v2_pieces(const DecodeArgs &a, uint64_t s, const BlockView &v,
                             uint64_t kb0) {
     uint64_t ent = ent0, kb = kb0;
     return for_each_piece(a, s, v, img, [&](const LdsBlockView &pv, uint32_t base) {
-        const Tally pt = tally_v2(pv);
+        // as a small block: the walks record the row positions of <= 4 regions in kbuf's row table, and
+        // the lane-per-row emit parses from them
+        lu16 *rows = (lu16 *)(kbuf + kRowTmp);
+        Tally pt{0, 0, 0, false};
+        uint64_t rc = ~0ull;
+#ifndef SDB_PIECE_ROWS
+#define SDB_PIECE_ROWS 1
+#endif
+        if (!SDB_PIECE_ROWS || (!tally_v2_spec(pv, pt, (uint16_t *)rows, &rc) && !tally_v2_fast(pv, pt, (uint16_t *)rows, &rc))) {
+            pt = tally_v2(pv);
+            rc = ~0ull;
+        }
+        rc = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)rc) |
+             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(rc >> 32)) << 32);  // lane 0 wrote it
         const bool lds_keys = pt.key_bytes + 16 <= kDecKeys;
-        emit_v2(a, pv, false, ent, kb, s + base, lds_keys ? kbuf : nullptr);
+        if (rc != ~0ull && pt.key_bytes + 16 <= kRowTmp) {
+            wave_sync_d();
+            emit_v2_rows(a, pv, rc, rows, ent, kb, s + base, kbuf);
+        } else {
+            emit_v2(a, pv, false, ent, kb, s + base, lds_keys ? kbuf : nullptr);
+        }
         if (lds_keys && !a.descending) {  // (descending: each lane stored its keys)
             wave_sync_d();
             wave_store_bytes(a.out.key_arena + kb, kbuf, pt.key_bytes);
