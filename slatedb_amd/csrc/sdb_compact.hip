@@ -801,7 +801,9 @@ __global__ void k_cx_gate(CxInputs in, const sdb_decode_summary *dsum, const uns
 __global__ void k_mg_pad(sdb_merged_out o, uint64_t cap) {
     const sdb_merge_summary *sm = o.summary;
     const bool ok = sm->status == SDB_OK;
-    const uint64_t from = ok ? sm->num_out + 1 : 0;  // a failed merge: the whole stream is empty entries
+    // from the first padding entry (its offset slot num_out already holds the totals: rewritten with the
+    // same value); a failed merge: the whole stream is empty entries
+    const uint64_t from = ok ? sm->num_out : 0;
     const uint64_t kt = ok ? sm->key_bytes : 0, vt = ok ? sm->val_bytes : 0;
     for (uint64_t i = from + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= cap;
          i += (uint64_t)gridDim.x * blockDim.x) {

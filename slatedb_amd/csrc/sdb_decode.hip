@@ -843,6 +843,9 @@ SDB_DEV uint32_t region_off(const BlockView &v, uint32_t q) { return (uint32_t)r
 template <typename F>
 SDB_DEV bool for_each_piece(const DecodeArgs &a, uint64_t s, const BlockView &v, lu8 *img, F f) {
     const uint32_t l = (uint32_t)lane_id(), R = v.count;
+    // only blocks parsed from HBM: a block load_block staged whole lives in this same LDS image (its
+    // trailer offsets would be overwritten by the first piece) and is walked there instead
+    if (v.d != a.blocks + s) return false;
     if (R == 0 || region_off(v, 0) != 0) return false;
     for (uint32_t q0 = 0; q0 < R; q0 += 64) {
         const uint32_t q = q0 + l;
@@ -896,21 +899,18 @@ SDB_DEV bool tally_v2_pieces(const DecodeArgs &a, uint64_t s, const BlockView &v
         // the small-block walks first (regular rows; no positions recorded), the general one decides the rest
         Tally pt{0, 0, 0, false};
         if (!tally_v2_spec(pv, pt, nullptr, nullptr) && !tally_v2_fast(pv, pt, nullptr, nullptr)) pt = tally_v2(pv);
-        if (pt.sequential) {
+        // an irregular piece, or a row that fails to parse against the piece's end (it may run on into the
+        // next piece, which the whole-block walk reads as an irregular block): the whole-block walk decides
+        if (pt.sequential || pt.status) {
             irregular = true;
             return false;
         }
-        if (pt.status) {  // the first failing region in block order; later pieces must still be regular
-            if (!acc.status) acc.status = pt.status;
-        } else if (!acc.status) {
-            acc.entries += pt.entries;
-            acc.key_bytes += pt.key_bytes;
-        }
+        acc.entries += pt.entries;
+        acc.key_bytes += pt.key_bytes;
         return true;
     });
     if (!ok || irregular) return false;
     t = acc;
-    if (t.status) t.entries = t.key_bytes = 0;
     return true;
 }
 

@@ -107,3 +107,43 @@ def test_decode_large_blocks_corrupt(rt):  # noqa: F811
     got = rt.Decoder().decode(data, e.block_off, 2)
     assert ref.status != 0
     assert_decode_same(ref, got, "corrupt big blocks")
+
+
+# ------------------------------------------------------------------------------------------------
+# size boundaries of the two passes' LDS staging (count: whole blocks up to 4096 bytes, emit: up to
+# 6144): a block staged whole is walked in place, never cut into pieces over the same LDS image; and
+# rows that straddle a piece boundary (the whole-block walk decides, exactly as the reference iterates)
+# ------------------------------------------------------------------------------------------------
+TAIL_SIZES = [4086, 4090, 4093, 4096, 4100, 4250, 5000, 5900, 6100, 6144, 6150, 7000]
+
+
+@pytest.mark.parametrize("restart_interval", [1, 16])
+def test_decode_tail_block_sizes(rt, restart_interval):  # noqa: F811
+    from .decode_cases import tail_block_case
+    from .test_descending import device_desc
+    from .test_gpu_parity import assert_decode_same
+    for target in TAIL_SIZES:
+        for seed in (0, 1):
+            b, e, _ = tail_block_case(target, restart_interval, seed=seed)
+            what = "tail %d B ri=%d seed=%d" % (target, restart_interval, seed)
+            ref = O.decode_blocks(e.data, e.block_off, 2)
+            assert ref.status == 0
+            got = rt.Decoder().decode(e.data, e.block_off, 2)
+            assert_decode_same(ref, got, what)
+            assert np.array_equal(got.key_arena, b.key_bytes), what
+            desc = O.decode_blocks(e.data, e.block_off, 2, descending=True)
+            assert_decode_same(desc, device_desc(rt, e.data, e.block_off, 2), what + " desc")
+
+
+@pytest.mark.parametrize("block_size", [8192, 16384])
+def test_decode_row_straddles_piece(rt, block_size):  # noqa: F811
+    from .decode_cases import _rows, straddle_variants
+    from .test_gpu_parity import assert_decode_same
+    e = O.encode_sst(_rows(3000, 5), O.params(block_size=block_size, bloom_bits_per_key=0))
+    statuses = set()
+    for d, data in straddle_variants(e, 1, range(1, 88, 3)):
+        ref = O.decode_blocks(data, e.block_off, 2)
+        got = rt.Decoder().decode(data, e.block_off, 2)
+        statuses.add(ref.status)
+        assert_decode_same(ref, got, "straddle +%d bs=%d" % (d, block_size))
+    assert len(statuses) >= 1
