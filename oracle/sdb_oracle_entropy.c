@@ -829,7 +829,63 @@ static int zstd_decode(const uint8_t *in, size_t n, sink *o) {
 /* ------------------------------------------------------------------------------------------- */
 /* Entry points for the codec dispatch in sdb_oracle.c                                          */
 /* ------------------------------------------------------------------------------------------- */
+/* The decoded size of a zstd stream from its frame headers alone (RFC 8878 3.1.1.1.4 Frame_Content_Size;
+ * the reference's encoder, zstd::bulk::compress at format/sst.rs:590, always writes it): frame and
+ * block headers are walked, nothing is entropy-decoded.  -1 when a frame has no content size or a
+ * header is malformed (the plan then decodes in count mode). */
+static int64_t zstd_frames_size(const uint8_t *in, size_t n) {
+    size_t ip = 0;
+    uint64_t sum = 0;
+    while (ip < n) {
+        if (n - ip < 4) return -1;
+        const uint32_t magic = rd32(in + ip);
+        ip += 4;
+        if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {
+            if (n - ip < 4) return -1;
+            const uint32_t sz = rd32(in + ip);
+            ip += 4;
+            if (n - ip < sz) return -1;
+            ip += sz;
+            continue;
+        }
+        if (magic != 0xFD2FB528u || ip >= n) return -1;
+        const unsigned fhd = in[ip++];
+        const unsigned fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, checksum = (fhd >> 2) & 1, did_flag = fhd & 3;
+        if (fhd & 8) return -1;
+        const size_t fcs_len = fcs_flag == 0 ? (single ? 1 : 0) : fcs_flag == 1 ? 2 : fcs_flag == 2 ? 4 : 8;
+        if (!fcs_len) return -1;
+        const size_t skip = (single ? 0 : 1) + (did_flag == 3 ? 4 : did_flag);
+        if (n - ip < skip + fcs_len) return -1;
+        ip += skip;
+        uint64_t fcs = 0;
+        for (size_t i = 0; i < fcs_len; i++) fcs |= (uint64_t)in[ip + i] << (8 * i);
+        if (fcs_len == 2) fcs += 256;
+        ip += fcs_len;
+        for (;;) {
+            if (n - ip < 3) return -1;
+            const uint32_t bh = in[ip] | (uint32_t)in[ip + 1] << 8 | (uint32_t)in[ip + 2] << 16;
+            ip += 3;
+            const unsigned type = (bh >> 1) & 3;
+            const size_t csz = type == 1 ? 1 : (size_t)(bh >> 3);
+            if (type == 3 || n - ip < csz) return -1;
+            ip += csz;
+            if (bh & 1) break;
+        }
+        if (checksum) {
+            if (n - ip < 4) return -1;
+            ip += 4;
+        }
+        sum += fcs;
+        if (sum > (64ull << 20)) return -1;
+    }
+    return (int64_t)sum;
+}
+
 int64_t orc_entropy_len(uint32_t codec, const uint8_t *in, size_t n) {
+    if (codec != 2) {
+        const int64_t f = zstd_frames_size(in, n);
+        if (f >= 0) return f;
+    }
     /* count mode, as the device plan: the bytes are not kept, so Adler-32 / XXH64 are verified only by
      * the decode proper (a stream whose checksum fails gets a slot here and fails in step 2) */
     sink o = {NULL, (size_t)1 << 40, 0, 0};
@@ -842,6 +898,8 @@ sdb_status orc_entropy_decompress(uint32_t codec, const uint8_t *in, size_t n, u
     sink o = {out, cap, 0, 0};
     const int r = codec == 2 ? zlib_decode(in, n, &o) : zstd_decode(in, n, &o);
     *out_len = o.len;
-    if (o.overflow) return SDB_INVALID_ARGUMENT;
+    /* zstd: a slot sized from the frames' content sizes overflows only when a frame decodes to more than
+     * it declares, which libzstd reports as corruption (the reference: BlockDecompressionError) */
+    if (o.overflow) return codec == 2 ? SDB_INVALID_ARGUMENT : SDB_DECOMPRESSION_ERROR;
     return r ? SDB_DECOMPRESSION_ERROR : SDB_OK;
 }

@@ -953,6 +953,58 @@ SDB_DEV int zstd_decode(const uint8_t *in, uint64_t n, EntOut &o, EntLds &t) {
     return 0;
 }
 
+// The decoded size of a zstd stream from its frame headers alone: zstd::bulk::compress, the
+// reference's encoder (format/sst.rs:590), writes Frame_Content_Size in every frame, so the plan walks
+// frame and block headers (3 bytes per block, no entropy decoding).  -1 when a frame has no content
+// size or a header is malformed: the caller then decodes the stream in count mode as before (and k_ent_run
+// rejects a frame whose decoded size disagrees with its header, zstd_decode above).
+SDB_DEV int zstd_frames_size(const uint8_t *in, uint64_t n, uint64_t *total) {
+    uint64_t ip = 0, sum = 0;
+    while (ip < n) {
+        if (n - ip < 4) return -1;
+        const uint32_t magic = rd32b(in + ip);
+        ip += 4;
+        if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {  // skippable frame
+            if (n - ip < 4) return -1;
+            const uint32_t sz = rd32b(in + ip);
+            ip += 4;
+            if (n - ip < sz) return -1;
+            ip += sz;
+            continue;
+        }
+        if (magic != 0xFD2FB528u || ip >= n) return -1;
+        const uint32_t fhd = in[ip++];
+        const int fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, checksum = (fhd >> 2) & 1, did_flag = fhd & 3;
+        if (fhd & 8) return -1;
+        const int fcs_len = fcs_flag == 0 ? (single ? 1 : 0) : fcs_flag == 1 ? 2 : fcs_flag == 2 ? 4 : 8;
+        if (fcs_len == 0) return -1;
+        const uint64_t hdr = (single ? 0 : 1) + (did_flag == 3 ? 4 : did_flag) + fcs_len;
+        if (n - ip < hdr) return -1;
+        ip += hdr - fcs_len;
+        uint64_t fcs = 0;
+        for (int i = 0; i < fcs_len; i++) fcs |= (uint64_t)in[ip + i] << (8 * i);
+        if (fcs_len == 2) fcs += 256;
+        ip += fcs_len;
+        for (;;) {
+            if (n - ip < 3) return -1;
+            const uint32_t bh = in[ip] | (uint32_t)in[ip + 1] << 8 | (uint32_t)in[ip + 2] << 16;
+            ip += 3;
+            const uint64_t csz = ((bh >> 1) & 3) == 1 ? 1 : (bh >> 3);  // RLE: one stored byte
+            if (((bh >> 1) & 3) == 3 || n - ip < csz) return -1;
+            ip += csz;
+            if (bh & 1) break;
+        }
+        if (checksum) {
+            if (n - ip < 4) return -1;
+            ip += 4;
+        }
+        sum += fcs;
+        if (sum > kEntMaxOut) return -1;
+    }
+    *total = sum;
+    return 0;
+}
+
 SDB_DEV int ent_decode(uint32_t codec, const uint8_t *in, uint64_t n, EntOut &o, EntLds &t) {
     return codec == SDB_CODEC_ZLIB ? zlib_decode(in, n, o, t) : zstd_decode(in, n, o, t);
 }
@@ -970,9 +1022,14 @@ __global__ __launch_bounds__(kEntThreads) void k_ent_plan(EntArgs a) {
         uint64_t slot = 0;
         if (k < a.nblocks) {
             const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
+            uint64_t fsz = 0;
             if (e >= s && e - s >= 4) {
-                EntOut o{nullptr, 0, kEntMaxOut, false};
-                if (!ent_decode(a.codec, a.blocks + s, e - s - 4, o, t) && !o.bad) slot = o.len + 4;
+                if (a.codec != SDB_CODEC_ZLIB && !zstd_frames_size(a.blocks + s, e - s - 4, &fsz)) {
+                    slot = fsz + 4;
+                } else {
+                    EntOut o{nullptr, 0, kEntMaxOut, false};
+                    if (!ent_decode(a.codec, a.blocks + s, e - s - 4, o, t) && !o.bad) slot = o.len + 4;
+                }
             }
         }
         a.slot[k] = slot;

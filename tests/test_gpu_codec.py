@@ -153,3 +153,28 @@ def test_entropy_codecs_levels_and_frames():
     want = ps + [big, big, b"hello world" + b"A" * 200, ps[8] + b"hello world" + b"A" * 200]
     for k, p in enumerate(want):
         assert out[int(start[k]):int(end[k]) - 4].tobytes() == p, k
+
+
+def test_zstd_plan_from_frame_content_size():
+    """The zstd plan reads Frame_Content_Size from the frame headers (zstd::bulk::compress writes it,
+    format/sst.rs:590) and decodes in count mode only for frames without one: device == oracle for
+    frames with and without a content size, a content size above / below what the frame decodes to,
+    and concatenated frames mixing both."""
+    from .test_codec_entropy import frame as zframe, payloads, zstd_compress
+    raw = (0, b"hello world", b"hello world")
+    rle = (1, bytes([0x41, 200]), b"A" * 200)
+    ps = payloads()
+    cases = [
+        ([zstd_compress(ps[8], 3), zframe([raw, rle]), zframe([raw], fcs=False)], None),
+        ([zframe([raw, rle], fcs=False) + zstd_compress(ps[8], 1)], None),
+        ([zframe([raw], content=b"hello world!")], 0),   # declares more than it decodes to
+        ([zframe([raw, rle], content=b"hello")], 0),     # declares less: overflows its slot
+        ([zstd_compress(ps[3], 3), zframe([raw], content=b"hello world!!", checksum=True)], 1),
+    ]
+    for i, (streams, bad) in enumerate(cases):
+        comp, coff = _raw_run(O.CODEC_ZSTD, streams)
+        out, start, end, err = _check(O.CODEC_ZSTD, comp, coff)
+        if bad is None:
+            assert err == 2**64 - 1, i
+        else:
+            assert err == (bad << 8) | _abi.SDB_DECOMPRESSION_ERROR, i
