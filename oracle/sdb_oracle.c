@@ -737,7 +737,7 @@ static sdb_status decode_one(dec_ctx *c, uint64_t base, size_t blen, uint16_t ve
             uint32_t sh, un, vl;
             if (!rd_varint(d, data_end, &pos, &sh) || !rd_varint(d, data_end, &pos, &un) ||
                 !rd_varint(d, data_end, &pos, &vl)) { st = SDB_CORRUPT_BLOCK; break; }
-            if (pos + (size_t)un + (size_t)vl + 9 > data_end || sh > curlen) { st = SDB_CORRUPT_BLOCK; break; }
+            if (pos + (size_t)un + (size_t)vl + 9 > data_end) { st = SDB_CORRUPT_BLOCK; break; }
             size_t suf = pos;
             pos += un;
             uint64_t vpos = base + pos;
@@ -751,6 +751,9 @@ static sdb_status decode_one(dec_ctx *c, uint64_t base, size_t blen, uint16_t ve
             if (pos + need > data_end) { st = SDB_CORRUPT_BLOCK; break; }
             if (f & SDB_FLAG_HAS_EXPIRE_TS) { ets = (int64_t)rd_be(d + pos, 8); pos += 8; }
             if (f & SDB_FLAG_HAS_CREATE_TS) { cts = (int64_t)rd_be(d + pos, 8); pos += 8; }
+            /* restore_full_key (row_codec_v2.rs:83-89) runs after SstRowCodecV2::decode returned the row
+             * (block_iterator_v2.rs:95-101): a bad flags byte is reported before an over-long prefix */
+            if (sh > curlen) { st = SDB_CORRUPT_BLOCK; break; }
             uint32_t out_vlen = (f & SDB_FLAG_TOMBSTONE) ? 0 : vl;
             if (!emit_entry(c, cur, sh, d + suf, un, vpos, out_vlen, seq, f, cts, ets)) { st = SDB_INVALID_ARGUMENT; break; }
             /* current_key = restored key (block_iterator_v2.rs:246) */
@@ -1464,7 +1467,7 @@ static sdb_status desc_row_v2(const uint8_t *d, size_t data_end, size_t *pos, co
     size_t p = *pos;
     if (!rd_varint(d, data_end, &p, &sh) || !rd_varint(d, data_end, &p, &un) || !rd_varint(d, data_end, &p, &vl))
         return SDB_CORRUPT_BLOCK;
-    if (p + (size_t)un + (size_t)vl + 9 > data_end || sh > curlen) return SDB_CORRUPT_BLOCK;
+    if (p + (size_t)un + (size_t)vl + 9 > data_end) return SDB_CORRUPT_BLOCK;
     size_t suf = p;
     p += un;
     e->vpos = base + p;
@@ -1478,6 +1481,7 @@ static sdb_status desc_row_v2(const uint8_t *d, size_t data_end, size_t *pos, co
     e->ets = e->cts = 0;
     if (f & SDB_FLAG_HAS_EXPIRE_TS) { e->ets = (int64_t)rd_be(d + p, 8); p += 8; }
     if (f & SDB_FLAG_HAS_CREATE_TS) { e->cts = (int64_t)rd_be(d + p, 8); p += 8; }
+    if (sh > curlen) return SDB_CORRUPT_BLOCK;  /* restore_full_key, after decode (block_iterator_v2.rs:95-101) */
     e->flags = f;
     e->vlen = (f & SDB_FLAG_TOMBSTONE) ? 0 : vl;
     if (!e->vlen) e->vpos = 0;
