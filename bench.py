@@ -12,10 +12,11 @@ timing barrier and the max / sum of scalars.  `--job-ssts 64` runs configs[4] as
 scaling); `--batch 1` is the single-SST configs[1] shape.  The single-SST latency (sdb_encode_sst,
 one SST per launch sequence) is reported beside the headline as `single_sst`.
 
-`--streams S` (default 2) runs S such builders per GPU concurrently, each on its own HIP stream with its
-own workspace and outputs (step i on stream i mod S): the flush / compaction builders of the reference
-run concurrently, and two launch sequences in flight let one's latency-bound prep kernels overlap the
-other's kernels and tails.  The same sequences back to back on ONE stream are reported as `one_stream`.
+`--streams S` (default 1) runs S such builders per GPU concurrently, each on its own HIP stream with its
+own workspace and outputs (step i on stream i mod S).  A kernel trace of two builders (DESIGN.md §5,
+profiles/r4_two_builders_trace.txt) shows why one is the default: k_emit takes every CU's VGPRs and most
+of its LDS, so nothing co-resides with it; the two builders fall into lock-step (both preps, then both
+emits one after the other) and lose to the same sequences back to back on one stream.
 
   python bench.py [--gpus N --steps K --warmup W --batch B]   (N > 1: spawns N ranks itself)
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -47,7 +48,7 @@ def parse():
     p.add_argument("--steps", type=int, default=2200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch", type=int, default=8, help="SSTs per GPU per step (one sdb_encode_ssts call)")
-    p.add_argument("--streams", type=int, default=2,
+    p.add_argument("--streams", type=int, default=1,
                    help="concurrent builders per GPU: step i runs on stream i mod S (its own workspace and outputs)")
     p.add_argument("--job-ssts", type=int, default=0,
                    help="configs[4] fixed job: J distinct SSTs over all ranks (SST j -> rank j mod N), one pass per step")
@@ -246,15 +247,12 @@ def main():
         st = stream if one_stream else streams[i % len(streams)]
         runtime.encode_ssts_device(sets[i % nsets], outs[q], prm, wss[q], st)
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-
-    # verify against the oracle (bit-exact) before timing: the first and the last SST of a set
+    # verify against the oracle (bit-exact) before the warmup, so the timed region follows the warmup
+    # steps directly (the host-side oracle check leaves the GPU idle for about a second)
     verified = None
+    step(0)
+    torch.cuda.synchronize()
     if not args.no_verify:
-        step(0)
-        torch.cuda.synchronize()
         from oracle import oracle as O
         oprm = O.params(block_size=args.block_size, sst_version=2, bloom_bits_per_key=args.bpk)
         verified = True
@@ -269,6 +267,10 @@ def main():
                 assert ok, "GPU output of SST %d differs from the oracle" % q
     sm = outs[0][0].summary_host()
     alg_sst = hosts[0].algorithmic_input_bytes() + sm.data_len + sm.bloom_len
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
 
     # timed region
     if dist:

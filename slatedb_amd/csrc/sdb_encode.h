@@ -236,8 +236,7 @@ struct SstSlot {
 struct SstSet {
     uint32_t count;
     uint32_t block_size, restart_interval, version, wal, seg_look;
-    uint32_t max_facts, max_chunks, max_groups, max_tiles, max_slices;
-    uint32_t emit_pool;  // k_emit: the set's last emit_pool / 64 of blocks are a shared pool (work stealing)
+    uint32_t max_facts, max_chunks, max_groups, max_tiles, max_slices, pad;
     SstSlot s[kMaxSsts];
 };
 

@@ -1913,32 +1913,21 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(SstSet P) {
     if (run) {
         lu32 *crc = (lu32 *)smem;
         (void)crc;
-        // schedule: workgroup b owns an equal share [r0, r1) of the set's first S blocks; its waves start
-        // on blocks r0 + wave and then take the rest in order from an LDS ticket, so a wave that runs fast
-        // takes more.  (One global ticket for all waves measured 3x slower: the atomics serialise.)  The
-        // last nb - S blocks (P.emit_pool / 64 of them) are a pool every wave draws from once its
-        // workgroup's share is taken (one global atomic per block), so workgroups that started late on
-        // CUs another builder's kernels still held take fewer blocks.
+        // schedule: workgroup b owns an equal share [r0, r1) of the set's blocks; its waves start on
+        // blocks r0 + wave and then take the rest in order from an LDS ticket, so a wave that runs fast
+        // takes more.  (One global ticket for all waves measured 3x slower: the atomics serialise.)
         const uint32_t nb = pre[kMaxSsts];
-        const uint32_t S = nb - (uint32_t)((uint64_t)nb * P.emit_pool / 64);
-        const uint32_t r0 = (uint32_t)((uint64_t)S * blockIdx.x / gridDim.x);
-        const uint32_t r1 = (uint32_t)((uint64_t)S * (blockIdx.x + 1) / gridDim.x);
-        uint32_t *gpool = make_args(P, 0).done + 1;  // zeroed by k_group (SST 0) before every launch set
-        auto pool_take = [&]() -> uint32_t {  // lane 0 only
-            if (S == nb) return nb;
-            const uint32_t u = __hip_atomic_fetch_add(gpool, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return u < nb - S ? S + u : nb;
-        };
+        const uint32_t r0 = (uint32_t)((uint64_t)nb * blockIdx.x / gridDim.x);
+        const uint32_t r1 = (uint32_t)((uint64_t)nb * (blockIdx.x + 1) / gridDim.x);
         uint32_t blk = r0 + wave, si = 0, lb = 0;
-        if (blk >= r1) blk = (uint32_t)__builtin_amdgcn_readfirstlane((int)(l == 0 ? pool_take() : 0u));
         locate(blk, si, lb);
         // the first block's descriptor is in flight while the CRC tables are copied, its values and
         // metadata while the workgroup does the slow blocks and sets up the ticket
-        const uint32_t dv0 = (blk < nb && l < 14) ? desc_dw(si)[14 * (uint64_t)lb + l] : 0;
+        const uint32_t dv0 = (blk < r1 && l < 14) ? desc_dw(si)[14 * (uint64_t)lb + l] : 0;
         crc_tables_to_lds(crc);
         BlockDesc dn = desc_from_lanes(dv0);
         EmitPre pn;
-        bool fn = blk < nb && emit_fast(dn);
+        bool fn = blk < r1 && emit_fast(dn);
         if (fn) emit_prefetch(make_args(P, si), dn, pn);
         __syncthreads();
         for (uint32_t i = 0; i < P.count; i++) {
@@ -1955,18 +1944,15 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(SstSet P) {
         lSpanCopy *rtab = (lSpanCopy *)(kst + kKeyStageCap);
         lu32 *ticket = (lu32 *)(smem + kCrcLds);
         auto take = [&]() -> uint32_t {
-            uint32_t g = 0;
-            if (l == 0) {
-                const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                g = r0 + t < r1 ? r0 + t : pool_take();
-            }
-            return (uint32_t)__builtin_amdgcn_readfirstlane((int)g);
+            uint32_t t = 0;
+            if (l == 0) t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return r0 + (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
         };
-        if (blk < nb) {
+        if (blk < r1) {
             uint32_t nblk = take(), nsi = 0, nlb = 0;
             locate(nblk, nsi, nlb);
-            uint32_t dv = (nblk < nb && l < 14) ? desc_dw(nsi)[14 * (uint64_t)nlb + l] : 0;
-            while (blk < nb) {
+            uint32_t dv = (nblk < r1 && l < 14) ? desc_dw(nsi)[14 * (uint64_t)nlb + l] : 0;
+            while (blk < r1) {
                 const BlockDesc d = dn;
                 const EmitPre p = pn;
                 const bool fast = fn;
@@ -1974,13 +1960,13 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(SstSet P) {
                 blk = nblk;
                 si = nsi;
                 lb = nlb;
-                if (blk < nb) {  // issue the next block (and the descriptor of the one after it)
+                if (blk < r1) {  // issue the next block (and the descriptor of the one after it)
                     dn = desc_from_lanes(dv);
                     fn = emit_fast(dn);
                     if (fn) emit_prefetch(make_args(P, si), dn, pn);
                     nblk = take();
                     locate(nblk, nsi, nlb);
-                    dv = (nblk < nb && l < 14) ? desc_dw(nsi)[14 * (uint64_t)nlb + l] : 0;
+                    dv = (nblk < r1 && l < 14) ? desc_dw(nsi)[14 * (uint64_t)nlb + l] : 0;
                 }
                 if (fast) emit_block<V>(make_args(P, csi), clb, d, p, img, kst, rtab, crc, ph);  // others: k_emit_big, slow path
             }
@@ -2271,7 +2257,6 @@ extern "C" int sdb_diag_phase_times(uint64_t *out, int nblocks) {
 
 static int g_cus = 0;
 static uint32_t g_emit_threads = kEmitThreads, g_emit_wg_per_cu = kEmitWgPerCu;
-static uint32_t g_emit_pool = 0;  // k_emit's shared tail pool, in 1/64 of the set's blocks (SDB_EMIT_POOL)
 static std::once_flag g_attrs_once;
 static uint32_t emit_grid() { return (uint32_t)(g_cus > 0 ? g_emit_wg_per_cu * g_cus : 512); }
 static uint32_t emit_lds() { return kCrcLds + 16 + (g_emit_threads / 64) * kEmitWaveLds; }
@@ -2284,10 +2269,6 @@ static void set_lds_attrs() {
         if (const char *e = getenv("SDB_EMIT_THREADS")) {
             uint32_t t = (uint32_t)atoi(e);
             if (t >= 64 && t <= kEmitThreads && t % 64 == 0) g_emit_threads = t;
-        }
-        if (const char *e = getenv("SDB_EMIT_POOL")) {
-            const int t = atoi(e);
-            if (t >= 0 && t <= 64) g_emit_pool = (uint32_t)t;
         }
         if (const char *e = getenv("SDB_EMIT_WG_PER_CU")) {
             uint32_t t = (uint32_t)atoi(e);
@@ -2312,11 +2293,9 @@ static void set_lds_attrs() {
 // ------------------------------------------------------------------------------------------------
 static_assert(kChunk == kFactsEntries && kFactsThreads == kBinThreads, "bloom tiles are k_facts' chunks of kChunk keys");
 
-hipError_t launch_encode_set(const SstSet &P0, size_t bin_lds, size_t fill_lds, hipStream_t st) {
+hipError_t launch_encode_set(const SstSet &P, size_t bin_lds, size_t fill_lds, hipStream_t st) {
     set_lds_attrs();
-    if (!P0.count) return hipSuccess;
-    SstSet P = P0;
-    P.emit_pool = g_emit_pool;
+    if (!P.count) return hipSuccess;
     // every kernel on the caller's stream, in dependency order: the set is large enough to fill the
     // chip at each step, and one stream keeps the sequence capturable into a HIP graph
     stage_mark(st, kStFacts, true);
