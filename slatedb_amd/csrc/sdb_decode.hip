@@ -34,7 +34,7 @@ constexpr uint32_t kDecImg = 4096 + 32;                  // fast path: staged bl
 constexpr uint32_t kDecKeys = 2048;                      // fast path: restored keys of one block
 constexpr uint32_t kDecGuard = 64;                       // zero lead-in of the right-aligned CRC segments
 constexpr uint32_t kDecWaveLds = kDecGuard + kDecImg + kDecKeys;
-constexpr uint32_t kDecLds = kCrcTablesLds + (kDecThreads / 64) * kDecWaveLds;
+constexpr uint32_t kDecLds = (kDecThreads / 64) * kDecWaveLds;  // emit passes: no CRC tables (the count pass checked)
 constexpr uint32_t kDecCap = kDecWaveLds - kDecGuard;
 // count pass: the CRC tables, the bank-replicated byte table (sdb_crc.h), then per wave a guard + image
 constexpr uint32_t kCntWaveLds = kDecGuard + kDecImg;
@@ -914,8 +914,48 @@ SDB_DEV bool tally_v2_pieces(const DecodeArgs &a, uint64_t s, const BlockView &v
     return true;
 }
 
-// D1 count.  LDS: the CRC tables at address 0 (sdb_crc.h: this kernel has no static LDS), then one
-// region of kDecWaveLds per wave.
+// Per-block flag bits (DecodeArgs::flag), written by the count passes, read by the emit passes.
+constexpr uint8_t kFlagSeq = 1;  // V2 block walked sequentially (irregular restart regions)
+constexpr uint8_t kFlagGen = 2;  // emitted by k_dec_emit_gen (V1, rows not recorded, keys over the row table, big)
+constexpr uint8_t kFlagBig = 4;  // over one wave image: counted by k_dec_count_big
+
+// The blocks of wave w in the passes that pick flagged blocks ([k0, k1), contiguous): the flags are
+// read 64 at a time (one byte per lane) and the flagged blocks taken in order from the ballot.
+template <typename F>
+SDB_DEV void for_flagged(const DecodeArgs &a, uint8_t bit, uint64_t gwave, uint64_t nwaves, F f) {
+    const uint64_t per = (a.nblocks + nwaves - 1) / nwaves, k0 = gwave * per;
+    const uint64_t k1 = k0 + per < a.nblocks ? k0 + per : a.nblocks;
+    for (uint64_t b = k0; b < k1; b += 64) {
+        const uint64_t k = b + lane_id();
+        uint64_t m = __ballot(k < k1 && (a.flag[k] & bit));
+        while (m) {
+            const uint32_t i = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            f(b + i);
+        }
+    }
+}
+
+SDB_DEV void count_result(const DecodeArgs &a, uint64_t k, const Tally &t, uint8_t gen) {
+    if (lane_id() != 0) return;
+    if (t.status) {
+        a.cnt[k] = 0;
+        a.kbytes[k] = 0;
+        a.flag[k] = 0;
+        atomicMin(a.err, (unsigned long long)((k << 8) | (uint64_t)t.status));
+        unsigned long long slot = atomicAdd(a.nbad, 1ull);
+        if (slot < a.bad_cap) a.bad_block[slot] = (uint32_t)k;
+    } else {
+        a.cnt[k] = t.entries;
+        a.kbytes[k] = t.key_bytes;
+        a.flag[k] = (uint8_t)((t.sequential ? kFlagSeq : 0) | gen);
+    }
+}
+
+// D1 count, blocks of one wave image (dec_fast); the others are flagged kFlagBig for k_dec_count_big.
+// A block the lane-per-row emit takes (V2, rows recorded, keys within the row table) is left unflagged;
+// the rest are flagged kFlagGen.  LDS: the CRC tables at address 0 (sdb_crc.h: this kernel has no
+// static LDS), then one region of kCntWaveLds per wave.
 __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if (lds_addr((const void *)smem) != 0) {  // sdb_crc.h's lookups assume the tables at LDS address 0
@@ -924,11 +964,9 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
     }
     crc_tables_to_lds((lu32 *)smem);
     __syncthreads();
-    const uint32_t(*crc)[256] = (const uint32_t(*)[256])smem;
     const uint32_t wave = threadIdx.x >> 6;
     lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kCntWaveLds + kDecGuard;
     if (lane_id() < kDecGuard / 4) ((lu32 *)(img - kDecGuard))[lane_id()] = 0;  // never written again
-    uint8_t *stage = (uint8_t *)img;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
     (void)gwave;
@@ -950,8 +988,12 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
             if (dec_fast(ns, ne)) gran_load(a, ns, ne, pre);
         }
         Tally t{0, 0, 0, false};
+        if (!dec_fast(s, e)) {
+            if (lane_id() == 0) a.flag[k] = kFlagBig;
+            continue;
+        }
         if (lane_id() == 0) a.rcnt[k] = ~0ull;  // row positions not recorded (tally_v2_fast overwrites)
-        if (dec_fast(s, e)) {
+        {
                         // slicing-by-8 CRC: the pass is VALU-bound, and the bank-replicated byte table costs twice the
             // VALU per byte for its conflict-free lookups (515 vs 479 us on configs[2])
             const LdsBlockView v = stage_lds(a, s, e, img, true, &cur);
@@ -968,31 +1010,44 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
             DEC_ACC(0, 0, t1 - t0);
             DEC_ACC(0, 1, t2 - t1);
             DEC_ACC(0, 3, 1);
-        } else {
-            const BlockView v = load_block(a, k, stage, crc, kDecImg);
-            t.status = v.status;
-            if (!v.status) {
-                if (a.version == 1) t = tally_v1(v);
-                else if (!tally_v2_pieces(a, s, v, img, t)) t = tally_v2(v);
-            }
-            if (!v.status && a.descending && a.version == 2) desc_rule(v.count, t);
         }
-        if (lane_id() == 0) {
-            if (t.status) {
-                a.cnt[k] = 0;
-                a.kbytes[k] = 0;
-                a.flag[k] = 0;
-                atomicMin(a.err, (unsigned long long)((k << 8) | (uint64_t)t.status));
-                unsigned long long slot = atomicAdd(a.nbad, 1ull);
-                if (slot < a.bad_cap) a.bad_block[slot] = (uint32_t)k;
-            } else {
-                a.cnt[k] = t.entries;
-                a.kbytes[k] = t.key_bytes;
-                a.flag[k] = t.sequential ? 1 : 0;
-            }
-        }
+        uint8_t gen = kFlagGen;
+        if (lane_id() == 0 && a.version == 2 && !t.sequential && t.key_bytes + 16 <= kRowTmp && a.rcnt[k] != ~0ull) gen = 0;
+        count_result(a, k, t, gen);
         wave_sync_d();
     }
+}
+
+// D1 count of the blocks over one wave image (kFlagBig): CRC through LDS windows, rows parsed from HBM
+// or as restart-region pieces staged in LDS.  Every such block is emitted by k_dec_emit_gen.
+__global__ __launch_bounds__(kDecThreads) void k_dec_count_big(DecodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (lds_addr((const void *)smem) != 0) {
+        if (threadIdx.x == 0) atomicMin(a.err, (unsigned long long)SDB_DEVICE_ERROR);
+        return;
+    }
+    crc_tables_to_lds((lu32 *)smem);
+    __syncthreads();
+    const uint32_t(*crc)[256] = (const uint32_t(*)[256])smem;
+    const uint32_t wave = threadIdx.x >> 6;
+    lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kCntWaveLds + kDecGuard;
+    if (lane_id() < kDecGuard / 4) ((lu32 *)(img - kDecGuard))[lane_id()] = 0;
+    uint8_t *stage = (uint8_t *)img;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    for_flagged(a, kFlagBig, gwave, nwaves, [&](uint64_t k) {
+        const uint64_t s = a.block_off[k];
+        Tally t{0, 0, 0, false};
+        const BlockView v = load_block(a, k, stage, crc, kDecImg);
+        t.status = v.status;
+        if (!v.status) {
+            if (a.version == 1) t = tally_v1(v);
+            else if (!tally_v2_pieces(a, s, v, img, t)) t = tally_v2(v);
+        }
+        if (!v.status && a.descending && a.version == 2) desc_rule(v.count, t);
+        count_result(a, k, t, kFlagGen);
+        wave_sync_d();
+    });
 }
 
 // --- emit -----------------------------------------------------------------------------------------
@@ -1387,9 +1442,13 @@ SDB_DEV void dec_finish(const DecodeArgs &a) {
 }
 
 // D3 emit: one wave per block, stage again (no CRC: the count pass checked it), write the columns.
-// Small batches (a.small: <= 1024 blocks, one per wave — a 2 MiB read_blocks range is ~520) skip the
-// three scan kernels: every workgroup scans the per-block counts itself (one 1024-thread scan), and
-// the last workgroup to finish writes the summary (no k_dec_finish launch).
+// k_dec_emit takes the blocks the count pass left unflagged (V2, one wave image, row positions recorded:
+// the lane-per-row emit) and writes every block's entry start; k_dec_emit_gen the kFlagGen blocks (V1,
+// sequential or unrecorded walks, blocks over one image), so the common path carries none of their
+// registers.  Small batches (a.small: <= 1024 blocks, one per wave — a 2 MiB read_blocks range is ~520)
+// skip the three scan kernels: every workgroup of k_dec_emit scans the per-block counts itself (one
+// 1024-thread scan, workgroup 0 stores the result for k_dec_emit_gen), and the last workgroup of
+// k_dec_emit_gen writes the summary (no k_dec_finish launch).
 // DESC: the order as a compile-time constant of the local copy, so the ascending instance carries none
 // of the mirroring
 template <bool DESC>
@@ -1398,14 +1457,10 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a0) {
     DecodeArgs a = a0;  // + the output totals (descending order mirrors every entry and key against them)
     a.descending = DESC ? 1u : 0u;
     bool run = true;
-    if (lds_addr((const void *)smem) != 0) {  // sdb_crc.h's lookups assume the tables at LDS address 0
-        if (threadIdx.x == 0) atomicMin(a.err, (unsigned long long)SDB_DEVICE_ERROR);
-        run = false;
-    }
     uint64_t s_ent0 = 0, s_ent1 = 0, s_kb0 = 0, s_kb1 = 0, tot_ent = 0, tot_kb = 0;
     if (a.small) {
         // exclusive scans of cnt / kbytes over all blocks; scratch in wave 0's (still unused) region
-        uint64_t *sw = (uint64_t *)(smem + kCrcTablesLds);
+        uint64_t *sw = (uint64_t *)smem;
         uint64_t *sres = sw + 32;
         const uint32_t t = threadIdx.x, b0 = blockIdx.x * (kDecThreads / 64);
         const uint64_t vx = t < a.nblocks ? a.cnt[t] : 0, vy = t < a.nblocks ? a.kbytes[t] : 0;
@@ -1441,14 +1496,10 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a0) {
         tot_ent = a.ent_start[a.nblocks];
         tot_kb = a.key_start[a.nblocks];
     }
-    // no CRC tables: every block was checked by the count pass (load_block / stage_lds run unchecked here)
-    __syncthreads();
-    const uint32_t(*crc)[256] = (const uint32_t(*)[256])smem;
     const uint32_t wave = threadIdx.x >> 6;
     const int l = lane_id();
-    lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kDecWaveLds + kDecGuard;
+    lu8 *img = (lu8 *)smem + wave * kDecWaveLds + kDecGuard;
     lu8 *kbuf = img + kDecImg;
-    uint8_t *stage = (uint8_t *)img;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
     (void)gwave;
@@ -1468,7 +1519,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a0) {
     struct Meta {
         uint64_t ent0, ent1, kb0, kb1, rcw;
         uint32_t fw;  // the dword of the flag array holding this block's flag
-        SDB_DEV uint64_t rc(uint64_t kk) const { return ((fw >> (8 * (kk & 3))) & 0xFF) ? ~0ull : rcw; }
+        SDB_DEV bool gen(uint64_t kk) const { return ((fw >> (8 * (kk & 3))) & kFlagGen) != 0; }
     };
     typedef const __attribute__((address_space(4))) uint32_t *cu32;
     auto meta_load = [&](uint64_t kk, Meta &m) {
@@ -1505,48 +1556,84 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a0) {
             meta_load(k + nwaves, m1);
         }
         const uint64_t ent0 = m.ent0;
-        const uint64_t n_ent = m.ent1 - ent0;
         if (l == 0) a.out.block_entry_start[k] = ent0;
-        if (n_ent == 0) continue;
+        if (m.ent1 == ent0 || m.gen(k)) continue;  // nothing to emit, or k_dec_emit_gen's
         const uint64_t kb0 = m.kb0;
-        const uint64_t kbn = m.kb1 - kb0;
-        const uint64_t rc = m.rc(k);
-        const bool seq = rc == ~0ull && ((m.fw >> (8 * (k & 3))) & 0xFF) != 0;
+        DEC_T(t0);
+        const LdsBlockView v = stage_lds(a, s, e, img, false, &cur);
+        if (v.status) continue;  // cannot happen: the count pass accepted it
+        DEC_T(t1);
+        ((lu32 *)(kbuf + kRowTmp))[l] = rp;
+        wave_sync_d();
+        emit_v2_rows(a, v, m.rcw, (const lu16 *)(kbuf + kRowTmp), ent0, kb0, s, kbuf);
+        DEC_T(t2);
+        if (!a.descending) {  // (descending: each lane stored its keys)
+            wave_sync_d();
+            wave_store_bytes(a.out.key_arena + kb0, kbuf, m.kb1 - kb0);
+        }
+        DEC_T(t3);
+        DEC_ACC(1, 0, t1 - t0);
+        DEC_ACC(1, 1, t2 - t1);
+        DEC_ACC(1, 2, t3 - t2);
+        DEC_ACC(1, 3, 1);
+        wave_sync_d();
+    }
+}
+
+// D3 emit of the kFlagGen blocks: V1 rows, V2 blocks walked sequentially or by regions without recorded
+// rows, keys over the row table, and blocks over one wave image (restart-region pieces, or the walk from
+// HBM).  Small batches: the last workgroup writes the summary.
+template <bool DESC>
+__global__ __launch_bounds__(kDecThreads) void k_dec_emit_gen(DecodeArgs a0) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    DecodeArgs a = a0;
+    a.descending = DESC ? 1u : 0u;
+    const uint64_t tot_ent = a.ent_start[a.nblocks], tot_kb = a.key_start[a.nblocks];
+    const bool run = tot_ent <= a.out.cap_entries && tot_kb <= a.out.key_arena_cap;
+    a.dn = tot_ent;
+    a.dkb = tot_kb;
+    const uint32_t wave = threadIdx.x >> 6;
+    const int l = lane_id();
+    lu8 *img = (lu8 *)smem + wave * kDecWaveLds + kDecGuard;
+    lu8 *kbuf = img + kDecImg;
+    uint8_t *stage = (uint8_t *)img;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    if (run) for_flagged(a, kFlagGen, gwave, nwaves, [&](uint64_t k) {
+        const uint64_t ent0 = a.ent_start[k], kb0 = a.key_start[k];
+        const uint64_t kbn = a.key_start[k + 1] - kb0;
+        if (a.ent_start[k + 1] == ent0) return;
+        const uint8_t f = a.flag[k];
+        const bool seq = (f & kFlagSeq) != 0;
+        const uint64_t s = a.block_off[k], e = block_end_of(a, k);
         if (dec_fast(s, e)) {
-            DEC_T(t0);
-            const LdsBlockView v = stage_lds(a, s, e, img, false, &cur);
-            if (v.status) continue;  // cannot happen: the count pass accepted it
-            DEC_T(t1);
+            const LdsBlockView v = stage_lds(a, s, e, img, false, nullptr);
+            if (v.status) return;
             if (a.version == 1) {
                 emit_v1(a, v, ent0, kb0, s);
             } else {
                 const bool lds_keys = kbn + 16 <= kDecKeys;
+                const uint64_t rc = seq ? ~0ull : a.rcnt[k];
                 if (rc != ~0ull && kbn + 16 <= kRowTmp) {
-                    ((lu32 *)(kbuf + kRowTmp))[l] = rp;
+                    ((lu32 *)(kbuf + kRowTmp))[l] = ((const uint32_t *)(a.rowpos + 128 * k))[l];
                     wave_sync_d();
                     emit_v2_rows(a, v, rc, (const lu16 *)(kbuf + kRowTmp), ent0, kb0, s, kbuf);
                 } else {
                     emit_v2(a, v, seq, ent0, kb0, s, lds_keys ? kbuf : nullptr);
                 }
-                DEC_T(t2);
-                if (lds_keys && !a.descending) {  // (descending: each lane stored its keys)
+                if (lds_keys && !a.descending) {
                     wave_sync_d();
                     wave_store_bytes(a.out.key_arena + kb0, kbuf, kbn);
                 }
-                DEC_T(t3);
-                DEC_ACC(1, 1, t2 - t1);
-                DEC_ACC(1, 2, t3 - t2);
             }
-            DEC_ACC(1, 0, t1 - t0);
-            DEC_ACC(1, 3, 1);
         } else {
-            const BlockView v = load_block(a, k, stage, crc, kDecCap, false);
-            if (v.status) continue;
+            const BlockView v = load_block(a, k, stage, nullptr, kDecCap, false);
+            if (v.status) return;
             if (a.version == 1) emit_v1(a, v, ent0, kb0, s);
             else if (seq || !emit_v2_pieces(a, s, v, img, kbuf, ent0, kb0)) emit_v2(a, v, seq, ent0, kb0, s, nullptr);
         }
         wave_sync_d();
-    }
+    });
     if (a.small) {
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -1651,11 +1738,12 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
         attr_err = hipFuncSetAttribute((const void *)k_dec_count, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)kCntLds);
         if (attr_err == hipSuccess)
-            attr_err = hipFuncSetAttribute((const void *)k_dec_emit<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)kDecLds);
-        if (attr_err == hipSuccess)
-            attr_err = hipFuncSetAttribute((const void *)k_dec_emit<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)kDecLds);
+            attr_err = hipFuncSetAttribute((const void *)k_dec_count_big, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)kCntLds);
+        for (const void *f : {(const void *)k_dec_emit<false>, (const void *)k_dec_emit<true>,
+                              (const void *)k_dec_emit_gen<false>, (const void *)k_dec_emit_gen<true>})
+            if (attr_err == hipSuccess)
+                attr_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDecLds);
     });
     if (attr_err != hipSuccess) return attr_err;
     hipLaunchKernelGGL(k_dec_init, dim3(1), dim3(64), 0, st, a);
@@ -1666,7 +1754,10 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
     if (cus > 0 && wgs > (uint64_t)cus) wgs = (uint64_t)cus;
     if (wgs == 0) wgs = 1;
     const size_t lds = kDecLds;
-    if (a.nblocks) hipLaunchKernelGGL(k_dec_count, dim3((uint32_t)wgs), dim3(kDecThreads), kCntLds, st, a);
+    if (a.nblocks) {
+        hipLaunchKernelGGL(k_dec_count, dim3((uint32_t)wgs), dim3(kDecThreads), kCntLds, st, a);
+        hipLaunchKernelGGL(k_dec_count_big, dim3((uint32_t)wgs), dim3(kDecThreads), kCntLds, st, a);
+    }
     // scans: ent_start = excl(cnt), key_start = excl(kbytes); small batches scan inside k_dec_emit
     a.small = a.nblocks > 0 && a.nblocks <= kScanTile && wgs * (kDecThreads / 64) >= a.nblocks ? 1u : 0u;
     uint64_t nt = (a.nblocks + kScanTile - 1) / kScanTile;
@@ -1682,8 +1773,13 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
         hipMemsetAsync(a.key_start, 0, 8, st);
     }
     if (a.nblocks) {
-        if (a.descending) hipLaunchKernelGGL(k_dec_emit<true>, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
-        else hipLaunchKernelGGL(k_dec_emit<false>, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
+        if (a.descending) {
+            hipLaunchKernelGGL(k_dec_emit<true>, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
+            hipLaunchKernelGGL(k_dec_emit_gen<true>, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
+        } else {
+            hipLaunchKernelGGL(k_dec_emit<false>, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
+            hipLaunchKernelGGL(k_dec_emit_gen<false>, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
+        }
     }
     if (!a.small) hipLaunchKernelGGL(k_dec_finish, dim3(1), dim3(64), 0, st, a);
     return hipGetLastError();
