@@ -20,16 +20,18 @@ if [ -z "${NOTEST:-}" ]; then
   step tests 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread
   tail -2 $O/tests.log
 fi
-for w in ${WORK:-}; do
+for w0 in ${WORK:-}; do
+  w=${w0%%:*}; v=""; unset SDB_LIBRARY
+  if [ "$w0" != "$w" ]; then v=${w0#*:}; export SDB_LIBRARY=libslatedb_amd_$v.so; echo "== variant $v"; fi
   case $w in
-    enc) step enc 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu
+    enc) step enc$v 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu
          python3 -c "
-import json; d=json.loads([l for l in open('$O/enc.log') if l.startswith('{')][0]); r=d['roofline']
+import json; d=json.loads([l for l in open('$O/enc$v.log') if l.startswith('{')][0]); r=d['roofline']
 print('enc value', d['value'], 'ms/SST', r['device_ms_per_sst'], 'frac', r['frac'], 'single', d['single_sst']['device_ms_per_sst'], {k: round(v/8*1000,1) for k,v in r['stage_ms_per_step'].items()})" ;;
     encprof) step encprof 300 rocprofv3 --kernel-trace --stats -d $O/encprof -o run --output-format csv -- python3 bench.py --steps 100 --warmup 10 --no-cpu --no-verify --single-steps 0 --stage-steps 0 ;;
-    dec) step dec 300 python3 scripts/bench_configs.py --decode --no-granular --reps 10 --cpu-seconds 0
-         grep '^{' $O/dec.log | cut -c1-400
-         step decprof 300 rocprofv3 --kernel-trace --stats -d $O/decprof -o run --output-format csv -- python3 scripts/bench_configs.py --decode --no-granular --reps 5 --cpu-seconds 0 ;;
+    dec) step dec$v 300 python3 scripts/bench_configs.py --decode --no-granular --reps 10 --cpu-seconds 0
+         grep '^{' $O/dec$v.log | cut -c1-400
+         [ -n "$v" ] || step decprof 300 rocprofv3 --kernel-trace --stats -d $O/decprof -o run --output-format csv -- python3 scripts/bench_configs.py --decode --no-granular --reps 5 --cpu-seconds 0 ;;
     bloom) step bloom 200 python3 scripts/bench_configs.py --bloom --reps 20
          grep '^{' $O/bloom.log | cut -c1-300
          step bloomprof 200 rocprofv3 --kernel-trace --stats -d $O/bloomprof -o run --output-format csv -- python3 scripts/bench_configs.py --bloom --reps 20 ;;

@@ -29,16 +29,30 @@ __device__ uint64_t g_dec_phase[2][8192][4];  // [count / emit][wave][phase] s_m
 #define DEC_T(var) do { } while (0)
 #define DEC_ACC(pass, ph, dt) do { } while (0)
 #endif
-constexpr uint32_t kDecThreads = 1024;                   // 16 waves: one workgroup (and CRC table copy) per CU
+// geometry of the count and emit passes (diagnostic knobs): threads per workgroup, workgroups per CU
+#ifndef SDB_CNT_THREADS
+#define SDB_CNT_THREADS 1024
+#endif
+#ifndef SDB_CNT_WG
+#define SDB_CNT_WG 1
+#endif
+#ifndef SDB_EM_THREADS
+#define SDB_EM_THREADS 1024
+#endif
+#ifndef SDB_EM_WG
+#define SDB_EM_WG 1
+#endif
+constexpr uint32_t kCntThreads = SDB_CNT_THREADS, kCntWg = SDB_CNT_WG, kEmThreads = SDB_EM_THREADS, kEmWg = SDB_EM_WG;
+constexpr uint32_t kCntEu = (kCntThreads / 64 * kCntWg + 3) / 4, kEmEu = (kEmThreads / 64 * kEmWg + 3) / 4;  // waves per SIMD
 constexpr uint32_t kDecImg = 4096 + 32;                  // fast path: staged block image per wave
 constexpr uint32_t kDecKeys = 2048;                      // fast path: restored keys of one block
 constexpr uint32_t kDecGuard = 64;                       // zero lead-in of the right-aligned CRC segments
 constexpr uint32_t kDecWaveLds = kDecGuard + kDecImg + kDecKeys;
-constexpr uint32_t kDecLds = (kDecThreads / 64) * kDecWaveLds;  // emit passes: no CRC tables (the count pass checked)
+constexpr uint32_t kDecLds = (kEmThreads / 64) * kDecWaveLds;  // emit passes: no CRC tables (the count pass checked)
 constexpr uint32_t kDecCap = kDecWaveLds - kDecGuard;
 // count pass: the CRC tables, the bank-replicated byte table (sdb_crc.h), then per wave a guard + image
 constexpr uint32_t kCntWaveLds = kDecGuard + kDecImg;
-constexpr uint32_t kCntLds = kCrcTablesLds + (kDecThreads / 64) * kCntWaveLds;
+constexpr uint32_t kCntLds = kCrcTablesLds + (kCntThreads / 64) * kCntWaveLds;
 static_assert(kCntLds <= 160 * 1024, "count pass LDS");
 constexpr uint32_t kRowTmp = kDecKeys - 256;  // emit: row positions of the lane-per-row path (4 x 32 u16) in kbuf
 typedef __attribute__((address_space(3))) uint16_t lu16;  // other blocks: generic staging per wave; larger ones parse from HBM
@@ -936,6 +950,17 @@ SDB_DEV void for_flagged(const DecodeArgs &a, uint8_t bit, uint64_t gwave, uint6
     }
 }
 
+// Whether any block of this workgroup's waves' ranges (for_flagged) carries `bit`: a workgroup without
+// one returns before it stages anything (the common case: a run of 4 KiB blocks has none).
+SDB_DEV bool wg_any_flagged(const DecodeArgs &a, uint8_t bit) {
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6), per = (a.nblocks + nwaves - 1) / nwaves;
+    const uint64_t k0 = (uint64_t)blockIdx.x * (blockDim.x >> 6) * per;
+    const uint64_t k1 = k0 + (blockDim.x >> 6) * per < a.nblocks ? k0 + (blockDim.x >> 6) * per : a.nblocks;
+    bool any = false;
+    for (uint64_t k = k0 + threadIdx.x; k < k1; k += blockDim.x) any |= (a.flag[k] & bit) != 0;
+    return __syncthreads_or(any) != 0;
+}
+
 SDB_DEV void count_result(const DecodeArgs &a, uint64_t k, const Tally &t, uint8_t gen) {
     if (lane_id() != 0) return;
     if (t.status) {
@@ -956,7 +981,7 @@ SDB_DEV void count_result(const DecodeArgs &a, uint64_t k, const Tally &t, uint8
 // A block the lane-per-row emit takes (V2, rows recorded, keys within the row table) is left unflagged;
 // the rest are flagged kFlagGen.  LDS: the CRC tables at address 0 (sdb_crc.h: this kernel has no
 // static LDS), then one region of kCntWaveLds per wave.
-__global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
+__global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(kCntEu))) void k_dec_count(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if (lds_addr((const void *)smem) != 0) {  // sdb_crc.h's lookups assume the tables at LDS address 0
         if (threadIdx.x == 0) atomicMin(a.err, (unsigned long long)SDB_DEVICE_ERROR);
@@ -1020,8 +1045,9 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_count(DecodeArgs a) {
 
 // D1 count of the blocks over one wave image (kFlagBig): CRC through LDS windows, rows parsed from HBM
 // or as restart-region pieces staged in LDS.  Every such block is emitted by k_dec_emit_gen.
-__global__ __launch_bounds__(kDecThreads) void k_dec_count_big(DecodeArgs a) {
+__global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(kCntEu))) void k_dec_count_big(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (!wg_any_flagged(a, kFlagBig)) return;
     if (lds_addr((const void *)smem) != 0) {
         if (threadIdx.x == 0) atomicMin(a.err, (unsigned long long)SDB_DEVICE_ERROR);
         return;
@@ -1452,7 +1478,7 @@ SDB_DEV void dec_finish(const DecodeArgs &a) {
 // DESC: the order as a compile-time constant of the local copy, so the ascending instance carries none
 // of the mirroring
 template <bool DESC>
-__global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a0) {
+__global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmEu))) void k_dec_emit(DecodeArgs a0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     DecodeArgs a = a0;  // + the output totals (descending order mirrors every entry and key against them)
     a.descending = DESC ? 1u : 0u;
@@ -1462,11 +1488,11 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a0) {
         // exclusive scans of cnt / kbytes over all blocks; scratch in wave 0's (still unused) region
         uint64_t *sw = (uint64_t *)smem;
         uint64_t *sres = sw + 32;
-        const uint32_t t = threadIdx.x, b0 = blockIdx.x * (kDecThreads / 64);
+        const uint32_t t = threadIdx.x, b0 = blockIdx.x * (kEmThreads / 64);
         const uint64_t vx = t < a.nblocks ? a.cnt[t] : 0, vy = t < a.nblocks ? a.kbytes[t] : 0;
         const uint64_t ex = block_excl_scan_u64(vx, sw, &tot_ent);
         const uint64_t ey = block_excl_scan_u64(vy, sw, &tot_kb);
-        if (t >= b0 && t < b0 + kDecThreads / 64) {
+        if (t >= b0 && t < b0 + kEmThreads / 64) {
             uint64_t *r = sres + 4 * (t - b0);
             r[0] = ex;
             r[1] = ex + vx;
@@ -1584,7 +1610,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit(DecodeArgs a0) {
 // rows, keys over the row table, and blocks over one wave image (restart-region pieces, or the walk from
 // HBM).  Small batches: the last workgroup writes the summary.
 template <bool DESC>
-__global__ __launch_bounds__(kDecThreads) void k_dec_emit_gen(DecodeArgs a0) {
+__global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmEu))) void k_dec_emit_gen(DecodeArgs a0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     DecodeArgs a = a0;
     a.descending = DESC ? 1u : 0u;
@@ -1599,7 +1625,7 @@ __global__ __launch_bounds__(kDecThreads) void k_dec_emit_gen(DecodeArgs a0) {
     uint8_t *stage = (uint8_t *)img;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-    if (run) for_flagged(a, kFlagGen, gwave, nwaves, [&](uint64_t k) {
+    if (run && wg_any_flagged(a, kFlagGen)) for_flagged(a, kFlagGen, gwave, nwaves, [&](uint64_t k) {
         const uint64_t ent0 = a.ent_start[k], kb0 = a.key_start[k];
         const uint64_t kbn = a.key_start[k + 1] - kb0;
         if (a.ent_start[k + 1] == ent0) return;
@@ -1750,16 +1776,19 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    uint64_t wgs = (a.nblocks + 15) / 16;  // one wave per block, one workgroup per CU at most
-    if (cus > 0 && wgs > (uint64_t)cus) wgs = (uint64_t)cus;
-    if (wgs == 0) wgs = 1;
+    auto grid = [&](uint32_t threads, uint32_t per_cu) {  // one wave per block, at most per_cu workgroups per CU
+        uint64_t g = (a.nblocks + threads / 64 - 1) / (threads / 64);
+        if (cus > 0 && g > (uint64_t)cus * per_cu) g = (uint64_t)cus * per_cu;
+        return g ? g : 1;
+    };
+    const uint64_t wgc = grid(kCntThreads, kCntWg), wgs = grid(kEmThreads, kEmWg);
     const size_t lds = kDecLds;
     if (a.nblocks) {
-        hipLaunchKernelGGL(k_dec_count, dim3((uint32_t)wgs), dim3(kDecThreads), kCntLds, st, a);
-        hipLaunchKernelGGL(k_dec_count_big, dim3((uint32_t)wgs), dim3(kDecThreads), kCntLds, st, a);
+        hipLaunchKernelGGL(k_dec_count, dim3((uint32_t)wgc), dim3(kCntThreads), kCntLds, st, a);
+        hipLaunchKernelGGL(k_dec_count_big, dim3((uint32_t)wgc), dim3(kCntThreads), kCntLds, st, a);
     }
     // scans: ent_start = excl(cnt), key_start = excl(kbytes); small batches scan inside k_dec_emit
-    a.small = a.nblocks > 0 && a.nblocks <= kScanTile && wgs * (kDecThreads / 64) >= a.nblocks ? 1u : 0u;
+    a.small = a.nblocks > 0 && a.nblocks <= kEmThreads && wgs * (kEmThreads / 64) >= a.nblocks ? 1u : 0u;
     uint64_t nt = (a.nblocks + kScanTile - 1) / kScanTile;
     if (a.small) {
     } else if (a.nblocks) {
@@ -1774,11 +1803,11 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t st) {
     }
     if (a.nblocks) {
         if (a.descending) {
-            hipLaunchKernelGGL(k_dec_emit<true>, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
-            hipLaunchKernelGGL(k_dec_emit_gen<true>, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
+            hipLaunchKernelGGL(k_dec_emit<true>, dim3((uint32_t)wgs), dim3(kEmThreads), lds, st, a);
+            hipLaunchKernelGGL(k_dec_emit_gen<true>, dim3((uint32_t)wgs), dim3(kEmThreads), lds, st, a);
         } else {
-            hipLaunchKernelGGL(k_dec_emit<false>, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
-            hipLaunchKernelGGL(k_dec_emit_gen<false>, dim3((uint32_t)wgs), dim3(kDecThreads), lds, st, a);
+            hipLaunchKernelGGL(k_dec_emit<false>, dim3((uint32_t)wgs), dim3(kEmThreads), lds, st, a);
+            hipLaunchKernelGGL(k_dec_emit_gen<false>, dim3((uint32_t)wgs), dim3(kEmThreads), lds, st, a);
         }
     }
     if (!a.small) hipLaunchKernelGGL(k_dec_finish, dim3(1), dim3(64), 0, st, a);
