@@ -951,14 +951,22 @@ SDB_DEV void for_flagged(const DecodeArgs &a, uint8_t bit, uint64_t gwave, uint6
 }
 
 // Whether any block of this workgroup's waves' ranges (for_flagged) carries `bit`: a workgroup without
-// one returns before it stages anything (the common case: a run of 4 KiB blocks has none).
-SDB_DEV bool wg_any_flagged(const DecodeArgs &a, uint8_t bit) {
+// one returns before it stages anything (the common case: a run of 4 KiB blocks has none).  scratch:
+// 16 dwords of the caller's dynamic LDS, free until the caller stages (__syncthreads_or would add
+// static LDS and move the dynamic region off address 0, where the CRC lookups expect their tables).
+SDB_DEV bool wg_any_flagged(const DecodeArgs &a, uint8_t bit, uint32_t *scratch) {
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6), per = (a.nblocks + nwaves - 1) / nwaves;
     const uint64_t k0 = (uint64_t)blockIdx.x * (blockDim.x >> 6) * per;
     const uint64_t k1 = k0 + (blockDim.x >> 6) * per < a.nblocks ? k0 + (blockDim.x >> 6) * per : a.nblocks;
     bool any = false;
     for (uint64_t k = k0 + threadIdx.x; k < k1; k += blockDim.x) any |= (a.flag[k] & bit) != 0;
-    return __syncthreads_or(any) != 0;
+    const bool wany = __ballot(any) != 0;
+    if (lane_id() == 0) scratch[threadIdx.x >> 6] = wany ? 1u : 0u;
+    __syncthreads();
+    uint32_t r = 0;
+    for (uint32_t q = 0; q < (blockDim.x >> 6); q++) r |= scratch[q];
+    __syncthreads();
+    return r != 0;
 }
 
 SDB_DEV void count_result(const DecodeArgs &a, uint64_t k, const Tally &t, uint8_t gen) {
@@ -1047,7 +1055,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(kCn
 // or as restart-region pieces staged in LDS.  Every such block is emitted by k_dec_emit_gen.
 __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(kCntEu))) void k_dec_count_big(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    if (!wg_any_flagged(a, kFlagBig)) return;
+    if (!wg_any_flagged(a, kFlagBig, (uint32_t *)smem)) return;
     if (lds_addr((const void *)smem) != 0) {
         if (threadIdx.x == 0) atomicMin(a.err, (unsigned long long)SDB_DEVICE_ERROR);
         return;
@@ -1625,7 +1633,7 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
     uint8_t *stage = (uint8_t *)img;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-    if (run && wg_any_flagged(a, kFlagGen)) for_flagged(a, kFlagGen, gwave, nwaves, [&](uint64_t k) {
+    if (run && wg_any_flagged(a, kFlagGen, (uint32_t *)smem)) for_flagged(a, kFlagGen, gwave, nwaves, [&](uint64_t k) {
         const uint64_t ent0 = a.ent_start[k], kb0 = a.key_start[k];
         const uint64_t kbn = a.key_start[k + 1] - kb0;
         if (a.ent_start[k + 1] == ent0) return;
