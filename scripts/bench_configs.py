@@ -415,6 +415,39 @@ def compact_bench(reps):
                                        "sample": "the whole job, oracle decode of the 4 SSTs + compact"}}), flush=True)
     comp2.close()
     comp.close()
+    # a job whose retention drops: four L0 runs over one key space (each key in ~3 runs), tombstones in the
+    # newest, no snapshot, the destination is the last run (filter_tombstone)
+    ohosts = datasets.overwrite_runs(nruns=4)
+    oruns = [Run.from_batch(h) for h in ohosts]
+    odruns = [runtime.DeviceRun.from_host(r) for r in oruns]
+    oret_d = _abi.Retention(0, 0, 0, 0, 0, 1, 0, 0)  # retention_min_seq None, no time window, filter_tombstone
+    ological = sum(h.logical_bytes() for h in ohosts)
+    comp3 = runtime.Compactor()
+    st3, ns3 = comp3.run(odruns, oret_d, prm, 256 << 20)
+    assert st3 == 0, st3
+    torch.cuda.synchronize()
+    walls3 = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        st3, ns3 = comp3.run(odruns, oret_d, prm, 256 << 20)
+        walls3.append((time.perf_counter() - t0) * 1e3)
+        assert st3 == 0
+    ms3 = float(np.median(walls3))
+    _, msum3 = comp3.merged()
+    t0 = time.perf_counter()
+    _, osm3, ocuts3, ossts3 = O.compact(oruns, O.retention(filter_tombstone=True),
+                                        O.params(block_size=4096, sst_version=2, bloom_bits_per_key=10), 256 << 20)
+    cpu3_s = time.perf_counter() - t0
+    same3 = len(ossts3) == ns3 and all(np.array_equal(comp3.sst(i)["data"], ossts3[i].data) for i in range(ns3))
+    print(json.dumps({"what": "compaction job (f2), overwrites: 4 L0 runs over one key space, tombstones in the newest, "
+                              "no snapshot, filter_tombstone -> merge + retention (drops) + cuts + encode",
+                      "entries_in": int(msum3.num_in), "entries_out": int(msum3.num_out), "output_ssts": ns3,
+                      "logical_bytes_in": ological, "ms_wall": round(ms3, 3),
+                      "GiB_per_s_logical": round(ological / (ms3 * 1e-3) / 2**30, 2), "bit_exact_vs_oracle": bool(same3),
+                      "cpu_baseline": {"kind": "port", "cores": 1, "s": round(cpu3_s, 3),
+                                       "GiB_per_s_logical": round(ological / cpu3_s / 2**30, 3),
+                                       "sample": "the whole job, oracle compact"}}), flush=True)
+    comp3.close()
 
 
 def codec_bench(reps):

@@ -28,6 +28,10 @@ for w0 in ${WORK:-}; do
          python3 -c "
 import json; d=json.loads([l for l in open('$O/enc$v.log') if l.startswith('{')][0]); r=d['roofline']
 print('enc value', d['value'], 'ms/SST', r['device_ms_per_sst'], 'frac', r['frac'], 'single', d['single_sst']['device_ms_per_sst'], {k: round(v/8*1000,1) for k,v in r['stage_ms_per_step'].items()}, 'one', d['one_stream'])" ;;
+    encx) step encx 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu ${ENCX_ARGS:-}
+         python3 -c "
+import json; d=json.loads([l for l in open('$O/encx.log') if l.startswith('{')][0]); r=d['roofline']
+print('encx ${ENCX_ARGS:-}: value', d['value'], 'ms/SST', r['device_ms_per_sst'], {k: round(v/8*1000,1) for k,v in r['stage_ms_per_step'].items()})" ;;
     encprof) step encprof 300 rocprofv3 --kernel-trace --stats -d $O/encprof -o run --output-format csv -- python3 bench.py --steps 100 --warmup 10 --no-cpu --no-verify --single-steps 0 --stage-steps 0 ;;
     dec) step dec$v 300 python3 scripts/bench_configs.py --decode --no-granular --reps 10 --cpu-seconds 0
          grep '^{' $O/dec$v.log | cut -c1-400

@@ -128,3 +128,37 @@ def d3(seed=3, n=3000):
         i += 1
     entries.sort(key=lambda e: (e[0], -e[3]))
     return Batch.from_entries(entries[:n])
+
+
+def overwrite_runs(nruns=4, n=D1_N, value_len=100, overlap=0.75, tomb_frac=0.1, seed=SEED_D1 + 77):
+    """A compaction whose retention drops entries: `nruns` L0 runs (newest first) of n entries each, drawn
+    from one key space of n / overlap 16-byte keys (D1's BE counter layout), so most keys have versions in
+    several runs; run r's seqs are (nruns - r) << 32 | position (newer runs are higher); the newest run
+    deletes tomb_frac of its keys (tombstones, no value).  With no snapshot (retention_min_seq None) and
+    filter_tombstone (the destination is the last run), retention keeps each key's newest version and
+    drops its tombstones (retention_iterator.rs:91-204, 381-398)."""
+    u = int(n / overlap)
+    start = splitmix64(seed, 0, 2)
+    hi0, lo0 = np.uint64(int(start[0]) >> 32), start[1]
+    runs = []
+    for r in range(nruns):
+        rng = np.random.default_rng(seed + r)
+        idx = np.sort(rng.choice(u, size=n, replace=False)).astype(np.uint64)
+        with np.errstate(over="ignore"):
+            lo = lo0 + idx
+            hiv = hi0 + (lo < lo0).astype(np.uint64)
+        keys = np.empty((n, 16), np.uint8)
+        keys[:, 0:4] = hiv.astype(">u4").view(np.uint8).reshape(-1, 4)
+        keys[:, 4:12] = _be_bytes_u64(lo)
+        keys[:, 12:16] = 0
+        kind = np.zeros(n, np.uint8)
+        if r == 0 and tomb_frac > 0:
+            kind[rng.random(n) < tomb_frac] = 2  # SDB_KIND_TOMBSTONE
+        vlen = np.where(kind == 2, 0, value_len).astype(np.uint64)
+        val_off = np.zeros(n + 1, np.uint64)
+        val_off[1:] = np.cumsum(vlen)
+        vals = random_bytes(seed + 1000 + r, 0, int(val_off[-1]))
+        seq = (np.uint64(nruns - r) << np.uint64(32)) | np.arange(n, dtype=np.uint64)
+        runs.append(Batch(keys.reshape(-1), np.arange(n + 1, dtype=np.uint64) * np.uint64(16), vals, val_off,
+                          kind, seq))
+    return runs

@@ -381,3 +381,19 @@ def test_compactor_run_ssts_bad_inputs(rt):
         assert st == _abi.SDB_INVALID_ARGUMENT and ns == 0, (f, st)
         setattr(inputs[2], f, getattr(inputs[2], f) - d)
     comp.close()
+
+
+def test_compactor_overwrites_drop(rt):
+    """Retention that drops: four L0 runs over one key space (most keys in several runs), tombstones in the
+    newest, no snapshot and filter_tombstone (the bench_configs.py overwrite job at reduced size): both
+    device jobs bit-exact, and the merged stream holds only each key's newest live version."""
+    from slatedb_amd import datasets
+    runs = [Run.from_batch(b) for b in datasets.overwrite_runs(n=30000)]
+    ret = O.retention(filter_tombstone=True)
+    prm_kw = dict(block_size=4096, bloom_bits_per_key=10)
+    comp, ssts = compact_both(rt, runs, ret, prm_kw, 1 << 20)
+    _, msum = comp.merged()
+    assert msum.num_out < msum.num_in // 3 and len(ssts) >= 2
+    comp.close()
+    st, ns, _ = compact_ssts_both(rt, runs, ret, prm_kw, 1 << 20)
+    assert st == 0 and ns == len(ssts)
