@@ -402,7 +402,8 @@ typedef struct sdb_run {
     const int64_t *create_ts;       /* n: valid iff flags & HAS_CREATE_TS (NULL: none anywhere) */
     const int64_t *expire_ts;       /* n: valid iff flags & HAS_EXPIRE_TS (NULL: none anywhere) */
 } sdb_run;
-enum { SDB_MAX_RUNS = 32 };
+enum { SDB_MAX_RUNS = 32 };        /* runs of one sdb_merge_runs call; the compactor merges more in groups of
+                                      this many first (up to SDB_MAX_RUNS^2 runs per job) */
 typedef struct sdb_retention {
     uint64_t min_seq;               /* retention_min_seq: the walk continues past seq > min_seq
                                        (retention_iterator.rs:188-190) when has_min_seq */
@@ -481,7 +482,9 @@ sdb_status sdb_compactor_run(sdb_compactor *c, const sdb_run *runs, uint32_t nru
  * section on the device and the counts its footer holds.  Runs: inputs [run_start[r], run_start[r+1]),
  * run_start == NULL: one run per input.  A failing input block fails the job with its status (lowest
  * block first; the merged summary's first_error_entry = that block's index among all inputs' blocks);
- * counts that disagree with the decoded blocks fail it with SDB_INVALID_ARGUMENT. */
+ * counts that disagree with the decoded blocks fail it with SDB_INVALID_ARGUMENT.  Any number of inputs
+ * (their block tables go to device memory); more than SDB_MAX_RUNS runs are merged in groups first (one
+ * more host synchronisation per group), up to SDB_MAX_RUNS^2 runs. */
 typedef struct sdb_compaction_input {
     const uint8_t *data;            /* device: the data section (encoded blocks, each ++ crc32) */
     const uint64_t *block_off;      /* device: num_blocks + 1 (BlockMeta.offset of each block, then the
@@ -491,7 +494,6 @@ typedef struct sdb_compaction_input {
     uint64_t key_bytes;             /* SstStats.raw_key_size */
     uint64_t val_bytes;             /* SstStats.raw_val_size */
 } sdb_compaction_input;
-enum { SDB_MAX_COMPACTION_INPUTS = 64 };
 sdb_status sdb_compactor_run_ssts(sdb_compactor *c, const sdb_compaction_input *inputs, uint32_t ninputs,
                                   const uint32_t *run_start, uint32_t nruns, uint16_t input_sst_version,
                                   const sdb_retention *retention, const sdb_sst_params *params,

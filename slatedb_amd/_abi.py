@@ -195,7 +195,6 @@ class CompactionInput(C.Structure):
     ]
 
 
-MAX_COMPACTION_INPUTS = 64
 
 DECODE_DESCENDING = 1
 

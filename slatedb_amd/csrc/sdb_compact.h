@@ -33,6 +33,7 @@ struct RunDesc {  // sdb_run + the run's first global entry index
 
 struct MergeArgs {
     uint32_t nruns, ntiles;
+    uint32_t raw, pad;           // raw: no retention, no merge-operand check (every entry kept as it is)
     uint64_t total;
     sdb_retention ret;
     sdb_merged_out out;
@@ -77,7 +78,10 @@ inline MergeWorkspace merge_workspace_layout(uint64_t total) {
 }
 
 sdb_status build_merge_args(const sdb_run *runs, uint32_t nruns, const sdb_retention *ret, const sdb_merged_out *out,
-                            void *workspace, uint64_t workspace_bytes, MergeArgs *a);
+                            void *workspace, uint64_t workspace_bytes, MergeArgs *a, bool raw = false);
+// A merged stream as an sdb_run (the per-entry value lengths and RowFlags the runs carry): val_len[i],
+// flags[i] for i < n (device, written on st).
+hipError_t launch_merged_as_run(const sdb_merged_out &out, uint64_t n, uint32_t *val_len, uint8_t *flags, hipStream_t st);
 // merge + retention (+ emit when `emit`), all on `st`
 hipError_t launch_merge(const MergeArgs &a, bool emit, hipStream_t st);
 hipError_t launch_merge_emit(const MergeArgs &a, hipStream_t st);
@@ -89,18 +93,17 @@ hipError_t launch_cuts(const SstSet &P, uint64_t max_sst_size, uint64_t *cut, ui
                        hipStream_t st, const uint64_t *n_real = nullptr);
 
 // ---- sdb_compactor_run_ssts (decode inside the job) ----
-constexpr uint32_t kMaxCxInputs = SDB_MAX_COMPACTION_INPUTS;
-struct CxInputs {  // kernel arguments: the input SSTs' blocks, in input order
+struct CxInputs {  // kernel arguments: the input SSTs' blocks, in input order (tables in device memory)
     uint32_t n, nruns;
-    uint64_t base;                          // the decoder's arena: block k = base + start[k] (mod 2^64)
-    const uint8_t *data[kMaxCxInputs];
-    const uint64_t *block_off[kMaxCxInputs];
-    uint64_t first_block[kMaxCxInputs + 1];  // prefix of num_blocks
-    uint64_t run_block[kMaxRuns + 1];        // first block of each run, then the total
-    uint64_t run_entry[kMaxRuns + 1];        // declared first entry of each run, then the total
-    uint64_t key_bytes;                      // declared total key bytes
+    uint64_t base;                     // the decoder's arena: block k = base + start[k] (mod 2^64)
+    uint64_t nblocks;                  // blocks of every input
+    const uint8_t *const *data;        // n: each input's data section
+    const uint64_t *const *block_off;  // n: each input's BlockMeta offsets
+    const uint64_t *first_block;       // n + 1: prefix of num_blocks
+    const uint64_t *run_block;         // nruns + 1: first block of each run, then the total
+    const uint64_t *run_entry;         // nruns + 1: declared first entry of each run, then the total
+    uint64_t key_bytes;                // declared total key bytes
 };
-static_assert(sizeof(CxInputs) < 4000, "CxInputs is passed as kernel arguments");
 // block k of the job -> arena offsets [start, end)
 hipError_t launch_cx_blocks(const CxInputs &in, uint64_t *start, uint64_t *end, hipStream_t st);
 // the decode's summary and run boundaries against the declared counts -> *gate (~0: the merge may run)

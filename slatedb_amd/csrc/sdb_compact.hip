@@ -257,7 +257,12 @@ __global__ __launch_bounds__(kPfxThreads) void k_mg_keys(MergeArgs a) {
             nkp = (uint64_t)ot.kp;
             nkn = ot.kn;
         }
-        if (live) {
+        if (live && a.raw) {  // a group of a job's runs merged ahead of the job (no retention): keep it
+            a.dec[p] = 1;
+            c = 1;
+            kb = me.kn;
+            vb = (me.flags & SDB_FLAG_TOMBSTONE) ? 0 : me.vlen;
+        } else if (live) {
             if (!a.ret.merge_operands && (me.flags & SDB_FLAG_MERGE_OPERAND))
                 report_error(a.err_merge, p, SDB_MERGE_OPERATOR_MISSING);
             const bool first = p == 0 || cmp_key(ppf, (const uint8_t *)pkp, pkn, me.pf, me.kp, me.kn, L0) != 0;
@@ -764,7 +769,7 @@ __global__ void k_cut_offsets(const uint64_t *cut, const uint64_t *num, const ui
 // the padding of the merged stream for the cut walk.
 // ------------------------------------------------------------------------------------------------
 __global__ void k_cx_blocks(CxInputs in, uint64_t *start, uint64_t *end) {
-    const uint64_t nb = in.first_block[in.n];
+    const uint64_t nb = in.nblocks;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nb; k += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t lo = 0, hi = in.n - 1;  // the input holding block k: last first_block <= k
         while (lo < hi) {
@@ -798,6 +803,16 @@ __global__ void k_cx_gate(CxInputs in, const sdb_decode_summary *dsum, const uns
     *gate = g;
 }
 
+// RowFlags and value lengths of a merged stream (kind + ts_mask, val_off[i + 1] - val_off[i]).
+__global__ void k_mg_asrun(sdb_merged_out o, uint64_t n, uint32_t *val_len, uint8_t *flags) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t k = o.kind[i], m = o.ts_mask[i];
+        flags[i] = (uint8_t)((k == SDB_KIND_TOMBSTONE ? SDB_FLAG_TOMBSTONE : 0) | (k == SDB_KIND_MERGE ? SDB_FLAG_MERGE_OPERAND : 0) |
+                             ((m & SDB_TS_EXPIRE) ? SDB_FLAG_HAS_EXPIRE_TS : 0) | ((m & SDB_TS_CREATE) ? SDB_FLAG_HAS_CREATE_TS : 0));
+        val_len[i] = (uint32_t)(o.val_off[i + 1] - o.val_off[i]);
+    }
+}
+
 __global__ void k_mg_pad(sdb_merged_out o, uint64_t cap) {
     const sdb_merge_summary *sm = o.summary;
     const bool ok = sm->status == SDB_OK;
@@ -819,8 +834,16 @@ __global__ void k_mg_pad(sdb_merged_out o, uint64_t cap) {
 
 }  // namespace
 
+hipError_t launch_merged_as_run(const sdb_merged_out &out, uint64_t n, uint32_t *val_len, uint8_t *flags, hipStream_t st) {
+    if (n) {
+        const uint64_t g = (n + 255) / 256;
+        hipLaunchKernelGGL(k_mg_asrun, dim3((uint32_t)(g < 4096 ? g : 4096)), dim3(256), 0, st, out, n, val_len, flags);
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_cx_blocks(const CxInputs &in, uint64_t *start, uint64_t *end, hipStream_t st) {
-    const uint64_t nb = in.first_block[in.n];
+    const uint64_t nb = in.nblocks;
     if (nb) {
         uint64_t g = (nb + 255) / 256;
         hipLaunchKernelGGL(k_cx_blocks, dim3((uint32_t)(g < 2048 ? g : 2048)), dim3(256), 0, st, in, start, end);
@@ -846,13 +869,14 @@ hipError_t launch_cut_offsets(const uint64_t *cut, const uint64_t *num, const ui
 }
 
 sdb_status build_merge_args(const sdb_run *runs, uint32_t nruns, const sdb_retention *ret, const sdb_merged_out *out,
-                            void *workspace, uint64_t workspace_bytes, MergeArgs *pa) {
+                            void *workspace, uint64_t workspace_bytes, MergeArgs *pa, bool raw) {
+    if (nruns > kMaxRuns) return SDB_LIMIT_EXCEEDED;  // per call (the compactor merges more in groups)
     if ((nruns && !runs) || !ret || !out || !out->summary || !out->key_off || !out->val_off || !pa)
         return SDB_INVALID_ARGUMENT;
-    if (nruns > kMaxRuns) return SDB_LIMIT_EXCEEDED;
     MergeArgs &a = *pa;
     a = MergeArgs{};
     a.nruns = nruns;
+    a.raw = raw ? 1u : 0u;
     uint64_t total = 0;
     for (uint32_t r = 0; r < nruns; r++) {
         const sdb_run &R = runs[r];

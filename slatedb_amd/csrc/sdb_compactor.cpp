@@ -79,43 +79,124 @@ struct PinBuf {  // pinned host staging (async device -> host copies)
     }
 };
 
+struct GroupBufs {  // a group of runs merged ahead of the job (runs beyond SDB_MAX_RUNS)
+    DevBuf cols, keys, vals, asrun;
+};
+
 struct sdb_compactor {
     int device = 0;
-    DevBuf merge_ws, cols, keys, vals, cut_ws, cuts, sst_meta, sst_data, sst_bloom, enc_ws, dec, dec_ws;
-    PinBuf pin;
+    DevBuf merge_ws, cols, keys, vals, cut_ws, cuts, sst_meta, sst_data, sst_bloom, enc_ws, dec, dec_ws, cx_tab;
+    std::vector<GroupBufs> groups;
+    PinBuf pin, pin_tab;
     sdb_kv_batch merged{};
     sdb_merge_summary msum{};
     std::vector<sdb_compacted_sst> ssts;
     ~sdb_compactor() {
         (void)hipSetDevice(device);
         for (DevBuf *b : {&merge_ws, &cols, &keys, &vals, &cut_ws, &cuts, &sst_meta, &sst_data, &sst_bloom, &enc_ws,
-                          &dec, &dec_ws})
+                          &dec, &dec_ws, &cx_tab})
             b->release();
+        for (GroupBufs &g : groups)
+            for (DevBuf *b : {&g.cols, &g.keys, &g.vals, &g.asrun}) b->release();
         pin.release();
+        pin_tab.release();
     }
 };
 
 namespace {
 
-// merged-stream columns for `total` entries in c->cols: the sdb_merged_out (byte arenas unset)
-sdb_status merged_columns(sdb_compactor *c, uint64_t total, sdb_merged_out *out) {
+// merged-stream columns for `total` entries in `cols`: the sdb_merged_out (byte arenas unset)
+sdb_status merged_columns_in(DevBuf &cols, uint64_t total, sdb_merged_out *out) {
     const uint64_t o_koff = 0, o_voff = al256(8 * (total + 1)), o_kind = o_voff + al256(8 * (total + 1));
     const uint64_t o_seq = o_kind + al256(total + 1), o_cts = o_seq + al256(8 * (total + 1));
     const uint64_t o_ets = o_cts + al256(8 * (total + 1)), o_mask = o_ets + al256(8 * (total + 1));
     const uint64_t o_sum = o_mask + al256(total + 1), cols_bytes = o_sum + al256(sizeof(sdb_merge_summary));
-    if (!c->cols.ensure(cols_bytes)) return SDB_DEVICE_ERROR;
+    if (!cols.ensure(cols_bytes)) return SDB_DEVICE_ERROR;
     *out = sdb_merged_out{};
     out->key_cap = ~0ull;
-    out->key_off = c->cols.at<uint64_t>(o_koff);
+    out->key_off = cols.at<uint64_t>(o_koff);
     out->val_cap = ~0ull;
-    out->val_off = c->cols.at<uint64_t>(o_voff);
-    out->kind = c->cols.at<uint8_t>(o_kind);
-    out->seq = c->cols.at<uint64_t>(o_seq);
-    out->create_ts = c->cols.at<int64_t>(o_cts);
-    out->expire_ts = c->cols.at<int64_t>(o_ets);
-    out->ts_mask = c->cols.at<uint8_t>(o_mask);
+    out->val_off = cols.at<uint64_t>(o_voff);
+    out->kind = cols.at<uint8_t>(o_kind);
+    out->seq = cols.at<uint64_t>(o_seq);
+    out->create_ts = cols.at<int64_t>(o_cts);
+    out->expire_ts = cols.at<int64_t>(o_ets);
+    out->ts_mask = cols.at<uint8_t>(o_mask);
     out->cap_entries = total;
-    out->summary = c->cols.at<sdb_merge_summary>(o_sum);
+    out->summary = cols.at<sdb_merge_summary>(o_sum);
+    return SDB_OK;
+}
+sdb_status merged_columns(sdb_compactor *c, uint64_t total, sdb_merged_out *out) {
+    return merged_columns_in(c->cols, total, out);
+}
+
+// A job with more runs than one merge takes (SDB_MAX_RUNS): groups of SDB_MAX_RUNS consecutive runs are
+// merged first without retention (every entry kept as it is, in the group's MergeIterator order: key asc,
+// seq desc, run), and the group streams become the job's runs.  Groups are consecutive runs, so equal keys
+// with equal seqs keep their run order and the job's merged stream is the one a single merge of every run
+// would give (merge_iterator.rs:55-69).  One host synchronisation per group (its byte sizes).  A run out
+// of order fails the job like the single merge: *fail = the group merge's summary, first_error_entry
+// rebased to the job's entry numbering.  gate: the decode gate of sdb_compactor_run_ssts (or NULL).
+sdb_status group_runs(sdb_compactor *c, const sdb_run *runs, uint32_t nruns, const unsigned long long *gate,
+                      std::vector<sdb_run> &grouped, sdb_merge_summary *fail, hipStream_t s) {
+    const uint32_t ng = (nruns + kMaxRuns - 1) / kMaxRuns;
+    if (ng > kMaxRuns) return SDB_LIMIT_EXCEEDED;
+    uint64_t job_total = 0;
+    for (uint32_t r = 0; r < nruns; r++) job_total += runs[r].n;
+    if (c->groups.size() < ng) c->groups.resize(ng);
+    grouped.clear();
+    uint64_t base = 0;
+    const sdb_retention none{};
+    for (uint32_t g = 0; g < ng; g++) {
+        const uint32_t r0 = g * kMaxRuns, r1 = std::min(nruns, r0 + kMaxRuns);
+        GroupBufs &B = c->groups[g];
+        uint64_t total = 0;
+        for (uint32_t r = r0; r < r1; r++) total += runs[r].n;
+        sdb_merged_out out{};
+        sdb_status st = merged_columns_in(B.cols, total, &out);
+        if (st) return st;
+        if (!c->merge_ws.ensure(sdb_merge_runs_workspace_bytes(runs + r0, r1 - r0))) return SDB_DEVICE_ERROR;
+        MergeArgs a;
+        st = build_merge_args(runs + r0, r1 - r0, &none, &out, c->merge_ws.p, c->merge_ws.cap, &a, true);
+        if (st) return st;
+        a.gate = gate;
+        sdb_merge_summary sm{};
+        if (launch_merge(a, false, s) != hipSuccess ||
+            hipMemcpyAsync(&sm, out.summary, sizeof(sm), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return SDB_DEVICE_ERROR;
+        if (sm.status) {
+            *fail = sm;
+            fail->num_in = job_total;
+            if (sm.status == SDB_INVALID_ARGUMENT && sm.first_error_entry != ~0ull && !(gate && g == 0))
+                fail->first_error_entry += base;
+            return (sdb_status)sm.status;
+        }
+        if (!B.keys.ensure(sm.key_bytes + 16) || !B.vals.ensure(sm.val_bytes + 16) ||
+            !B.asrun.ensure(al256(4 * (total + 1)) + al256(total + 1)))
+            return SDB_DEVICE_ERROR;
+        a.out.key_bytes = B.keys.at<uint8_t>(0);
+        a.out.key_cap = sm.key_bytes;
+        a.out.val_bytes = B.vals.at<uint8_t>(0);
+        a.out.val_cap = sm.val_bytes;
+        uint32_t *vlen = B.asrun.at<uint32_t>(0);
+        uint8_t *flags = B.asrun.at<uint8_t>(al256(4 * (total + 1)));
+        if (launch_merge_emit(a, s) != hipSuccess || launch_merged_as_run(a.out, total, vlen, flags, s) != hipSuccess)
+            return SDB_DEVICE_ERROR;
+        sdb_run R{};
+        R.n = total;
+        R.key_arena = a.out.key_bytes;
+        R.key_off = a.out.key_off;
+        R.val_base = a.out.val_bytes;
+        R.val_off = a.out.val_off;
+        R.val_len = vlen;
+        R.seq = a.out.seq;
+        R.flags = flags;
+        R.create_ts = a.out.create_ts;
+        R.expire_ts = a.out.expire_ts;
+        grouped.push_back(R);
+        base += total;
+    }
     return SDB_OK;
 }
 
@@ -242,6 +323,13 @@ sdb_status sdb_compactor_run(sdb_compactor *c, const sdb_run *runs, uint32_t nru
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     uint64_t total = 0;
     for (uint32_t r = 0; r < nruns && runs; r++) total += runs[r].n;
+    std::vector<sdb_run> grouped;
+    if (nruns > kMaxRuns) {  // more runs than one merge takes: groups merged ahead (group_runs)
+        const sdb_status gs = group_runs(c, runs, nruns, nullptr, grouped, &c->msum, s);
+        if (gs) return gs;
+        runs = grouped.data();
+        nruns = (uint32_t)grouped.size();
+    }
 
     // 1. merge + retention, sized with unbounded byte capacities, then emitted
     sdb_merged_out out{};
@@ -315,9 +403,8 @@ sdb_status sdb_compactor_run_ssts(sdb_compactor *c, const sdb_compaction_input *
     c->msum = sdb_merge_summary{};
     if (params->sst_type != SDB_SST_COMPACTED) return SDB_INVALID_ARGUMENT;
     if (input_sst_version != 1 && input_sst_version != 2) return SDB_INVALID_VERSION;
-    if (ninputs > kMaxCxInputs) return SDB_LIMIT_EXCEEDED;
     if (!run_start) nruns = ninputs;
-    if (nruns > kMaxRuns) return SDB_LIMIT_EXCEEDED;
+    if ((uint64_t)nruns > (uint64_t)kMaxRuns * kMaxRuns) return SDB_LIMIT_EXCEEDED;  // two merge levels
     if (run_start) {
         if (run_start[0] != 0 || run_start[nruns] != ninputs) return SDB_INVALID_ARGUMENT;
         for (uint32_t r = 0; r < nruns; r++)
@@ -326,40 +413,59 @@ sdb_status sdb_compactor_run_ssts(sdb_compactor *c, const sdb_compaction_input *
     if (hipSetDevice(c->device) != hipSuccess) return SDB_DEVICE_ERROR;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 
-    // the inputs' blocks, in input order, as offsets from the lowest data address
+    // the inputs' blocks, in input order, as offsets from the lowest data address; the per-input and per-run
+    // tables go to device memory (any number of inputs)
     CxInputs in{};
     in.n = ninputs;
     in.nruns = nruns;
+    const uint64_t t_data = 0, t_boff = al256(8ull * ninputs), t_first = t_boff + al256(8ull * ninputs);
+    const uint64_t t_rblk = t_first + al256(8ull * (ninputs + 1)), t_rent = t_rblk + al256(8ull * (nruns + 1));
+    const uint64_t t_total = t_rent + al256(8ull * (nruns + 1));
+    if (!c->pin_tab.ensure(t_total) || !c->cx_tab.ensure(t_total)) return SDB_DEVICE_ERROR;
+    // (the previous job's table upload read this pinned buffer: it completed with that job's synchronisations)
+    uint8_t *th = static_cast<uint8_t *>(c->pin_tab.p);
+    const uint8_t **h_data = reinterpret_cast<const uint8_t **>(th + t_data);
+    const uint64_t **h_boff = reinterpret_cast<const uint64_t **>(th + t_boff);
+    uint64_t *h_first = reinterpret_cast<uint64_t *>(th + t_first), *h_rblk = reinterpret_cast<uint64_t *>(th + t_rblk);
+    uint64_t *h_rent = reinterpret_cast<uint64_t *>(th + t_rent);
     uint64_t E = 0, K = 0, V = 0, B = 0;
     uintptr_t base = ~(uintptr_t)0;
     for (uint32_t i = 0; i < ninputs; i++) {
         const sdb_compaction_input &x = inputs[i];
         if (x.num_blocks && (!x.data || !x.block_off)) return SDB_INVALID_ARGUMENT;
         if (x.num_blocks && (uintptr_t)x.data < base) base = (uintptr_t)x.data;
-        in.data[i] = x.data;
-        in.block_off[i] = x.block_off;
-        in.first_block[i] = B;
+        h_data[i] = x.data;
+        h_boff[i] = x.block_off;
+        h_first[i] = B;
         B += x.num_blocks;
         E += x.num_entries;
         K += x.key_bytes;
         V += x.val_bytes;
     }
-    in.first_block[ninputs] = B;
+    h_first[ninputs] = B;
     if (base == ~(uintptr_t)0) base = 0;
     in.base = base;
+    in.nblocks = B;
+    std::vector<uint64_t> run_entry(nruns + 1);
     {
         uint64_t e = 0;
         for (uint32_t r = 0; r < nruns; r++) {
             const uint32_t i0 = run_start ? run_start[r] : r, i1 = run_start ? run_start[r + 1] : r + 1;
-            in.run_block[r] = in.first_block[i0];
-            in.run_entry[r] = e;
+            h_rblk[r] = h_first[i0];
+            h_rent[r] = run_entry[r] = e;
             for (uint32_t i = i0; i < i1; i++) e += inputs[i].num_entries;
         }
-        in.run_block[nruns] = B;
-        in.run_entry[nruns] = e;
+        h_rblk[nruns] = B;
+        h_rent[nruns] = run_entry[nruns] = e;
     }
     in.key_bytes = K;
     if (E >= (1ull << 31)) return SDB_LIMIT_EXCEEDED;
+    if (hipMemcpyAsync(c->cx_tab.p, th, t_total, hipMemcpyHostToDevice, s) != hipSuccess) return SDB_DEVICE_ERROR;
+    in.data = c->cx_tab.at<const uint8_t *const>(t_data);
+    in.block_off = c->cx_tab.at<const uint64_t *const>(t_boff);
+    in.first_block = c->cx_tab.at<const uint64_t>(t_first);
+    in.run_block = c->cx_tab.at<const uint64_t>(t_rblk);
+    in.run_entry = c->cx_tab.at<const uint64_t>(t_rent);
 
     // 1. decode every input block into one columnar output (run r = entries [run_entry[r], run_entry[r+1]))
     const uint64_t o_bs = 0, o_be = o_bs + al256(8 * (B + 1)), o_bes = o_be + al256(8 * (B + 1));
@@ -397,11 +503,11 @@ sdb_status sdb_compactor_run_ssts(sdb_compactor *c, const sdb_compaction_input *
         reinterpret_cast<const unsigned long long *>(static_cast<uint8_t *>(c->dec_ws.p) + decode_workspace_layout(B).err);
     if (launch_cx_gate(in, dout.summary, dec_err, dout.block_entry_start, gate, s) != hipSuccess)
         return SDB_DEVICE_ERROR;
-    sdb_run runs[kMaxRuns];
+    std::vector<sdb_run> runs(nruns);
     for (uint32_t r = 0; r < nruns; r++) {
-        const uint64_t e0 = in.run_entry[r];
+        const uint64_t e0 = run_entry[r];
         sdb_run &R = runs[r];
-        R.n = in.run_entry[r + 1] - e0;
+        R.n = run_entry[r + 1] - e0;
         R.key_arena = dout.key_arena;
         R.key_off = dout.key_off + e0;
         R.val_base = arena;
@@ -423,9 +529,18 @@ sdb_status sdb_compactor_run_ssts(sdb_compactor *c, const sdb_compaction_input *
     out.key_cap = K;
     out.val_bytes = c->vals.at<uint8_t>(0);
     out.val_cap = V;
-    if (!c->merge_ws.ensure(sdb_merge_runs_workspace_bytes(runs, nruns))) return SDB_DEVICE_ERROR;
+    const sdb_run *mruns = runs.data();
+    uint32_t mn = nruns;
+    std::vector<sdb_run> grouped;
+    if (nruns > kMaxRuns) {  // more runs than one merge takes: groups merged ahead (group_runs)
+        const sdb_status gs = group_runs(c, mruns, nruns, gate, grouped, &c->msum, s);
+        if (gs) return gs;
+        mruns = grouped.data();
+        mn = (uint32_t)grouped.size();
+    }
+    if (!c->merge_ws.ensure(sdb_merge_runs_workspace_bytes(mruns, mn))) return SDB_DEVICE_ERROR;
     MergeArgs a;
-    st = build_merge_args(runs, nruns, ret, &out, c->merge_ws.p, c->merge_ws.cap, &a);
+    st = build_merge_args(mruns, mn, ret, &out, c->merge_ws.p, c->merge_ws.cap, &a);
     if (st) return st;
     a.gate = gate;
     if (launch_merge(a, true, s) != hipSuccess || launch_merge_pad(out, E, s) != hipSuccess) return SDB_DEVICE_ERROR;

@@ -397,3 +397,53 @@ def test_compactor_overwrites_drop(rt):
     comp.close()
     st, ns, _ = compact_ssts_both(rt, runs, ret, prm_kw, 1 << 20)
     assert st == 0 and ns == len(ssts)
+
+
+# ------------------------------------------------------------------------------------------------
+# limits: one sdb_merge_runs call takes SDB_MAX_RUNS (32) runs; the compactor merges more in groups of
+# 32 first (sdb_compactor.cpp group_runs) and takes any number of input SSTs
+# ------------------------------------------------------------------------------------------------
+def test_merge_runs_limit(rt):
+    """33 runs in one sdb_merge_runs call: SDB_LIMIT_EXCEEDED (documented per-call limit)."""
+    import ctypes as C
+    runs = [Run.from_entries([(b"k%03d" % i, 0, b"v", 1, None, None)]) for i in range(33)]
+    druns = [rt.DeviceRun.from_host(r) for r in runs]
+    cr = (_abi.Run * 33)(*[r.to_ctypes() for r in druns])
+    assert rt.lib().sdb_merge_runs(cr, 33, C.byref(O.retention()), C.byref(_abi.MergedOut()), None, 0, None) == \
+        _abi.SDB_LIMIT_EXCEEDED
+    merged, sm = rt.merge_runs_device(druns[:32], O.retention())
+    assert sm.status == 0 and sm.num_out == 32
+
+
+@pytest.mark.parametrize("nruns", [32, 33, 70])
+def test_compactor_many_runs(rt, nruns):
+    """Jobs of 32, 33 and 70 runs (one merge; groups of 32 merged first): bit-exact with the oracle's
+    single merge of every run, including versions with equal seqs in different groups (run order)."""
+    rng = random.Random(100 + nruns)
+    runs = [Run.from_entries(r) for r in rand_runs(rng, nruns, 600, 5, dup_seq=True)]
+    compact_both(rt, runs, O.retention(min_seq=300, compaction_start_ts=900, filter_tombstone=True),
+                 dict(block_size=1024), 4000)
+    compact_both(rt, runs, O.retention(min_seq=10 ** 9), dict(block_size=4096, bloom_bits_per_key=10), 10 ** 9)
+
+
+@pytest.mark.parametrize("ninputs,split", [(64, 1), (65, 1), (70, 5)])
+def test_compactor_run_ssts_many_inputs(rt, ninputs, split):
+    """64, 65 and 70 input SSTs (70 as 14 sorted runs of 5 SSTs): the decode takes every input's blocks,
+    the runs beyond 32 merge in groups."""
+    rng = random.Random(200 + ninputs)
+    nruns = ninputs // split
+    runs = [Run.from_entries(r) for r in rand_runs(rng, nruns, 3000, 4, dup_seq=True) if len(r) >= split]
+    if split == 1:
+        runs = [r for r in runs if r.n > 0]
+    st, ns, _ = compact_ssts_both(rt, runs, O.retention(min_seq=500, compaction_start_ts=900), dict(block_size=512),
+                                  20000, split=split)
+    assert st == 0 and ns >= 1
+
+
+def test_compactor_many_runs_order_error(rt):
+    """A run out of order in the second group fails the job at its global entry index, as one merge would."""
+    rng = random.Random(7)
+    runs = [Run.from_entries(r) for r in rand_runs(rng, 40, 400, 3)]
+    ents = [(b"zz", 0, b"x", 5, None, None), (b"aa", 0, b"y", 4, None, None)]  # descending keys
+    runs[35] = Run.from_entries(ents)
+    compact_both(rt, runs, O.retention(), dict(), 10 ** 9)
