@@ -283,8 +283,13 @@ sdb_status sdb_decode_blocks_at(const uint8_t *arena, const uint64_t *block_star
  *     (block_iterator.rs:159-224).  Keys / columns are in that order; block_entry_start keeps the
  *     ascending prefix of the per-block counts, so block k's entries are [N - bes[k+1], N - bes[k]).
  *     A V2 block whose restart regions do not start at restarts with shared == 0 and end at the next
- *     one reports SDB_CORRUPT_BLOCK (the reference asserts there, block_iterator_v2.rs:76). */
-enum { SDB_DECODE_DESCENDING = 1 };
+ *     one reports SDB_CORRUPT_BLOCK (the reference asserts there, block_iterator_v2.rs:76).
+ *   SDB_DECODE_FAIL_FAST   read_blocks semantics (format/sst.rs:938-1038, all or nothing): the status is
+ *     the first failing block's, in block order, with its checksum verified before its rows as
+ *     decode_block does, and every column is unspecified when the call fails (without the flag the
+ *     good blocks are still decoded and the bad ones listed).  The checksums are then verified by the
+ *     emit pass, which re-reads every block anyway, instead of the count pass. */
+enum { SDB_DECODE_DESCENDING = 1, SDB_DECODE_FAIL_FAST = 2 };
 sdb_status sdb_decode_blocks_ex(const uint8_t *arena, const uint64_t *block_start, const uint64_t *block_end,
                                 uint64_t nblocks, uint16_t sst_version, uint32_t flags, const sdb_decoded_out *out,
                                 void *workspace, uint64_t workspace_bytes, void *stream);
@@ -301,8 +306,9 @@ sdb_status sdb_decode_blocks_ex(const uint8_t *arena, const uint64_t *block_star
  *   SDB_CODEC_ZSTD    zstd 0.13.3 stream::decode_all (zstd frames and skippable frames in sequence).
  * Two steps, so the caller can size the output:
  *   1. sdb_decompress_plan writes out_start[0..nblocks] (device): block k's output slot starts at
- *      out_start[k] and holds its decompressed length + 4 (the declared length for Lz4 / Snappy; Zlib /
- *      Zstd are decoded to count it, their Adler-32 / XXH64 checksums are verified in step 2);
+ *      out_start[k] and holds its decompressed length + 4 (the declared length for Lz4 / Snappy, the
+ *      frames' Frame_Content_Size for Zstd — zstd::bulk::compress writes it — and a count-mode decode
+ *      for Zlib and for Zstd frames without one; Adler-32 / XXH64 checksums are verified in step 2);
  *      out_start[nblocks] = the bytes `out` needs.  A header that cannot be read, a Zlib / Zstd stream
  *      that fails to decode, or more than 64 MiB gets an empty slot (that block then fails in step 2).
  *   2. sdb_decompress_blocks fills out[out_start[k] .. out_end[k]) with the uncompressed block followed

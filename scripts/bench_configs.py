@@ -152,6 +152,22 @@ def decode_bench(reps, granular=True, cpu_s=0.0):
                       "ms": round(ms, 4), "GiB_per_s_encoded": round(enc / (ms * 1e-3) / 2**30, 2),
                       "algorithmic_bytes": alg, "achieved_GBps": round(gbs, 1), "frac": round(gbs / PEAK, 4),
                       "verified_keys": bool(ok)}), flush=True)
+    # read_blocks semantics (SDB_DECODE_FAIL_FAST): the checksums verified by the emit pass
+    def run_ff():
+        st = lib.sdb_decode_blocks_ex(blocks.data_ptr(), block_off.data_ptr(), None, nb, 2, _abi.DECODE_FAIL_FAST,
+                                      C.byref(dout), ws.data_ptr(), wsb, s.cuda_stream)
+        assert st == 0, st
+
+    with torch.cuda.stream(s):
+        ms_ff = timed(run_ff, reps, s)
+    torch.cuda.synchronize()
+    sm_ff = _abi.DecodeSummary.from_buffer_copy(smy.cpu().numpy().tobytes()[:C.sizeof(_abi.DecodeSummary)])
+    ok_ff = sm_ff.status == 0 and sm_ff.num_entries == nent and np.array_equal(ka[:kbytes].cpu().numpy(), np.concatenate(keys))
+    gbs_ff = alg / (ms_ff * 1e-3) / 1e9
+    print(json.dumps({"what": "decode configs[2], fail-fast (read_blocks semantics: checksums in the emit pass)",
+                      "ms": round(ms_ff, 4), "GiB_per_s_encoded": round(enc / (ms_ff * 1e-3) / 2**30, 2),
+                      "achieved_GBps": round(gbs_ff, 1), "frac": round(gbs_ff / PEAK, 4), "verified_keys": bool(ok_ff)}),
+          flush=True)
     # descending iteration order (SDB_DECODE_DESCENDING): written mirrored by the emit pass
     asc_keys = ka[:kbytes].cpu().numpy().copy()
     asc_seq = sq[:nent].cpu().numpy().copy()

@@ -21,8 +21,9 @@ if [ -z "${NOTEST:-}" ]; then
   tail -2 $O/tests.log
 fi
 for w0 in ${WORK:-}; do
-  w=${w0%%:*}; v=""; unset SDB_LIBRARY
+  w=${w0%%:*}; v=""; unset SDB_LIBRARY SDB_DEC_PHASE
   if [ "$w0" != "$w" ]; then v=${w0#*:}; export SDB_LIBRARY=libslatedb_amd_$v.so; echo "== variant $v"; fi
+  [ "$v" = pt ] && export SDB_DEC_PHASE=1
   case $w in
     enc) step enc$v 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu
          python3 -c "
@@ -34,7 +35,7 @@ import json; d=json.loads([l for l in open('$O/encx.log') if l.startswith('{')][
 print('encx ${ENCX_ARGS:-}: value', d['value'], 'ms/SST', r['device_ms_per_sst'], {k: round(v/8*1000,1) for k,v in r['stage_ms_per_step'].items()})" ;;
     encprof) step encprof 300 rocprofv3 --kernel-trace --stats -d $O/encprof -o run --output-format csv -- python3 bench.py --steps 100 --warmup 10 --no-cpu --no-verify --single-steps 0 --stage-steps 0 ;;
     dec) step dec$v 300 python3 scripts/bench_configs.py --decode --no-granular --reps 10 --cpu-seconds 0
-         grep '^{' $O/dec$v.log | cut -c1-400
+         grep '^{\|ticks' $O/dec$v.log | cut -c1-400
          [ -n "$v" ] || step decprof 300 rocprofv3 --kernel-trace --stats -d $O/decprof -o run --output-format csv -- python3 scripts/bench_configs.py --decode --no-granular --reps 5 --cpu-seconds 0 ;;
     bloom) step bloom 200 python3 scripts/bench_configs.py --bloom --reps 20
          grep '^{' $O/bloom.log | cut -c1-300

@@ -197,6 +197,7 @@ class CompactionInput(C.Structure):
 
 
 DECODE_DESCENDING = 1
+DECODE_FAIL_FAST = 2  # SDB_DECODE_FAIL_FAST
 
 LOOKUP_FILTERED, LOOKUP_EXHAUSTED, LOOKUP_POSITIONED, LOOKUP_FOUND = 0, 1, 2, 3
 

@@ -386,6 +386,7 @@ static sdb_status decode_common(const uint8_t *blocks, const uint64_t *block_off
     a.nblocks = nblocks;
     a.version = sst_version;
     a.descending = (flags & SDB_DECODE_DESCENDING) ? 1u : 0u;
+    a.fail_fast = (flags & SDB_DECODE_FAIL_FAST) ? 1u : 0u;
     a.out = *out;
     a.cnt = carve<uint64_t>(workspace, wl.cnt);
     a.kbytes = carve<uint64_t>(workspace, wl.kbytes);
@@ -414,7 +415,7 @@ sdb_status sdb_decode_blocks(const uint8_t *blocks, const uint64_t *block_off, u
 sdb_status sdb_decode_blocks_ex(const uint8_t *arena, const uint64_t *block_start, const uint64_t *block_end,
                                 uint64_t nblocks, uint16_t sst_version, uint32_t flags, const sdb_decoded_out *out,
                                 void *workspace, uint64_t workspace_bytes, void *stream) {
-    if (flags & ~(uint32_t)SDB_DECODE_DESCENDING) return SDB_INVALID_ARGUMENT;
+    if (flags & ~(uint32_t)(SDB_DECODE_DESCENDING | SDB_DECODE_FAIL_FAST)) return SDB_INVALID_ARGUMENT;
     if (block_end && nblocks && !block_start) return SDB_INVALID_ARGUMENT;
     return decode_common(arena, block_start, block_end, nblocks, sst_version, out, workspace, workspace_bytes, stream,
                          flags);

@@ -496,7 +496,9 @@ sdb_status sdb_compactor_run_ssts(sdb_compactor *c, const sdb_compaction_input *
     unsigned long long *gate = c->dec.at<unsigned long long>(o_gate);
     const uint8_t *arena = reinterpret_cast<const uint8_t *>(base);
     if (launch_cx_blocks(in, bstart, bend, s) != hipSuccess) return SDB_DEVICE_ERROR;
-    sdb_status st = sdb_decode_blocks_at(arena, bstart, bend, B, input_sst_version, &dout, c->dec_ws.p, c->dec_ws.cap,
+    // fail-fast (a failing block fails the job anyway, as load_iterators' reads would): checksums in the emit pass
+    sdb_status st = sdb_decode_blocks_ex(arena, bstart, bend, B, input_sst_version, SDB_DECODE_FAIL_FAST, &dout,
+                                         c->dec_ws.p, c->dec_ws.cap,
                                          stream);
     if (st) return st;
     const unsigned long long *dec_err =

@@ -25,6 +25,8 @@ struct DecodeArgs {
     uint32_t *done;                    // k_dec_emit workgroups finished (small batches: the last one finishes)
     uint32_t small;                    // 1: nblocks <= 1024 and one block per wave: k_dec_emit scans the counts itself
     uint32_t descending;               // 1: output in descending iteration order (written mirrored by k_dec_emit)
+    uint32_t fail_fast, pad_ff;        // 1: read_blocks semantics (the first failing block fails the call, the
+                                       //    columns are unspecified then): the checksums move to the emit pass
     uint32_t *bad_block;
     uint64_t bad_cap;
     uint64_t dn, dkb;                  // descending: entries and key bytes of the whole output (k_dec_emit)

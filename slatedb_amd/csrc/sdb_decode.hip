@@ -48,7 +48,7 @@ constexpr uint32_t kDecImg = 4096 + 32;                  // fast path: staged bl
 constexpr uint32_t kDecKeys = 2048;                      // fast path: restored keys of one block
 constexpr uint32_t kDecGuard = 64;                       // zero lead-in of the right-aligned CRC segments
 constexpr uint32_t kDecWaveLds = kDecGuard + kDecImg + kDecKeys;
-constexpr uint32_t kDecLds = (kEmThreads / 64) * kDecWaveLds;  // emit passes: no CRC tables (the count pass checked)
+constexpr uint32_t kDecLds = kCrcTablesLds + (kEmThreads / 64) * kDecWaveLds;  // emit: tables (fail-fast CRC), waves
 constexpr uint32_t kDecCap = kDecWaveLds - kDecGuard;
 // count pass: the CRC tables, the bank-replicated byte table (sdb_crc.h), then per wave a guard + image
 constexpr uint32_t kCntWaveLds = kDecGuard + kDecImg;
@@ -434,6 +434,25 @@ SDB_DEV void gran_store(uint64_t s, uint64_t e, const Granules &r, lu8 *img) {
     }
 }
 
+// validate_checksum (format/sst.rs:1029-1038) of a block staged by stage_lds (image byte p0 = block byte
+// 0, the 64 bytes before img zero): zero the bytes before p0, fold crc32fast's init into the first four,
+// one wave CRC, restore.  Every lane gets the verdict.
+SDB_DEV bool crc_staged_ok(lu8 *img, uint32_t p0, uint32_t blen) {
+    const uint32_t l = (uint32_t)lane_id();
+    const lu8 *d = img + p0;
+    const uint32_t stored = ((uint32_t)d[blen] << 24) | ((uint32_t)d[blen + 1] << 16) | ((uint32_t)d[blen + 2] << 8) |
+                            (uint32_t)d[blen + 3];
+    wave_sync_d();
+    if (l < p0) img[l] = 0;
+    if (l < 4) img[p0 + l] ^= 0xFF;
+    wave_sync_d();
+    const uint32_t c = wave_crc_image_ra(img, p0 + blen);
+    wave_sync_d();
+    if (l < 4) img[p0 + l] ^= 0xFF;
+    wave_sync_d();
+    return c == stored;
+}
+
 SDB_DEV LdsBlockView stage_lds(const DecodeArgs &a, uint64_t s, uint64_t e, lu8 *img, bool check,
                                const Granules *pre = nullptr) {
     LdsBlockView v{};
@@ -448,22 +467,11 @@ SDB_DEV LdsBlockView stage_lds(const DecodeArgs &a, uint64_t s, uint64_t e, lu8 
     }
     wave_sync_d();
     const lu8 *d = img + p0;
-    if (check) {
-        const uint32_t stored = ((uint32_t)d[blen] << 24) | ((uint32_t)d[blen + 1] << 16) | ((uint32_t)d[blen + 2] << 8) |
-                                (uint32_t)d[blen + 3];
-        wave_sync_d();
-        if (l < p0) img[l] = 0;
-        if (l < 4) img[p0 + l] ^= 0xFF;
-        wave_sync_d();
-        // zeros before img (the guard) and before p0
-        const uint32_t c = wave_crc_image_ra(img, Lc);
-        wave_sync_d();
-        if (l < 4) img[p0 + l] ^= 0xFF;
-        wave_sync_d();
-        if (c != stored) {
-            v.status = SDB_CHECKSUM_MISMATCH;  // validate_checksum (format/sst.rs:1029-1038)
-            return v;
-        }
+    (void)l;
+    (void)Lc;
+    if (check && !crc_staged_ok(img, p0, blen)) {
+        v.status = SDB_CHECKSUM_MISMATCH;  // validate_checksum (format/sst.rs:1029-1038)
+        return v;
     }
     const uint32_t cnt = (uint32_t)rd_be(d + blen - 2, 2);  // Block::decode (format/block.rs:28-46)
     if (2 + 2 * (uint64_t)cnt > blen) {
@@ -932,6 +940,7 @@ SDB_DEV bool tally_v2_pieces(const DecodeArgs &a, uint64_t s, const BlockView &v
 constexpr uint8_t kFlagSeq = 1;  // V2 block walked sequentially (irregular restart regions)
 constexpr uint8_t kFlagGen = 2;  // emitted by k_dec_emit_gen (V1, rows not recorded, keys over the row table, big)
 constexpr uint8_t kFlagBig = 4;  // over one wave image: counted by k_dec_count_big
+constexpr uint8_t kFlagBad = 8;  // failed in a count pass (its checksum already verified there)
 
 // The blocks of wave w in the passes that pick flagged blocks ([k0, k1), contiguous): the flags are
 // read 64 at a time (one byte per lane) and the flagged blocks taken in order from the ballot.
@@ -974,7 +983,7 @@ SDB_DEV void count_result(const DecodeArgs &a, uint64_t k, const Tally &t, uint8
     if (t.status) {
         a.cnt[k] = 0;
         a.kbytes[k] = 0;
-        a.flag[k] = 0;
+        a.flag[k] = kFlagBad;
         atomicMin(a.err, (unsigned long long)((k << 8) | (uint64_t)t.status));
         unsigned long long slot = atomicAdd(a.nbad, 1ull);
         if (slot < a.bad_cap) a.bad_block[slot] = (uint32_t)k;
@@ -1029,7 +1038,9 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(kCn
         {
                         // slicing-by-8 CRC: the pass is VALU-bound, and the bank-replicated byte table costs twice the
             // VALU per byte for its conflict-free lookups (515 vs 479 us on configs[2])
-            const LdsBlockView v = stage_lds(a, s, e, img, true, &cur);
+            // fail-fast: the emit pass verifies the checksums (a block that fails here is checked now, so a
+            // corrupt block reports CHECKSUM_MISMATCH before anything its rows would raise)
+            const LdsBlockView v = stage_lds(a, s, e, img, !a.fail_fast, &cur);
             DEC_T(t1);
             t.status = v.status;
             if (!v.status) {
@@ -1039,6 +1050,8 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(kCn
                     t = tally_v2(v);
                 if (a.descending && a.version == 2) desc_rule(v.count, t);
             }
+            if (a.fail_fast && t.status && !crc_staged_ok(img, (uint32_t)(s & 15), (uint32_t)(e - s - 4)))
+                t.status = SDB_CHECKSUM_MISMATCH;
             DEC_T(t2);
             DEC_ACC(0, 0, t1 - t0);
             DEC_ACC(0, 1, t2 - t1);
@@ -1532,11 +1545,21 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
     }
     const uint32_t wave = threadIdx.x >> 6;
     const int l = lane_id();
-    lu8 *img = (lu8 *)smem + wave * kDecWaveLds + kDecGuard;
+    lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kDecWaveLds + kDecGuard;
     lu8 *kbuf = img + kDecImg;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
     (void)gwave;
+    const bool ff = a.fail_fast != 0;
+    if (ff) {  // fail-fast: this pass verifies the checksums (tables at LDS address 0, zero guards)
+        if (lds_addr((const void *)smem) != 0) {
+            if (threadIdx.x == 0) atomicMin(a.err, (unsigned long long)SDB_DEVICE_ERROR);
+            return;
+        }
+        crc_tables_to_lds((lu32 *)smem);
+        if (l < kDecGuard / 4) ((lu32 *)(img - kDecGuard))[l] = 0;
+        __syncthreads();
+    }
     // capacity guard: if the counted output does not fit the caller's arrays, write nothing
     if (tot_ent > a.out.cap_entries || tot_kb > a.out.key_arena_cap) run = false;
     a.dn = tot_ent;
@@ -1591,11 +1614,22 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
         }
         const uint64_t ent0 = m.ent0;
         if (l == 0) a.out.block_entry_start[k] = ent0;
-        if (m.ent1 == ent0 || m.gen(k)) continue;  // nothing to emit, or k_dec_emit_gen's
+        const uint32_t fb = (m.fw >> (8 * (k & 3))) & 0xFF;
+        const bool skip = m.ent1 == ent0 || (fb & kFlagGen);  // nothing to emit, or k_dec_emit_gen's
+        // fail-fast: every block of one wave image the count pass did not reject is checked here
+        if (skip && !(ff && !(fb & kFlagBad) && dec_fast(s, e))) continue;
         const uint64_t kb0 = m.kb0;
         DEC_T(t0);
-        const LdsBlockView v = stage_lds(a, s, e, img, false, &cur);
-        if (v.status) continue;  // cannot happen: the count pass accepted it
+        const LdsBlockView v = stage_lds(a, s, e, img, ff, &cur);
+        if (v.status) {  // fail-fast: a checksum mismatch (the count pass accepted the rest)
+            if (l == 0) {
+                atomicMin(a.err, (unsigned long long)((k << 8) | (uint64_t)v.status));
+                const unsigned long long slot = atomicAdd(a.nbad, 1ull);
+                if (slot < a.bad_cap) a.bad_block[slot] = (uint32_t)k;
+            }
+            continue;
+        }
+        if (skip) continue;
         DEC_T(t1);
         ((lu32 *)(kbuf + kRowTmp))[l] = rp;
         wave_sync_d();
@@ -1628,7 +1662,7 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
     a.dkb = tot_kb;
     const uint32_t wave = threadIdx.x >> 6;
     const int l = lane_id();
-    lu8 *img = (lu8 *)smem + wave * kDecWaveLds + kDecGuard;
+    lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kDecWaveLds + kDecGuard;
     lu8 *kbuf = img + kDecImg;
     uint8_t *stage = (uint8_t *)img;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);

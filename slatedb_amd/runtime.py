@@ -576,9 +576,11 @@ def decode_blocks_at_device(arena, block_start, block_end, nblocks, out, sst_ver
         raise SdbError(st, "sdb_decode_blocks_at")
 
 
-def decode_blocks_ex_device(arena, block_start, block_end, nblocks, out, sst_version=2, descending=False, stream=None):
-    """Enqueue sdb_decode_blocks_ex (block_end None: contiguous blocks, block_start has nblocks + 1 entries)."""
-    flags = _abi.DECODE_DESCENDING if descending else 0
+def decode_blocks_ex_device(arena, block_start, block_end, nblocks, out, sst_version=2, descending=False, stream=None,
+                            fail_fast=False):
+    """Enqueue sdb_decode_blocks_ex (block_end None: contiguous blocks, block_start has nblocks + 1 entries).
+    fail_fast: read_blocks semantics (SDB_DECODE_FAIL_FAST: columns unspecified when the call fails)."""
+    flags = (_abi.DECODE_DESCENDING if descending else 0) | (_abi.DECODE_FAIL_FAST if fail_fast else 0)
     st = lib().sdb_decode_blocks_ex(arena.data_ptr(), block_start.data_ptr(),
                                     None if block_end is None else block_end.data_ptr(), nblocks, sst_version, flags,
                                     C.byref(out.out), out.workspace.data_ptr(), out.workspace.numel(), _sp(stream))
