@@ -178,6 +178,24 @@ def cpu_baseline(budget_s, threads):
                           os.cpu_count() or 0)}
 
 
+def measured_copy_gbs(dev, nbytes=1 << 30, reps=8):
+    """The box's attainable HBM copy bandwidth (torch copy_, read + write bytes), beside the 8 TB/s spec."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev).fill_(1)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    torch.cuda.empty_cache()
+    return 2 * nbytes / (ms * 1e-3) / 1e9
+
+
 def pmc_traffic():
     """HBM bytes per SST of the encode from the committed PMC passes over this same bench command
     (profiles/r3_pmc_traffic.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes, corrected per
@@ -318,6 +336,8 @@ def main():
         single = {"device_ms_per_sst": round(sms, 5), "GiB_per_s": round(logical / (sms * 1e-3) / 2**30, 2),
                   "achieved_GBps": round(sg, 1), "frac": round(sg / PEAK_HBM_GBS, 4)}
 
+    copy_gbs = measured_copy_gbs(dev)
+
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -378,12 +398,15 @@ def main():
                                                "k_enum, k_emit; the bloom slice fill runs in k_seg's grid: one launch sequence per step)",
                      "achieved": round(pipe_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(pipe_gbs / PEAK_HBM_GBS, 4),
+                     "measured_copy_GBps": round(copy_gbs, 1),
+                     "frac_of_measured_copy": round(pipe_gbs / copy_gbs, 4) if copy_gbs else None,
                      "traffic": traffic_sst * batch if traffic_sst else None,
                      "traffic_source": ("committed PMC passes profiles/%s (same command, per SST x batch)" % PMC_FILE)
                      if traffic_sst else None,
                      "algorithmic_bytes_per_step": batch * alg_sst, "algorithmic_bytes_per_sst": alg_sst,
                      "device_ms_per_step": round(set_ms, 5), "device_ms_per_sst": round(set_ms / batch, 5),
                      "k_emit": {"achieved": round(emit_gbs, 1), "frac": round(emit_gbs / PEAK_HBM_GBS, 4),
+                                "frac_of_measured_copy": round(emit_gbs / copy_gbs, 4) if copy_gbs else None,
                                 "avg_launch_ms": round(emit_ms, 5), "algorithmic_bytes_per_launch": emit_bytes,
                                 "traffic_per_sst": traffic_kernels.get("k_emit")},
                      "stage_ms_per_step": {k: round(v, 5) for k, v in stage_ms.items()}},

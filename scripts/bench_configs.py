@@ -279,9 +279,17 @@ def bloom_bench(reps):
                                  s.cuda_stream)
         assert st == 0
 
+    def run_atomic():  # no workspace: k_bloom_atomic, device-scope atomicOr per probe (comparison only)
+        st = lib.sdb_bloom_build(dk.data_ptr(), do.data_ptr(), n, 10, bm.data_ptr(), fb, 0, 0, s.cuda_stream)
+        assert st == 0
+
     with torch.cuda.stream(s):
+        ms_at = timed(run_atomic, reps, s)
+        got_at = bm[:fb].cpu().numpy()
         ms = timed(run, reps, s)
     got = bm[:fb].cpu().numpy()
+    print(json.dumps({"what": "bloom configs[3], device-atomic path (no workspace)", "ms": round(ms_at, 4),
+                      "same_bitmap_as_dense": bool(np.array_equal(got_at, got))}), flush=True)
     t0 = time.perf_counter()
     ref = O.bloom_build(kb, ko, 10)
     cpu_s = time.perf_counter() - t0
@@ -603,6 +611,46 @@ def lookup_bench(reps):
                                        "sample": "first %d of the same keys, oracle orc_sst_lookup" % ns}}), flush=True)
 
 
+def encode_variants_bench(reps):
+    """Headline-shaped encode (8 SSTs per sdb_encode_ssts call, resident) on the other SURVEY §8(d)
+    datasets: D2 (sorted random 16 B keys, shared prefix ~2 B) and D1-L0 (N = 489,740, the memtable size
+    at which a real L0 flush freezes).  SST 0 of each set is checked bit-exact against the oracle."""
+    from oracle import oracle as O
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(device=dev)
+    prm = runtime.params(block_size=4096, sst_version=2, restart_interval=16, bloom_bits_per_key=10)
+    oprm = O.params(block_size=4096, sst_version=2, bloom_bits_per_key=10)
+    variants = [("D2 random-sorted", lambda j: datasets.d2(seed=datasets.SEED_D2 + j)),
+                ("D1-L0 (N=489,740)", lambda j: datasets.d1(sst_index=j, n=489_740))]
+    for name, make in variants:
+        hosts = [make(j) for j in range(8)]
+        dbs = [h.to_device(dev) for h in hosts]
+        outs = [runtime.DeviceSstOutput(h.n, h.logical_bytes(), h.logical_bytes(), prm, device=dev,
+                                        workspace=False) for h in hosts]
+        ws = runtime.ssts_workspace(dbs, prm, device=dev)
+        run = lambda: runtime.encode_ssts_device(dbs, outs, prm, ws, s)
+        run()
+        torch.cuda.synchronize()
+        got = outs[0].to_host()
+        ref = O.encode_sst(hosts[0], oprm)
+        ok = (got["summary"].status == 0 and np.array_equal(got["data"], ref.data)
+              and np.array_equal(got["bloom"], ref.bloom) and np.array_equal(got["block_off"], ref.block_off))
+        ms = timed(run, reps, s)
+        logical = sum(h.logical_bytes() for h in hosts)
+        alg = 0
+        for h, o in zip(hosts, outs):
+            sm = o.summary_host()
+            alg += h.algorithmic_input_bytes() + sm.data_len + sm.bloom_len
+        print(json.dumps({"what": "encode %s, 8 SSTs per call (headline shape)" % name, "entries_per_sst": hosts[0].n,
+                          "ms_per_call": round(ms, 4), "ms_per_sst": round(ms / 8, 4),
+                          "GiBps_logical": round(logical / (ms * 1e-3) / 2**30, 1),
+                          "alg_GBps": round(alg / (ms * 1e-3) / 1e9, 1),
+                          "frac_of_8TBps": round(alg / (ms * 1e-3) / 1e9 / PEAK, 3),
+                          "matches_oracle_sst0": bool(ok)}), flush=True)
+        del dbs, outs, ws
+        torch.cuda.empty_cache()
+
+
 def hbm_bench(reps):
     """STREAM-like: torch's copy kernel over 4 GiB (read + write) and a read-only int64 sum."""
     dev = torch.device("cuda", 0)
@@ -631,11 +679,12 @@ def main():
     p.add_argument("--hbm", action="store_true")
     p.add_argument("--codec", action="store_true")
     p.add_argument("--lookup", action="store_true")
+    p.add_argument("--encode", action="store_true", help="encode D2 and D1-L0 (headline shape)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="decode CPU baseline budget (0: skip)")
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--no-granular", action="store_true", help="decode: skip the 2 MiB granularity run")
     a = p.parse_args()
-    allp = not (a.decode or a.bloom or a.e2e or a.compact or a.hbm or a.codec or a.lookup)
+    allp = not (a.decode or a.bloom or a.e2e or a.compact or a.hbm or a.codec or a.lookup or a.encode)
     torch.cuda.set_device(0)
     runtime.require_device()
     if a.bloom or allp:
@@ -652,6 +701,8 @@ def main():
         compact_bench(max(3, a.reps // 4))
     if a.lookup or allp:
         lookup_bench(a.reps)
+    if a.encode or allp:
+        encode_variants_bench(a.reps)
 
 
 if __name__ == "__main__":

@@ -2,6 +2,7 @@
 # Round 4 iteration: the whole -m gpu suite, then the workloads named in $WORK (space separated):
 #   enc     bench.py driver shape (20 steps, 5 warmup) without the CPU leg
 #   dec     configs[2] decode (bench_configs.py --decode) + its kernel trace stats
+#   encv    encode throughput on D2 and D1-L0 (headline shape)
 #   bloom   configs[3] bloom + kernel trace stats
 #   compact the compaction job + kernel trace stats
 #   codec   the f3 decompression workloads + kernel trace stats
@@ -37,9 +38,11 @@ print('encx ${ENCX_ARGS:-}: value', d['value'], 'ms/SST', r['device_ms_per_sst']
     dec) step dec$v 300 python3 scripts/bench_configs.py --decode --no-granular --reps 10 --cpu-seconds 0
          grep '^{\|ticks' $O/dec$v.log | cut -c1-400
          [ -n "$v" ] || step decprof 300 rocprofv3 --kernel-trace --stats -d $O/decprof -o run --output-format csv -- python3 scripts/bench_configs.py --decode --no-granular --reps 5 --cpu-seconds 0 ;;
-    bloom) step bloom 200 python3 scripts/bench_configs.py --bloom --reps 20
-         grep '^{' $O/bloom.log | cut -c1-300
-         step bloomprof 200 rocprofv3 --kernel-trace --stats -d $O/bloomprof -o run --output-format csv -- python3 scripts/bench_configs.py --bloom --reps 20 ;;
+    encv) step encv 300 python3 scripts/bench_configs.py --encode --reps 20
+         grep '^{' $O/encv.log | cut -c1-400 ;;
+    bloom) step bloom$v 200 python3 scripts/bench_configs.py --bloom --reps 20
+         grep '^{' $O/bloom$v.log | cut -c1-300
+         [ -n "$v" ] || step bloomprof 200 rocprofv3 --kernel-trace --stats -d $O/bloomprof -o run --output-format csv -- python3 scripts/bench_configs.py --bloom --reps 20 ;;
     compact) step compact 300 python3 scripts/bench_configs.py --compact --reps 8
          grep '^{' $O/compact.log | cut -c1-300
          step compactprof 300 rocprofv3 --kernel-trace --stats -d $O/compactprof -o run --output-format csv -- python3 scripts/bench_configs.py --compact --reps 8 ;;
