@@ -38,7 +38,7 @@ sys.path.insert(0, ROOT)
 from slatedb_amd import _abi, datasets, job, runtime  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s); the box's STREAM copy: DESIGN.md §5
-PMC_FILES = ("r3_pmc_traffic.json", "r2_pmc_traffic.json")  # newest first
+PMC_FILES = ("r4_pmc_traffic.json", "r3_pmc_traffic.json", "r2_pmc_traffic.json")  # newest first
 PMC_FILE = PMC_FILES[0]
 
 
@@ -198,7 +198,7 @@ def measured_copy_gbs(dev, nbytes=1 << 30, reps=8):
 
 def pmc_traffic():
     """HBM bytes per SST of the encode from the committed PMC passes over this same bench command
-    (profiles/r3_pmc_traffic.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes, corrected per
+    (profiles/r4_pmc_traffic.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes, corrected per
     MI355X_MICROARCH.md, written by scripts/collect_profiles.py).  PMC counters are collected in
     their own rocprofv3 runs, never inside the timed region."""
     global PMC_FILE
