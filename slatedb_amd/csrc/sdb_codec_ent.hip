@@ -74,74 +74,105 @@ constexpr uint32_t kEntWaveLds = (sizeof(EntLds) + 15) & ~15u;
 constexpr uint32_t kEntLds = 8 * 1024 + (kEntThreads / 64) * kEntWaveLds;
 static_assert(kEntLds <= 160 * 1024, "entropy decoder LDS");
 
-// output of one decode: p == nullptr counts only
+// output of one decode: p == nullptr counts only.  wide: every lane of the wave runs this decode with
+// the same state (the run kernel), so the byte moves are spread over the lanes: lane l moves 16-byte
+// chunks l, l + 64, ... (or bytes l, l + 64, ...) of each copy — the serial decoder's state machine
+// stays uniform, only its copies are parallel.  A wave's memory instructions reach memory in program
+// order, so a later instruction (any lane) reads what an earlier one stored (as in the one-lane form).
 struct EntOut {
     uint8_t *p;
     uint64_t len, cap;
     bool bad;
+    bool wide;
+    SDB_DEV uint32_t lane() const { return wide ? (uint32_t)lane_id() : 0u; }
+    SDB_DEV uint32_t lanes() const { return wide ? 64u : 1u; }
     SDB_DEV bool put(uint8_t b) {
         if (len >= cap) {
             bad = true;
             return false;
         }
-        if (p) p[len] = b;
+        if (p) p[len] = b;  // (wide: every lane stores the same byte)
         len++;
         return true;
     }
-    SDB_DEV uint8_t back(uint64_t d) const { return p ? p[len - d] : 0; }
-    // n bytes from src (not overlapping the output still to be written), 16 at a time
-    SDB_DEV bool copy(const uint8_t *src, uint64_t n) {
+    SDB_DEV bool room(uint64_t n) {
         if (n > cap - len) {
             bad = true;
             return false;
         }
+        return true;
+    }
+    // n bytes from src (not overlapping the output still to be written)
+    SDB_DEV bool copy(const uint8_t *src, uint64_t n) {
+        if (!room(n)) return false;
         if (p) {
-            uint64_t i = 0;
-            for (; i + 16 <= n; i += 16) {
+            const uint64_t n16 = n & ~15ull, l = lane(), L = lanes();
+            for (uint64_t i = 16 * l; i < n16; i += 16 * L) {
                 uint4 w;
                 __builtin_memcpy(&w, src + i, 16);
                 __builtin_memcpy(p + len + i, &w, 16);
             }
-            for (; i < n; i++) p[len + i] = src[i];
+            for (uint64_t i = n16 + l; i < n; i += L) p[len + i] = src[i];
         }
         len += n;
         return true;
     }
-    // n bytes from src >= the write position (zstd's literal stage in the slot): forward, 16 at a time
-    // while the source is at least 16 bytes ahead
+    // n copies of byte b (zstd RLE blocks and literals)
+    SDB_DEV bool fill(uint8_t b, uint64_t n) {
+        if (!room(n)) return false;
+        if (p)
+            for (uint64_t i = lane(); i < n; i += lanes()) p[len + i] = b;
+        len += n;
+        return true;
+    }
+    // n bytes from src >= the write position (zstd's literal stage in the slot), forward.  Chunk i is
+    // loaded before it is stored, and no store reaches a source byte a later chunk still reads (src >=
+    // dst), so lanes may move consecutive chunks at once for any src - dst >= 16; a closer source goes
+    // bytewise in order on one lane.
     SDB_DEV bool copy_fwd(const uint8_t *src, uint64_t n) {
-        if (n > cap - len) {
-            bad = true;
-            return false;
-        }
+        if (!room(n)) return false;
         uint8_t *dst = p + len;
         uint64_t i = 0;
-        if (src - dst >= 16)
-            for (; i + 16 <= n; i += 16) {
+        if (src - dst >= 16) {
+            const uint64_t n16 = n & ~15ull, l = lane(), L = lanes();
+            for (uint64_t j = 16 * l; j < n16; j += 16 * L) {
                 uint4 w;
-                __builtin_memcpy(&w, src + i, 16);
-                __builtin_memcpy(dst + i, &w, 16);
+                __builtin_memcpy(&w, src + j, 16);
+                __builtin_memcpy(dst + j, &w, 16);
             }
+            for (uint64_t j = n16 + l; j < n; j += L) dst[j] = src[j];
+            i = n;
+        }
         if (src != dst)
             for (; i < n; i++) dst[i] = src[i];
         len += n;
         return true;
     }
-    // a match of n bytes at distance d: 16 at a time when d >= 16 (chunks never overlap their source)
+    // a match of n bytes at distance d: byte i comes from len - d + (i mod d), always below len (a
+    // byte written before this call), so every byte can move at once; one lane: 16 at a time when d >= 16
     SDB_DEV bool match(uint64_t d, uint64_t n) {
-        if (n > cap - len) {
-            bad = true;
-            return false;
-        }
+        if (!room(n)) return false;
         if (p) {
-            uint64_t i = 0;
-            if (d >= 16)
-                for (; i + 16 <= n; i += 16) {
-                    uint4 w;
-                    __builtin_memcpy(&w, p + len - d + i, 16);
-                    __builtin_memcpy(p + len + i, &w, 16);
+            if (wide) {
+                const uint8_t *src = p + len - d;  // d <= the output so far (the callers check)
+                const uint32_t d32 = d < 0x80000000ull ? (uint32_t)d : 0x80000000u;
+                uint64_t i = lane_id(), r = d > 64 ? i : (uint32_t)i % d32;
+                const uint64_t step = d > 64 ? 64 : 64u % d32;
+                for (; i < n; i += 64) {
+                    p[len + i] = src[r];
+                    r += step;
+                    r = r >= d ? r - d : r;
                 }
-            for (; i < n; i++) p[len + i] = p[len + i - d];
+            } else {
+                uint64_t i = 0;
+                if (d >= 16)
+                    for (; i + 16 <= n; i += 16) {
+                        uint4 w;
+                        __builtin_memcpy(&w, p + len - d + i, 16);
+                        __builtin_memcpy(p + len + i, &w, 16);
+                    }
+                for (; i < n; i++) p[len + i] = p[len + i - d];
+            }
         }
         len += n;
         return true;
@@ -370,7 +401,22 @@ SDB_DEV int zlib_decode(const uint8_t *in, uint64_t n, EntOut &o, EntLds &t) {
         if (!s.get(8, b)) return 0;
         a = a << 8 | b;
     }
-    if (o.p) {
+    if (o.p && o.wide) {
+        // Adler-32 over n bytes as sums: A = 1 + sum b_i, B = n + sum (n - i) b_i (mod 65521), lane l
+        // taking bytes l, l + 64, ... (coalesced); (n - i) b_i < 2^34 and a lane adds at most 2^20 of
+        // them per 64 MiB, so the u64 sums never wrap
+        const uint64_t n = o.len;
+        uint64_t sa = 0, sb = 0;
+        for (uint64_t i = (uint64_t)lane_id(); i < n; i += 64) {
+            const uint64_t b = o.p[i];
+            sa += b;
+            sb += (n - i) * b;
+        }
+        sa = wave_sum(sa);
+        sb = wave_sum(sb);
+        const uint32_t x = (uint32_t)((1 + sa) % 65521u), y = (uint32_t)((n % 65521u + sb % 65521u) % 65521u);
+        if ((y << 16 | x) != a) return -1;
+    } else if (o.p) {
         uint32_t x = 1, y = 0;
         for (uint64_t i = 0; i < o.len; i++) {
             x += o.p[i];
@@ -703,19 +749,19 @@ SDB_DEV int zstd_block(EntLds &t, ZstdState &z, const uint8_t *in, uint64_t n, E
     if (ltype == 0) {
         if (ip + regen > n) return -1;
         if (lit) {  // the stage sits past every byte still to be written: a plain 16-byte copy
-            uint64_t i = 0;
-            for (; i + 16 <= regen; i += 16) {
+            const uint64_t n16 = regen & ~15ull, l = o.lane(), L = o.lanes();
+            for (uint64_t i = 16 * l; i < n16; i += 16 * L) {
                 uint4 w;
                 __builtin_memcpy(&w, in + ip + i, 16);
                 __builtin_memcpy(lit + i, &w, 16);
             }
-            for (; i < regen; i++) lit[i] = in[ip + i];
+            for (uint64_t i = n16 + l; i < regen; i += L) lit[i] = in[ip + i];
         }
         ip += regen;
     } else if (ltype == 1) {
         if (ip + 1 > n) return -1;
         if (lit)
-            for (uint64_t i = 0; i < regen; i++) lit[i] = in[ip];
+            for (uint64_t i = o.lane(); i < regen; i += o.lanes()) lit[i] = in[ip];
         ip += 1;
     } else {
         if (ip + csize > n) return -1;
@@ -738,11 +784,18 @@ SDB_DEV int zstd_block(EntLds &t, ZstdState &z, const uint8_t *in, uint64_t n, E
             if (6 + s1 + s2 + s3 > cn) return -1;
             const uint64_t s4 = cn - 6 - s1 - s2 - s3, q = (regen + 3) / 4;
             const uint8_t *p = c + 6;
-            if (huf_stream(t, z.huf_bits, p, s1, lit, q) ||
-                huf_stream(t, z.huf_bits, p + s1, s2, lit ? lit + q : nullptr, q) ||
-                huf_stream(t, z.huf_bits, p + s1 + s2, s3, lit ? lit + 2 * q : nullptr, q) ||
-                huf_stream(t, z.huf_bits, p + s1 + s2 + s3, s4, lit ? lit + 3 * q : nullptr, regen - 3 * q))
+            if (o.wide) {  // lane l decodes stream l & 3 (four lanes per stream store the same bytes)
+                const uint32_t j = (uint32_t)lane_id() & 3;
+                const uint64_t off = j == 0 ? 0 : j == 1 ? s1 : j == 2 ? s1 + s2 : s1 + s2 + s3;
+                const uint64_t sz = j == 0 ? s1 : j == 1 ? s2 : j == 2 ? s3 : s4;
+                const int r = huf_stream(t, z.huf_bits, p + off, sz, lit ? lit + j * q : nullptr, j < 3 ? q : regen - 3 * q);
+                if (__ballot(r != 0)) return -1;
+            } else if (huf_stream(t, z.huf_bits, p, s1, lit, q) ||
+                       huf_stream(t, z.huf_bits, p + s1, s2, lit ? lit + q : nullptr, q) ||
+                       huf_stream(t, z.huf_bits, p + s1 + s2, s3, lit ? lit + 2 * q : nullptr, q) ||
+                       huf_stream(t, z.huf_bits, p + s1 + s2 + s3, s4, lit ? lit + 3 * q : nullptr, regen - 3 * q)) {
                 return -1;
+            }
         }
         ip += csize;
     }
@@ -928,14 +981,12 @@ SDB_DEV int zstd_decode(const uint8_t *in, uint64_t n, EntOut &o, EntLds &t) {
             if (type == 3) return -1;
             if (type == 1) {
                 if (bs > bmax || ip >= n) return -1;
-                for (uint64_t i = 0; i < bs; i++)
-                    if (!o.put(in[ip])) return -1;
+                if (!o.fill(in[ip], bs)) return -1;
                 ip += 1;
             } else {
                 if (n - ip < bs || bs > bmax) return -1;
                 if (type == 0) {
-                    for (uint64_t i = 0; i < bs; i++)
-                        if (!o.put(in[ip + i])) return -1;
+                    if (!o.copy(in + ip, bs)) return -1;
                 } else if (zstd_block(t, z, in + ip, bs, o, fstart, window)) {
                     return -1;
                 }
@@ -1027,7 +1078,7 @@ __global__ __launch_bounds__(kEntThreads) void k_ent_plan(EntArgs a) {
                 if (a.codec != SDB_CODEC_ZLIB && !zstd_frames_size(a.blocks + s, e - s - 4, &fsz)) {
                     slot = fsz + 4;
                 } else {
-                    EntOut o{nullptr, 0, kEntMaxOut, false};
+                    EntOut o{nullptr, 0, kEntMaxOut, false, false};
                     if (!ent_decode(a.codec, a.blocks + s, e - s - 4, o, t) && !o.bad) slot = o.len + 4;
                 }
             }
@@ -1071,15 +1122,11 @@ __global__ __launch_bounds__(kEntThreads) void k_ent_run(EntArgs a) {
             } else if (o + slot > a.out_cap) {
                 st = SDB_INVALID_ARGUMENT;
             } else {
-                int r = 0;
-                uint64_t w = 0;
-                if (l == 0) {
-                    EntOut out{a.out + o, 0, slot - 4, false};
-                    r = ent_decode(a.codec, in, bl, out, t) || out.bad ? SDB_DECOMPRESSION_ERROR : 0;
-                    w = out.len;
-                }
+                // every lane runs the decoder (same state; the copies spread over the lanes, EntOut::wide)
+                EntOut out{a.out + o, 0, slot - 4, false, true};
+                const int r = ent_decode(a.codec, in, bl, out, t) || out.bad ? SDB_DECOMPRESSION_ERROR : 0;
                 st = __shfl(r, 0, 64);
-                ol = (uint64_t)__shfl((long long)w, 0, 64);
+                ol = (uint64_t)__shfl((long long)out.len, 0, 64);
                 __threadfence_block();
                 __builtin_amdgcn_wave_barrier();
                 if (!st) {
