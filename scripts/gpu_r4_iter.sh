@@ -2,6 +2,7 @@
 # Round 4 iteration: the whole -m gpu suite, then the workloads named in $WORK (space separated):
 #   enc     bench.py driver shape (20 steps, 5 warmup) without the CPU leg
 #   dec     configs[2] decode (bench_configs.py --decode) + its kernel trace stats
+#   bsz     every SstBlockSize: encode and decode per SST
 #   encv    encode throughput on D2 and D1-L0 (headline shape)
 #   bloom   configs[3] bloom + kernel trace stats
 #   compact the compaction job + kernel trace stats
@@ -38,6 +39,8 @@ print('encx ${ENCX_ARGS:-}: value', d['value'], 'ms/SST', r['device_ms_per_sst']
     dec) step dec$v 300 python3 scripts/bench_configs.py --decode --no-granular --reps 10 --cpu-seconds 0
          grep '^{\|ticks' $O/dec$v.log | cut -c1-400
          [ -n "$v" ] || step decprof 300 rocprofv3 --kernel-trace --stats -d $O/decprof -o run --output-format csv -- python3 scripts/bench_configs.py --decode --no-granular --reps 5 --cpu-seconds 0 ;;
+    bsz) step bsz$v 400 python3 scripts/bench_block_sizes.py
+         grep "^{" $O/bsz$v.log | cut -c1-300 ;;
     encv) step encv 300 python3 scripts/bench_configs.py --encode --reps 20
          grep '^{' $O/encv.log | cut -c1-400 ;;
     bloom) step bloom$v 200 python3 scripts/bench_configs.py --bloom --reps 20
