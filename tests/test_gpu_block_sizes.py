@@ -72,7 +72,7 @@ def _decode_cases():
             ("huge-rows", big_rows, {})]
 
 
-@pytest.mark.parametrize("block_size", [8192, 16384, 65536])
+@pytest.mark.parametrize("block_size", [8192, 16384, 32768, 65536])
 def test_decode_large_blocks(rt, block_size):  # noqa: F811
     from .test_descending import device_desc
     from .test_gpu_parity import assert_decode_same
@@ -107,6 +107,42 @@ def test_decode_large_blocks_corrupt(rt):  # noqa: F811
     got = rt.Decoder().decode(data, e.block_off, 2)
     assert ref.status != 0
     assert_decode_same(ref, got, "corrupt big blocks")
+
+
+def test_decode_64k_block_corrupt(rt):  # noqa: F811
+    """A 64 KiB block (its CRC through sixteen 4 KiB LDS windows, its rows as restart-region pieces):
+    a flipped byte in each part of the block, a flipped CRC byte, a corrupt trailer count and a corrupt
+    region offset (CRC recomputed: the whole-block walk decides), each alone and in descending order."""
+    import struct
+    import zlib
+    from .test_descending import device_desc
+    from .test_gpu_parity import assert_decode_same
+    b = datasets.d1(n=60000, sst_index=5)
+    e = O.encode_sst(b, O.params(block_size=65536))
+    k = 2
+    s, t = int(e.block_off[k]), int(e.block_off[k + 1])
+    n = t - s - 4
+    variants = []
+    for frac in (0.0, 0.1, 0.3, 0.55, 0.8, 0.99):  # a byte in each part of the block (incl. its trailer)
+        d = e.data.copy()
+        d[s + min(n - 1, int(frac * n))] ^= 0x04
+        variants.append(("flip %.2f" % frac, d))
+    d = e.data.copy()
+    d[t - 1] ^= 0x01
+    variants.append(("crc byte", d))
+    for what, pos, val in (("count", n - 2, 0x7F), ("offset", n - 2 - 2 * 3, 0xFF)):
+        blk = bytearray(e.data[s:t - 4].tobytes())
+        blk[pos] = val
+        d = e.data.copy()
+        d[s:t - 4] = np.frombuffer(bytes(blk), np.uint8)
+        d[t - 4:t] = np.frombuffer(struct.pack(">I", zlib.crc32(bytes(blk))), np.uint8)
+        variants.append((what, d))
+    for what, d in variants:
+        ref = O.decode_blocks(d, e.block_off, 2)
+        assert ref.status != 0 or what in ("count", "offset"), what  # (a bad offset may not matter ascending)
+        assert_decode_same(ref, rt.Decoder().decode(d, e.block_off, 2), "64k " + what)
+        desc = O.decode_blocks(d, e.block_off, 2, descending=True)
+        assert_decode_same(desc, device_desc(rt, d, e.block_off, 2), "64k desc " + what)
 
 
 # ------------------------------------------------------------------------------------------------
