@@ -502,7 +502,10 @@ def codec_bench(reps):
         del db, out
     data, block_off = np.concatenate(datas), np.concatenate(offs)
     nb = len(block_off) - 1
+    only = os.environ.get("SDB_CODECS", "lz4,snappy,zlib,zstd").split(",")  # (per-codec PMC passes)
     for codec, name in ((O.CODEC_LZ4, "lz4"), (O.CODEC_SNAPPY, "snappy"), (O.CODEC_ZLIB, "zlib"), (O.CODEC_ZSTD, "zstd")):
+        if name not in only:
+            continue
         comp, coff = compress_run(codec, data, block_off)
         dc = torch.from_numpy(comp).to(dev)
         do = torch.from_numpy(coff.view(np.int64)).to(dev)
