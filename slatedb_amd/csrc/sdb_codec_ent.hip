@@ -54,13 +54,14 @@ struct Canon {
     uint16_t count[16];
     uint16_t sym[320];
 };
-struct EntLds {  // one wave's tables (zlib uses the first three Canon, aliasing the zstd tables)
+struct ZTab {  // deflate's code tables
+    Canon lit, dist, clc;
+    uint8_t lens[320];
+    uint16_t fast_lit[512], fast_dist[512];  // 9-bit lookup: sym | len << 12 (len 0: longer code)
+};
+struct EntLds {  // one wave's tables (zlib's alias the zstd ones)
     union {
-        struct {
-            Canon lit, dist, clc;
-            uint8_t lens[320];
-            uint16_t fast_lit[512], fast_dist[512];  // 9-bit lookup: sym | len << 12 (len 0: longer code)
-        } z;
+        ZTab z;
         struct {
             FseCell ll[512], of[256], ml[512], wt[64];  // wt: the Huffman weights' table (accuracy <= 6)
             uint16_t huf[2048];  // sym | nb << 8
@@ -187,13 +188,17 @@ struct LsbBits {
     uint64_t n, pos;
     uint64_t buf;
     int cnt;
-    SDB_DEV void refill() {  // up to 32 more bits: one unaligned dword load when 4 bytes remain
-        if (cnt <= 32 && pos + 4 <= n) {
-            uint32_t w;
-            __builtin_memcpy(&w, p + pos, 4);
-            buf |= (uint64_t)w << cnt;
-            cnt += 32;
-            pos += 4;
+    SDB_DEV void refill() {  // to >= 57 bits: one unaligned 8-byte load when 8 bytes remain
+        if (cnt <= 56 && pos + 8 <= n) {
+            // the load's bytes past the whole ones taken land above cnt; a later refill ORs the same
+            // bytes at the same bit positions, so they need no masking
+            uint64_t w;
+            __builtin_memcpy(&w, p + pos, 8);
+            buf |= w << cnt;
+            const uint32_t take = (63 - (uint32_t)cnt) >> 3;
+            pos += take;
+            cnt += 8 * (int)take;
+            return;
         }
         while (cnt <= 56 && pos < n) {
             buf |= (uint64_t)p[pos++] << cnt;
@@ -276,9 +281,9 @@ __constant__ uint8_t c_cl_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 
 
 enum { kZOk = 0, kZTrunc = 1, kZErr = -1 };
 
-SDB_DEV int inflate_raw(LsbBits &s, EntOut &o, EntLds &t) {
+SDB_DEV int inflate_raw(LsbBits &s, EntOut &o, ZTab &t) {
     uint32_t last = 0;
-    uint8_t *lens = t.z.lens;
+    uint8_t *lens = t.lens;
     do {
         uint32_t type;
         if (!s.get(1, last) || !s.get(2, type)) return kZTrunc;
@@ -314,10 +319,10 @@ SDB_DEV int inflate_raw(LsbBits &s, EntOut &o, EntLds &t) {
                 if (!s.get(3, v)) return kZTrunc;
                 cl[c_cl_order[i]] = (uint8_t)v;
             }
-            if (canon_build(t.z.clc, cl, 19)) return kZErr;
+            if (canon_build(t.clc, cl, 19)) return kZErr;
             int i = 0;
             while (i < nlen + ndist) {
-                const int sym = canon_decode(s, t.z.clc);
+                const int sym = canon_decode(s, t.clc);
                 if (sym == -1) return kZTrunc;
                 if (sym < 0) return kZErr;
                 if (sym < 16) {
@@ -344,9 +349,9 @@ SDB_DEV int inflate_raw(LsbBits &s, EntOut &o, EntLds &t) {
             if (lens[256] == 0) return kZErr;
             for (int q = ndist - 1; q >= 0; q--) lens[288 + q] = lens[nlen + q];
         }
-        if (canon_build(t.z.lit, lens, nlen) || canon_build(t.z.dist, lens + 288, ndist)) return kZErr;
-        canon_fast(t.z.lit, t.z.fast_lit);
-        canon_fast(t.z.dist, t.z.fast_dist);
+        if (canon_build(t.lit, lens, nlen) || canon_build(t.dist, lens + 288, ndist)) return kZErr;
+        canon_fast(t.lit, t.fast_lit);
+        canon_fast(t.dist, t.fast_dist);
         // a symbol through the fast table when its code is <= 9 bits and the bits are there
         auto fast_decode = [&](const uint16_t *fast, const Canon &h) -> int {
             if (s.cnt < 9) s.refill();
@@ -360,7 +365,7 @@ SDB_DEV int inflate_raw(LsbBits &s, EntOut &o, EntLds &t) {
             return canon_decode(s, h);
         };
         for (;;) {
-            int sym = fast_decode(t.z.fast_lit, t.z.lit);
+            int sym = fast_decode(t.fast_lit, t.lit);
             if (sym == -1) return kZTrunc;
             if (sym < 0) return kZErr;
             if (sym < 256) {
@@ -373,7 +378,7 @@ SDB_DEV int inflate_raw(LsbBits &s, EntOut &o, EntLds &t) {
             uint32_t v;
             if (!s.get(c_len_extra[sym], v)) return kZTrunc;
             const uint32_t len = c_len_base[sym] + v;
-            const int ds = fast_decode(t.z.fast_dist, t.z.dist);
+            const int ds = fast_decode(t.fast_dist, t.dist);
             if (ds == -1) return kZTrunc;
             if (ds < 0 || ds >= 30) return kZErr;
             if (!s.get(c_dist_extra[ds], v)) return kZTrunc;
@@ -386,7 +391,7 @@ SDB_DEV int inflate_raw(LsbBits &s, EntOut &o, EntLds &t) {
 }
 
 // 0 or -1; Adler-32 checked when the bytes are kept
-SDB_DEV int zlib_decode(const uint8_t *in, uint64_t n, EntOut &o, EntLds &t) {
+SDB_DEV int zlib_decode(const uint8_t *in, uint64_t n, EntOut &o, ZTab &t) {
     if (n < 2) return 0;
     const uint32_t cmf = in[0], flg = in[1];
     if ((cmf & 0x0F) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 != 0 || (flg & 0x20)) return -1;
@@ -444,8 +449,12 @@ struct RevBits {
         wb = w0;
         uint64_t v = 0;
         const int64_t b0 = w0 >> 3;
-        for (int i = 0; i < 8; i++)
-            if (b0 + i < n) v |= (uint64_t)p[b0 + i] << (8 * i);
+        if (b0 + 8 <= n) {
+            __builtin_memcpy(&v, p + b0, 8);  // one unaligned 8-byte load
+        } else {
+            for (int i = 0; i < 8; i++)
+                if (b0 + i < n) v |= (uint64_t)p[b0 + i] << (8 * i);
+        }
         win = v;
     }
     SDB_DEV bool init(const uint8_t *q, int64_t len) {
@@ -1057,7 +1066,7 @@ SDB_DEV int zstd_frames_size(const uint8_t *in, uint64_t n, uint64_t *total) {
 }
 
 SDB_DEV int ent_decode(uint32_t codec, const uint8_t *in, uint64_t n, EntOut &o, EntLds &t) {
-    return codec == SDB_CODEC_ZLIB ? zlib_decode(in, n, o, t) : zstd_decode(in, n, o, t);
+    return codec == SDB_CODEC_ZLIB ? zlib_decode(in, n, o, t.z) : zstd_decode(in, n, o, t);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1149,6 +1158,110 @@ __global__ __launch_bounds__(kEntThreads) void k_ent_run(EntArgs a) {
     }
 }
 
+// Zlib has smaller code tables than zstd (ZTab, 4.3 KB), which leaves room in every wave's LDS for the
+// compressed block itself: the bit reader's refills then hit LDS instead of HBM, one dependent round
+// trip per 56 bits less.  Blocks over the stage are read from HBM as before.
+constexpr uint32_t kZThreads = 1024;  // 16 waves per workgroup
+constexpr uint32_t kZStage = 4352;
+struct ZWave {
+    ZTab t;
+    uint8_t in[kZStage];
+};
+constexpr uint32_t kZWaveLds = (sizeof(ZWave) + 15) & ~15u;
+constexpr uint32_t kZLds = 8 * 1024 + (kZThreads / 64) * kZWaveLds;
+static_assert(kZLds <= 160 * 1024, "zlib decoder LDS");
+
+// the block's bytes [g, g + n) staged in the wave's LDS (16-byte granules; the returned pointer is
+// byte 0), or g itself when they do not fit.  Called by the whole wave.
+SDB_DEV const uint8_t *zl_stage(const uint8_t *g, uint64_t n, uint8_t *buf) {
+    const uintptr_t a0 = (uintptr_t)g & ~(uintptr_t)15;
+    const uint32_t off = (uint32_t)((uintptr_t)g & 15);
+    if (off + n + 15 > kZStage) return g;
+    const uint32_t ng = (uint32_t)((off + n + 15) >> 4);
+    for (uint32_t q = (uint32_t)lane_id(); q < ng; q += 64) ((uint4 *)buf)[q] = ((const uint4 *)a0)[q];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return buf + off;
+}
+
+__global__ __launch_bounds__(kZThreads) void k_zl_plan(EntArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t l = (uint32_t)lane_id(), wave = threadIdx.x >> 6;
+    ZWave &zw = *(ZWave *)(smem + 8 * 1024 + wave * kZWaveLds);
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave; k <= a.nblocks; k += nw) {
+        uint64_t slot = 0;
+        if (k < a.nblocks) {
+            const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
+            if (e >= s && e - s >= 4) {
+                const uint8_t *in = zl_stage(a.blocks + s, e - s - 4, zw.in);
+                if (l == 0) {
+                    EntOut o{nullptr, 0, kEntMaxOut, false, false};
+                    if (!zlib_decode(in, e - s - 4, o, zw.t) && !o.bad) slot = o.len + 4;
+                }
+            }
+        }
+        if (l == 0) a.slot[k] = slot;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+__global__ __launch_bounds__(kZThreads) void k_zl_run(EntArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    crc_slice_tables_to_lds((lu32 *)smem);
+    __syncthreads();
+    const uint32_t(*tab)[256] = (const uint32_t(*)[256])smem;
+    const uint32_t l = (uint32_t)lane_id(), wave = threadIdx.x >> 6;
+    ZWave &zw = *(ZWave *)(smem + 8 * 1024 + wave * kZWaveLds);
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave; k < a.nblocks; k += nw) {
+        const uint64_t s = a.block_off[k], e = a.block_off[k + 1], o = a.out_start[k];
+        const uint64_t slot = a.out_start[k + 1] - o;
+        int st = 0;
+        uint64_t ol = 0;
+        if (e < s || e - s < 4 || e - s > 0xFFFFFFFFull) {
+            st = SDB_CORRUPT_BLOCK;
+        } else {
+            const uint64_t bl = e - s - 4;
+            const uint8_t *g = a.blocks + s;
+            const uint32_t stored = (uint32_t)g[bl] << 24 | (uint32_t)g[bl + 1] << 16 | (uint32_t)g[bl + 2] << 8 |
+                                    (uint32_t)g[bl + 3];
+            const uint8_t *in = zl_stage(g, bl, zw.in);
+            if (ent_crc(in, bl, tab) != stored) {
+                st = SDB_CHECKSUM_MISMATCH;  // validate_checksum (format/sst.rs:1029-1038)
+            } else if (slot == 0) {
+                st = SDB_DECOMPRESSION_ERROR;
+            } else if (o + slot > a.out_cap) {
+                st = SDB_INVALID_ARGUMENT;
+            } else {
+                // every lane runs the decoder (same state; the copies spread over the lanes, EntOut::wide)
+                EntOut out{a.out + o, 0, slot - 4, false, true};
+                const int r = zlib_decode(in, bl, out, zw.t) || out.bad ? SDB_DECOMPRESSION_ERROR : 0;
+                st = __shfl(r, 0, 64);
+                ol = (uint64_t)__shfl((long long)out.len, 0, 64);
+                __threadfence_block();
+                __builtin_amdgcn_wave_barrier();
+                if (!st) {
+                    const uint32_t c = ent_crc(a.out + o, ol, tab);
+                    if (l == 0) {
+                        uint8_t *gw = a.out + o;
+                        gw[ol] = (uint8_t)(c >> 24);
+                        gw[ol + 1] = (uint8_t)(c >> 16);
+                        gw[ol + 2] = (uint8_t)(c >> 8);
+                        gw[ol + 3] = (uint8_t)c;
+                    }
+                }
+            }
+        }
+        if (l == 0) {
+            a.out_end[k] = st ? o : o + ol + 4;
+            if (st) atomicMin(a.err, (unsigned long long)((k << 8) | (uint64_t)st));
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 static std::once_flag g_ent_once;
 static hipError_t g_ent_attr = hipSuccess;
 static void ent_attrs() {
@@ -1156,13 +1269,17 @@ static void ent_attrs() {
         g_ent_attr = hipFuncSetAttribute((const void *)k_ent_plan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEntLds);
         if (g_ent_attr == hipSuccess)
             g_ent_attr = hipFuncSetAttribute((const void *)k_ent_run, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEntLds);
+        if (g_ent_attr == hipSuccess)
+            g_ent_attr = hipFuncSetAttribute((const void *)k_zl_plan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kZLds);
+        if (g_ent_attr == hipSuccess)
+            g_ent_attr = hipFuncSetAttribute((const void *)k_zl_run, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kZLds);
     });
 }
-static uint32_t ent_grid(uint64_t nwaves) {
+static uint32_t ent_grid(uint64_t nwaves, uint32_t threads = kEntThreads) {
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    uint64_t wgs = (nwaves + kEntThreads / 64 - 1) / (kEntThreads / 64);
+    uint64_t wgs = (nwaves + threads / 64 - 1) / (threads / 64);
     const uint64_t most = (uint64_t)(cus > 0 ? cus : 256);
     if (wgs > most) wgs = most;
     return (uint32_t)(wgs ? wgs : 1);
@@ -1179,7 +1296,10 @@ hipError_t launch_ent_slots(uint32_t codec, const uint8_t *blocks, const uint64_
     a.block_off = block_off;
     a.nblocks = nblocks;
     a.slot = slot;
-    hipLaunchKernelGGL(k_ent_plan, dim3(ent_grid(nblocks + 1)), dim3(kEntThreads), kEntLds, st, a);
+    if (codec == SDB_CODEC_ZLIB)
+        hipLaunchKernelGGL(k_zl_plan, dim3(ent_grid(nblocks + 1, kZThreads)), dim3(kZThreads), kZLds, st, a);
+    else
+        hipLaunchKernelGGL(k_ent_plan, dim3(ent_grid(nblocks + 1)), dim3(kEntThreads), kEntLds, st, a);
     return hipGetLastError();
 }
 
@@ -1198,7 +1318,10 @@ hipError_t launch_ent_run(uint32_t codec, const uint8_t *blocks, const uint64_t 
     a.out_start = out_start;
     a.out_end = out_end;
     a.err = err;
-    if (nblocks) hipLaunchKernelGGL(k_ent_run, dim3(ent_grid(nblocks)), dim3(kEntThreads), kEntLds, st, a);
+    if (nblocks && codec == SDB_CODEC_ZLIB)
+        hipLaunchKernelGGL(k_zl_run, dim3(ent_grid(nblocks, kZThreads)), dim3(kZThreads), kZLds, st, a);
+    else if (nblocks)
+        hipLaunchKernelGGL(k_ent_run, dim3(ent_grid(nblocks)), dim3(kEntThreads), kEntLds, st, a);
     return hipGetLastError();
 }
 
