@@ -49,9 +49,10 @@ print('encx ${ENCX_ARGS:-}: value', d['value'], 'ms/SST', r['device_ms_per_sst']
     compact) step compact 300 python3 scripts/bench_configs.py --compact --reps 8
          grep '^{' $O/compact.log | cut -c1-300
          step compactprof 300 rocprofv3 --kernel-trace --stats -d $O/compactprof -o run --output-format csv -- python3 scripts/bench_configs.py --compact --reps 8 ;;
-    codec) step codec 400 python3 scripts/bench_configs.py --codec --reps 3
-         grep '^{' $O/codec.log | cut -c1-300
-         step codecprof 400 rocprofv3 --kernel-trace --stats -d $O/codecprof -o run --output-format csv -- python3 scripts/bench_configs.py --codec --reps 3 ;;
+    codec) [ -z "$v" ] || step codectest$v 300 python3 -u -m pytest tests/test_gpu_codec.py -x -q --timeout 200 --timeout-method thread
+         SDB_CODECS=${SDB_CODECS:-lz4,snappy,zlib,zstd} step codec$v 400 python3 scripts/bench_configs.py --codec --reps 3
+         grep '^{' $O/codec$v.log | cut -c1-300
+         [ -n "$v" ] || step codecprof 400 rocprofv3 --kernel-trace --stats -d $O/codecprof -o run --output-format csv -- python3 scripts/bench_configs.py --codec --reps 3 ;;
   esac
 done
 for f in $O/*prof/run_kernel_stats.csv; do [ -f $f ] && { echo "== $f"; cut -d, -f1-8 $f | head -14; }; done
