@@ -85,6 +85,9 @@ struct EntOut {
     uint64_t len, cap;
     bool bad;
     bool wide;
+    bool adler_defer;     // zlib: leave the Adler-32 check to the caller (adler_want, have_adler)
+    bool have_adler;
+    uint32_t adler_want;
     SDB_DEV uint32_t lane() const { return wide ? (uint32_t)lane_id() : 0u; }
     SDB_DEV uint32_t lanes() const { return wide ? 64u : 1u; }
     SDB_DEV bool put(uint8_t b) {
@@ -406,7 +409,10 @@ SDB_DEV int zlib_decode(const uint8_t *in, uint64_t n, EntOut &o, ZTab &t) {
         if (!s.get(8, b)) return 0;
         a = a << 8 | b;
     }
-    if (o.p && o.wide) {
+    if (o.p && o.adler_defer) {  // the caller checks it (a whole wave, after the decode)
+        o.have_adler = true;
+        o.adler_want = a;
+    } else if (o.p && o.wide) {
         // Adler-32 over n bytes as sums: A = 1 + sum b_i, B = n + sum (n - i) b_i (mod 65521), lane l
         // taking bytes l, l + 64, ... (coalesced); (n - i) b_i < 2^34 and a lane adds at most 2^20 of
         // them per 64 MiB, so the u64 sums never wrap
@@ -1207,6 +1213,130 @@ __global__ __launch_bounds__(kZThreads) void k_zl_plan(EntArgs a) {
     }
 }
 
+// The count-mode plan with several decoders per wave: lanes 0 .. D - 1 each decode their own block
+// with their own code tables, reading the compressed bytes from HBM (the plan's speed tracks the number
+// of decoders per CU, not where its input lives).
+#ifndef SDB_ZL_PLAN_D
+#define SDB_ZL_PLAN_D 4
+#endif
+constexpr uint32_t kZpD = SDB_ZL_PLAN_D, kZpTab = (sizeof(ZTab) + 15) & ~15u;
+constexpr uint32_t kZpThreads = kZpD <= 2 ? 1024u : 2048u / kZpD;  // 32 decoders per workgroup (CU)
+constexpr uint32_t kZpLds = (kZpThreads / 64) * kZpD * kZpTab;
+static_assert(kZpLds <= 160 * 1024, "zlib plan LDS");
+__global__ __launch_bounds__(kZpThreads) void k_zl_plan_multi(EntArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t l = (uint32_t)lane_id(), wave = threadIdx.x >> 6;
+    if (l >= kZpD) return;
+    ZTab &t = *(ZTab *)(smem + (wave * kZpD + l) * kZpTab);
+    const uint64_t ndec = (uint64_t)gridDim.x * (blockDim.x >> 6) * kZpD;
+    for (uint64_t k = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * kZpD + l; k <= a.nblocks; k += ndec) {
+        uint64_t slot = 0;
+        if (k < a.nblocks) {
+            const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
+            if (e >= s && e - s >= 4) {
+                EntOut o{nullptr, 0, kEntMaxOut, false, false};
+                if (!zlib_decode(a.blocks + s, e - s - 4, o, t) && !o.bad) slot = o.len + 4;
+            }
+        }
+        a.slot[k] = slot;
+    }
+}
+
+// Adler-32 of p[0, n) by the whole wave (the sums of zlib_decode's wide path), in every lane
+SDB_DEV uint32_t wave_adler32(const uint8_t *p, uint64_t n) {
+    uint64_t sa = 0, sb = 0;
+    for (uint64_t i = (uint64_t)lane_id(); i < n; i += 64) {
+        const uint64_t b = p[i];
+        sa += b;
+        sb += (n - i) * b;
+    }
+    sa = wave_sum(sa);
+    sb = wave_sum(sb);
+    const uint32_t x = (uint32_t)((1 + sa) % 65521u), y = (uint32_t)((n % 65521u + sb % 65521u) % 65521u);
+    return y << 16 | x;
+}
+
+// The run the same way: each wave takes kZpD blocks, checks their stored CRCs one after the other with
+// the whole wave, lets lanes 0 .. kZpD - 1 decode one block each (copies and Adler-32 on that lane), then
+// computes and appends the output CRCs with the whole wave again.
+#ifndef SDB_ZL_RUN_MULTI
+#define SDB_ZL_RUN_MULTI 1
+#endif
+constexpr uint32_t kZrLds = 8 * 1024 + kZpLds;
+static_assert(kZrLds <= 160 * 1024, "zlib run LDS");
+__global__ __launch_bounds__(kZpThreads) void k_zl_run_multi(EntArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    crc_slice_tables_to_lds((lu32 *)smem);
+    __syncthreads();
+    const uint32_t(*tab)[256] = (const uint32_t(*)[256])smem;
+    const uint32_t l = (uint32_t)lane_id(), wave = threadIdx.x >> 6;
+    ZTab &t = *(ZTab *)(smem + 8 * 1024 + (wave * kZpD + (l < kZpD ? l : 0)) * kZpTab);
+    const uint64_t ndec = (uint64_t)gridDim.x * (blockDim.x >> 6) * kZpD;
+    for (uint64_t k0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * kZpD; k0 < a.nblocks; k0 += ndec) {
+        // 1. the stored CRCs (validate_checksum, format/sst.rs:1029-1038): lane j keeps block k0 + j's status
+        int st = 0;
+        for (uint32_t j = 0; j < kZpD; j++) {
+            const uint64_t k = k0 + j;
+            if (k >= a.nblocks) break;
+            const uint64_t s = a.block_off[k], e = a.block_off[k + 1], o = a.out_start[k];
+            const uint64_t slot = a.out_start[k + 1] - o;
+            int sj = 0;
+            if (e < s || e - s < 4 || e - s > 0xFFFFFFFFull) {
+                sj = SDB_CORRUPT_BLOCK;
+            } else {
+                const uint64_t bl = e - s - 4;
+                const uint8_t *g = a.blocks + s;
+                const uint32_t stored = (uint32_t)g[bl] << 24 | (uint32_t)g[bl + 1] << 16 | (uint32_t)g[bl + 2] << 8 |
+                                        (uint32_t)g[bl + 3];
+                if (ent_crc(g, bl, tab) != stored) sj = SDB_CHECKSUM_MISMATCH;
+                else if (slot == 0) sj = SDB_DECOMPRESSION_ERROR;
+                else if (o + slot > a.out_cap) sj = SDB_INVALID_ARGUMENT;
+            }
+            if (l == j) st = sj;
+        }
+        // 2. lane j decodes block k0 + j (its Adler-32 checked below by the whole wave)
+        uint64_t ol = 0;
+        uint32_t have = 0, want = 0;
+        const uint64_t kl = k0 + l;
+        if (l < kZpD && kl < a.nblocks && !st) {
+            const uint64_t s = a.block_off[kl], e = a.block_off[kl + 1], o = a.out_start[kl];
+            const uint64_t slot = a.out_start[kl + 1] - o;
+            EntOut out{a.out + o, 0, slot - 4, false, false, true, false, 0};
+            st = zlib_decode(a.blocks + s, e - s - 4, out, t) || out.bad ? SDB_DECOMPRESSION_ERROR : 0;
+            ol = out.len;
+            have = out.have_adler ? 1u : 0u;
+            want = out.adler_want;
+        }
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        // 3. the output CRCs, trailers and out_end
+        for (uint32_t j = 0; j < kZpD; j++) {
+            const uint64_t k = k0 + j;
+            if (k >= a.nblocks) break;
+            int sj = __shfl(st, (int)j, 64);
+            const uint64_t olj = (uint64_t)__shfl((long long)ol, (int)j, 64);
+            const uint64_t o = a.out_start[k];
+            if (!sj && __shfl((int)have, (int)j, 64) && wave_adler32(a.out + o, olj) != (uint32_t)__shfl((int)want, (int)j, 64))
+                sj = SDB_DECOMPRESSION_ERROR;
+            if (!sj) {
+                const uint32_t c = ent_crc(a.out + o, olj, tab);
+                if (l == 0) {
+                    uint8_t *gw = a.out + o;
+                    gw[olj] = (uint8_t)(c >> 24);
+                    gw[olj + 1] = (uint8_t)(c >> 16);
+                    gw[olj + 2] = (uint8_t)(c >> 8);
+                    gw[olj + 3] = (uint8_t)c;
+                }
+            }
+            if (l == 0) {
+                a.out_end[k] = sj ? o : o + olj + 4;
+                if (sj) atomicMin(a.err, (unsigned long long)((k << 8) | (uint64_t)sj));
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 __global__ __launch_bounds__(kZThreads) void k_zl_run(EntArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     crc_slice_tables_to_lds((lu32 *)smem);
@@ -1273,6 +1403,12 @@ static void ent_attrs() {
             g_ent_attr = hipFuncSetAttribute((const void *)k_zl_plan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kZLds);
         if (g_ent_attr == hipSuccess)
             g_ent_attr = hipFuncSetAttribute((const void *)k_zl_run, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kZLds);
+        if (g_ent_attr == hipSuccess)
+            g_ent_attr = hipFuncSetAttribute((const void *)k_zl_plan_multi, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)kZpLds);
+        if (g_ent_attr == hipSuccess)
+            g_ent_attr = hipFuncSetAttribute((const void *)k_zl_run_multi, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)kZrLds);
     });
 }
 static uint32_t ent_grid(uint64_t nwaves, uint32_t threads = kEntThreads) {
@@ -1296,7 +1432,9 @@ hipError_t launch_ent_slots(uint32_t codec, const uint8_t *blocks, const uint64_
     a.block_off = block_off;
     a.nblocks = nblocks;
     a.slot = slot;
-    if (codec == SDB_CODEC_ZLIB)
+    if (codec == SDB_CODEC_ZLIB && kZpD > 1)
+        hipLaunchKernelGGL(k_zl_plan_multi, dim3(ent_grid((nblocks + kZpD) / kZpD, kZpThreads)), dim3(kZpThreads), kZpLds, st, a);
+    else if (codec == SDB_CODEC_ZLIB)
         hipLaunchKernelGGL(k_zl_plan, dim3(ent_grid(nblocks + 1, kZThreads)), dim3(kZThreads), kZLds, st, a);
     else
         hipLaunchKernelGGL(k_ent_plan, dim3(ent_grid(nblocks + 1)), dim3(kEntThreads), kEntLds, st, a);
@@ -1318,7 +1456,10 @@ hipError_t launch_ent_run(uint32_t codec, const uint8_t *blocks, const uint64_t 
     a.out_start = out_start;
     a.out_end = out_end;
     a.err = err;
-    if (nblocks && codec == SDB_CODEC_ZLIB)
+    if (nblocks && codec == SDB_CODEC_ZLIB && SDB_ZL_RUN_MULTI)
+        hipLaunchKernelGGL(k_zl_run_multi, dim3(ent_grid((nblocks + kZpD - 1) / kZpD, kZpThreads)), dim3(kZpThreads), kZrLds,
+                           st, a);
+    else if (nblocks && codec == SDB_CODEC_ZLIB)
         hipLaunchKernelGGL(k_zl_run, dim3(ent_grid(nblocks, kZThreads)), dim3(kZThreads), kZLds, st, a);
     else if (nblocks)
         hipLaunchKernelGGL(k_ent_run, dim3(ent_grid(nblocks)), dim3(kEntThreads), kEntLds, st, a);
