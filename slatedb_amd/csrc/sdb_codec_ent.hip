@@ -13,6 +13,8 @@
 //   E2 run   one wave per block: the wave CRC32 of the stored bytes (validate_checksum), lane 0 decodes
 //            into the block's slot in HBM (matches read back its own stores), the wave CRC32 of the
 //            output, the CRC trailer and out_end.
+// (Zlib runs both steps with four decoders per wave, lanes 0-3 each on its own block: k_zl_plan_multi,
+// k_zl_run_multi; zstd runs one decoder per wave on all lanes, EntOut::wide and the *_wide table builds.)
 // Entropy decoding is serial within a stream, so the parallelism is across blocks (a read_blocks range
 // holds hundreds).  Per wave, the LDS holds the code tables: deflate's canonical codes (count + symbols
 // by code order), zstd's three FSE sequence tables and the literal Huffman table.  zstd literals are
@@ -27,6 +29,12 @@
 
 namespace sdb {
 
+#ifndef SDB_ZS_WFSE
+#define SDB_ZS_WFSE 1
+#endif
+#ifndef SDB_ZS_WHUF
+#define SDB_ZS_WHUF 1
+#endif
 constexpr uint32_t kEntThreads = 768;  // 12 waves per workgroup
 constexpr uint64_t kEntMaxOut = 64ull << 20;
 
@@ -68,6 +76,7 @@ struct EntLds {  // one wave's tables (zlib's alias the zstd ones)
             int16_t norm[256];
             uint16_t next[256];
             uint8_t w[256];
+            uint32_t llv[36], mlv[53];  // the length codes' baseline | extra bits << 24 (seq_codes_to_lds)
         } s;
     };
 };
@@ -183,6 +192,47 @@ struct EntOut {
     }
 };
 
+// One-lane decoder output with the literals gathered into 8-byte stores (k_zl_run_multi): the last pn
+// bytes of the output wait in pend; every call that reads or writes p otherwise flushes them first.
+struct EntOutWC : EntOut {
+    uint32_t pn;
+    uint64_t pend;
+    SDB_DEV bool put(uint8_t b) {
+        if (len >= cap) {
+            bad = true;
+            return false;
+        }
+        pend |= (uint64_t)b << (8 * pn);
+        len++;
+        if (++pn == 8) {
+            __builtin_memcpy(p + len - 8, &pend, 8);
+            pend = 0;
+            pn = 0;
+        }
+        return true;
+    }
+    // one 8-byte store when it stays inside the slot and its CRC trailer (cap + 4; the bytes past len
+    // are written again, in order, before anything reads them), else bytewise
+    SDB_DEV void flush() {
+        if (!pn) return;
+        if (len - pn + 8 <= cap + 4) {
+            __builtin_memcpy(p + len - pn, &pend, 8);
+        } else {
+            for (uint32_t i = 0; i < pn; i++) p[len - pn + i] = (uint8_t)(pend >> (8 * i));
+        }
+        pend = 0;
+        pn = 0;
+    }
+    SDB_DEV bool copy(const uint8_t *src, uint64_t n) {
+        flush();
+        return EntOut::copy(src, n);
+    }
+    SDB_DEV bool match(uint64_t d, uint64_t n) {
+        flush();
+        return EntOut::match(d, n);
+    }
+};
+
 // ------------------------------------------------------------------------------------------------
 // zlib / deflate
 // ------------------------------------------------------------------------------------------------
@@ -284,7 +334,8 @@ __constant__ uint8_t c_cl_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 
 
 enum { kZOk = 0, kZTrunc = 1, kZErr = -1 };
 
-SDB_DEV int inflate_raw(LsbBits &s, EntOut &o, ZTab &t) {
+template <class Out>
+SDB_DEV int inflate_raw(LsbBits &s, Out &o, ZTab &t) {
     uint32_t last = 0;
     uint8_t *lens = t.lens;
     do {
@@ -394,7 +445,8 @@ SDB_DEV int inflate_raw(LsbBits &s, EntOut &o, ZTab &t) {
 }
 
 // 0 or -1; Adler-32 checked when the bytes are kept
-SDB_DEV int zlib_decode(const uint8_t *in, uint64_t n, EntOut &o, ZTab &t) {
+template <class Out>
+SDB_DEV int zlib_decode(const uint8_t *in, uint64_t n, Out &o, ZTab &t) {
     if (n < 2) return 0;
     const uint32_t cmf = in[0], flg = in[1];
     if ((cmf & 0x0F) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 != 0 || (flg & 0x20)) return -1;
@@ -491,6 +543,13 @@ struct RevBits {
     }
 };
 
+// an FSE cell {sym, nb, base} as one dword: sym | nb << 8 | base << 16
+SDB_DEV uint32_t fse_cell(const FseCell *t, uint32_t st) {
+    uint32_t v;
+    __builtin_memcpy(&v, t + st, 4);
+    return v;
+}
+
 SDB_DEV int fse_build(FseCell *t, int16_t *norm, uint16_t *next, int nsym, int al) {
     const int size = 1 << al;
     int high = size - 1;
@@ -521,17 +580,82 @@ SDB_DEV int fse_build(FseCell *t, int16_t *norm, uint16_t *next, int nsym, int a
     return 0;
 }
 
+// The same table built by the whole wave (every lane calls it with the same arguments), for tables of
+// <= 64 cells and <= 64 symbols (all of zstd's predefined tables; accuracy log 6 or less): lane s holds
+// symbol s's count, lane k the spread's k-th step.  Step k lands on cell (k * step) & mask; the steps
+// that land below the low-probability cells take the positive-count cells in symbol order (ballot rank
+// of the valid steps), and a cell's state counter is its symbol's count plus the cell's rank among that
+// symbol's cells in cell order (a ballot per symbol).  Other tables: the serial build.
+__device__ __attribute__((noinline)) int fse_build_wide(FseCell *t, int16_t *norm, uint16_t *next, int nsym, int al) {
+    const int size = 1 << al;
+    if (!SDB_ZS_WFSE || size > 64 || nsym > 64) return fse_build(t, norm, next, nsym, al);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // norm, as every lane stored it
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t l = (uint32_t)lane_id();
+    const uint64_t lt = (1ull << l) - 1;
+    const int ns = (int)l < nsym ? norm[l] : 0;
+    const uint32_t npos = ns > 0 ? (uint32_t)ns : 0u;
+    const uint64_t mlow = __ballot(ns == -1);
+    const int high = size - 1 - __popcll(mlow);
+    const uint32_t incl = wave_incl_scan(npos), total = wave_readlane(incl, 63), cum = incl - npos;
+    if ((int)total != high + 1) return fse_build(t, norm, next, nsym, al);
+    uint16_t *symc = next;  // scratch: the symbol of the c-th positive cell (norm stays in registers)
+    for (uint32_t i = 0; i < npos; i++) symc[cum + i] = (uint16_t)l;
+    if (ns == -1) t[size - 1 - __popcll(mlow & lt)].sym = (uint8_t)l;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int step = (size >> 1) + (size >> 3) + 3, mask = size - 1;
+    const int pk = ((int)l * step) & mask;
+    const bool valid = (int)l < size && pk <= high;
+    const uint32_t c = (uint32_t)__popcll(__ballot(valid) & lt);
+    if (valid) t[pk].sym = (uint8_t)symc[c];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const bool cell = (int)l < size;
+    const uint32_t sym = cell ? t[l].sym : 0xFFu;
+    uint32_t rank = 0;
+    for (int q = 0; q < nsym; q++) {
+        const uint64_t m = __ballot(sym == (uint32_t)q);
+        if (sym == (uint32_t)q) rank = (uint32_t)__popcll(m & lt);
+    }
+    const uint32_t nx = (uint32_t)__shfl(ns == -1 ? 1 : ns, cell ? (int)sym : 0, 64);
+    if (cell) {
+        const uint32_t x = nx + rank;
+        const int nb = al - hb32(x);
+        t[l].nb = (uint8_t)nb;
+        t[l].base = (uint16_t)((x << nb) - (uint32_t)size);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return 0;
+}
+
 // FSE table description (forward, LSB-first) -> norm; bytes used or -1
 SDB_DEV int fse_read_ncount(const uint8_t *in, uint64_t n, int16_t *norm, int *nsym, int max_sym, int max_al, int *al_out) {
     if (n < 1) return -1;
-    uint64_t bitpos = 0;
-    auto bits = [&](int k) -> uint32_t {
-        uint32_t v = 0;
-        for (int i = 0; i < k; i++) {
-            const uint64_t q = bitpos + i;
-            if ((q >> 3) < n) v |= (uint32_t)((in[q >> 3] >> (q & 7)) & 1u) << i;
+    // bits [bitpos, bitpos + k) LSB-first, those past the end reading as 0, from a 64-bit window (one
+    // unaligned 8-byte load per <= 57 bits)
+    uint64_t bitpos = 0, wbase = 0, win = 0;
+    auto load = [&]() {
+        const uint64_t b0 = bitpos >> 3;
+        wbase = b0 << 3;
+        uint64_t v = 0;
+        if (b0 + 8 <= n) {
+            __builtin_memcpy(&v, in + b0, 8);
+        } else {
+            for (uint64_t i = 0; i < 8; i++)
+                if (b0 + i < n) v |= (uint64_t)in[b0 + i] << (8 * i);
         }
-        return v;
+        win = v;
+    };
+    load();
+    auto bits = [&](int k) -> uint32_t {  // k <= 16
+        if (bitpos + (uint64_t)k > wbase + 64) load();
+        return (uint32_t)((win >> (bitpos - wbase)) & ((1u << k) - 1));
     };
     const int al = (int)bits(4) + 5;
     bitpos += 4;
@@ -597,7 +721,80 @@ SDB_DEV int huf_from_weights(EntLds &t, int nw, int *maxbits_out) {
     return 0;
 }
 
-SDB_DEV int huf_read(EntLds &t, const uint8_t *in, uint64_t n, int *maxbits) {
+// The same table built by the whole wave (every lane calls it with the same arguments): symbol s of
+// weight v owns the run of 2^(v-1) cells starting at the cells of every lighter symbol and of every
+// lower symbol of the same weight (ballot ranks per weight), each run's first cell takes its entry and
+// the cells between are filled forward from the last entry before them (a wave max-scan over lanes'
+// 32-cell segments).  The serial fill walks weight x symbol: ≈ 2,800 steps per table.
+__device__ __attribute__((noinline)) int huf_from_weights_wide(EntLds &t, int nw, int *maxbits_out) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the weights every lane stored
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint8_t *w = t.s.w;
+    const uint32_t l = (uint32_t)lane_id();
+    uint32_t wv[4], tot = 0;
+    bool bad = false;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const int i = (int)l + 64 * c;
+        wv[c] = i < nw ? w[i] : 0u;
+        bad |= wv[c] > 11;
+        if (wv[c] && wv[c] <= 11) tot += 1u << (wv[c] - 1);
+    }
+    if (__ballot(bad)) return -1;
+    const uint32_t total = wave_sum(tot);
+    if (total == 0) return -1;
+    const int maxbits = hb32(total) + 1;
+    if (maxbits > 11) return -1;
+    const uint32_t rest = (1u << maxbits) - total;
+    if (rest & (rest - 1)) return -1;
+    const uint32_t wl = hb32(rest) + 1;  // the last symbol's weight (nw <= 255, so it is in chunk nw / 64)
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+        if ((int)l + 64 * c == nw) wv[c] = wl;
+    uint32_t pos[4] = {0, 0, 0, 0}, run = 0;
+    const uint64_t lt = (1ull << l) - 1;
+    for (uint32_t v = 1; v <= (uint32_t)maxbits; v++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint64_t m = __ballot(wv[c] == v);
+            if (wv[c] == v) pos[c] = run + ((uint32_t)__popcll(m & lt) << (v - 1));
+            run += (uint32_t)__popcll(m) << (v - 1);
+        }
+    const uint32_t size = 1u << maxbits, g = size >= 64 ? size >> 6 : 1u, u0 = l * g;
+    uint16_t *huf = t.s.huf;
+    for (uint32_t u = l; u < size; u += 64) huf[u] = 0xFFFF;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+        if (wv[c]) huf[pos[c]] = (uint16_t)((l + 64 * c) | (uint32_t)(maxbits + 1 - (int)wv[c]) << 8);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t last = 0;  // (cell + 1) << 16 | entry of the segment's last first-cell
+    if (u0 < size)
+        for (uint32_t j = 0; j < g; j++) {
+            const uint32_t e = huf[u0 + j];
+            if (e != 0xFFFF) last = (u0 + j + 1) << 16 | e;
+        }
+    const uint32_t before = wave_prev_lane(wave_incl_scan_op(last, [](uint32_t x, uint32_t y) { return x > y ? x : y; }));
+    uint32_t cur = before & 0xFFFF;
+    if (u0 < size)
+        for (uint32_t j = 0; j < g; j++) {
+            const uint32_t e = huf[u0 + j];
+            if (e != 0xFFFF) cur = e;
+            else huf[u0 + j] = (uint16_t)cur;
+        }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    *maxbits_out = maxbits;
+    return 0;
+}
+
+SDB_DEV int huf_read(EntLds &t, const uint8_t *in, uint64_t n, int *maxbits, bool wide) {
     if (n < 1) return -1;
     const int hb = in[0];
     uint8_t *w = t.s.w;
@@ -607,7 +804,7 @@ SDB_DEV int huf_read(EntLds &t, const uint8_t *in, uint64_t n, int *maxbits) {
         const int nb = (nw + 1) / 2;
         if ((uint64_t)nb + 1 > n) return -1;
         for (int i = 0; i < nw; i++) w[i] = (i & 1) ? (in[1 + i / 2] & 15) : (in[1 + i / 2] >> 4);
-        if (huf_from_weights(t, nw, maxbits)) return -1;
+        if (wide && SDB_ZS_WHUF ? huf_from_weights_wide(t, nw, maxbits) : huf_from_weights(t, nw, maxbits)) return -1;
         return 1 + nb;
     }
     if ((uint64_t)hb + 1 > n || hb == 0) return -1;
@@ -616,30 +813,32 @@ SDB_DEV int huf_read(EntLds &t, const uint8_t *in, uint64_t n, int *maxbits) {
     const int used = fse_read_ncount(p, (uint64_t)hb, t.s.norm, &nsym, 255, 6, &al);
     if (used < 0) return -1;
     FseCell *ft = t.s.wt;
-    if (fse_build(ft, t.s.norm, t.s.next, nsym, al)) return -1;
+    if (wide ? fse_build_wide(ft, t.s.norm, t.s.next, nsym, al) : fse_build(ft, t.s.norm, t.s.next, nsym, al)) return -1;
     RevBits b;
     if (!b.init(p + used, hb - used)) return -1;
     uint32_t s1 = b.get(al), s2 = b.get(al);
     if (b.pos < 0) return -1;
     for (;;) {
         if (nw >= 255) return -1;
-        w[nw++] = ft[s1].sym;
-        s1 = ft[s1].base + b.get(ft[s1].nb);
+        const uint32_t c1 = fse_cell(ft, s1);
+        w[nw++] = (uint8_t)c1;
+        s1 = (c1 >> 16) + b.get((int)((c1 >> 8) & 0xFF));
         if (b.pos < 0) {
             if (nw >= 255) return -1;
-            w[nw++] = ft[s2].sym;
+            w[nw++] = (uint8_t)fse_cell(ft, s2);
             break;
         }
         if (nw >= 255) return -1;
-        w[nw++] = ft[s2].sym;
-        s2 = ft[s2].base + b.get(ft[s2].nb);
+        const uint32_t c2 = fse_cell(ft, s2);
+        w[nw++] = (uint8_t)c2;
+        s2 = (c2 >> 16) + b.get((int)((c2 >> 8) & 0xFF));
         if (b.pos < 0) {
             if (nw >= 255) return -1;
-            w[nw++] = ft[s1].sym;
+            w[nw++] = (uint8_t)fse_cell(ft, s1);
             break;
         }
     }
-    if (huf_from_weights(t, nw, maxbits)) return -1;
+    if (wide && SDB_ZS_WHUF ? huf_from_weights_wide(t, nw, maxbits) : huf_from_weights(t, nw, maxbits)) return -1;
     return 1 + hb;
 }
 
@@ -676,6 +875,15 @@ __constant__ uint8_t c_ml_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 
                                       0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11,
                                       12, 13, 14, 15, 16};
 
+// the literal / match length codes (baseline, extra bits) into the wave's LDS: looked up once per
+// sequence each, an LDS read instead of a global one on the sequence loop's dependent path.  Whole wave.
+SDB_DEV void seq_codes_to_lds(EntLds &t) {
+    for (uint32_t i = (uint32_t)lane_id(); i < 36 + 53; i += 64) {
+        if (i < 36) t.s.llv[i] = c_ll_base[i] | (uint32_t)c_ll_bits[i] << 24;
+        else t.s.mlv[i - 36] = c_ml_base[i - 36] | (uint32_t)c_ml_bits[i - 36] << 24;
+    }
+}
+
 struct ZstdState {
     int al_ll, al_of, al_ml;
     bool have_ll, have_of, have_ml, have_huf;
@@ -685,10 +893,13 @@ struct ZstdState {
 
 // one sequence table by mode: 0 predefined, 1 RLE, 2 FSE description, 3 repeat; bytes or -1
 SDB_DEV int seq_table(EntLds &t, FseCell *ft, int *al, bool *have, int mode, const uint8_t *in, uint64_t n,
-                      const int16_t *def, int ndef, int def_al, int max_sym, int max_al) {
+                      const int16_t *def, int ndef, int def_al, int max_sym, int max_al, bool wide) {
+    auto build = [&](int ns, int a) {
+        return wide ? fse_build_wide(ft, t.s.norm, t.s.next, ns, a) : fse_build(ft, t.s.norm, t.s.next, ns, a);
+    };
     if (mode == 0) {
         for (int i = 0; i < ndef; i++) t.s.norm[i] = def[i];
-        if (fse_build(ft, t.s.norm, t.s.next, ndef, def_al)) return -1;
+        if (build(ndef, def_al)) return -1;
         *al = def_al;
         *have = true;
         return 0;
@@ -705,7 +916,7 @@ SDB_DEV int seq_table(EntLds &t, FseCell *ft, int *al, bool *have, int mode, con
     if (mode == 2) {
         int nsym, a;
         const int used = fse_read_ncount(in, n, t.s.norm, &nsym, max_sym, max_al, &a);
-        if (used < 0 || fse_build(ft, t.s.norm, t.s.next, nsym, a)) return -1;
+        if (used < 0 || build(nsym, a)) return -1;
         *al = a;
         *have = true;
         return used;
@@ -783,7 +994,7 @@ SDB_DEV int zstd_block(EntLds &t, ZstdState &z, const uint8_t *in, uint64_t n, E
         const uint8_t *c = in + ip;
         uint64_t cn = csize;
         if (ltype == 2) {
-            const int used = huf_read(t, c, cn, &z.huf_bits);
+            const int used = huf_read(t, c, cn, &z.huf_bits, o.wide);
             if (used < 0) return -1;
             z.have_huf = true;
             c += used;
@@ -832,45 +1043,49 @@ SDB_DEV int zstd_block(EntLds &t, ZstdState &z, const uint8_t *in, uint64_t n, E
         if (ip >= n) return -1;
         const int modes = in[ip++];
         if (modes & 3) return -1;
-        int u = seq_table(t, t.s.ll, &z.al_ll, &z.have_ll, modes >> 6, in + ip, n - ip, c_ll_def, 36, 6, 35, 9);
+        int u = seq_table(t, t.s.ll, &z.al_ll, &z.have_ll, modes >> 6, in + ip, n - ip, c_ll_def, 36, 6, 35, 9, o.wide);
         if (u < 0) return -1;
         ip += (uint64_t)u;
-        u = seq_table(t, t.s.of, &z.al_of, &z.have_of, (modes >> 4) & 3, in + ip, n - ip, c_of_def, 29, 5, 31, 8);
+        u = seq_table(t, t.s.of, &z.al_of, &z.have_of, (modes >> 4) & 3, in + ip, n - ip, c_of_def, 29, 5, 31, 8, o.wide);
         if (u < 0) return -1;
         ip += (uint64_t)u;
-        u = seq_table(t, t.s.ml, &z.al_ml, &z.have_ml, (modes >> 2) & 3, in + ip, n - ip, c_ml_def, 53, 6, 52, 9);
+        u = seq_table(t, t.s.ml, &z.al_ml, &z.have_ml, (modes >> 2) & 3, in + ip, n - ip, c_ml_def, 53, 6, 52, 9, o.wide);
         if (u < 0) return -1;
         ip += (uint64_t)u;
         RevBits b;
         if (!b.init(in + ip, (int64_t)(n - ip))) return -1;
         uint32_t sll = b.get(z.al_ll), sof = b.get(z.al_of), sml = b.get(z.al_ml);
+        uint32_t r0 = z.rep[0], r1 = z.rep[1], r2 = z.rep[2];
         for (uint64_t k = 0; k < nseq; k++) {
-            const uint32_t ofc = t.s.of[sof].sym, mlc = t.s.ml[sml].sym, llc = t.s.ll[sll].sym;
+            const uint32_t cof = fse_cell(t.s.of, sof), cml = fse_cell(t.s.ml, sml),
+                           cll = fse_cell(t.s.ll, sll);
+            const uint32_t ofc = cof & 0xFF, mlc = cml & 0xFF, llc = cll & 0xFF;
             if (ofc > 31 || mlc > 52 || llc > 35) return -1;
             const uint32_t ofv = (1u << ofc) + b.get((int)ofc);
-            const uint32_t ml = c_ml_base[mlc] + b.get(c_ml_bits[mlc]);
-            const uint32_t ll = c_ll_base[llc] + b.get(c_ll_bits[llc]);
+            const uint32_t mv = t.s.mlv[mlc], lv = t.s.llv[llc];
+            const uint32_t ml = (mv & 0xFFFFFF) + b.get((int)(mv >> 24));
+            const uint32_t ll = (lv & 0xFFFFFF) + b.get((int)(lv >> 24));
             if (k + 1 < nseq) {
-                sll = t.s.ll[sll].base + b.get(t.s.ll[sll].nb);
-                sml = t.s.ml[sml].base + b.get(t.s.ml[sml].nb);
-                sof = t.s.of[sof].base + b.get(t.s.of[sof].nb);
+                sll = (cll >> 16) + b.get((int)((cll >> 8) & 0xFF));
+                sml = (cml >> 16) + b.get((int)((cml >> 8) & 0xFF));
+                sof = (cof >> 16) + b.get((int)((cof >> 8) & 0xFF));
             }
             if (b.pos < 0) return -1;
             uint32_t off;
             if (ofv > 3) {
                 off = ofv - 3;
-                z.rep[2] = z.rep[1];
-                z.rep[1] = z.rep[0];
-                z.rep[0] = off;
+                r2 = r1;
+                r1 = r0;
+                r0 = off;
             } else {
                 const uint32_t idx = ll == 0 ? ofv : ofv - 1;
                 if (idx == 0) {
-                    off = z.rep[0];
+                    off = r0;
                 } else {
-                    off = idx == 3 ? z.rep[0] - 1 : z.rep[idx];
-                    if (idx > 1) z.rep[2] = z.rep[1];
-                    z.rep[1] = z.rep[0];
-                    z.rep[0] = off;
+                    off = idx == 3 ? r0 - 1 : idx == 1 ? r1 : r2;
+                    if (idx > 1) r2 = r1;
+                    r1 = r0;
+                    r0 = off;
                 }
             }
             if (ll > regen - lp) return -1;
@@ -880,6 +1095,9 @@ SDB_DEV int zstd_block(EntLds &t, ZstdState &z, const uint8_t *in, uint64_t n, E
             if (off == 0 || off > o.len - fstart || off > window) return -1;
             if (!o.match(off, ml)) return -1;
         }
+        z.rep[0] = r0;
+        z.rep[1] = r1;
+        z.rep[2] = r2;
         if (b.pos != 0) return -1;
     } else if (ip != n) {
         return -1;
@@ -1082,6 +1300,8 @@ __global__ __launch_bounds__(kEntThreads) void k_ent_plan(EntArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t l = (uint32_t)lane_id(), wave = threadIdx.x >> 6;
     EntLds &t = *(EntLds *)(smem + 8 * 1024 + wave * kEntWaveLds);
+    seq_codes_to_lds(t);
+    __syncthreads();
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave; k <= a.nblocks; k += nw) {
         if (l != 0) continue;
@@ -1113,10 +1333,11 @@ SDB_DEV uint32_t ent_crc(const uint8_t *msg, uint64_t n, const uint32_t (*tab)[2
 __global__ __launch_bounds__(kEntThreads) void k_ent_run(EntArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     crc_slice_tables_to_lds((lu32 *)smem);
-    __syncthreads();
-    const uint32_t(*tab)[256] = (const uint32_t(*)[256])smem;
     const uint32_t l = (uint32_t)lane_id(), wave = threadIdx.x >> 6;
     EntLds &t = *(EntLds *)(smem + 8 * 1024 + wave * kEntWaveLds);
+    seq_codes_to_lds(t);
+    __syncthreads();
+    const uint32_t(*tab)[256] = (const uint32_t(*)[256])smem;
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t k = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave; k < a.nblocks; k += nw) {
         const uint64_t s = a.block_off[k], e = a.block_off[k + 1], o = a.out_start[k];
@@ -1259,6 +1480,9 @@ SDB_DEV uint32_t wave_adler32(const uint8_t *p, uint64_t n) {
 // The run the same way: each wave takes kZpD blocks, checks their stored CRCs one after the other with
 // the whole wave, lets lanes 0 .. kZpD - 1 decode one block each (copies and Adler-32 on that lane), then
 // computes and appends the output CRCs with the whole wave again.
+#ifndef SDB_ZL_WC
+#define SDB_ZL_WC 1
+#endif
 #ifndef SDB_ZL_RUN_MULTI
 #define SDB_ZL_RUN_MULTI 1
 #endif
@@ -1301,11 +1525,20 @@ __global__ __launch_bounds__(kZpThreads) void k_zl_run_multi(EntArgs a) {
         if (l < kZpD && kl < a.nblocks && !st) {
             const uint64_t s = a.block_off[kl], e = a.block_off[kl + 1], o = a.out_start[kl];
             const uint64_t slot = a.out_start[kl + 1] - o;
-            EntOut out{a.out + o, 0, slot - 4, false, false, true, false, 0};
-            st = zlib_decode(a.blocks + s, e - s - 4, out, t) || out.bad ? SDB_DECOMPRESSION_ERROR : 0;
-            ol = out.len;
-            have = out.have_adler ? 1u : 0u;
-            want = out.adler_want;
+            if (SDB_ZL_WC) {
+                EntOutWC out{{a.out + o, 0, slot - 4, false, false, true, false, 0}, 0, 0};
+                st = zlib_decode(a.blocks + s, e - s - 4, out, t) || out.bad ? SDB_DECOMPRESSION_ERROR : 0;
+                out.flush();
+                ol = out.len;
+                have = out.have_adler ? 1u : 0u;
+                want = out.adler_want;
+            } else {
+                EntOut out{a.out + o, 0, slot - 4, false, false, true, false, 0};
+                st = zlib_decode(a.blocks + s, e - s - 4, out, t) || out.bad ? SDB_DECOMPRESSION_ERROR : 0;
+                ol = out.len;
+                have = out.have_adler ? 1u : 0u;
+                want = out.adler_want;
+            }
         }
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
