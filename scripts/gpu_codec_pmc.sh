@@ -13,6 +13,6 @@ for c in lz4 snappy zstd zlib; do
     SDB_CODECS=$c timeout -k 10 -s KILL 240 rocprofv3 --kernel-trace --pmc $grp -d $O/$c/p$i -o run --output-format csv -- python3 scripts/bench_configs.py --codec --reps 3 > $O/$c.p$i.log 2>&1 || { echo "$c p$i failed"; tail -5 $O/$c.p$i.log; exit 1; }
   done
   python3 scripts/pmc_kernels.py $O/$c/p* > $O/$c.txt
-  echo "== $c"; grep -E "k_dz|k_ent" $O/$c.txt | cut -c1-400
+  echo "== $c"; grep -E "k_dz|k_ent|k_zl" $O/$c.txt | cut -c1-400
 done
 echo done
