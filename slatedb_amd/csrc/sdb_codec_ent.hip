@@ -58,14 +58,25 @@ struct FseCell {
     uint8_t sym, nb;
     uint16_t base;
 };
-struct Canon {
+constexpr int kFastLit = 9, kFastDist = 8;  // the fast tables' index bits
+template <int N>  // N: the alphabet's size (lengths 288, distances 32, code lengths 19)
+struct CanonT {
     uint16_t count[16];
-    uint16_t sym[320];
+    uint16_t sym[N];
 };
 struct ZTab {  // deflate's code tables
-    Canon lit, dist, clc;
-    uint8_t lens[320];
-    uint16_t fast_lit[512], fast_dist[512];  // 9-bit lookup: sym | len << 12 (len 0: longer code)
+    CanonT<288> lit;
+    CanonT<32> dist;
+    union {  // the code-length code and the lengths are dead once lit / dist are built from them
+        struct {
+            CanonT<20> clc;
+            uint8_t lens[320];
+        };
+        struct {
+            // 9-bit (lengths) / 8-bit (distances) lookups: sym | len << 12 (len 0: a longer code)
+            uint16_t fast_lit[1 << kFastLit], fast_dist[1 << kFastDist];
+        };
+    };
 };
 struct EntLds {  // one wave's tables (zlib's alias the zstd ones)
     union {
@@ -272,7 +283,8 @@ struct LsbBits {
     }
 };
 
-SDB_DEV int canon_build(Canon &h, const uint8_t *len, int n) {
+template <int N>
+SDB_DEV int canon_build(CanonT<N> &h, const uint8_t *len, int n) {
     uint16_t offs[16];
     for (int l = 0; l < 16; l++) h.count[l] = 0;
     for (int s = 0; s < n; s++) h.count[len[s]]++;
@@ -291,24 +303,26 @@ SDB_DEV int canon_build(Canon &h, const uint8_t *len, int n) {
     return 0;
 }
 
-// the 9-bit fast table of a usable code: every code of <= 9 bits, bit-reversed (deflate sends a code's
+// the K-bit fast table of a usable code: every code of <= K bits, bit-reversed (deflate sends a code's
 // bits most significant first into an LSB-first stream), replicated over the bits that follow it
-SDB_DEV void canon_fast(const Canon &h, uint16_t *fast) {
-    for (int i = 0; i < 512; i++) fast[i] = 0;
+template <int K, int N>
+SDB_DEV void canon_fast(const CanonT<N> &h, uint16_t *fast) {
+    for (int i = 0; i < (1 << K); i++) fast[i] = 0;
     int code = 0, index = 0;
-    for (int l = 1; l <= 9; l++) {
+    for (int l = 1; l <= K; l++) {
         for (int c = 0; c < h.count[l]; c++, code++, index++) {
             int r = 0;
             for (int b = 0; b < l; b++) r |= ((code >> b) & 1) << (l - 1 - b);
             const uint16_t e = (uint16_t)(h.sym[index] | l << 12);
-            for (int j = r; j < 512; j += 1 << l) fast[j] = e;
+            for (int j = r; j < (1 << K); j += 1 << l) fast[j] = e;
         }
         code <<= 1;
     }
 }
 
 // -1 input ended, -2 invalid code
-SDB_DEV int canon_decode(LsbBits &s, const Canon &h) {
+template <int N>
+SDB_DEV int canon_decode(LsbBits &s, const CanonT<N> &h) {
     int code = 0, first = 0, index = 0;
     for (int l = 1; l < 16; l++) {
         uint32_t b;
@@ -404,12 +418,13 @@ SDB_DEV int inflate_raw(LsbBits &s, Out &o, ZTab &t) {
             for (int q = ndist - 1; q >= 0; q--) lens[288 + q] = lens[nlen + q];
         }
         if (canon_build(t.lit, lens, nlen) || canon_build(t.dist, lens + 288, ndist)) return kZErr;
-        canon_fast(t.lit, t.fast_lit);
-        canon_fast(t.dist, t.fast_dist);
-        // a symbol through the fast table when its code is <= 9 bits and the bits are there
-        auto fast_decode = [&](const uint16_t *fast, const Canon &h) -> int {
+        canon_fast<kFastLit>(t.lit, t.fast_lit);
+        canon_fast<kFastDist>(t.dist, t.fast_dist);
+        // a symbol through the fast table (mask: its size - 1) when its code is short enough and the bits
+        // are there
+        auto fast_decode = [&](const uint16_t *fast, uint32_t mask, const auto &h) -> int {
             if (s.cnt < 9) s.refill();
-            const uint16_t e = fast[s.buf & 511];
+            const uint16_t e = fast[s.buf & mask];
             const int L = e >> 12;
             if (L && L <= s.cnt) {
                 s.buf >>= L;
@@ -419,7 +434,7 @@ SDB_DEV int inflate_raw(LsbBits &s, Out &o, ZTab &t) {
             return canon_decode(s, h);
         };
         for (;;) {
-            int sym = fast_decode(t.fast_lit, t.lit);
+            int sym = fast_decode(t.fast_lit, (1u << kFastLit) - 1, t.lit);
             if (sym == -1) return kZTrunc;
             if (sym < 0) return kZErr;
             if (sym < 256) {
@@ -432,7 +447,7 @@ SDB_DEV int inflate_raw(LsbBits &s, Out &o, ZTab &t) {
             uint32_t v;
             if (!s.get(c_len_extra[sym], v)) return kZTrunc;
             const uint32_t len = c_len_base[sym] + v;
-            const int ds = fast_decode(t.fast_dist, t.dist);
+            const int ds = fast_decode(t.fast_dist, (1u << kFastDist) - 1, t.dist);
             if (ds == -1) return kZTrunc;
             if (ds < 0 || ds >= 30) return kZErr;
             if (!s.get(c_dist_extra[ds], v)) return kZTrunc;
@@ -1441,7 +1456,10 @@ __global__ __launch_bounds__(kZThreads) void k_zl_plan(EntArgs a) {
 #define SDB_ZL_PLAN_D 4
 #endif
 constexpr uint32_t kZpD = SDB_ZL_PLAN_D, kZpTab = (sizeof(ZTab) + 15) & ~15u;
-constexpr uint32_t kZpThreads = kZpD <= 2 ? 1024u : 2048u / kZpD;  // 32 decoders per workgroup (CU)
+#ifndef SDB_ZL_WAVES
+#define SDB_ZL_WAVES 14
+#endif
+constexpr uint32_t kZpThreads = 64 * SDB_ZL_WAVES;  // 56 decoders per workgroup (CU)
 constexpr uint32_t kZpLds = (kZpThreads / 64) * kZpD * kZpTab;
 static_assert(kZpLds <= 160 * 1024, "zlib plan LDS");
 __global__ __launch_bounds__(kZpThreads) void k_zl_plan_multi(EntArgs a) {
