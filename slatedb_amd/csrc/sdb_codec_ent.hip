@@ -58,7 +58,10 @@ struct FseCell {
     uint8_t sym, nb;
     uint16_t base;
 };
-constexpr int kFastLit = 9, kFastDist = 8;  // the fast tables' index bits
+#ifndef SDB_ZL_FAST_DIST
+#define SDB_ZL_FAST_DIST 8
+#endif
+constexpr int kFastLit = 9, kFastDist = SDB_ZL_FAST_DIST;  // the fast tables' index bits
 template <int N>  // N: the alphabet's size (lengths 288, distances 32, code lengths 19)
 struct CanonT {
     uint16_t count[16];
