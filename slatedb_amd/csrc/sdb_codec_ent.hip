@@ -13,7 +13,7 @@
 //   E2 run   one wave per block: the wave CRC32 of the stored bytes (validate_checksum), lane 0 decodes
 //            into the block's slot in HBM (matches read back its own stores), the wave CRC32 of the
 //            output, the CRC trailer and out_end.
-// (Zlib runs both steps with four decoders per wave, lanes 0-3 each on its own block: k_zl_plan_multi,
+// (Zlib runs both steps with five decoders per wave, lanes 0-4 each on its own block: k_zl_plan_multi,
 // k_zl_run_multi; zstd runs one decoder per wave on all lanes, EntOut::wide and the *_wide table builds.)
 // Entropy decoding is serial within a stream, so the parallelism is across blocks (a read_blocks range
 // holds hundreds).  Per wave, the LDS holds the code tables: deflate's canonical codes (count + symbols
@@ -59,7 +59,7 @@ struct FseCell {
     uint16_t base;
 };
 #ifndef SDB_ZL_FAST_DIST
-#define SDB_ZL_FAST_DIST 8
+#define SDB_ZL_FAST_DIST 7
 #endif
 constexpr int kFastLit = 9, kFastDist = SDB_ZL_FAST_DIST;  // the fast tables' index bits
 template <int N>  // N: the alphabet's size (lengths 288, distances 32, code lengths 19)
@@ -76,7 +76,7 @@ struct ZTab {  // deflate's code tables
             uint8_t lens[320];
         };
         struct {
-            // 9-bit (lengths) / 8-bit (distances) lookups: sym | len << 12 (len 0: a longer code)
+            // 9-bit (lengths) / 7-bit (distances) lookups: sym | len << 12 (len 0: a longer code)
             uint16_t fast_lit[1 << kFastLit], fast_dist[1 << kFastDist];
         };
     };
@@ -1456,13 +1456,13 @@ __global__ __launch_bounds__(kZThreads) void k_zl_plan(EntArgs a) {
 // with their own code tables, reading the compressed bytes from HBM (the plan's speed tracks the number
 // of decoders per CU, not where its input lives).
 #ifndef SDB_ZL_PLAN_D
-#define SDB_ZL_PLAN_D 4
+#define SDB_ZL_PLAN_D 5
 #endif
 constexpr uint32_t kZpD = SDB_ZL_PLAN_D, kZpTab = (sizeof(ZTab) + 15) & ~15u;
 #ifndef SDB_ZL_WAVES
 #define SDB_ZL_WAVES 14
 #endif
-constexpr uint32_t kZpThreads = 64 * SDB_ZL_WAVES;  // 56 decoders per workgroup (CU)
+constexpr uint32_t kZpThreads = 64 * SDB_ZL_WAVES;  // 70 decoders per workgroup (CU)
 constexpr uint32_t kZpLds = (kZpThreads / 64) * kZpD * kZpTab;
 static_assert(kZpLds <= 160 * 1024, "zlib plan LDS");
 __global__ __launch_bounds__(kZpThreads) void k_zl_plan_multi(EntArgs a) {
