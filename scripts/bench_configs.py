@@ -673,6 +673,45 @@ def hbm_bench(reps):
     del a, b, a64
 
 
+def footer_bench(reps):
+    """Host footer of one D1 SST (sdb_sst_footer: filter block, index, stats, SsTableInfo; 17,016 blocks):
+    the C call alone, its inputs prepared once (the first keys gathered as runtime.sst_footer does)."""
+    from oracle import oracle as O
+    b = datasets.d1(sst_index=3)
+    e = O.encode_sst(b, O.params())
+    ref = runtime.sst_footer(b, e)
+    sm = e.summary if isinstance(e.summary, _abi.SstSummary) else _abi.SstSummary(**e.summary)
+    nb = len(e.block_off) - 1
+    starts = np.asarray(e.block_first_entry[:nb], np.int64)
+    ikl = np.asarray(e.index_key_len[:nb], np.uint64)
+    fko = np.zeros(nb + 1, np.uint64)
+    fko[1:] = np.cumsum(ikl)
+    idx = np.repeat(b.key_off[starts] - fko[:-1], ikl.astype(np.int64)) + np.arange(int(fko[-1]), dtype=np.uint64)
+    fk = np.ascontiguousarray(b.key_bytes[idx.astype(np.int64)])
+    boff = np.ascontiguousarray(e.block_off[:nb], np.uint64)
+    bst = np.ascontiguousarray(np.asarray(e.block_stats, np.uint16).reshape(-1))
+    bloom = np.ascontiguousarray(np.asarray(e.bloom, np.uint8))
+    first, last = b.key(0), b.key(b.n - 1)
+    fi = _abi.FooterIn(2, _abi.SST_COMPACTED, 1, sm.num_probes, int(sm.data_len), nb, boff.ctypes.data,
+                       fk.ctypes.data, fko.ctypes.data, first, len(first), last, len(last), C.addressof(sm),
+                       bst.ctypes.data, bloom.ctypes.data, int(sm.bloom_len), None)
+    L = runtime.lib()
+    cap = L.sdb_sst_footer_bound(C.byref(fi))
+    out = np.empty(cap, np.uint8)
+    n = C.c_uint64(0)
+    ts = []
+    for _ in range(reps + 3):
+        t0 = time.perf_counter()
+        st = L.sdb_sst_footer(C.byref(fi), out.ctypes.data, cap, C.byref(n))
+        ts.append(time.perf_counter() - t0)
+        assert st == 0
+    assert out[:n.value].tobytes() == ref, "footer bytes changed"
+    ts = sorted(ts[3:])
+    print(json.dumps({"what": "host SST footer (sdb_sst_footer) of one D1 SST", "blocks": nb, "footer_bytes": n.value,
+                      "ms_median": round(1e3 * ts[len(ts) // 2], 3), "ms_min": round(1e3 * ts[0], 3),
+                      "cpu": cpu_model()}), flush=True)
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--decode", action="store_true")
@@ -683,11 +722,16 @@ def main():
     p.add_argument("--codec", action="store_true")
     p.add_argument("--lookup", action="store_true")
     p.add_argument("--encode", action="store_true", help="encode D2 and D1-L0 (headline shape)")
+    p.add_argument("--footer", action="store_true", help="host footer of one D1 SST (no device)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="decode CPU baseline budget (0: skip)")
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--no-granular", action="store_true", help="decode: skip the 2 MiB granularity run")
     a = p.parse_args()
-    allp = not (a.decode or a.bloom or a.e2e or a.compact or a.hbm or a.codec or a.lookup or a.encode)
+    allp = not (a.decode or a.bloom or a.e2e or a.compact or a.hbm or a.codec or a.lookup or a.encode or a.footer)
+    if a.footer or allp:
+        footer_bench(max(a.reps, 20))
+    if a.footer and not allp:
+        return
     torch.cuda.set_device(0)
     runtime.require_device()
     if a.bloom or allp:

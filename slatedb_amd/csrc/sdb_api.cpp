@@ -184,6 +184,7 @@ SstSlot plan_slot(const sdb_kv_batch *b, const sdb_sst_params *p, const sdb_sst_
     s.has_filter_ws = (p->bloom_bits_per_key && filter_bytes_for(n, p->bloom_bits_per_key)) ? 1 : 0;
     s.nchunks = (uint32_t)((n + kChunk - 1) / kChunk);
     s.nfacts = (uint32_t)((n + kFactsEntries - 1) / kFactsEntries);
+    fill_ws_layout(s);
     {   // chunks per group: about sqrt(nchunks), so k_enum walks <= ~2 sqrt(nchunks) tables
         uint32_t g = 16;
         while ((uint64_t)g * g < s.nchunks) g++;

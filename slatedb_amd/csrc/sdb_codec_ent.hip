@@ -1291,8 +1291,9 @@ SDB_DEV int zstd_frames_size(const uint8_t *in, uint64_t n, uint64_t *total) {
             if (n - ip < 3) return -1;
             const uint32_t bh = in[ip] | (uint32_t)in[ip + 1] << 8 | (uint32_t)in[ip + 2] << 16;
             ip += 3;
-            const uint64_t csz = ((bh >> 1) & 3) == 1 ? 1 : (bh >> 3);  // RLE: one stored byte
-            if (((bh >> 1) & 3) == 3 || n - ip < csz) return -1;
+            const uint32_t bt = (bh >> 1) & 3;
+            const uint64_t csz = bt == 1 ? 1 : (bh >> 3);  // RLE: one stored byte
+            if (bt == 3 || n - ip < csz) return -1;
             ip += csz;
             if (bh & 1) break;
         }
@@ -1300,8 +1301,10 @@ SDB_DEV int zstd_frames_size(const uint8_t *in, uint64_t n, uint64_t *total) {
             if (n - ip < 4) return -1;
             ip += 4;
         }
+        // an untrusted header: a content size that would carry the sum past the output bound (or wrap it) is
+        // malformed (a size its blocks do not produce is rejected by the run, zstd_decode)
+        if (fcs > kEntMaxOut - sum) return -1;
         sum += fcs;
-        if (sum > kEntMaxOut) return -1;
     }
     *total = sum;
     return 0;

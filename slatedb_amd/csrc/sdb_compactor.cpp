@@ -88,6 +88,10 @@ struct sdb_compactor {
     DevBuf merge_ws, cols, keys, vals, cut_ws, cuts, sst_meta, sst_data, sst_bloom, enc_ws, dec, dec_ws, cx_tab;
     std::vector<GroupBufs> groups;
     PinBuf pin, pin_tab;
+    // recorded on the job's stream when a run_ssts job returns (every path): the next job waits for it
+    // before it rewrites pin_tab / cx_tab, which that job's upload and kernels may still be reading
+    hipEvent_t tab_ev = nullptr;
+    bool tab_ev_live = false;
     sdb_kv_batch merged{};
     sdb_merge_summary msum{};
     std::vector<sdb_compacted_sst> ssts;
@@ -98,8 +102,10 @@ struct sdb_compactor {
             b->release();
         for (GroupBufs &g : groups)
             for (DevBuf *b : {&g.cols, &g.keys, &g.vals, &g.asrun}) b->release();
+        if (tab_ev) (void)hipEventSynchronize(tab_ev);
         pin.release();
         pin_tab.release();
+        if (tab_ev) (void)hipEventDestroy(tab_ev);
     }
 };
 
@@ -168,8 +174,9 @@ sdb_status group_runs(sdb_compactor *c, const sdb_run *runs, uint32_t nruns, con
         if (sm.status) {
             *fail = sm;
             fail->num_in = job_total;
-            if (sm.status == SDB_INVALID_ARGUMENT && sm.first_error_entry != ~0ull && !(gate && g == 0))
-                fail->first_error_entry += base;
+            // the group's entry numbering starts at `base` in the job's (a gate error can only come from
+            // group 0, whose base is 0)
+            if (sm.status == SDB_INVALID_ARGUMENT && sm.first_error_entry != ~0ull) fail->first_error_entry += base;
             return (sdb_status)sm.status;
         }
         if (!B.keys.ensure(sm.key_bytes + 16) || !B.vals.ensure(sm.val_bytes + 16) ||
@@ -319,6 +326,7 @@ sdb_status sdb_compactor_run(sdb_compactor *c, const sdb_run *runs, uint32_t nru
     c->merged = sdb_kv_batch{};
     c->msum = sdb_merge_summary{};
     if (params->sst_type != SDB_SST_COMPACTED) return SDB_INVALID_ARGUMENT;  // compactions write compacted SSTs
+    if ((nruns && !runs) || !ret) return SDB_INVALID_ARGUMENT;  // before group_runs reads runs[]
     if (hipSetDevice(c->device) != hipSuccess) return SDB_DEVICE_ERROR;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     uint64_t total = 0;
@@ -421,8 +429,15 @@ sdb_status sdb_compactor_run_ssts(sdb_compactor *c, const sdb_compaction_input *
     const uint64_t t_data = 0, t_boff = al256(8ull * ninputs), t_first = t_boff + al256(8ull * ninputs);
     const uint64_t t_rblk = t_first + al256(8ull * (ninputs + 1)), t_rent = t_rblk + al256(8ull * (nruns + 1));
     const uint64_t t_total = t_rent + al256(8ull * (nruns + 1));
+    // the previous job's upload and kernels may still read pin_tab / cx_tab (a job that failed early
+    // returns without a synchronisation, and the caller may alternate streams)
+    if (c->tab_ev_live && hipEventSynchronize(c->tab_ev) != hipSuccess) return SDB_DEVICE_ERROR;
+    c->tab_ev_live = false;
+    if (!c->tab_ev && hipEventCreateWithFlags(&c->tab_ev, hipEventDisableTiming) != hipSuccess) {
+        c->tab_ev = nullptr;
+        return SDB_DEVICE_ERROR;
+    }
     if (!c->pin_tab.ensure(t_total) || !c->cx_tab.ensure(t_total)) return SDB_DEVICE_ERROR;
-    // (the previous job's table upload read this pinned buffer: it completed with that job's synchronisations)
     uint8_t *th = static_cast<uint8_t *>(c->pin_tab.p);
     const uint8_t **h_data = reinterpret_cast<const uint8_t **>(th + t_data);
     const uint64_t **h_boff = reinterpret_cast<const uint64_t **>(th + t_boff);
@@ -461,6 +476,11 @@ sdb_status sdb_compactor_run_ssts(sdb_compactor *c, const sdb_compaction_input *
     in.key_bytes = K;
     if (E >= (1ull << 31)) return SDB_LIMIT_EXCEEDED;
     if (hipMemcpyAsync(c->cx_tab.p, th, t_total, hipMemcpyHostToDevice, s) != hipSuccess) return SDB_DEVICE_ERROR;
+    struct TabRelease {  // on every return from here: everything enqueued so far precedes the event
+        sdb_compactor *c;
+        hipStream_t s;
+        ~TabRelease() { c->tab_ev_live = hipEventRecord(c->tab_ev, s) == hipSuccess; }
+    } tab_release{c, s};
     in.data = c->cx_tab.at<const uint8_t *const>(t_data);
     in.block_off = c->cx_tab.at<const uint64_t *const>(t_boff);
     in.first_block = c->cx_tab.at<const uint64_t>(t_first);

@@ -1484,7 +1484,9 @@ SDB_DEV void dec_finish(const DecodeArgs &a) {
     s->status = e == ~0ull ? 0 : (int32_t)(e & 0xFF);
     s->pad = 0;
     a.out.block_entry_start[a.nblocks] = ne;
-    if (ne > a.out.cap_entries || kb > a.out.key_arena_cap) s->status = SDB_INVALID_ARGUMENT;
+    // over capacity nothing was written; fail-fast still reports a bad block's error first (read_blocks fails
+    // on the block; k_dec_emit checked the deferred checksums without emitting)
+    if (ne > a.out.cap_entries || kb > a.out.key_arena_cap) s->status = (a.fail_fast && e != ~0ull) ? s->status : SDB_INVALID_ARGUMENT;
     else a.out.key_off[ne] = kb;
 }
 
@@ -1560,7 +1562,9 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
         if (l < kDecGuard / 4) ((lu32 *)(img - kDecGuard))[l] = 0;
         __syncthreads();
     }
-    // capacity guard: if the counted output does not fit the caller's arrays, write nothing
+    // capacity guard: if the counted output does not fit the caller's arrays, write nothing (fail-fast still
+    // walks the blocks to verify the checksums the count pass deferred: a corrupt block whose garbage
+    // raises the counts must report CHECKSUM_MISMATCH, not the capacity)
     if (tot_ent > a.out.cap_entries || tot_kb > a.out.key_arena_cap) run = false;
     a.dn = tot_ent;
     a.dkb = tot_kb;
@@ -1593,14 +1597,14 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
     Granules pre;
     Meta m1{};
     uint32_t rp1 = 0;
-    if (run && k < a.nblocks) {
+    if ((run || ff) && k < a.nblocks) {
         ns = off_s(k);
         ne = off_e(k);
         if (dec_fast(ns, ne)) gran_load(a, ns, ne, pre);
         rp1 = rowpos_load(k);
         meta_load(k, m1);
     }
-    for (; run && k < a.nblocks; k += nwaves) {
+    for (; (run || ff) && k < a.nblocks; k += nwaves) {
         const uint64_t s = ns, e = ne;
         const Granules cur = pre;
         const Meta m = m1;
@@ -1613,11 +1617,11 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
             meta_load(k + nwaves, m1);
         }
         const uint64_t ent0 = m.ent0;
-        if (l == 0) a.out.block_entry_start[k] = ent0;
+        if (run && l == 0) a.out.block_entry_start[k] = ent0;
         const uint32_t fb = (m.fw >> (8 * (k & 3))) & 0xFF;
         const bool skip = m.ent1 == ent0 || (fb & kFlagGen);  // nothing to emit, or k_dec_emit_gen's
         // fail-fast: every block of one wave image the count pass did not reject is checked here
-        if (skip && !(ff && !(fb & kFlagBad) && dec_fast(s, e))) continue;
+        if ((skip || !run) && !(ff && !(fb & kFlagBad) && dec_fast(s, e))) continue;
         const uint64_t kb0 = m.kb0;
         DEC_T(t0);
         const LdsBlockView v = stage_lds(a, s, e, img, ff, &cur);
@@ -1629,7 +1633,7 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
             }
             continue;
         }
-        if (skip) continue;
+        if (skip || !run) continue;
         DEC_T(t1);
         ((lu32 *)(kbuf + kRowTmp))[l] = rp;
         wave_sync_d();

@@ -207,6 +207,12 @@ hipError_t launch_bloom_match(const uint8_t *bitmap, uint64_t bytes, uint32_t k,
 // segmentation kernels of all of them at once.  Passed by value (kernel arguments).
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t kMaxSsts = 8;
+enum WsField {
+    kWsLcp = 0, kWsSzr, kWsSznr, kWsHd, kWsRowScratch, kWsNext, kWsBbytes, kWsTabExit, kWsTabCnt, kWsTabBytes,
+    kWsAnchorE, kWsAnchorBlk, kWsAnchorByte, kWsErr, kWsWmax, kWsSlowCount, kWsSlowList, kWsBigCount, kWsBigList,
+    kWsDesc, kWsStatPart, kWsHugePart, kWsWmaxPart, kWsBloomRep, kWsErrPart, kWsDone, kWsGtabExit, kWsGtabCnt,
+    kWsGtabBytes, kWsMode, kWsBlen, kWsFields
+};
 struct SstSlot {
     const uint8_t *key_bytes;
     const uint64_t *key_off;
@@ -232,6 +238,9 @@ struct SstSlot {
     uint32_t nchunks, nfacts, group, slot_cap;
     uint32_t prefix_bloom, pad2;  // the filter is a prefix-extractor one: its length is device-counted
     BloomPlan bpl;            // fused bloom plan (bloom_fused)
+    // encode_workspace_offsets(n, has_filter_ws) in 256-byte units, filled on the host (fill_ws_layout):
+    // the kernels load them instead of re-deriving the layout's 64-bit offset chain on the scalar unit
+    uint32_t wso[kWsFields];
 };
 struct SstSet {
     uint32_t count;
@@ -260,48 +269,48 @@ __host__ __device__ inline EncodeArgs make_args(const SstSet &P, uint32_t i) {
     a.wal = P.wal;
     a.nchunks = s.nchunks;
     a.seg_look = P.seg_look;
-    const EncodeWorkspace w = encode_workspace_offsets(s.n, s.has_filter_ws != 0);
     uint8_t *b = s.ws;
-    a.lcp = (uint32_t *)(b + w.lcp);
-    a.szr = (uint32_t *)(b + w.szr);
-    a.sznr = (uint32_t *)(b + w.sznr);
-    a.hd = (uint64_t *)(b + w.hd);
+    auto W = [&](int f) { return b + ((uint64_t)s.wso[f] << 8); };
+    a.lcp = (uint32_t *)W(kWsLcp);
+    a.szr = (uint32_t *)W(kWsSzr);
+    a.sznr = (uint32_t *)W(kWsSznr);
+    a.hd = (uint64_t *)W(kWsHd);
     a.nfacts = s.nfacts;
-    a.row_scratch = (uint32_t *)(b + w.row_scratch);
-    a.next = (uint32_t *)(b + w.next);
-    a.bbytes = (uint32_t *)(b + w.bbytes);
-    a.tab_exit = (uint32_t *)(b + w.tab_exit);
-    a.tab_cnt = (uint32_t *)(b + w.tab_cnt);
-    a.tab_bytes = (uint64_t *)(b + w.tab_bytes);
-    a.anchor_e = (uint32_t *)(b + w.anchor_e);
-    a.anchor_blk = (uint32_t *)(b + w.anchor_blk);
-    a.anchor_byte = (uint64_t *)(b + w.anchor_byte);
-    a.err = (unsigned long long *)(b + w.err);
-    a.wmax = (uint32_t *)(b + w.wmax);
-    a.slow_count = (uint32_t *)(b + w.slow_count);
-    a.slow_list = (uint32_t *)(b + w.slow_list);
-    a.big_count = (uint32_t *)(b + w.big_count);
-    a.big_list = (uint32_t *)(b + w.big_list);
-    a.desc = (BlockDesc *)(b + w.desc);
-    a.stat_part = (uint64_t *)(b + w.stat_part);
-    a.huge_part = (uint32_t *)(b + w.huge_part);
-    a.wmax_part = (uint32_t *)(b + w.wmax_part);
-    a.err_part = (unsigned long long *)(b + w.err_part);
-    a.gtab_exit = (uint32_t *)(b + w.gtab_exit);
-    a.gtab_cnt = (uint32_t *)(b + w.gtab_cnt);
-    a.gtab_bytes = (uint64_t *)(b + w.gtab_bytes);
-    a.mode = (uint32_t *)(b + w.mode);
+    a.row_scratch = (uint32_t *)W(kWsRowScratch);
+    a.next = (uint32_t *)W(kWsNext);
+    a.bbytes = (uint32_t *)W(kWsBbytes);
+    a.tab_exit = (uint32_t *)W(kWsTabExit);
+    a.tab_cnt = (uint32_t *)W(kWsTabCnt);
+    a.tab_bytes = (uint64_t *)W(kWsTabBytes);
+    a.anchor_e = (uint32_t *)W(kWsAnchorE);
+    a.anchor_blk = (uint32_t *)W(kWsAnchorBlk);
+    a.anchor_byte = (uint64_t *)W(kWsAnchorByte);
+    a.err = (unsigned long long *)W(kWsErr);
+    a.wmax = (uint32_t *)W(kWsWmax);
+    a.slow_count = (uint32_t *)W(kWsSlowCount);
+    a.slow_list = (uint32_t *)W(kWsSlowList);
+    a.big_count = (uint32_t *)W(kWsBigCount);
+    a.big_list = (uint32_t *)W(kWsBigList);
+    a.desc = (BlockDesc *)W(kWsDesc);
+    a.stat_part = (uint64_t *)W(kWsStatPart);
+    a.huge_part = (uint32_t *)W(kWsHugePart);
+    a.wmax_part = (uint32_t *)W(kWsWmaxPart);
+    a.err_part = (unsigned long long *)W(kWsErrPart);
+    a.gtab_exit = (uint32_t *)W(kWsGtabExit);
+    a.gtab_cnt = (uint32_t *)W(kWsGtabCnt);
+    a.gtab_bytes = (uint64_t *)W(kWsGtabBytes);
+    a.mode = (uint32_t *)W(kWsMode);
     a.group = s.group;
     a.bloom_fused = s.bloom_fused;
     a.bpl = s.bpl;
     {  // bloom slots (BloomSlots, sdb_bloom.hip): counts then slots, 256-byte aligned
-        uint8_t *q = b + w.bloom_rep;
+        uint8_t *q = W(kWsBloomRep);
         a.bq.count = (uint32_t *)q;
         a.bq.slot = (uint32_t *)(q + (((uint64_t)s.bpl.tiles * s.bpl.nslices * 4 + 255) & ~255ull));
         a.bq.cap = s.slot_cap;
     }
     a.bloom_out = s.bloom_out;
-    a.done = (uint32_t *)(b + w.done);
+    a.done = (uint32_t *)W(kWsDone);
     a.nprep_wg = s.nchunks;
     a.seg_lds = kSegLds;
     a.out_data = s.out_data;
@@ -315,8 +324,18 @@ __host__ __device__ inline EncodeArgs make_args(const SstSet &P, uint32_t i) {
     a.bloom_len = s.bloom_len;
     a.num_probes = s.num_probes;
     a.filter_built = s.filter_built;
-    a.bloom_len_dev = s.prefix_bloom ? (uint64_t *)(b + w.blen) : nullptr;
+    a.bloom_len_dev = s.prefix_bloom ? (uint64_t *)W(kWsBlen) : nullptr;
     return a;
+}
+
+// The slot's workspace layout (wso) from its n and has_filter_ws (host, after both are set).
+inline void fill_ws_layout(SstSlot &s) {
+    const EncodeWorkspace w = encode_workspace_offsets(s.n, s.has_filter_ws != 0);
+    const uint64_t off[kWsFields] = {w.lcp, w.szr, w.sznr, w.hd, w.row_scratch, w.next, w.bbytes, w.tab_exit, w.tab_cnt,
+                                     w.tab_bytes, w.anchor_e, w.anchor_blk, w.anchor_byte, w.err, w.wmax, w.slow_count,
+                                     w.slow_list, w.big_count, w.big_list, w.desc, w.stat_part, w.huge_part, w.wmax_part,
+                                     w.bloom_rep, w.err_part, w.done, w.gtab_exit, w.gtab_cnt, w.gtab_bytes, w.mode, w.blen};
+    for (int f = 0; f < kWsFields; f++) s.wso[f] = (uint32_t)(off[f] >> 8);
 }
 
 // Enqueue the encode of every SST of the set on `st` (one launch sequence).
@@ -345,3 +364,4 @@ hipError_t launch_bloom_query(const uint8_t *bitmap, uint64_t bitmap_bytes, uint
 }  // namespace sdb
 static_assert(sdb::kSegSpan % sdb::kSegThreads == 0 && sdb::kChunk % 64 == 0, "k_seg geometry");
 static_assert(sdb::kEmitLds <= 160 * 1024, "k_emit LDS");
+static_assert(sizeof(sdb::SstSet) <= 4096, "SstSet is passed as kernel arguments");

@@ -297,7 +297,11 @@ __global__ __launch_bounds__(kFactsThreads, 8) void k_facts(SstSet P) {
             a.sznr[e] = x.s_nr;
             if (a.bloom_fused) {  // filter_hash (filter.rs:196-204) -> first probe and step
                 const uint64_t kl = f.ko1 - f.ko0;
+#ifdef SDB_EXP_FACTS_NOHASH  // diagnostic: wrong filter bits by design (cost of SipHash)
+                const uint64_t h = (f.ck0 * 0x9E3779B97F4A7C15ull) ^ (f.ck1 + kl);
+#else
                 const uint64_t h = kl == 16 ? siphash13_16(f.ck0, f.ck1) : siphash13(a.key_bytes + f.ko0, kl);
+#endif
                 hh[r] = fastmod_u32((uint32_t)h, a.bpl.mmod, a.bpl.m);
                 dd[r] = fastmod_u32((uint32_t)(h >> 32), a.bpl.mmod, a.bpl.m);
             }
@@ -346,7 +350,11 @@ __global__ __launch_bounds__(kFactsThreads, 8) void k_facts(SstSet P) {
     if (a.bloom_fused) {
         const uint64_t k0 = (uint64_t)blockIdx.x * kFactsEntries;
         const uint32_t nk = (uint32_t)((k0 + kFactsEntries < n ? k0 + kFactsEntries : n) - k0);
+#ifdef SDB_EXP_FACTS_NOBIN  // diagnostic: every (tile, slice) run empty
+        bloom_bin_core<kFactsPerT>(blockIdx.x, hh, dd, 0, a.bpl, a.bq, blds);
+#else
         bloom_bin_core<kFactsPerT>(blockIdx.x, hh, dd, nk, a.bpl, a.bq, blds);
+#endif
     }
 }
 
@@ -1161,6 +1169,345 @@ __global__ __launch_bounds__(kEnumThreads) void k_enum(SstSet P) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// K2' anchor (the encode's k_group + the table walks k_enum did per chunk): one workgroup per SST.
+//   1. workgroup 0's part of k_group: the SstStats / error partials, the longest candidate block (W)
+//      and the device state of the later kernels;
+//   2. every chunk's anchor (entry point, first block, first byte) from k_seg's chunk transfer tables,
+//      staged in LDS (u16 exit, u16 blocks, u64 bytes): composed per group of a.group chunks (a lane per
+//      (group, candidate)), the groups walked from entry 0 (one lane), then each group's chunks from its
+//      entry (a lane per group) — about 3 sqrt(nchunks) dependent LDS steps for the SST, where every
+//      k_enum workgroup used to stage its own group tables and walk them.  Tables over the LDS are
+//      walked the same way straight from HBM.
+//   Mode 0 (blocks longer than the lookahead): the serial walk of next(), as k_group.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kAnchorThreads = 1024;
+constexpr uint32_t kAnchorLds = 148 * 1024;
+
+__global__ __launch_bounds__(kAnchorThreads) void k_anchor(SstSet P) {
+    const EncodeArgs a = make_args(P, blockIdx.y);
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ uint32_t s_W;
+    __shared__ unsigned long long s_err;
+    __shared__ uint64_t s_stat[5][kAnchorThreads / 64];
+    const uint32_t K = a.nchunks, G = a.group, ngroups = (K + G - 1) / G;
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    if (tid == 0) {
+        s_W = 0;
+        s_err = ~0ull;
+    }
+    __syncthreads();
+    {
+        uint32_t m = 0;
+        unsigned long long em = ~0ull;
+        uint64_t st[5] = {0, 0, 0, 0, 0};
+        for (uint32_t q = tid; q < K; q += nt) {
+            const uint32_t w = a.wmax_part[q];
+            m = w > m ? w : m;
+        }
+        for (uint32_t q = tid; q < a.nfacts; q += nt) {
+            const unsigned long long ep = a.err_part[q];
+            em = ep < em ? ep : em;
+#pragma unroll
+            for (int f = 0; f < 5; f++) st[f] += a.stat_part[5 * (uint64_t)q + f];
+        }
+        m = wave_max(m);
+        if (lane_id() == 0) atomicMax(&s_W, m);
+        if (em != ~0ull) atomicMin(&s_err, em);
+#pragma unroll
+        for (int f = 0; f < 5; f++) {
+            const uint64_t t = wave_sum(st[f]);
+            if (lane_id() == 0) s_stat[f][tid >> 6] = t;
+        }
+    }
+    __syncthreads();
+    const uint32_t W = s_W;
+    const bool fast = W >= 1 && W <= a.seg_look;
+    sdb_sst_summary *sm = a.summary;
+    if (tid == 0) {
+        *a.wmax = W;
+        *a.err = s_err;
+        *a.slow_count = 0;
+        *a.big_count = 0;
+        a.done[0] = 0;
+        a.done[1] = 0;
+        *a.mode = fast ? 1u : 0u;
+        uint64_t t[5];
+        for (int f = 0; f < 5; f++) {
+            t[f] = 0;
+            for (uint32_t q = 0; q < nt / 64; q++) t[f] += s_stat[f][q];
+        }
+        sm->raw_key_size = t[0];
+        sm->raw_val_size = t[1];
+        sm->num_puts = t[2];
+        sm->num_deletes = t[3];
+        sm->num_merges = t[4];
+        sm->num_entries = a.n;
+        sm->bloom_len = 0;
+        sm->num_probes = 0;
+        sm->filter_built = 0;
+        sm->status = 0;
+        sm->max_block_entries = 0;
+        sm->first_error_entry = ~0ull;
+    }
+    uint64_t tb = 0, ty = 0;  // the chain's blocks and bytes (thread 0)
+    if (!fast) {
+        if (tid == 0) {  // serial walk of the block chain (one next() step per block)
+            uint64_t e = 0;
+            for (uint32_t k = 0; k < K; k++) {
+                const uint64_t cs = (uint64_t)k * kChunk, ce = cs + kChunk < a.n ? cs + kChunk : a.n;
+                a.anchor_e[k] = (uint32_t)e;
+                a.anchor_blk[k] = (uint32_t)tb;
+                a.anchor_byte[k] = ty;
+                while (e < ce) {
+                    ty += a.bbytes[e];
+                    tb++;
+                    e = a.next[e];
+                }
+            }
+        }
+    } else {
+        const uint64_t ntab = (uint64_t)K * W, ng = (uint64_t)ngroups * W;
+        const uint64_t o_cn = (2 * ntab + 15) & ~15ull, o_by = o_cn + ((2 * ntab + 15) & ~15ull);
+        const uint64_t o_gex = o_by + 8 * ntab, o_gcn = o_gex + 4 * ng, o_gby = o_gcn + 4 * ng, o_ent = o_gby + 8 * ng;
+        const bool in_lds = o_ent + 16ull * ngroups <= kAnchorLds;
+        uint16_t *t_ex = (uint16_t *)smem, *t_cn = (uint16_t *)(smem + o_cn);
+        uint64_t *t_by = (uint64_t *)(smem + o_by);
+        uint32_t *g_ex = (uint32_t *)(smem + o_gex), *g_cn = (uint32_t *)(smem + o_gcn);
+        uint64_t *g_by = (uint64_t *)(smem + o_gby);
+        uint32_t *g_ent = (uint32_t *)(smem + o_ent);  // per group: entry offset, blocks before (bytes: g_ent64)
+        uint64_t *g_b64 = (uint64_t *)(smem + o_ent + 8ull * ngroups);
+        // chunk k's table at candidate o (exit clamped into [0, W): candidates past a chunk's own bound are
+        // never entry points, their stale slots only need to stay in range)
+        auto tab_hbm = [&](uint32_t k, uint32_t o, uint32_t &x, uint32_t &c, uint64_t &b) {
+            const uint64_t cs = (uint64_t)k * kChunk, ce = cs + kChunk < a.n ? cs + kChunk : a.n;
+            x = c = 0;
+            b = 0;
+            if (cs + o < ce) {
+                const uint64_t t = (uint64_t)k * a.seg_look + o;
+                const uint32_t te = a.tab_exit[t];
+                x = te >= ce && te - ce < W ? (uint32_t)(te - ce) : W - 1;
+                c = a.tab_cnt[t];
+                b = a.tab_bytes[t];
+            }
+        };
+        auto tab = [&](uint32_t k, uint32_t o, uint32_t &x, uint32_t &c, uint64_t &b) {
+            if (in_lds) {
+                const uint64_t i = (uint64_t)k * W + o;
+                x = t_ex[i];
+                c = t_cn[i];
+                b = t_by[i];
+            } else {
+                tab_hbm(k, o, x, c, b);
+            }
+        };
+        if (in_lds) {  // stage the tables: eight entries per thread in flight
+            constexpr uint32_t kU = 8;
+            for (uint64_t base = 0; base < ntab; base += kU * nt) {
+                uint32_t x[kU], c[kU];
+                uint64_t b[kU];
+#pragma unroll
+                for (uint32_t u = 0; u < kU; u++) {
+                    const uint64_t i = base + u * nt + tid;
+                    x[u] = c[u] = 0;
+                    b[u] = 0;
+                    if (i < ntab) tab_hbm((uint32_t)(i / W), (uint32_t)(i % W), x[u], c[u], b[u]);
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < kU; u++) {
+                    const uint64_t i = base + u * nt + tid;
+                    if (i >= ntab) continue;
+                    t_ex[i] = (uint16_t)x[u];
+                    t_cn[i] = (uint16_t)c[u];  // a block count inside one chunk: <= kChunk
+                    t_by[i] = b[u];
+                }
+            }
+            __syncthreads();
+        }
+        // group tables: lane per (group, candidate)
+        for (uint64_t i = tid; i < ng && in_lds; i += nt) {
+            const uint32_t q = (uint32_t)(i / W), k1 = (q + 1) * G < K ? (q + 1) * G : K;
+            uint32_t e = (uint32_t)(i % W), c = 0;
+            uint64_t b = 0;
+            for (uint32_t k = q * G; k < k1; k++) {
+                uint32_t x, cc;
+                uint64_t bb;
+                tab(k, e, x, cc, bb);
+                c += cc;
+                b += bb;
+                e = x;
+            }
+            g_ex[i] = e;
+            g_cn[i] = c;
+            g_by[i] = b;
+        }
+        __syncthreads();
+        if (tid == 0) {  // the groups from entry 0
+            uint32_t e = 0;
+            for (uint32_t q = 0; q < ngroups; q++) {
+                if (in_lds) {
+                    g_ent[2 * q] = e;
+                    g_ent[2 * q + 1] = (uint32_t)tb;
+                    g_b64[q] = ty;
+                    const uint64_t i = (uint64_t)q * W + e;
+                    tb += g_cn[i];
+                    ty += g_by[i];
+                    e = g_ex[i];
+                } else {  // tables in HBM: this lane walks every chunk (anchors written on the way)
+                    const uint32_t k1 = (q + 1) * G < K ? (q + 1) * G : K;
+                    for (uint32_t k = q * G; k < k1; k++) {
+                        a.anchor_e[k] = (uint32_t)((uint64_t)k * kChunk + e);
+                        a.anchor_blk[k] = (uint32_t)tb;
+                        a.anchor_byte[k] = ty;
+                        uint32_t x, c;
+                        uint64_t b;
+                        tab_hbm(k, e, x, c, b);
+                        tb += c;
+                        ty += b;
+                        e = x;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t q = tid; q < ngroups && in_lds; q += nt) {  // each group's chunks from its entry
+            uint32_t e = g_ent[2 * q];
+            uint64_t blk = g_ent[2 * q + 1], by = g_b64[q];
+            const uint32_t k1 = (q + 1) * G < K ? (q + 1) * G : K;
+            for (uint32_t k = q * G; k < k1; k++) {
+                a.anchor_e[k] = (uint32_t)((uint64_t)k * kChunk + e);
+                a.anchor_blk[k] = (uint32_t)blk;
+                a.anchor_byte[k] = by;
+                uint32_t x, c;
+                uint64_t b;
+                tab(k, e, x, c, b);
+                blk += c;
+                by += b;
+                e = x;
+            }
+        }
+    }
+    if (tid == 0) {
+        a.anchor_e[K] = (uint32_t)a.n;
+        a.anchor_blk[K] = (uint32_t)tb;
+        a.anchor_byte[K] = ty;
+        sm->num_blocks = tb;
+        sm->data_len = ty;
+        if (tb > a.block_cap || ty > a.data_cap) report_error(a.err, 0, SDB_INVALID_ARGUMENT);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// K5a' blocks (the encode's k_enum, from k_anchor's anchors): per chunk a 256-thread workgroup with
+// 16 KiB of LDS (eight per CU): next() and the block bytes of the chunk's entries staged in LDS, the
+// chunk's block chain walked from its anchor by one lane, then the blocks in batches of 256: offsets by
+// a workgroup scan of their bytes, BlockMeta outputs, descriptors and the big / slow block lists.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kBlkThreads = 256;
+
+__global__ __launch_bounds__(kBlkThreads) void k_blocks(SstSet P) {
+    const EncodeArgs a = make_args(P, blockIdx.y);
+    __shared__ uint16_t s_nx[kChunk];  // next(cs + x) - cs, clamped to cn
+    __shared__ uint32_t s_bb[kChunk];  // block bytes of a block starting at cs + x
+    __shared__ uint16_t s_bs[kChunk];  // block t of the chunk starts at cs + s_bs[t]
+    __shared__ uint64_t s_w[17];
+    __shared__ uint32_t s_nbig, s_bigbase;
+    __shared__ uint32_t s_big[kBlkThreads];
+    const uint32_t k = blockIdx.x, K = a.nchunks;
+    if (k >= K) return;
+    if (*a.err != ~0ull) return;
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    const uint64_t cs = (uint64_t)k * kChunk, ce = cs + kChunk < a.n ? cs + kChunk : a.n;
+    const uint32_t cn = (uint32_t)(ce - cs);
+    const uint64_t e0 = a.anchor_e[k], byte0 = a.anchor_byte[k];
+    const uint32_t blk0 = a.anchor_blk[k], nb = a.anchor_blk[k + 1] - blk0;
+    if (blk0 + (uint64_t)nb > a.block_cap) {  // capacity: k_anchor reports it
+        return;
+    }
+    if (k + 1 == K && tid == 0) {
+        a.out_block_off[blk0 + nb] = a.anchor_byte[K];
+        a.out_block_first[blk0 + nb] = (uint32_t)a.n;
+    }
+    if (!nb) return;
+    {
+        constexpr uint32_t kU = kChunk / kBlkThreads;
+        uint32_t nx[kU], eb[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t x = u * nt + tid;
+            nx[u] = x < cn ? a.next[cs + x] : 0;
+            eb[u] = x < cn ? a.bbytes[cs + x] : 0;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t x = u * nt + tid;
+            if (x < cn) {
+                s_nx[x] = (uint16_t)(nx[u] >= ce ? cn : (uint32_t)(nx[u] - cs));
+                s_bb[x] = eb[u];
+            }
+        }
+    }
+    if (tid == 0) s_nbig = 0;
+    __syncthreads();
+    if (tid == 0) {  // the chain from the anchor: one dependent LDS read per block
+        uint32_t x = (uint32_t)(e0 - cs);
+        for (uint32_t t = 0; t < nb; t++) {
+            s_bs[t] = (uint16_t)x;
+            x = s_nx[x];
+        }
+    }
+    __syncthreads();
+    uint64_t carry = byte0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += nt) {
+        const uint32_t t = b0 + tid;
+        const bool v = t < nb;
+        const uint32_t xs = v ? s_bs[t] : 0;
+        const uint32_t bb = v ? s_bb[xs] : 0;
+        uint64_t tot;
+        const uint64_t off = carry + block_excl_scan_u64(bb, s_w, &tot);
+        carry += tot;
+        if (v) {
+            const uint64_t s = cs + xs, e = t + 1 < nb ? cs + s_bs[t + 1] : a.next[s];
+            const uint32_t blk = blk0 + t;
+            a.out_block_off[blk] = off;
+            a.out_block_first[blk] = (uint32_t)s;
+            BlockDesc d;
+            d.s = (uint32_t)s;
+            d.e = (uint32_t)e;
+            d.off = off;
+            d.vs = a.val_off[s];
+            d.ve = a.val_off[e];
+            d.ks = a.key_off[s];
+            d.ke = a.key_off[e];
+            d.bb = bb;
+            d.pad = 0;
+            if (!emit_fast(d)) {
+                // too big for one wave image: k_emit's piece path, unless a row is too large for a piece
+                // (then the workgroup path, marked pad = 1)
+                uint32_t h = 0;
+                for (uint64_t q = s / kChunk; q <= (e - 1) / kChunk; q++) h |= a.huge_part[q];
+                if (h) {
+                    d.pad = 1;
+                    a.slow_list[atomicAdd(a.slow_count, 1u)] = blk;
+                } else {
+                    s_big[atomicAdd(&s_nbig, 1u)] = blk;  // one global reservation per batch below
+                }
+            }
+            a.desc[blk] = d;
+        }
+        __syncthreads();
+        const uint32_t nbig = s_nbig;
+        if (nbig) {  // (a global atomic per big block serialised on the counter: 65 us per SST at 8 KiB blocks)
+            if (tid == 0) s_bigbase = atomicAdd(a.big_count, nbig);
+            __syncthreads();
+            for (uint32_t i = tid; i < nbig; i += nt) a.big_list[s_bigbase + i] = s_big[i];
+            __syncthreads();
+            if (tid == 0) s_nbig = 0;
+            __syncthreads();
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // K5b: emit.  One wave per block; a workgroup shares the CRC tables (LDS).
 //   1. lane = row: row metadata from HBM (offsets, kind, seq, timestamps, LCP), row sizes, a wave
 //      scan for the row offsets;
@@ -1522,7 +1869,11 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     wave_sync();  // stages written (DS instructions of one wave complete in order)
     WAVE_T(t2);
     // 2. key suffixes + values: lane = row from registers, or cooperative by the span table
+#ifdef SDB_EXP_EMIT_NOCOPY  // diagnostic: image without key / value bytes
+    if (false) {
+#else
     if (!copy_rows(img, row, sc)) {
+#endif
         if (row) {
             rtab[l].a = sc.a;
             rtab[l].jk = sc.jk;
@@ -1568,7 +1919,11 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     wave_sync();
     WAVE_T(t4);
     // 4. CRC32 (format/sst.rs:541-552) of the image [0, Lc)
+#ifdef SDB_EXP_EMIT_NOCRC  // diagnostic: wrong CRC by design
+    const uint32_t crc32 = 0;
+#else
     const uint32_t crc32 = wave_crc_image_ra(img, Lc);
+#endif
     if (l == 0) {
         img[Lc] = (uint8_t)(crc32 >> 24);
         img[Lc + 1] = (uint8_t)(crc32 >> 16);
@@ -1878,57 +2233,55 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(SstSet P) {
     (void)gw;
     const uint32_t l = (uint32_t)lane_id();
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    // the set's blocks, SST after SST: pre[i] = blocks of SSTs < i (an SST with an earlier error,
-    // incl. capacity, emits nothing)
-    uint32_t pre[kMaxSsts + 1];
-    pre[0] = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < kMaxSsts; i++) {
-        uint32_t nb = 0;
-        if (i < P.count) {
-            const EncodeArgs ai = make_args(P, i);
-            if (*ai.err == ~0ull) nb = ai.anchor_blk[ai.nchunks];
-        }
-        pre[i + 1] = pre[i] + nb;
+    // the set's blocks, SST after SST: lane j < count holds pre[j + 1] = blocks of SSTs <= j (an SST with
+    // an earlier error, incl. capacity, emits nothing).  Kept in a VGPR, not an SGPR array: the loop's
+    // scalar state must stay small (k_emit ran out of SGPRs and spilled them to VGPR lanes).
+    uint32_t nbl = 0;
+    if (l < P.count) {
+        const EncodeArgs ai = make_args(P, l);
+        if (*ai.err == ~0ull) nbl = ai.anchor_blk[ai.nchunks];
     }
-    bool run = pre[kMaxSsts] > 0;
+    const uint32_t vpre = wave_incl_scan(nbl);
+    const uint32_t nb = (uint32_t)__builtin_amdgcn_readlane((int)vpre, kMaxSsts - 1);
+    bool run = nb > 0;
     if (lds_addr((const void *)smem) != 0) {  // crc_tab / crc_mul256_lds / crc_tree_mul assume LDS address 0
         if (threadIdx.x == 0)
             for (uint32_t i = 0; i < P.count; i++) report_error(make_args(P, i).err, 0, SDB_DEVICE_ERROR);
         run = false;
     }
-    // global block g -> (SST, block of that SST); g is wave-uniform
+    // global block g -> (SST, block of that SST); g is wave-uniform: si = #{j in [1, 8): pre[j] <= g, pre[j] < nb}
     auto locate = [&](uint32_t g, uint32_t &si, uint32_t &lb) {
-        uint32_t i = 0, base = 0;
-#pragma unroll
-        for (uint32_t j = 1; j < kMaxSsts; j++)
-            if (g >= pre[j] && pre[j] < pre[kMaxSsts]) {
-                i = j;
-                base = pre[j];
-            }
-        si = i;
-        lb = g - base;
+        const uint64_t m = __ballot(l + 1 < kMaxSsts && vpre <= g && vpre < nb);
+        si = (uint32_t)__popcll(m);
+        lb = g - (si ? (uint32_t)__builtin_amdgcn_readlane((int)vpre, (int)si - 1) : 0u);
     };
-    auto desc_dw = [&](uint32_t si) { return (const uint32_t *)make_args(P, si).desc; };
+    auto desc_lanes = [&](uint32_t g, uint32_t r1) -> uint32_t {  // lanes 0..13: the 14 dwords of g's desc
+        uint32_t si, lb;
+        locate(g, si, lb);
+        return (g < r1 && l < 14) ? ((const uint32_t *)make_args(P, si).desc)[14 * (uint64_t)lb + l] : 0u;
+    };
     if (run) {
         lu32 *crc = (lu32 *)smem;
         (void)crc;
         // schedule: workgroup b owns an equal share [r0, r1) of the set's blocks; its waves start on
         // blocks r0 + wave and then take the rest in order from an LDS ticket, so a wave that runs fast
         // takes more.  (One global ticket for all waves measured 3x slower: the atomics serialise.)
-        const uint32_t nb = pre[kMaxSsts];
         const uint32_t r0 = (uint32_t)((uint64_t)nb * blockIdx.x / gridDim.x);
         const uint32_t r1 = (uint32_t)((uint64_t)nb * (blockIdx.x + 1) / gridDim.x);
-        uint32_t blk = r0 + wave, si = 0, lb = 0;
-        locate(blk, si, lb);
+        uint32_t blk = r0 + wave;
         // the first block's descriptor is in flight while the CRC tables are copied, its values and
         // metadata while the workgroup does the slow blocks and sets up the ticket
-        const uint32_t dv0 = (blk < r1 && l < 14) ? desc_dw(si)[14 * (uint64_t)lb + l] : 0;
+        uint32_t dvn = desc_lanes(blk, r1);
         crc_tables_to_lds(crc);
-        BlockDesc dn = desc_from_lanes(dv0);
         EmitPre pn;
-        bool fn = blk < r1 && emit_fast(dn);
-        if (fn) emit_prefetch(make_args(P, si), dn, pn);
+        bool fn = false;
+        if (blk < r1) {
+            uint32_t si, lb;
+            locate(blk, si, lb);
+            const BlockDesc dn = desc_from_lanes(dvn);
+            fn = emit_fast(dn);
+            if (fn) emit_prefetch(make_args(P, si), dn, pn);
+        }
         __syncthreads();
         for (uint32_t i = 0; i < P.count; i++) {
             const EncodeArgs ai = make_args(P, i);
@@ -1949,26 +2302,29 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(SstSet P) {
             return r0 + (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
         };
         if (blk < r1) {
-            uint32_t nblk = take(), nsi = 0, nlb = 0;
-            locate(nblk, nsi, nlb);
-            uint32_t dv = (nblk < r1 && l < 14) ? desc_dw(nsi)[14 * (uint64_t)nlb + l] : 0;
+            uint32_t nblk = take();
+            uint32_t dv = desc_lanes(nblk, r1);
             while (blk < r1) {
-                const BlockDesc d = dn;
+                const uint32_t dcur = dvn;
                 const EmitPre p = pn;
                 const bool fast = fn;
-                const uint32_t csi = si, clb = lb;
+                const uint32_t cblk = blk;
                 blk = nblk;
-                si = nsi;
-                lb = nlb;
                 if (blk < r1) {  // issue the next block (and the descriptor of the one after it)
-                    dn = desc_from_lanes(dv);
+                    dvn = dv;
+                    uint32_t si, lb;
+                    locate(blk, si, lb);
+                    const BlockDesc dn = desc_from_lanes(dvn);
                     fn = emit_fast(dn);
                     if (fn) emit_prefetch(make_args(P, si), dn, pn);
                     nblk = take();
-                    locate(nblk, nsi, nlb);
-                    dv = (nblk < r1 && l < 14) ? desc_dw(nsi)[14 * (uint64_t)nlb + l] : 0;
+                    dv = desc_lanes(nblk, r1);
                 }
-                if (fast) emit_block<V>(make_args(P, csi), clb, d, p, img, kst, rtab, crc, ph);  // others: k_emit_big, slow path
+                if (fast) {  // others: k_emit_big, slow path
+                    uint32_t csi, clb;
+                    locate(cblk, csi, clb);
+                    emit_block<V>(make_args(P, csi), clb, desc_from_lanes(dcur), p, img, kst, rtab, crc, ph);
+                }
             }
         }
     }
@@ -2280,6 +2636,7 @@ static void set_lds_attrs() {
         (void)hipFuncSetAttribute((const void *)k_emit_big<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds);
         (void)hipFuncSetAttribute((const void *)k_enum, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEnumLds);
         (void)hipFuncSetAttribute((const void *)k_group, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGroupLds);
+        (void)hipFuncSetAttribute((const void *)k_anchor, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAnchorLds);
         (void)hipFuncSetAttribute((const void *)k_seg, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
         (void)hipFuncSetAttribute((const void *)k_facts, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLds);
         (void)hipGetLastError();  // an unsupported attribute value must not poison the next launch status
@@ -2306,11 +2663,12 @@ hipError_t launch_encode_set(const SstSet &P, size_t bin_lds, size_t fill_lds, h
     const size_t seg_lds = kSegLds > fill_lds ? kSegLds : fill_lds;
     hipLaunchKernelGGL(k_seg, dim3(P.max_chunks + P.max_slices, P.count), dim3(kSegThreads), seg_lds, st, P);
     stage_mark(st, kStSeg, false);
+    // the chain: every chunk's anchor (one workgroup per SST), then each chunk's blocks
     stage_mark(st, kStGroup, true);
-    hipLaunchKernelGGL(k_group, dim3(P.max_groups, P.count), dim3(kGroupThreads), kGroupLds, st, P);
+    hipLaunchKernelGGL(k_anchor, dim3(1, P.count), dim3(kAnchorThreads), kAnchorLds, st, P);
     stage_mark(st, kStGroup, false);
     stage_mark(st, kStEnum, true);
-    hipLaunchKernelGGL(k_enum, dim3(P.max_chunks, P.count), dim3(kEnumThreads), kEnumLds, st, P);
+    hipLaunchKernelGGL(k_blocks, dim3(P.max_chunks, P.count), dim3(kBlkThreads), 0, st, P);
     stage_mark(st, kStEnum, false);
     stage_mark(st, kStEmit, true);
     // blocks over one wave image: every block at SstBlockSize 8 - 64 KiB, only blocks of > 64 tiny rows

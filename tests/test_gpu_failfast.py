@@ -73,3 +73,36 @@ def test_fail_fast_corruption(rt):  # noqa: F811
     check(rt, d4, off, 2, "both in one block")
     for desc in (False, True):
         check(rt, d3, off, 2, "crc before rows desc=%d" % desc, descending=desc)
+
+
+@pytest.mark.parametrize("small", [True, False])
+def test_fail_fast_over_capacity_reports_checksum(rt, small):  # noqa: F811
+    """Counts that exceed the caller's capacity (here: the capacity one entry short) with a block whose
+    checksum the count pass deferred: read_blocks fails on the block, so the status is
+    CHECKSUM_MISMATCH (the oracle's), not the capacity error, and the block is listed."""
+    import torch
+    from slatedb_amd import _abi
+    b = datasets.d1(n=2000 if small else 60000, sst_index=7)
+    e = O.encode_sst(b, O.params())
+    off = e.block_off
+    nb = len(off) - 1
+    bad = nb // 2
+    data = e.data.copy()
+    data[int(off[bad]) + 200] ^= 0x10  # payload byte: the rows still parse, only the checksum is wrong
+    ref = O.decode_blocks(data, off, 2)
+    assert ref.status == _abi.SDB_CHECKSUM_MISMATCH
+    for cap_e, cap_k in ((b.n - 1, len(b.key_bytes) + 64), (b.n + 64, len(b.key_bytes) - 1)):
+        dout = rt.DeviceDecodeOutput(nb, cap_e, cap_k)
+        arena = torch.from_numpy(np.concatenate([data, np.zeros(64, np.uint8)])).cuda()
+        boff = torch.from_numpy(np.asarray(off, np.uint64).view(np.int64)).cuda()
+        rt.decode_blocks_ex_device(arena, boff, None, nb, dout, 2, fail_fast=True)
+        torch.cuda.synchronize()
+        got = dout.to_host()
+        assert got.status == _abi.SDB_CHECKSUM_MISMATCH, (cap_e, cap_k, got.status)
+        assert bad in got.bad_block.tolist()
+        # without the corruption the same capacities are a plain capacity error
+        dout = rt.DeviceDecodeOutput(nb, cap_e, cap_k)
+        clean = torch.from_numpy(np.concatenate([e.data, np.zeros(64, np.uint8)])).cuda()
+        rt.decode_blocks_ex_device(clean, boff, None, nb, dout, 2, fail_fast=True)
+        torch.cuda.synchronize()
+        assert dout.to_host().status == _abi.SDB_INVALID_ARGUMENT
