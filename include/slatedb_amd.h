@@ -328,6 +328,27 @@ sdb_status sdb_decompress_blocks(uint32_t codec, const uint8_t *blocks, const ui
                                  uint8_t *out, uint64_t out_cap, const uint64_t *out_start, uint64_t *out_end,
                                  uint64_t *err, void *stream);
 
+/* The compressing write side: compress_and_transform (format/sst.rs:525-554) with SsTableFormat::compress
+ * (format/sst.rs:557-594) for every block of an encoded data section (each Block::encode() ++ CRC32 BE, as
+ * sdb_encode_sst writes it): block k becomes the codec's bytes of its Block::encode() followed by the CRC32
+ * (BE) of those compressed bytes, at out[out_off[k], out_off[k + 1]):
+ *   SDB_CODEC_LZ4     u32 LE length ++ one LZ4 block (lz4_flex block::compress_prepend_size);
+ *   SDB_CODEC_SNAPPY  varint length ++ Snappy raw elements (snap raw::Encoder::compress_vec);
+ *   SDB_CODEC_ZLIB    78 9C ++ deflate (fixed-Huffman or stored) ++ Adler-32 BE (flate2 ZlibEncoder);
+ *   SDB_CODEC_ZSTD    one zstd frame with Frame_Content_Size (zstd::bulk::compress).
+ * One wave per block, a greedy LZ77 parse in the wave's LDS.  The streams are valid for their formats and
+ * decode (the crates' decompressors, sdb_decompress_blocks) to the block; they are not the crates' own
+ * bytes (a match finder's choices are its own).  in_bytes = block_off[nblocks] - block_off[0];
+ * out_off (device, nblocks + 1) = the compressed blocks' offsets from out (BlockMeta.offset when the data
+ * section starts the SST), out_off[nblocks] = the compressed data section's length.  *err (device u64) =
+ * block << 8 | status of the first failing block (~0: none): SDB_CORRUPT_BLOCK (a block under 4 bytes),
+ * SDB_LIMIT_EXCEEDED (the section is over out_cap: nothing is written).
+ * Workspace: sdb_compress_workspace_bytes(nblocks, in_bytes). */
+uint64_t sdb_compress_workspace_bytes(uint64_t nblocks, uint64_t in_bytes);
+sdb_status sdb_compress_blocks(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                               uint64_t in_bytes, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *err,
+                               void *workspace, uint64_t workspace_bytes, void *stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Point lookups / seeks on one encoded SST (device): the read path of Db::get and of an SstIterator
  * positioned on a key:
@@ -537,6 +558,10 @@ typedef struct sdb_footer_in {
     uint64_t bloom_len;
     const char *filter_name;          /* FilterPolicy::name: NULL = "_bf"; a prefix / no-whole-key policy
                                          is "_bf:p=<extractor>[:wh=0]" (filter_policy.rs:237-250) */
+    uint32_t compression;             /* SsTableInfo.compression_format (SDB_CODEC_*): the filter, index and
+                                         stats blocks go through compress_and_transform with that codec, as
+                                         literal-only streams of the format (the data blocks: sdb_compress_blocks) */
+    uint32_t pad;
 } sdb_footer_in;
 /* Writes the footer into out[0..cap) and its length into *len.  out == NULL: size query only.
  * cap too small: SDB_LIMIT_EXCEEDED (with *len set). */
@@ -616,6 +641,17 @@ sdb_status sdb_decoder_decode_host(sdb_decoder *dec, const uint8_t *blocks,
  * encodes measured into *launches, clears the record, and returns the number of stages. */
 void sdb_diag_enable_stage_timing(int on);
 int sdb_diag_stage_times(double *ms, int max_stages, uint64_t *launches);
+/* The block CRC32 (crc32fast::hash, the checksum compress_and_transform appends, format/sst.rs:541-552)
+ * of n device ranges data[off[i], off[i+1]), 4 <= length <= 4096, one wave per range: method 0 the
+ * slicing-by-8 wave CRC, 1 the matrix-core (MFMA) wave CRC the kernels use.  Results in out[0, n). */
+sdb_status sdb_diag_crc32_blocks(const uint8_t *data, const uint64_t *off, uint64_t n, uint32_t *out, int method,
+                                 void *stream);
+/* One v_mfma_i32_32x32x32_i8 with lane-supplied operands (a, b: 64 lanes x 4 dwords; d: 64 x 16
+ * dwords, lane-major): pins the operand / result lane maps the MFMA CRC relies on. */
+sdb_status sdb_diag_mfma_i8(const int32_t *a, const int32_t *b, int32_t *d, void *stream);
+/* A hand-written STREAM copy (16 bytes per lane, grid-stride) of `bytes` (a multiple of 16, 16-byte aligned):
+ * bench.py's attainable-HBM ceiling beside the 8 TB/s spec. */
+sdb_status sdb_diag_copy(void *dst, const void *src, uint64_t bytes, void *stream);
 
 /* Device query: number of visible HIP devices (0 on a machine without a GPU). */
 int sdb_device_count(void);

@@ -307,14 +307,48 @@ def parse_sst(obj):
         return b[:-4]
 
     info = parse_info(unck(raw))
-    index = parse_index(unck(obj[info["index_offset"]:info["index_offset"] + info["index_len"]]))
+    codec = info["compression"]
+
+    def block(off, ln):  # decode_block's first half for a footer block: checksum, then the codec
+        b = unck(obj[off:off + ln])
+        return decompress_payload(codec, b) if codec else b
+
+    index = parse_index(block(info["index_offset"], info["index_len"]))
     stats = None
     if info["stats_len"]:
-        stats = parse_stats(unck(obj[info["stats_offset"]:info["stats_offset"] + info["stats_len"]]))
+        stats = parse_stats(block(info["stats_offset"], info["stats_len"]))
     filt = None
     if info["filter_len"]:
-        filt = unck(obj[info["filter_offset"]:info["filter_offset"] + info["filter_len"]])
+        filt = block(info["filter_offset"], info["filter_len"])
     return version, info, index, stats, filt
+
+
+def decompress_payload(codec, b):
+    """SsTableFormat::decompress (format/sst.rs:884-917) through this image's canonical codecs (test
+    infrastructure): pyarrow LZ4 (u32 LE size first) / Snappy / zstd, Python zlib."""
+    import pyarrow as pa
+    b = bytes(b)
+    if codec == 2:
+        return zlib.decompress(b)
+    if codec == 3:
+        n = struct.unpack("<I", b[:4])[0]
+        return pa.decompress(b[4:], decompressed_size=n, codec="lz4_raw", asbytes=True)
+    if codec == 1:
+        n, i, sh = 0, 0, 0
+        while True:
+            n |= (b[i] & 0x7F) << sh
+            sh += 7
+            i += 1
+            if not b[i - 1] & 0x80:
+                break
+        return pa.decompress(b, decompressed_size=n, codec="snappy", asbytes=True)
+    # zstd: the frame header's content size
+    fhd = b[4]
+    fcs_flag, single = fhd >> 6, (fhd >> 5) & 1
+    p = 5 + (0 if single else 1) + [0, 1, 2, 4][fhd & 3]
+    ln = [1 if single else 0, 2, 4, 8][fcs_flag]
+    n = int.from_bytes(b[p:p + ln], "little") + (256 if ln == 2 else 0)
+    return pa.Codec("zstd").decompress(b, decompressed_size=n, asbytes=True)
 
 
 def sst_object(batch, res, sst_version=2, sst_type=0, bloom_bits_per_key=10, filter_name=b"_bf"):

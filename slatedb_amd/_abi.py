@@ -121,7 +121,7 @@ class FooterIn(C.Structure):
         ("first_entry", C.c_char_p), ("first_entry_len", C.c_uint64),
         ("last_entry", C.c_char_p), ("last_entry_len", C.c_uint64),
         ("stats", C.c_void_p), ("block_stats", C.c_void_p), ("bloom", C.c_void_p),
-        ("bloom_len", C.c_uint64), ("filter_name", C.c_char_p),
+        ("bloom_len", C.c_uint64), ("filter_name", C.c_char_p), ("compression", C.c_uint32), ("pad", C.c_uint32),
     ]
 
 
@@ -277,6 +277,12 @@ SIGNATURES = {
                                           C.c_uint16, C.POINTER(DecodeHostResult)]),
     "sdb_diag_enable_stage_timing": (None, [C.c_int]),
     "sdb_diag_stage_times": (C.c_int, [C.POINTER(C.c_double), C.c_int, u64p]),
+    "sdb_diag_crc32_blocks": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_int, C.c_void_p]),
+    "sdb_diag_mfma_i8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "sdb_diag_copy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    "sdb_compress_workspace_bytes": (C.c_uint64, [C.c_uint64, C.c_uint64]),
+    "sdb_compress_blocks": (C.c_int, [C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
+                                      C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
     "sdb_device_count": (C.c_int, []),
     "sdb_status_name": (C.c_char_p, [C.c_int]),
 }
@@ -285,9 +291,14 @@ SIGNATURES = {
 STAGES = ["bloom", "facts", "seg", "group", "enum", "emit", "emit_slow", "bloom_fill"]
 
 
-def bind(lib):
+def bind(lib, partial=False):
+    """Sets restype/argtypes on every entry point. ``partial`` (diagnostic
+    variant libraries picked with SDB_LIBRARY, possibly built from an older
+    tree) skips symbols the library does not export instead of failing."""
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None) if partial else getattr(lib, name)
+        if fn is None:
+            continue
         fn.restype = res
         fn.argtypes = args
     return lib

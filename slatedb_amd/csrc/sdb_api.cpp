@@ -455,6 +455,21 @@ sdb_status sdb_decompress_blocks(uint32_t codec, const uint8_t *blocks, const ui
                                  (unsigned long long *)err, S(stream)) == hipSuccess ? SDB_OK : SDB_DEVICE_ERROR;
 }
 
+uint64_t sdb_compress_workspace_bytes(uint64_t nblocks, uint64_t in_bytes) {
+    return compress_workspace_bytes(nblocks, in_bytes) + 256;
+}
+
+sdb_status sdb_compress_blocks(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                               uint64_t in_bytes, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *err,
+                               void *workspace, uint64_t workspace_bytes, void *stream) {
+    if (!lz_codec(codec)) return SDB_INVALID_ARGUMENT;
+    if (!out_off || !err || (nblocks && (!blocks || !block_off || (out_cap && !out)))) return SDB_INVALID_ARGUMENT;
+    if (!workspace || workspace_bytes < sdb_compress_workspace_bytes(nblocks, in_bytes)) return SDB_INVALID_ARGUMENT;
+    if (!device_ok()) return SDB_DEVICE_ERROR;
+    return launch_compress(codec, blocks, block_off, nblocks, in_bytes, out, out_cap, out_off,
+                           (unsigned long long *)err, workspace, S(stream)) == hipSuccess ? SDB_OK : SDB_DEVICE_ERROR;
+}
+
 uint64_t sdb_merge_runs_workspace_bytes(const sdb_run *runs, uint32_t nruns) {
     if (nruns && !runs) return 0;
     uint64_t total = 0;

@@ -185,24 +185,53 @@ SDB_DEV void bloom_bin_core(uint32_t tile, const uint32_t (&hh)[KPT], const uint
             if (tid + j * nt < nk)
                 probes_hd(hh[j], dd[j], pl.k, pl.m, [&](uint32_t p) {
                     const uint32_t sl = p >> pl.sb, pos = atomicAdd(&cnt[sl], 1u);
+#ifndef SDB_EXP_BIN_NOWRITE  // diagnostic: the atomics alone
                     if (pos < cap) bkt[__umul24(sl, cap) + pos] = (uint16_t)(p & mask);  // sl < 256: full-rate mul
+#endif
                 });
         __syncthreads();
+#if defined(SDB_EXP_BIN_NOWRITE) || defined(SDB_EXP_BIN_NOCOPY)  // diagnostic: no slot copy-out (empty runs)
+        for (uint32_t x = tid; x < S; x += nt) q.count[(uint64_t)tile * S + x] = cnt[x] == 0x7FFFFFFF ? 1 : 0;
+        return;
+#endif
         for (uint32_t x = tid; x < S; x += nt) {
             const uint32_t c = cnt[x];
             q.count[(uint64_t)tile * S + x] = c <= cap ? c : kSlotOverflow;
         }
-        // wave w copies buckets w, w + nw, ...: two offsets per lane per step (cap is a multiple of 4)
+        // wave w copies buckets w, w + nw, ...: two offsets per lane per step (cap is a multiple of 4).  The
+        // first 256 offsets of kU buckets are read from LDS before any of them is stored (one LDS round trip
+        // for the wave's buckets instead of one per bucket and step: the copy-out was 3 us of k_facts' 12.7
+        // per SST, r5)
         const uint64_t stride = (uint64_t)pl.tiles * cap;
         uint16_t *slots = (uint16_t *)q.slot + (uint64_t)tile * cap;
         const uint32_t w = tid >> 6, nw = nt >> 6, l = tid & 63;
-        for (uint32_t sl = w; sl < S; sl += nw) {
-            const uint32_t c0 = cnt[sl], c = c0 < cap ? c0 : cap;
-            const uint32_t *src = (const uint32_t *)(bkt + sl * cap);
-            uint32_t *dst = (uint32_t *)(slots + sl * stride);
-            for (uint32_t i = 2 * l; i < c; i += 128) {
-                if (i + 1 < c) dst[i >> 1] = src[i >> 1];
-                else ((uint16_t *)dst)[i] = (uint16_t)src[i >> 1];
+        constexpr uint32_t kU = 6;
+        for (uint32_t sl0 = w; sl0 < S; sl0 += nw * kU) {
+            uint32_t c[kU], v0[kU], v1[kU];
+#pragma unroll
+            for (uint32_t u = 0; u < kU; u++) {
+                const uint32_t sl = sl0 + u * nw, sc = sl < S ? sl : 0;
+                const uint32_t c0 = sl < S ? cnt[sc] : 0;
+                c[u] = c0 < cap ? c0 : cap;
+                const uint32_t *src = (const uint32_t *)(bkt + sc * cap);
+                v0[u] = src[l];  // (the granule's tail beyond the run: stale bucket words)
+                v1[u] = 2 * l + 128 < cap ? src[l + 64] : 0;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kU; u++) {
+                const uint32_t sl = sl0 + u * nw;
+                if (sl >= S) continue;
+                // whole 64-byte granules (32 offsets; cap is a multiple of 32): the words past the run carry
+                // stale bucket bytes, which the fill never reads
+                uint32_t *dst = (uint32_t *)(slots + sl * stride);
+                const uint32_t cg = (c[u] + 31) & ~31u;
+                if (2 * l < cg) dst[l] = v0[u];
+                if (2 * l + 128 < cg) dst[l + 64] = v1[u];
+                const uint32_t *src = (const uint32_t *)(bkt + sl * cap);
+                for (uint32_t i = 2 * l + 256; i < c[u]; i += 128) {  // runs over 256 offsets (cap > 256)
+                    if (i + 1 < c[u]) dst[i >> 1] = src[i >> 1];
+                    else ((uint16_t *)dst)[i] = (uint16_t)src[i >> 1];
+                }
             }
         }
         return;

@@ -414,9 +414,11 @@ uint32_t bloom_slot_cap(const BloomPlan &pl) {
     const double frac = pl.m ? (double)(1ull << pl.sb) / pl.m : 1.0;
     const double mean = (double)pl.T * pl.k * (frac < 1.0 ? frac : 1.0);
     uint64_t cap = (uint64_t)(mean + 6.0 * __builtin_sqrt(mean + 1.0)) + 16;
-    cap = (cap + 7) & ~7ull;  // a multiple of 8: u16 slots start 16-byte aligned (bloom_fill_slice)
+    // a multiple of 32: u16 slots start 64-byte aligned, so the binning writes whole 64-byte granules (a
+    // partial one costs the memory a read-modify-write) and bloom_fill_slice's 16-byte loads stay aligned
+    cap = (cap + 31) & ~31ull;
     const uint64_t most = (uint64_t)pl.T * pl.k;  // a slot never holds more than the tile's probes
-    if (cap > most) cap = (most + 7) & ~7ull;
+    if (cap > most) cap = (most + 31) & ~31ull;
     return (uint32_t)cap;
 }
 

@@ -16,6 +16,7 @@
 
 #include "sdb_decode.h"
 #include "sdb_crc.h"
+#include "sdb_crc_mfma.h"
 #include "sdb_device.h"
 
 namespace sdb {
@@ -48,11 +49,25 @@ constexpr uint32_t kDecImg = 4096 + 32;                  // fast path: staged bl
 constexpr uint32_t kDecKeys = 2048;                      // fast path: restored keys of one block
 constexpr uint32_t kDecGuard = 64;                       // zero lead-in of the right-aligned CRC segments
 constexpr uint32_t kDecWaveLds = kDecGuard + kDecImg + kDecKeys;
-constexpr uint32_t kDecLds = kCrcTablesLds + (kEmThreads / 64) * kDecWaveLds;  // emit: tables (fail-fast CRC), waves
+// the checksum of a staged block (crc_staged_ok: the count pass, fail-fast emit) on the matrix cores
+// (sdb_crc_mfma.h: weights + tree tables, 56 KiB at LDS 0), or (SDB_DEC_CRC_SLICE) slicing-by-8 (36 KiB)
+#ifdef SDB_DEC_CRC_SLICE
+constexpr uint32_t kDecTabLds = kCrcTablesLds;
+#else
+constexpr uint32_t kDecTabLds = kCrcMfmaLds;
+#endif
+SDB_DEV void dec_crc_tables_to_lds(lu32 *at) {
+#ifdef SDB_DEC_CRC_SLICE
+    crc_tables_to_lds(at);
+#else
+    crc_mfma_tables_to_lds(at);
+#endif
+}
+constexpr uint32_t kDecLds = kDecTabLds + (kEmThreads / 64) * kDecWaveLds;  // emit: tables (fail-fast CRC), waves
 constexpr uint32_t kDecCap = kDecWaveLds - kDecGuard;
 // count pass: the CRC tables, the bank-replicated byte table (sdb_crc.h), then per wave a guard + image
 constexpr uint32_t kCntWaveLds = kDecGuard + kDecImg;
-constexpr uint32_t kCntLds = kCrcTablesLds + (kCntThreads / 64) * kCntWaveLds;
+constexpr uint32_t kCntLds = kDecTabLds + (kCntThreads / 64) * kCntWaveLds;
 static_assert(kCntLds <= 160 * 1024, "count pass LDS");
 constexpr uint32_t kRowTmp = kDecKeys - 256;  // emit: row positions of the lane-per-row path (4 x 32 u16) in kbuf
 typedef __attribute__((address_space(3))) uint16_t lu16;  // other blocks: generic staging per wave; larger ones parse from HBM
@@ -446,7 +461,11 @@ SDB_DEV bool crc_staged_ok(lu8 *img, uint32_t p0, uint32_t blen) {
     if (l < p0) img[l] = 0;
     if (l < 4) img[p0 + l] ^= 0xFF;
     wave_sync_d();
+#ifdef SDB_DEC_CRC_SLICE
     const uint32_t c = wave_crc_image_ra(img, p0 + blen);
+#else
+    const uint32_t c = wave_crc_image_mfma<0, kCrcMfmaTreeKiB>(img, p0 + blen);
+#endif
     wave_sync_d();
     if (l < 4) img[p0 + l] ^= 0xFF;
     wave_sync_d();
@@ -1004,10 +1023,10 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(kCn
         if (threadIdx.x == 0) atomicMin(a.err, (unsigned long long)SDB_DEVICE_ERROR);
         return;
     }
-    crc_tables_to_lds((lu32 *)smem);
+    dec_crc_tables_to_lds((lu32 *)smem);
     __syncthreads();
     const uint32_t wave = threadIdx.x >> 6;
-    lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kCntWaveLds + kDecGuard;
+    lu8 *img = (lu8 *)smem + kDecTabLds + wave * kCntWaveLds + kDecGuard;
     if (lane_id() < kDecGuard / 4) ((lu32 *)(img - kDecGuard))[lane_id()] = 0;  // never written again
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
@@ -1547,7 +1566,7 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
     }
     const uint32_t wave = threadIdx.x >> 6;
     const int l = lane_id();
-    lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kDecWaveLds + kDecGuard;
+    lu8 *img = (lu8 *)smem + kDecTabLds + wave * kDecWaveLds + kDecGuard;
     lu8 *kbuf = img + kDecImg;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
@@ -1558,7 +1577,7 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
             if (threadIdx.x == 0) atomicMin(a.err, (unsigned long long)SDB_DEVICE_ERROR);
             return;
         }
-        crc_tables_to_lds((lu32 *)smem);
+        dec_crc_tables_to_lds((lu32 *)smem);
         if (l < kDecGuard / 4) ((lu32 *)(img - kDecGuard))[l] = 0;
         __syncthreads();
     }
@@ -1666,7 +1685,7 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
     a.dkb = tot_kb;
     const uint32_t wave = threadIdx.x >> 6;
     const int l = lane_id();
-    lu8 *img = (lu8 *)smem + kCrcTablesLds + wave * kDecWaveLds + kDecGuard;
+    lu8 *img = (lu8 *)smem + kDecTabLds + wave * kDecWaveLds + kDecGuard;
     lu8 *kbuf = img + kDecImg;
     uint8_t *stage = (uint8_t *)img;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);

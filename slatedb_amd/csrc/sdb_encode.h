@@ -9,7 +9,17 @@ namespace sdb {
 
 constexpr uint32_t kChunk = 2048;            // entries per chunk (K3 / K5)
 constexpr uint32_t kResolveLds = 96 * 1024;  // LDS budget of the resolve tables (u16 exits)
-constexpr uint32_t kCrcLds = 36 * 1024;      // slicing-by-8 tables + x^256 byte tables + 6 combine-tree steps
+// k_emit's CRC tables: slicing-by-8 tables + x^256 byte tables + 6 combine-tree steps (36 KiB), or
+// (SDB_EMIT_CRC_MFMA) the matrix-core CRC's weights + the tree steps (sdb_crc_mfma.h, 56 KiB): 43.1 vs
+// 41.0 us per SST (r5) — the emit's LDS is not its bound, and 32 dependent MFMAs per block add latency
+#ifndef SDB_EMIT_CRC_MFMA
+#define SDB_EMIT_CRC_SLICE
+#endif
+#ifdef SDB_EMIT_CRC_SLICE
+constexpr uint32_t kCrcLds = 36 * 1024;
+#else
+constexpr uint32_t kCrcLds = 56 * 1024;
+#endif
 constexpr uint32_t kImgCap = 4096 + 64;      // LDS block image per wave (fast path)
 constexpr uint32_t kStageCap = 4096;         // value staging per wave (LDS-DMA, 1 KiB per instruction), in place
 constexpr uint32_t kStageGuard = 64;         // LDS bytes before each image the value stage may use

@@ -30,6 +30,7 @@
 
 #include "sdb_bloom.h"
 #include "sdb_crc.h"
+#include "sdb_crc_mfma.h"
 
 namespace sdb {
 
@@ -1795,12 +1796,16 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     const uint32_t vstage = lds_addr((const void *)img) - kStageGuard;
     const uint32_t kstage = lds_addr((const void *)kst);
     // 0. prefetched granules -> LDS stages
+#ifndef SDB_EXP_EMIT_NOSTAGE  // diagnostic: granules loaded, never staged
 #pragma unroll
     for (uint32_t q = 0; q < kStageCap / 1024; q++)
         if (64 * q + l < nv16) *(lu128 *)(uintptr_t)(vstage + 16 * (64 * q + l)) = *(const u32x4 *)&p.vg[q];
 #pragma unroll
     for (uint32_t q = 0; q < kKeyStageCap / 1024; q++)
         if (64 * q + l < nk16) *(lu128 *)(uintptr_t)(kstage + 16 * (64 * q + l)) = *(const u32x4 *)&p.kg[q];
+#else
+    if (l == 0 && p.vg[0].x == 0x12345678u && p.kg[0].y == 0x9abcdefu) img[0] = 1;  // keep the loads
+#endif
     // 1. row metadata (lane = row)
     const bool row = l < ne;
     const uint64_t ko = p.ko, vo = p.vo, seq = p.seq;
@@ -1886,7 +1891,11 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     WAVE_T(t3);
     // 3. literals: header, the key bytes sharing a dword with non-key bytes, trailer; then the
     //    restart table, count and the zero padding of the last CRC segment
+#ifdef SDB_EXP_EMIT_NOLIT  // diagnostic: no header / trailer / key-edge literals
+    if (false) {
+#else
     if (row) {
+#endif
         write_row_hdr_trailer<V>(img + row_off, r, seq, ets, cts);
         // the <= 3 key bytes that share a dword with value / trailer bytes (predicated, no loop)
         const uint32_t kj = (kend & ~3u) > kstart ? (kend & ~3u) : kstart;
@@ -1919,10 +1928,12 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     wave_sync();
     WAVE_T(t4);
     // 4. CRC32 (format/sst.rs:541-552) of the image [0, Lc)
-#ifdef SDB_EXP_EMIT_NOCRC  // diagnostic: wrong CRC by design
+#if defined(SDB_EXP_EMIT_NOCRC)  // diagnostic: wrong CRC by design
     const uint32_t crc32 = 0;
-#else
+#elif defined(SDB_EMIT_CRC_SLICE)
     const uint32_t crc32 = wave_crc_image_ra(img, Lc);
+#else
+    const uint32_t crc32 = wave_crc_image_mfma<0, kCrcMfmaTreeKiB>(img, Lc);
 #endif
     if (l == 0) {
         img[Lc] = (uint8_t)(crc32 >> 24);
@@ -1936,12 +1947,16 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     // 5. store [0, Lc + 4) -> out_data + off
     uint8_t *gdst = a.out_data + d.off;
     const uint32_t L = Lc + 4, nfull = L >> 4;
+#ifndef SDB_EXP_EMIT_NOSTORE  // diagnostic: the image is never stored
     for (uint32_t cc = l; cc < nfull; cc += 64) {
         u32x4 v = ((const lu128 *)img)[cc];
         if (cc == 0) v.x = ~v.x;  // the CRC's init fold
         __builtin_memcpy(gdst + 16 * cc, &v, 16);
     }
     if (l < (L & 15)) gdst[(nfull << 4) + l] = img[(nfull << 4) + l];  // L >= 16: never image bytes [0, 4)
+#else
+    if (l == 0 && crc32 == 0x12345678u) gdst[0] = img[5];
+#endif
     WAVE_T(t6);
 #ifdef SDB_PHASE_TIMING
     ph[0] += t1 - t0;
@@ -2272,7 +2287,11 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(SstSet P) {
         // the first block's descriptor is in flight while the CRC tables are copied, its values and
         // metadata while the workgroup does the slow blocks and sets up the ticket
         uint32_t dvn = desc_lanes(blk, r1);
+#ifdef SDB_EMIT_CRC_SLICE
         crc_tables_to_lds(crc);
+#else
+        crc_mfma_tables_to_lds(crc);
+#endif
         EmitPre pn;
         bool fn = false;
         if (blk < r1) {
@@ -2286,7 +2305,11 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(SstSet P) {
         for (uint32_t i = 0; i < P.count; i++) {
             const EncodeArgs ai = make_args(P, i);
             if (*ai.err == ~0ull && *ai.slow_count)
+#ifdef SDB_EMIT_CRC_SLICE
                 emit_slow_blocks<V>(ai, (uint8_t *)smem + kCrcLds + 16, (const uint32_t(*)[256])smem);
+#else  // (the rare workgroup path reads the slicing tables from constant memory)
+                emit_slow_blocks<V>(ai, (uint8_t *)smem + kCrcLds + 16, (const uint32_t(*)[256])c_crc.t);
+#endif
         }
         __syncthreads();
         if (threadIdx.x == 0) *(lu32 *)(smem + kCrcLds) = blockDim.x >> 6;  // block ticket (first blocks: r0 + wave)

@@ -343,6 +343,74 @@ uint8_t *put_be(uint8_t *o, uint64_t v, int nbytes) {
     return o;
 }
 
+// compress_and_transform's codec step for the footer's blocks (format/sst.rs:557-594): a literal-only
+// stream of the format — the stored / raw form every decoder of it reads (zlib: stored deflate blocks +
+// Adler-32; zstd: a frame of raw blocks with Frame_Content_Size; lz4: one literal sequence after the u32 LE
+// length; snappy: the varint length and one literal element).  Appended to `o`.
+void literal_stream(uint32_t codec, const uint8_t *in, uint64_t n, std::vector<uint8_t> &o) {
+    auto le = [&](uint64_t v, int nb) {
+        for (int i = 0; i < nb; i++) o.push_back((uint8_t)(v >> (8 * i)));
+    };
+    if (codec == SDB_CODEC_LZ4) {
+        le(n, 4);
+        o.push_back((uint8_t)((n >= 15 ? 15 : n) << 4));
+        if (n >= 15) {
+            uint64_t x = n - 15;
+            for (; x >= 255; x -= 255) o.push_back(255);
+            o.push_back((uint8_t)x);
+        }
+        o.insert(o.end(), in, in + n);
+    } else if (codec == SDB_CODEC_SNAPPY) {
+        for (uint64_t x = n;; x >>= 7) {
+            o.push_back((uint8_t)(x >= 0x80 ? (x & 0x7F) | 0x80 : x));
+            if (x < 0x80) break;
+        }
+        if (n) {
+            const uint64_t v = n - 1;
+            const int nb = v < 60 ? 0 : v < 256 ? 1 : v < 65536 ? 2 : v < (1u << 24) ? 3 : 4;
+            o.push_back((uint8_t)((nb ? 59 + nb : v) << 2));
+            le(v, nb);
+            o.insert(o.end(), in, in + n);
+        }
+    } else if (codec == SDB_CODEC_ZLIB) {
+        o.push_back(0x78);
+        o.push_back(0x9C);
+        uint64_t a = 1, b = 0, done = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            a = (a + in[i]) % 65521;
+            b = (b + a) % 65521;
+        }
+        do {
+            const uint64_t c = n - done < 65535 ? n - done : 65535;
+            o.push_back(done + c == n ? 1 : 0);
+            le(c, 2);
+            le(~c & 0xFFFF, 2);
+            o.insert(o.end(), in + done, in + done + c);
+            done += c;
+        } while (done < n);
+        put_be(&*o.insert(o.end(), 4, 0), (b << 16) | a, 4);
+    } else {  // zstd
+        le(0xFD2FB528u, 4);
+        if (n < 256) {
+            o.push_back(0x20);
+            le(n, 1);
+        } else if (n < 65536 + 256) {
+            o.push_back(0x60);
+            le(n - 256, 2);
+        } else {
+            o.push_back(0xA0);
+            le(n, 4);
+        }
+        uint64_t done = 0;
+        do {
+            const uint64_t c = n - done < (128u << 10) ? n - done : (128u << 10);
+            le((done + c == n ? 1u : 0u) | (c << 3), 3);  // Raw_Block
+            o.insert(o.end(), in + done, in + done + c);
+            done += c;
+        } while (done < n);
+    }
+}
+
 // A thread's reusable buffers: a footer is ~1.7 MB of flatbuffer bytes for a D1 SST, and fresh buffers
 // cost it a page fault per 4 KiB on every call.
 struct FooterScratch {
@@ -360,6 +428,7 @@ extern "C" uint64_t sdb_sst_footer_bound(const sdb_footer_in *in) {
     if (in->has_filter) b += 32 + in->bloom_len + (in->filter_name ? strlen(in->filter_name) : 3);  // composite filter block
     b += 64 + keys + 48 * nb;                                      // index: key, len, pads, BlockMeta, vtable, slot
     if (in->stats) b += 128 + 32 * nb;                             // stats: BlockStats tables + vector
+    if (in->compression) b += b / 64 + 256;                        // the codecs' framing (literal streams)
     return b;
 }
 
@@ -370,7 +439,7 @@ extern "C" sdb_status sdb_sst_footer(const sdb_footer_in *in, uint8_t *out, uint
     if (nb && (!in->block_off || !in->first_key_off || !in->first_key_bytes)) return SDB_INVALID_ARGUMENT;
     if (in->stats && nb && !in->block_stats) return SDB_INVALID_ARGUMENT;
     if (in->has_filter && in->bloom_len && !in->bloom) return SDB_INVALID_ARGUMENT;
-    if (in->sst_type > 1) return SDB_INVALID_ARGUMENT;
+    if (in->sst_type > 1 || in->compression > SDB_CODEC_ZSTD) return SDB_INVALID_ARGUMENT;
     for (uint64_t k = 0; k < nb; k++)
         if (in->first_key_off[k + 1] < in->first_key_off[k]) return SDB_INVALID_ARGUMENT;
     const HostCrc &crc = host_crc();
@@ -446,6 +515,29 @@ extern "C" sdb_status sdb_sst_footer(const sdb_footer_in *in, uint8_t *out, uint
     }
     if (in->has_filter && !(in->stats && nb >= 2048))
         filter_crc = ~crc.update(crc.update(0xFFFFFFFFu, fh.data(), fh.size()), in->bloom, in->bloom_len);
+    // a compression codec (format/sst.rs:557-594): the three blocks become the codec's streams, checksummed
+    // after compression
+    const uint32_t codec = in->compression;
+    std::vector<uint8_t> zf, zi, zs;
+    if (codec) {
+        if (in->has_filter) {
+            std::vector<uint8_t> composite(fh);
+            composite.insert(composite.end(), in->bloom, in->bloom + in->bloom_len);
+            literal_stream(codec, composite.data(), composite.size(), zf);
+            filter_crc = crc(zf.data(), zf.size());
+            filter_len = zf.size() + 4;
+        }
+        literal_stream(codec, idx_p, idx_n, zi);
+        idx_p = zi.data();
+        idx_n = zi.size();
+        idx_crc = crc(idx_p, idx_n);
+        if (in->stats) {
+            literal_stream(codec, st_p, st_n, zs);
+            st_p = zs.data();
+            st_n = zs.size();
+            st_crc = crc(st_p, st_n);
+        }
+    }
     const uint64_t index_offset = base + filter_len, index_len = idx_n + 4;
     uint64_t stats_offset = 0, stats_len = 0;
     if (in->stats) {
@@ -473,7 +565,7 @@ extern "C" sdb_status sdb_sst_footer(const sdb_footer_in *in, uint8_t *out, uint
         if (in->first_entry) w.field_offset(4, fe);
         w.field<uint8_t>(24, 1);  // FilterFormat::Composite
         w.field<uint8_t>(16, in->sst_type);
-        w.field<uint8_t>(14, 0);  // CompressionFormat::None
+        w.field<uint8_t>(14, (uint8_t)codec);  // CompressionFormat (None is the default: omitted)
         w.finish(w.end(t), &info_p, &info_n);
     }
     const uint64_t total = meta_offset - base + info_n + 4 + 10;
@@ -482,7 +574,10 @@ extern "C" sdb_status sdb_sst_footer(const sdb_footer_in *in, uint8_t *out, uint
     if (cap < total) return SDB_LIMIT_EXCEEDED;
     // compress_and_transform with no codec / transformer: bytes ++ crc32 BE (format/sst.rs:525-554)
     uint8_t *o = out;
-    if (in->has_filter) {
+    if (in->has_filter && codec) {
+        memcpy(o, zf.data(), zf.size());
+        o = put_be(o + zf.size(), filter_crc, 4);
+    } else if (in->has_filter) {
         memcpy(o, fh.data(), fh.size());
         o += fh.size();
         if (in->bloom_len) memcpy(o, in->bloom, in->bloom_len);

@@ -51,7 +51,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError("libslatedb_amd.so not built: run `python __graft_entry__.py build` "
                               "(hipcc --offload-arch=gfx950)")
-        _lib = _abi.bind(C.CDLL(LIB_PATH))
+        _lib = _abi.bind(C.CDLL(LIB_PATH), partial=bool(os.environ.get("SDB_LIBRARY")))
     return _lib
 
 
@@ -177,7 +177,7 @@ class EncodedSst:
         return comp + struct.pack(">I", zlib.crc32(comp))
 
 
-def sst_footer(batch, enc, sst_version=2, sst_type=_abi.SST_COMPACTED, filter_name=None):
+def sst_footer(batch, enc, sst_version=2, sst_type=_abi.SST_COMPACTED, filter_name=None, compression=0):
     """Footer bytes after the data section (sdb_sst_footer; EncodedSsTableFooterBuilder::build,
     format/sst.rs:383-487).  `enc` is an encode result with host arrays (EncodedSst, the
     DeviceSstOutput.to_host() dict wrapped by `_FooterView`, or anything with data/block_off/
@@ -212,7 +212,7 @@ def sst_footer(batch, enc, sst_version=2, sst_type=_abi.SST_COMPACTED, filter_na
                        first, len(first or b""), last, len(last or b""),
                        None if wal else C.addressof(sm), bst.ctypes.data if len(bst) else None,
                        bloom.ctypes.data if len(bloom) else None, 0 if wal else int(sm.bloom_len),
-                       filter_name)
+                       filter_name, compression, 0)
     n = C.c_uint64(0)
     cap = lib().sdb_sst_footer_bound(C.byref(fi))
     out = np.empty(max(cap, 1), np.uint8)
@@ -617,6 +617,28 @@ def decompress_blocks_device(codec, blocks, block_off, stream=None):
     if st:
         raise SdbError(st, "sdb_decompress_blocks")
     return out, out_start, out_end[:nb], err
+
+
+def compress_blocks_device(codec, blocks, block_off, in_bytes=None, out_cap=None, stream=None):
+    """An encoded data section -> the same blocks compressed (sdb_compress_blocks; compress_and_transform,
+    format/sst.rs:525-594).  blocks: device u8 tensor, block_off: device int64 tensor of nblocks + 1.
+    Returns (out, out_off, err) device tensors; out_off[nblocks] = the compressed section's length."""
+    import torch
+    dev = blocks.device
+    nb = block_off.numel() - 1
+    if in_bytes is None:
+        in_bytes = int(block_off[nb].item() - block_off[0].item()) if nb else 0
+    if out_cap is None:
+        out_cap = in_bytes + in_bytes // 8 + 64 * (nb + 1)
+    ws = torch.empty(int(lib().sdb_compress_workspace_bytes(nb, in_bytes)), dtype=torch.uint8, device=dev)
+    out = torch.empty(max(out_cap, 1) + 16, dtype=torch.uint8, device=dev)
+    out_off = torch.empty(nb + 1, dtype=torch.int64, device=dev)
+    err = torch.empty(1, dtype=torch.int64, device=dev)
+    st = lib().sdb_compress_blocks(codec, blocks.data_ptr(), block_off.data_ptr(), nb, in_bytes, out.data_ptr(), out_cap,
+                                   out_off.data_ptr(), err.data_ptr(), ws.data_ptr(), ws.numel(), _sp(stream))
+    if st:
+        raise SdbError(st, "sdb_compress_blocks")
+    return out, out_off, err
 
 
 LOOKUP_FIELDS = (("state", "uint8"), ("status", "int32"), ("block", "int32"), ("entry", "int32"),

@@ -208,3 +208,19 @@ def test_wal_insertion_order():
     assert d.status == 0 and d.n == b.n and np.array_equal(d.key_arena, b.key_bytes)
     assert np.array_equal(d.seq, b.seq)
     assert O.encode_sst(b, O.params(sst_version=1, sst_type=_abi.SST_WAL)).status == _abi.SDB_INVALID_ARGUMENT
+
+
+@pytest.mark.parametrize("codec", [1, 2, 3, 4])
+def test_compressed_footer_blocks(codec):
+    """SsTableInfo.compression_format set: the filter, index and stats blocks go through the codec before
+    their checksums (compress_and_transform, format/sst.rs:394-452) and parse back to the same contents."""
+    b = datasets.d3(n=2000)
+    res = O.encode_sst(b, O.params())
+    plain = runtime.sst_footer(b, res)
+    comp = runtime.sst_footer(b, res, compression=codec)
+    data = np.asarray(res.data, np.uint8).tobytes()
+    v0, i0, x0, s0, f0 = F.parse_sst(data + plain)
+    v1, i1, x1, s1, f1 = F.parse_sst(data + comp)
+    assert i1["compression"] == codec and i0["compression"] == 0
+    assert (v1, x1, s1, f1) == (v0, x0, s0, f0)
+    assert i1["first_entry"] == i0["first_entry"] and i1["last_entry"] == i0["last_entry"]
