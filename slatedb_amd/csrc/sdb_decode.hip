@@ -49,8 +49,12 @@ constexpr uint32_t kDecImg = 4096 + 32;                  // fast path: staged bl
 constexpr uint32_t kDecKeys = 2048;                      // fast path: restored keys of one block
 constexpr uint32_t kDecGuard = 64;                       // zero lead-in of the right-aligned CRC segments
 constexpr uint32_t kDecWaveLds = kDecGuard + kDecImg + kDecKeys;
-// the checksum of a staged block (crc_staged_ok: the count pass, fail-fast emit) on the matrix cores
-// (sdb_crc_mfma.h: weights + tree tables, 56 KiB at LDS 0), or (SDB_DEC_CRC_SLICE) slicing-by-8 (36 KiB)
+// the checksum of a staged block (crc_staged_ok: the count pass, fail-fast emit): slicing-by-8 (36 KiB
+// of tables), or (SDB_DEC_CRC_MFMA) on the matrix cores (sdb_crc_mfma.h: weights + tree tables, 56 KiB
+// at LDS 0), which measured slower on configs[2] (0.947 vs 0.898 ms)
+#ifndef SDB_DEC_CRC_MFMA
+#define SDB_DEC_CRC_SLICE
+#endif
 #ifdef SDB_DEC_CRC_SLICE
 constexpr uint32_t kDecTabLds = kCrcTablesLds;
 #else

@@ -279,6 +279,16 @@ SDB_DEV uint32_t wave_xor(uint32_t v) {
 SDB_DEV uint32_t wave_max(uint32_t v) {
     return wave_readlane(wave_incl_scan_op(v, [](uint32_t x, uint32_t y) { return x > y ? x : y; }), 63);
 }
+// A raw buffer descriptor over [p, p + n) for range-checked loads / stores (an access past n is dropped,
+// a load past n returns 0).  The inputs are readfirstlane'd so the compiler can see the descriptor is
+// wave-uniform (it must be), otherwise it wraps every access in a waterfall loop.
+SDB_DEV __amdgpu_buffer_rsrc_t wave_rsrc(const void *p, uint32_t n) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+    const int nr = __builtin_amdgcn_readfirstlane((int)n);
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, nr, 0x00020000);
+}
 // lane l gets lane l + 1's value (lane 63 gets 0)
 template <typename T>
 SDB_DEV T wave_next_lane(T v) {

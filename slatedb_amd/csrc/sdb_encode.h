@@ -35,7 +35,12 @@ constexpr uint32_t kFactsEntries = kFactsThreads * kFactsPerT;
 constexpr uint32_t kSegLds = (2 * kSegSpan + 4) * 4 + kChunk * 6;  // 36 KiB: four workgroups per CU
 constexpr uint32_t kSegLdsMax = 64 * 1024;          // k_seg's LDS with the fused bloom binning
 constexpr uint32_t kHashPerT = kChunk / kSegThreads;  // chunk entries (hashes) per k_seg thread
-constexpr uint32_t kEmitThreads = 1024;      // 16 waves per workgroup (two blocks in flight each), 1 per CU
+#ifndef SDB_EMIT_WAVES
+#define SDB_EMIT_WAVES 16
+#endif
+// SDB_EMIT_WAVES waves per workgroup, 1 per CU: each wave assembles one block while the next one's data
+// is in flight (16 waves: 128 VGPRs each, which hold it without spilling)
+constexpr uint32_t kEmitThreads = 64 * SDB_EMIT_WAVES;
 constexpr uint32_t kEmitWgPerCu = 1;
 constexpr uint32_t kEmitWaveLds = kStageGuard + kImgCap + 16 + kKeyStageCap + 64 * 16;  // guard, image, key stage, spans
 constexpr uint32_t kEmitLds = kCrcLds + 16 + (kEmitThreads / 64) * kEmitWaveLds;  // tables, ticket, waves

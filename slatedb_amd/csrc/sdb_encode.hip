@@ -1725,11 +1725,14 @@ SDB_DEV uint32_t write_row_hdr_trailer(lu8 *dst, const RowInfo &r, uint64_t seq,
 // the block's value / key granules (lane l holds granules l, 64 + l, ...) and the row metadata
 // (lane = row).  Plain loads only: the compute phase of the current block issues no global load,
 // so the compiler's in-order vmcnt waits never drain the prefetch early.
-struct EmitPre {
+// A block's prefetched data (16-byte granules of its values and keys, lane l holding granules l, l + 64,
+// ...) and row metadata (lane = row).
+struct EmitData {
     uint4 vg[kStageCap / 1024];
     uint4 kg[kKeyStageCap / 1024];
+};
+struct EmitMeta {
     uint64_t ko, vo, seq;
-    int64_t cts, ets;
     uint64_t pko;  // lane 0: key_off[s - 1] (previous key, index-key rule)
     uint32_t lcp;
     uint32_t kind, mask;
@@ -1754,48 +1757,56 @@ SDB_DEV BlockDesc desc_from_lanes(uint32_t dv) {  // lanes 0..13 hold the 14 dwo
 static_assert(sizeof(BlockDesc) == 56, "BlockDesc is 14 dwords");
 
 
-SDB_DEV void emit_prefetch(const EncodeArgs &a, const BlockDesc &d, EmitPre &p) {
-    const uint32_t l = (uint32_t)lane_id();
-    const uint32_t ne = d.e - d.s;
-    const uint64_t va = d.vs & ~15ull, ka = d.ks & ~15ull;
-    const uint32_t nv16 = d.ve > d.vs ? (uint32_t)((d.ve - va + 15) >> 4) : 0;
-    const uint32_t nk16 = (uint32_t)((d.ke - ka + 15) >> 4);
-    const uint4 *vsrc = (const uint4 *)(a.val_bytes + va), *ksrc = (const uint4 *)(a.key_bytes + ka);
-#pragma unroll
-    for (uint32_t q = 0; q < kStageCap / 1024; q++)
-        if (64 * q + l < nv16) p.vg[q] = vsrc[64 * q + l];
-#pragma unroll
-    for (uint32_t q = 0; q < kKeyStageCap / 1024; q++)
-        if (64 * q + l < nk16) p.kg[q] = ksrc[64 * q + l];
-    const bool row = l < ne;
-    const uint64_t j = d.s + (row ? l : 0);
-    p.ko = a.key_off[j];
-    p.vo = a.val_off[j];
-    p.seq = a.seq ? a.seq[j] : 0;
-    p.lcp = a.lcp[j];
-    p.kind = a.kind ? a.kind[j] : 0;      // rows >= ne read entry s (masked at use)
-    p.mask = a.ts_mask ? a.ts_mask[j] : 0;
-    // unconditional loads (selected by the mask at use): a load whose address or predicate hangs on
-    // another prefetched value would make the compiler wait for the whole prefetch here
-    p.cts = a.create_ts ? a.create_ts[j] : 0;
-    p.ets = a.expire_ts ? a.expire_ts[j] : 0;
-    p.pko = (l == 0 && d.s > 0) ? a.key_off[d.s - 1] : 0;
+// A block k_emit skips (not fast, or past the workgroup's share) is emitted as an empty block with its
+// stores dropped, so that every iteration issues the same memory instructions (see k_emit).
+SDB_DEV BlockDesc desc_or_empty(BlockDesc d, bool live) {
+    if (!live) {
+        d.e = d.s;
+        d.ve = d.vs;
+        d.ke = d.ks;
+    }
+    return d;
 }
 
-template <int V>
-SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, const EmitPre &p, lu8 *img,
-                        lu8 *kst, lSpanCopy *rtab, const lu32 *crc, uint64_t *ph) {
-    WAVE_T(t0);
+// Every load is unconditional, from a clamped in-bounds address (lanes past the block re-read its last
+// granule; an absent column reads key_off and is masked at use): a load under a branch, even a lane
+// predicate, leaves the compiler's vmcnt bookkeeping at the join with the worst case, and k_emit's
+// wait for THIS block's data would then also wait for the next block's prefetch.
+SDB_DEV void emit_prefetch_data(const EncodeArgs &a, const BlockDesc &d, EmitData &p) {
     const uint32_t l = (uint32_t)lane_id();
-    const uint32_t ne = d.e - d.s;
     const uint64_t va = d.vs & ~15ull, ka = d.ks & ~15ull;
     const uint32_t nv16 = d.ve > d.vs ? (uint32_t)((d.ve - va + 15) >> 4) : 0;
     const uint32_t nk16 = (uint32_t)((d.ke - ka + 15) >> 4);
-    // value stage: value byte x lands at LDS (img - kStageGuard) + (x - va), i.e. at or below its
-    // image position (see copy_spans); keys land in the key stage
+    const uint4 *vsrc = nv16 ? (const uint4 *)(a.val_bytes + va) : (const uint4 *)a.key_off;
+    const uint4 *ksrc = nk16 ? (const uint4 *)(a.key_bytes + ka) : (const uint4 *)a.key_off;
+    const uint32_t vlast = nv16 ? nv16 - 1 : 0, klast = nk16 ? nk16 - 1 : 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kStageCap / 1024; q++) p.vg[q] = vsrc[64 * q + l < vlast ? 64 * q + l : vlast];
+#pragma unroll
+    for (uint32_t q = 0; q < kKeyStageCap / 1024; q++) p.kg[q] = ksrc[64 * q + l < klast ? 64 * q + l : klast];
+}
+SDB_DEV void emit_prefetch_meta(const EncodeArgs &a, const BlockDesc &d, EmitMeta &p) {
+    const uint32_t l = (uint32_t)lane_id();
+    const uint32_t ne = d.e - d.s;
+    const uint64_t j = d.s + (l < ne ? l : 0);  // rows >= ne read entry s (masked at use)
+    p.ko = a.key_off[j];
+    p.vo = a.val_off[j];
+    p.seq = (a.seq ? a.seq : a.key_off)[j];
+    p.lcp = a.lcp[j];
+    p.kind = (a.kind ? a.kind : (const uint8_t *)a.key_off)[j];
+    p.mask = (a.ts_mask ? a.ts_mask : (const uint8_t *)a.key_off)[j];
+    p.pko = a.key_off[d.s > 0 ? d.s - 1 : 0];  // lane 0 uses it when s > 0
+}
+
+// 0. the prefetched granules -> the LDS stages: value byte x lands at LDS (img - kStageGuard) + (x - va),
+//    i.e. at or below its image position (see copy_spans); keys land in the key stage
+SDB_DEV void emit_stage(const BlockDesc &d, const EmitData &p, lu8 *img, lu8 *kst) {
+    const uint32_t l = (uint32_t)lane_id();
+    const uint64_t va = d.vs & ~15ull, ka = d.ks & ~15ull;
+    const uint32_t nv16 = d.ve > d.vs ? (uint32_t)((d.ve - va + 15) >> 4) : 0;
+    const uint32_t nk16 = (uint32_t)((d.ke - ka + 15) >> 4);
     const uint32_t vstage = lds_addr((const void *)img) - kStageGuard;
     const uint32_t kstage = lds_addr((const void *)kst);
-    // 0. prefetched granules -> LDS stages
 #ifndef SDB_EXP_EMIT_NOSTAGE  // diagnostic: granules loaded, never staged
 #pragma unroll
     for (uint32_t q = 0; q < kStageCap / 1024; q++)
@@ -1806,12 +1817,33 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
 #else
     if (l == 0 && p.vg[0].x == 0x12345678u && p.kg[0].y == 0x9abcdefu) img[0] = 1;  // keep the loads
 #endif
+}
+
+template <int V>
+SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, bool live, const EmitMeta &p, lu8 *img,
+                        lu8 *kst, lSpanCopy *rtab, const lu32 *crc, uint64_t *ph) {
+    WAVE_T(t0);
+    const uint32_t l = (uint32_t)lane_id();
+    const uint32_t ne = d.e - d.s;
+    const uint64_t va = d.vs & ~15ull, ka = d.ks & ~15ull;
+    const uint32_t vstage = lds_addr((const void *)img) - kStageGuard;
+    const uint32_t kstage = lds_addr((const void *)kst);
+    // (0. the stages are written by the caller: emit_stage)
     // 1. row metadata (lane = row)
     const bool row = l < ne;
-    const uint64_t ko = p.ko, vo = p.vo, seq = p.seq;
+    const uint64_t ko = p.ko, vo = p.vo, seq = a.seq ? p.seq : 0;
     const uint32_t lcp = p.lcp;
-    const uint8_t kind = row ? (uint8_t)p.kind : 0, mask = row ? (uint8_t)p.mask : 0;
-    const int64_t cts = (mask & SDB_TS_CREATE) ? p.cts : 0, ets = (mask & SDB_TS_EXPIRE) ? p.ets : 0;
+    const uint8_t kind = row && a.kind ? (uint8_t)p.kind : 0, mask = row && a.ts_mask ? (uint8_t)p.mask : 0;
+    // timestamps: loaded here, only by a block that carries any (rare; the prefetch keeps its registers)
+    int64_t cts = 0, ets = 0;
+    if (__ballot(mask & (SDB_TS_CREATE | SDB_TS_EXPIRE))) {
+        const uint64_t j = d.s + (row ? l : 0);
+        if ((mask & SDB_TS_CREATE) && a.create_ts) cts = a.create_ts[j];
+        if ((mask & SDB_TS_EXPIRE) && a.expire_ts) ets = a.expire_ts[j];
+        // land them here: a load still pending at the join would make every later write of its
+        // registers (reused by the common path) wait for all memory traffic
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    }
     uint32_t prev_klen = 0;
     if (l == 0 && d.s > 0) prev_klen = (uint32_t)(d.ks - p.pko);
     uint64_t ko1 = wave_next_lane(ko), vo1 = wave_next_lane(vo);
@@ -1874,8 +1906,10 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     wave_sync();  // stages written (DS instructions of one wave complete in order)
     WAVE_T(t2);
     // 2. key suffixes + values: lane = row from registers, or cooperative by the span table
-#ifdef SDB_EXP_EMIT_NOCOPY  // diagnostic: image without key / value bytes
+#if defined(SDB_EXP_EMIT_NOCOPY)  // diagnostic: image without key / value bytes
     if (false) {
+#elif defined(SDB_EMIT_SPANS)  // the cooperative span copy for every block
+    if (true) {
 #else
     if (!copy_rows(img, row, sc)) {
 #endif
@@ -1940,22 +1974,32 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
         img[Lc + 1] = (uint8_t)(crc32 >> 16);
         img[Lc + 2] = (uint8_t)(crc32 >> 8);
         img[Lc + 3] = (uint8_t)crc32;
-        if (Lc + 4 != d.bb) report_error(a.err, d.s, SDB_DEVICE_ERROR);  // internal consistency
+        if (live && Lc + 4 != d.bb) report_error(a.err, d.s, SDB_DEVICE_ERROR);  // internal consistency
     }
     wave_sync();
     WAVE_T(t5);
-    // 5. store [0, Lc + 4) -> out_data + off
-    uint8_t *gdst = a.out_data + d.off;
+    // 5. store [0, Lc + 4) -> out_data + off: a fixed set of buffer stores (L <= 4096: four 16-byte granule
+    //    stores and one tail-byte store per lane), the range check of the buffer descriptor dropping what
+    //    lies past the block (or everything: !live) -- no branch, so the count of memory instructions is
+    //    the same on every path (see k_emit)
     const uint32_t L = Lc + 4, nfull = L >> 4;
 #ifndef SDB_EXP_EMIT_NOSTORE  // diagnostic: the image is never stored
-    for (uint32_t cc = l; cc < nfull; cc += 64) {
-        u32x4 v = ((const lu128 *)img)[cc];
-        if (cc == 0) v.x = ~v.x;  // the CRC's init fold
-        __builtin_memcpy(gdst + 16 * cc, &v, 16);
+    {
+        uint8_t *gdst = a.out_data + d.off;
+        const __amdgpu_buffer_rsrc_t rg = wave_rsrc(gdst, live ? nfull << 4 : 0);
+        const __amdgpu_buffer_rsrc_t rt = wave_rsrc(gdst, live ? L : 0);
+#pragma unroll
+        for (uint32_t q = 0; q < kStageCap / 1024; q++) {
+            const uint32_t cc = 64 * q + l;
+            u32x4 v = ((const lu128 *)img)[cc];
+            if (cc == 0) v.x = ~v.x;  // the CRC's init fold
+            __builtin_amdgcn_raw_buffer_store_b128(v, rg, (int)(16 * cc), 0, 0);
+        }
+        const uint32_t tb = (nfull << 4) + l;  // L >= 16: never image bytes [0, 4)
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)img[tb < kImgCap ? tb : 0], rt, (int)(l < (L & 15) ? tb : L), 0, 0);
     }
-    if (l < (L & 15)) gdst[(nfull << 4) + l] = img[(nfull << 4) + l];  // L >= 16: never image bytes [0, 4)
 #else
-    if (l == 0 && crc32 == 0x12345678u) gdst[0] = img[5];
+    if (l == 0 && crc32 == 0x12345678u) a.out_data[d.off] = img[5];
 #endif
     WAVE_T(t6);
 #ifdef SDB_PHASE_TIMING
@@ -1967,17 +2011,19 @@ SDB_DEV void emit_block(const EncodeArgs &a, uint32_t blk, const BlockDesc &d, c
     ph[5] += t6 - t5;
     ph[6] += 1;
 #endif
-    // 6. BlockStats (sst_stats.rs:9-16) and the index key (compute_index_key, utils.rs:198-226)
+    // 6. BlockStats (sst_stats.rs:9-16) and the index key (compute_index_key, utils.rs:198-226): lanes
+    //    0..2 store the three counts, lane 0 the index key length, through range-checked buffer stores
     const uint64_t pu = __ballot(row && kind == SDB_KIND_VALUE);
     const uint64_t de = __ballot(row && kind == SDB_KIND_TOMBSTONE);
     const uint64_t me = __ballot(row && kind == SDB_KIND_MERGE);
-    if (l == 0) {
-        a.out_block_stats[3 * (uint64_t)blk] = (uint16_t)__popcll(pu);
-        a.out_block_stats[3 * (uint64_t)blk + 1] = (uint16_t)__popcll(de);
-        a.out_block_stats[3 * (uint64_t)blk + 2] = (uint16_t)__popcll(me);
+    {
+        const __amdgpu_buffer_rsrc_t rs = wave_rsrc(a.out_block_stats + 3 * (uint64_t)blk, live ? 6 : 0);
+        const __amdgpu_buffer_rsrc_t rk = wave_rsrc(a.out_index_key_len + blk, live ? 4 : 0);
+        const uint32_t c = (uint32_t)__popcll(l == 0 ? pu : l == 1 ? de : me);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)c, rs, (int)(l < 3 ? 2 * l : 6), 0, 0);
         uint32_t ik = 0;
         if (d.s > 0 && !a.wal) ik = (lcp == prev_klen && prev_klen == klen) ? klen : lcp + 1;
-        a.out_index_key_len[blk] = ik;
+        __builtin_amdgcn_raw_buffer_store_b32(ik, rk, (int)(l == 0 ? 0 : 4), 0, 0);
     }
     wave_sync();
 }
@@ -2270,10 +2316,12 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(SstSet P) {
         si = (uint32_t)__popcll(m);
         lb = g - (si ? (uint32_t)__builtin_amdgcn_readlane((int)vpre, (int)si - 1) : 0u);
     };
-    auto desc_lanes = [&](uint32_t g, uint32_t r1) -> uint32_t {  // lanes 0..13: the 14 dwords of g's desc
+    // lanes 0..13: the 14 dwords of g's desc (g clamped to the share's last block, r1 > r0: an
+    // unconditional load, see emit_prefetch)
+    auto desc_lanes = [&](uint32_t g, uint32_t r1) -> uint32_t {
         uint32_t si, lb;
-        locate(g, si, lb);
-        return (g < r1 && l < 14) ? ((const uint32_t *)make_args(P, si).desc)[14 * (uint64_t)lb + l] : 0u;
+        locate(g < r1 ? g : r1 - 1, si, lb);
+        return ((const uint32_t *)make_args(P, si).desc)[14 * (uint64_t)lb + (l < 14 ? l : 13)];
     };
     if (run) {
         lu32 *crc = (lu32 *)smem;
@@ -2284,22 +2332,25 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(SstSet P) {
         const uint32_t r0 = (uint32_t)((uint64_t)nb * blockIdx.x / gridDim.x);
         const uint32_t r1 = (uint32_t)((uint64_t)nb * (blockIdx.x + 1) / gridDim.x);
         uint32_t blk = r0 + wave;
+        const bool any = blk < r1;
         // the first block's descriptor is in flight while the CRC tables are copied, its values and
         // metadata while the workgroup does the slow blocks and sets up the ticket
-        uint32_t dvn = desc_lanes(blk, r1);
+        uint32_t dvc = any ? desc_lanes(blk, r1) : 0u;
 #ifdef SDB_EMIT_CRC_SLICE
         crc_tables_to_lds(crc);
 #else
         crc_mfma_tables_to_lds(crc);
 #endif
-        EmitPre pn;
-        bool fn = false;
-        if (blk < r1) {
+        EmitData pd;
+        EmitMeta mc;
+        bool fc = false;
+        if (any) {
             uint32_t si, lb;
             locate(blk, si, lb);
-            const BlockDesc dn = desc_from_lanes(dvn);
-            fn = emit_fast(dn);
-            if (fn) emit_prefetch(make_args(P, si), dn, pn);
+            const BlockDesc d0 = desc_from_lanes(dvc);
+            fc = emit_fast(d0);
+            emit_prefetch_data(make_args(P, si), desc_or_empty(d0, fc), pd);
+            emit_prefetch_meta(make_args(P, si), desc_or_empty(d0, fc), mc);
         }
         __syncthreads();
         for (uint32_t i = 0; i < P.count; i++) {
@@ -2324,30 +2375,41 @@ __global__ __launch_bounds__(kEmitThreads, 1) void k_emit(SstSet P) {
             if (l == 0) t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             return r0 + (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
         };
-        if (blk < r1) {
+        if (any) {
+            // Software pipeline, one block deep: while block `blk` is assembled (its data pc landed), the
+            // next block's data and the descriptor of the one after it are in flight.  Every iteration
+            // issues exactly the same memory instructions (unconditional loads, range-checked stores, the
+            // last iteration's prefetch wasted), and the state entering the loop has nothing in flight, so
+            // the compiler's only vmcnt waits are the end-of-iteration hand-overs (pn -> pc, dv2 -> dvn),
+            // which leave this block's stores in flight.
             uint32_t nblk = take();
-            uint32_t dv = desc_lanes(nblk, r1);
-            while (blk < r1) {
-                const uint32_t dcur = dvn;
-                const EmitPre p = pn;
-                const bool fast = fn;
-                const uint32_t cblk = blk;
+            uint32_t dvn = desc_lanes(nblk, r1);
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            while (true) {
+                // block blk's data landed (the hand-over wait at the end of the previous iteration): stage
+                // it, then its registers take the next block's data
+                emit_stage(desc_or_empty(desc_from_lanes(dvc), fc), pd, img, kst);
+                const bool more = nblk < r1;
+                uint32_t si, lb;
+                locate(more ? nblk : r1 - 1, si, lb);
+                const BlockDesc dn0 = desc_from_lanes(dvn);
+                const bool fn = more && emit_fast(dn0);
+                const BlockDesc dn = desc_or_empty(dn0, fn);
+                emit_prefetch_data(make_args(P, si), dn, pd);
+                EmitMeta mn;
+                emit_prefetch_meta(make_args(P, si), dn, mn);
+                const uint32_t n2 = take();
+                const uint32_t dv2 = desc_lanes(n2, r1);
+                uint32_t csi, clb;
+                locate(blk, csi, clb);  // others: k_emit_big, slow path (emitted empty, stores dropped)
+                emit_block<V>(make_args(P, csi), clb, desc_or_empty(desc_from_lanes(dvc), fc), fc, mc, img, kst, rtab, crc, ph);
+                if (!more) break;
                 blk = nblk;
-                if (blk < r1) {  // issue the next block (and the descriptor of the one after it)
-                    dvn = dv;
-                    uint32_t si, lb;
-                    locate(blk, si, lb);
-                    const BlockDesc dn = desc_from_lanes(dvn);
-                    fn = emit_fast(dn);
-                    if (fn) emit_prefetch(make_args(P, si), dn, pn);
-                    nblk = take();
-                    dv = desc_lanes(nblk, r1);
-                }
-                if (fast) {  // others: k_emit_big, slow path
-                    uint32_t csi, clb;
-                    locate(cblk, csi, clb);
-                    emit_block<V>(make_args(P, csi), clb, desc_from_lanes(dcur), p, img, kst, rtab, crc, ph);
-                }
+                nblk = n2;
+                dvc = dvn;
+                dvn = dv2;
+                mc = mn;
+                fc = fn;
             }
         }
     }
