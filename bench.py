@@ -179,28 +179,33 @@ def cpu_baseline(budget_s, threads):
 
 
 def measured_copy_gbs(dev, nbytes=1 << 30, reps=8):
-    """The box's attainable HBM copy bandwidth (read + write bytes) beside the 8 TB/s spec: sdb_diag_copy, a
-    hand-written 16-byte-per-lane STREAM copy (torch's copy_ measured ~4.8 TB/s, under what a plain kernel
-    reaches), on torch's current stream."""
+    """The box's attainable HBM copy bandwidth (read + write bytes) beside the 8 TB/s spec: the best of the
+    hand-written 16-byte-per-lane copy probes (sdb_diag_bw modes 0 and 2: grid-stride nontemporal, and 4 KiB
+    per wave and step; 4 and 32 workgroups per CU), on torch's current stream.  scripts/bw_probe.py has the
+    full set (read only, write only)."""
     L = runtime.lib()
-    if not hasattr(L, "sdb_diag_copy"):  # an older diagnostic variant library (SDB_LIBRARY)
+    if not hasattr(L, "sdb_diag_bw"):  # an older diagnostic variant library (SDB_LIBRARY)
         return None
     a = torch.empty(nbytes, dtype=torch.uint8, device=dev).fill_(1)
     b = torch.empty_like(a)
     st = torch.cuda.current_stream().cuda_stream
-    assert L.sdb_diag_copy(b.data_ptr(), a.data_ptr(), nbytes, st) == 0
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        L.sdb_diag_copy(b.data_ptr(), a.data_ptr(), nbytes, st)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+    best = 0.0
+    for mode in (0, 2):
+        for wpc in (4, 32):
+            assert L.sdb_diag_bw(b.data_ptr(), a.data_ptr(), nbytes, mode, wpc, st) == 0
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                L.sdb_diag_bw(b.data_ptr(), a.data_ptr(), nbytes, mode, wpc, st)
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            best = max(best, 2 * nbytes / (ms * 1e-3) / 1e9)
     assert torch.equal(a[:4096], b[:4096]) and torch.equal(a[-4096:], b[-4096:])
     del a, b
     torch.cuda.empty_cache()
-    return 2 * nbytes / (ms * 1e-3) / 1e9
+    return best
 
 
 def pmc_traffic():

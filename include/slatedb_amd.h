@@ -652,6 +652,10 @@ sdb_status sdb_diag_mfma_i8(const int32_t *a, const int32_t *b, int32_t *d, void
 /* A hand-written STREAM copy (16 bytes per lane, grid-stride) of `bytes` (a multiple of 16, 16-byte aligned):
  * bench.py's attainable-HBM ceiling beside the 8 TB/s spec. */
 sdb_status sdb_diag_copy(void *dst, const void *src, uint64_t bytes, void *stream);
+/* Bandwidth probes over `bytes` (a multiple of 4096, 16-byte aligned), wg_per_cu x CUs workgroups of 256
+ * threads: mode 0 sdb_diag_copy, 1 the same copy with plain loads / stores, 2 a copy by 4 KiB per wave
+ * and step, 3 read only, 4 write only. */
+sdb_status sdb_diag_bw(void *dst, const void *src, uint64_t bytes, int mode, int wg_per_cu, void *stream);
 
 /* Device query: number of visible HIP devices (0 on a machine without a GPU). */
 int sdb_device_count(void);

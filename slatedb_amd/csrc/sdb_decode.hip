@@ -436,6 +436,20 @@ SDB_DEV void gran_load(const DecodeArgs &a, uint64_t s, uint64_t e, Granules &r)
         if (q < ng) r.g[i] = src[q];
     }
 }
+// The same granules by unconditional loads (lanes past the block re-read its last granule; a block that
+// is not dec_fast reads only its first granule): no load sits under a branch, so the compiler's vmcnt
+// bookkeeping stays exact and a prefetch is never waited on before its use (see k_emit).
+SDB_DEV void gran_load_u(const DecodeArgs &a, uint64_t s, uint64_t e, Granules &r) {
+    const uint32_t l = (uint32_t)lane_id();
+    const uint64_t a0 = s & ~15ull;
+    const uint32_t ng = dec_fast(s, e) ? (uint32_t)((((e + 15) & ~15ull) - a0) >> 4) : 1u;
+    const uint4 *src = (const uint4 *)(a.blocks + a0);
+#pragma unroll
+    for (int i = 0; i < kGranRegs; i++) {
+        const uint32_t q = l + 64 * i;
+        r.g[i] = src[q < ng ? q : ng - 1];
+    }
+}
 SDB_DEV void gran_store(uint64_t s, uint64_t e, const Granules &r, lu8 *img) {
     const uint32_t l = (uint32_t)lane_id();
     const uint32_t ng = (uint32_t)((((e + 15) & ~15ull) - (s & ~15ull)) >> 4);
@@ -477,11 +491,12 @@ SDB_DEV bool crc_staged_ok(lu8 *img, uint32_t p0, uint32_t blen) {
 }
 
 SDB_DEV LdsBlockView stage_lds(const DecodeArgs &a, uint64_t s, uint64_t e, lu8 *img, bool check,
-                               const Granules *pre = nullptr) {
+                               const Granules *pre = nullptr, bool staged = false) {
     LdsBlockView v{};
     const uint32_t l = (uint32_t)lane_id();
     const uint32_t p0 = (uint32_t)(s & 15), len = (uint32_t)(e - s), blen = len - 4, Lc = p0 + blen;
-    if (pre) {
+    if (staged) {  // the caller wrote the granules (gran_store)
+    } else if (pre) {
         gran_store(s, e, *pre, img);
     } else {
         Granules g;
@@ -534,12 +549,8 @@ SDB_DEV void wave_store_bytes(uint8_t *g, const lu8 *kbuf, uint64_t n) {
         const lu8 *li = kbuf + 16 * c;
         if (ga >= d0 && ga + 16 <= d1) {
             const u32x4 w = *(const lu128 *)li;
-            uint4 o;
-            o.x = w.x;
-            o.y = w.y;
-            o.z = w.z;
-            o.w = w.w;
-            *(uint4 *)ga = o;
+            // global, not flat: a flat store counts in both wait counters and forces the compiler's waits to 0
+            *(__attribute__((address_space(1))) u32x4 *)ga = w;
         } else {
             // an edge granule (shared with the neighbouring block's keys): bytes [s, e) of it as at most
             // four unaligned 8 / 4 / 2 / 1-byte stores instead of a store per byte
@@ -553,11 +564,12 @@ SDB_DEV void wave_store_bytes(uint8_t *g, const lu8 *kbuf, uint64_t n) {
                 lo = (lo >> (8 * s)) | (hi << (64 - 8 * s));
                 hi >>= 8 * s;
             }
-            uint8_t *dst = (uint8_t *)ga + s;
+            typedef __attribute__((address_space(1))) uint8_t gu8;
+            gu8 *dst = (gu8 *)ga + s;
             const uint32_t n = e - s, b8 = n & 8, b4 = n & 4, b2 = n & 2;
-            typedef uint64_t u64u __attribute__((aligned(1)));
-            typedef uint32_t u32u __attribute__((aligned(1)));
-            typedef uint16_t u16u __attribute__((aligned(1)));
+            typedef __attribute__((address_space(1))) uint64_t u64u __attribute__((aligned(1)));
+            typedef __attribute__((address_space(1))) uint32_t u32u __attribute__((aligned(1)));
+            typedef __attribute__((address_space(1))) uint16_t u16u __attribute__((aligned(1)));
             if (b8) *(u64u *)dst = lo;
             const uint64_t t = b8 ? hi : lo;
             if (b4) *(u32u *)(dst + b8) = (uint32_t)t;
@@ -1035,32 +1047,28 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(kCn
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
     (void)gwave;
-    // one block ahead: its offsets and (fast path) its granules in registers
-    uint64_t k = gwave, ns = 0, ne = 0;
-    Granules pre;
-    if (k < a.nblocks) {
-        ns = a.block_off[k];
-        ne = block_end_of(a, k);
-        if (dec_fast(ns, ne)) gran_load(a, ns, ne, pre);
-    }
-    for (; k < a.nblocks; k += nwaves) {
+    // software pipeline: block k's granules landed, block k + nwaves's in flight (its offsets landed one
+    // block earlier), the offsets of block k + 2 nwaves in flight; unconditional loads and result stores,
+    // so the compiler's only vmcnt waits are the hand-overs at the end of an iteration
+    uint64_t k = gwave;
+    if (k >= a.nblocks) return;
+    const uint64_t last = a.nblocks - 1;
+    auto clampk = [&](uint64_t x) { return x < a.nblocks ? x : last; };
+    uint64_t s = a.block_off[k], e = block_end_of(a, k);
+    uint64_t s1 = a.block_off[clampk(k + nwaves)], e1 = block_end_of(a, clampk(k + nwaves));
+    Granules cur;
+    gran_load_u(a, s, e, cur);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the pipeline starts with nothing in flight
+    for (;;) {
+        Granules nxt;
+        gran_load_u(a, s1, e1, nxt);
+        const uint64_t k2 = clampk(k + 2 * nwaves);
+        const uint64_t s2 = a.block_off[k2], e2 = block_end_of(a, k2);
         DEC_T(t0);
-        const uint64_t s = ns, e = ne;
-        const Granules cur = pre;
-        if (k + nwaves < a.nblocks) {
-            ns = a.block_off[k + nwaves];
-            ne = block_end_of(a, k + nwaves);
-            if (dec_fast(ns, ne)) gran_load(a, ns, ne, pre);
-        }
         Tally t{0, 0, 0, false};
-        if (!dec_fast(s, e)) {
-            if (lane_id() == 0) a.flag[k] = kFlagBig;
-            continue;
-        }
-        if (lane_id() == 0) a.rcnt[k] = ~0ull;  // row positions not recorded (tally_v2_fast overwrites)
-        {
-                        // slicing-by-8 CRC: the pass is VALU-bound, and the bank-replicated byte table costs twice the
-            // VALU per byte for its conflict-free lookups (515 vs 479 us on configs[2])
+        const bool fast = dec_fast(s, e);
+        uint64_t rcv = ~0ull;  // per-region row counts when the rows are recorded (tally_v2_spec / _fast)
+        if (fast) {
             // fail-fast: the emit pass verifies the checksums (a block that fails here is checked now, so a
             // corrupt block reports CHECKSUM_MISMATCH before anything its rows would raise)
             const LdsBlockView v = stage_lds(a, s, e, img, !a.fail_fast, &cur);
@@ -1068,8 +1076,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(kCn
             t.status = v.status;
             if (!v.status) {
                 if (a.version == 1) t = tally_v1(v);
-                else if (!tally_v2_spec(v, t, a.rowpos + 128 * k, a.rcnt + k) &&
-                         !tally_v2_fast(v, t, a.rowpos + 128 * k, a.rcnt + k))
+                else if (!tally_v2_spec(v, t, a.rowpos + 128 * k, &rcv) && !tally_v2_fast(v, t, a.rowpos + 128 * k, &rcv))
                     t = tally_v2(v);
                 if (a.descending && a.version == 2) desc_rule(v.count, t);
             }
@@ -1079,11 +1086,32 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(kCn
             DEC_ACC(0, 0, t1 - t0);
             DEC_ACC(0, 1, t2 - t1);
             DEC_ACC(0, 3, 1);
+            wave_sync_d();
         }
+        // the block's results: every lane stores lane 0's values (one write per address), unconditionally
+        const int st = __builtin_amdgcn_readfirstlane(t.status);
+        const uint64_t ent = wave_readlane(t.entries, 0), kb = wave_readlane(t.key_bytes, 0);
+        const bool seq = __builtin_amdgcn_readfirstlane((int)t.sequential) != 0;
+        rcv = wave_readlane(rcv, 0);  // (the tally functions set it in lane 0)
         uint8_t gen = kFlagGen;
-        if (lane_id() == 0 && a.version == 2 && !t.sequential && t.key_bytes + 16 <= kRowTmp && a.rcnt[k] != ~0ull) gen = 0;
-        count_result(a, k, t, gen);
+        if (fast && a.version == 2 && !seq && kb + 16 <= kRowTmp && rcv != ~0ull) gen = 0;
+        a.rcnt[k] = rcv;
+        a.cnt[k] = st || !fast ? 0 : ent;
+        a.kbytes[k] = st || !fast ? 0 : kb;
+        a.flag[k] = !fast ? kFlagBig : st ? kFlagBad : (uint8_t)((seq ? kFlagSeq : 0) | gen);
+        if (st && fast && lane_id() == 0) {
+            atomicMin(a.err, (unsigned long long)((k << 8) | (uint64_t)st));
+            unsigned long long slot = atomicAdd(a.nbad, 1ull);
+            if (slot < a.bad_cap) a.bad_block[slot] = (uint32_t)k;
+        }
         wave_sync_d();
+        k += nwaves;
+        if (k >= a.nblocks) break;
+        cur = nxt;
+        s = s1;
+        e = e1;
+        s1 = s2;
+        e1 = e2;
     }
 }
 
@@ -1591,87 +1619,91 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
     if (tot_ent > a.out.cap_entries || tot_kb > a.out.key_arena_cap) run = false;
     a.dn = tot_ent;
     a.dkb = tot_kb;
-    // one block ahead: its offsets (scalar loads: these arrays are read-only here) and, fast path, its
-    // granules in registers, so the block's HBM latency overlaps the previous block's work
-    typedef const __attribute__((address_space(4))) uint64_t *cu64;
+    // Software pipeline (as k_dec_count): block k's granules, scan results / flag / row count and row
+    // positions landed; block k + nwaves's granules, metadata and row positions in flight, with the
+    // offsets of block k + 2 nwaves.  The metadata come in ONE vector load (lane j: 32-bit word j of
+    // the block's scan results, row count, flag word and the offsets two blocks ahead), every load is
+    // unconditional (clamped block indices), so the compiler's only vmcnt waits are the hand-overs.
+    if (!(run || ff) || gwave >= a.nblocks) return;
     const bool small = a.small != 0;
-    auto off_s = [&](uint64_t kk) { return ((cu64)a.block_off)[kk]; };
-    auto off_e = [&](uint64_t kk) { return a.block_end ? ((cu64)a.block_end)[kk] : ((cu64)a.block_off)[kk + 1]; };
-    // the per-block scan results, flag and row counts (scalar loads) and the recorded row positions
-    // (one dword per lane, loaded whether or not the block recorded them) are fetched one block ahead
-    // with its granules, so no block starts on a dependent HBM round trip
-    struct Meta {
-        uint64_t ent0, ent1, kb0, kb1, rcw;
-        uint32_t fw;  // the dword of the flag array holding this block's flag
-        SDB_DEV bool gen(uint64_t kk) const { return ((fw >> (8 * (kk & 3))) & kFlagGen) != 0; }
+    const uint64_t lastk = a.nblocks - 1;
+    auto clampk = [&](uint64_t x) { return x < a.nblocks ? x : lastk; };
+    auto gather = [&](uint64_t kn, uint64_t k2) -> uint32_t {
+        const uint32_t *p = (const uint32_t *)(a.block_off + k2);  // lanes 11, 12 (and lanes >= 15: unused)
+        if (l < 4) p = (const uint32_t *)(a.ent_start + kn) + l;
+        else if (l < 8) p = (const uint32_t *)(a.key_start + kn) + (l - 4);
+        else if (l < 10) p = (const uint32_t *)(a.rcnt + kn) + (l - 8);
+        else if (l == 10) p = (const uint32_t *)(a.flag + (kn & ~3ull));  // 256-byte aligned array
+        else if (l == 12) p = (const uint32_t *)(a.block_off + k2) + 1;
+        else if (l == 13 || l == 14)
+            p = (const uint32_t *)(a.block_end ? a.block_end + k2 : a.block_off + k2 + 1) + (l - 13);
+        return *p;
     };
-    typedef const __attribute__((address_space(4))) uint32_t *cu32;
-    auto meta_load = [&](uint64_t kk, Meta &m) {
-        if (kk >= a.nblocks) return;
-        m.ent0 = small ? s_ent0 : ((cu64)a.ent_start)[kk];
-        m.ent1 = small ? s_ent1 : ((cu64)a.ent_start)[kk + 1];
-        m.kb0 = small ? s_kb0 : ((cu64)a.key_start)[kk];
-        m.kb1 = small ? s_kb1 : ((cu64)a.key_start)[kk + 1];
-        m.fw = ((cu32)a.flag)[kk >> 2];  // the flag array is 256-byte aligned (decode_workspace_layout)
-        m.rcw = ((cu64)a.rcnt)[kk];
+    auto u64_at = [](uint32_t g, int lane) {
+        return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)g, lane) |
+               ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)g, lane + 1) << 32);
     };
     auto rowpos_load = [&](uint64_t kk) -> uint32_t { return ((const uint32_t *)(a.rowpos + 128 * kk))[l]; };
-    uint64_t k = gwave, ns = 0, ne = 0;
-    Granules pre;
-    Meta m1{};
-    uint32_t rp1 = 0;
-    if ((run || ff) && k < a.nblocks) {
-        ns = off_s(k);
-        ne = off_e(k);
-        if (dec_fast(ns, ne)) gran_load(a, ns, ne, pre);
-        rp1 = rowpos_load(k);
-        meta_load(k, m1);
-    }
-    for (; (run || ff) && k < a.nblocks; k += nwaves) {
-        const uint64_t s = ns, e = ne;
-        const Granules cur = pre;
-        const Meta m = m1;
-        const uint32_t rp = rp1;
-        if (k + nwaves < a.nblocks) {
-            ns = off_s(k + nwaves);
-            ne = off_e(k + nwaves);
-            if (dec_fast(ns, ne)) gran_load(a, ns, ne, pre);
-            rp1 = rowpos_load(k + nwaves);
-            meta_load(k + nwaves, m1);
-        }
-        const uint64_t ent0 = m.ent0;
-        if (run && l == 0) a.out.block_entry_start[k] = ent0;
-        const uint32_t fb = (m.fw >> (8 * (k & 3))) & 0xFF;
-        const bool skip = m.ent1 == ent0 || (fb & kFlagGen);  // nothing to emit, or k_dec_emit_gen's
-        // fail-fast: every block of one wave image the count pass did not reject is checked here
-        if ((skip || !run) && !(ff && !(fb & kFlagBad) && dec_fast(s, e))) continue;
-        const uint64_t kb0 = m.kb0;
-        DEC_T(t0);
-        const LdsBlockView v = stage_lds(a, s, e, img, ff, &cur);
-        if (v.status) {  // fail-fast: a checksum mismatch (the count pass accepted the rest)
-            if (l == 0) {
-                atomicMin(a.err, (unsigned long long)((k << 8) | (uint64_t)v.status));
-                const unsigned long long slot = atomicAdd(a.nbad, 1ull);
-                if (slot < a.bad_cap) a.bad_block[slot] = (uint32_t)k;
+    uint64_t k = gwave;
+    uint64_t s = a.block_off[k], e = block_end_of(a, k);
+    uint32_t gcur = gather(k, clampk(k + nwaves));
+    uint32_t rp = rowpos_load(k);
+    Granules cur;
+    gran_load_u(a, s, e, cur);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the pipeline starts with nothing in flight
+    uint64_t s1 = u64_at(gcur, 11), e1 = u64_at(gcur, 13);
+    for (;;) {
+        // block k's granules -> its LDS image first, so their registers take the next block's
+        if (dec_fast(s, e)) gran_store(s, e, cur, img);
+        const uint64_t kn = clampk(k + nwaves), k2 = clampk(k + 2 * nwaves);
+        gran_load_u(a, s1, e1, cur);
+        const uint32_t gnx = gather(kn, k2);
+        const uint32_t rpn = rowpos_load(kn);
+        do {
+            const uint64_t ent0 = small ? s_ent0 : u64_at(gcur, 0), ent1 = small ? s_ent1 : u64_at(gcur, 2);
+            const uint64_t kb0 = small ? s_kb0 : u64_at(gcur, 4), kb1 = small ? s_kb1 : u64_at(gcur, 6);
+            const uint64_t rcw = u64_at(gcur, 8);
+            const uint32_t fw = (uint32_t)__builtin_amdgcn_readlane((int)gcur, 10);
+            if (run && l == 0) a.out.block_entry_start[k] = ent0;
+            const uint32_t fb = (fw >> (8 * (k & 3))) & 0xFF;
+            const bool skip = ent1 == ent0 || (fb & kFlagGen);  // nothing to emit, or k_dec_emit_gen's
+            // fail-fast: every block of one wave image the count pass did not reject is checked here
+            if ((skip || !run) && !(ff && !(fb & kFlagBad) && dec_fast(s, e))) break;
+            DEC_T(t0);
+            const LdsBlockView v = stage_lds(a, s, e, img, ff, nullptr, true);
+            if (v.status) {  // fail-fast: a checksum mismatch (the count pass accepted the rest)
+                if (l == 0) {
+                    atomicMin(a.err, (unsigned long long)((k << 8) | (uint64_t)v.status));
+                    const unsigned long long slot = atomicAdd(a.nbad, 1ull);
+                    if (slot < a.bad_cap) a.bad_block[slot] = (uint32_t)k;
+                }
+                break;
             }
-            continue;
-        }
-        if (skip || !run) continue;
-        DEC_T(t1);
-        ((lu32 *)(kbuf + kRowTmp))[l] = rp;
-        wave_sync_d();
-        emit_v2_rows(a, v, m.rcw, (const lu16 *)(kbuf + kRowTmp), ent0, kb0, s, kbuf);
-        DEC_T(t2);
-        if (!a.descending) {  // (descending: each lane stored its keys)
+            if (skip || !run) break;
+            DEC_T(t1);
+            ((lu32 *)(kbuf + kRowTmp))[l] = rp;
             wave_sync_d();
-            wave_store_bytes(a.out.key_arena + kb0, kbuf, m.kb1 - kb0);
-        }
-        DEC_T(t3);
-        DEC_ACC(1, 0, t1 - t0);
-        DEC_ACC(1, 1, t2 - t1);
-        DEC_ACC(1, 2, t3 - t2);
-        DEC_ACC(1, 3, 1);
+            emit_v2_rows(a, v, rcw, (const lu16 *)(kbuf + kRowTmp), ent0, kb0, s, kbuf);
+            DEC_T(t2);
+            if (!a.descending) {  // (descending: each lane stored its keys)
+                wave_sync_d();
+                wave_store_bytes(a.out.key_arena + kb0, kbuf, kb1 - kb0);
+            }
+            DEC_T(t3);
+            DEC_ACC(1, 0, t1 - t0);
+            DEC_ACC(1, 1, t2 - t1);
+            DEC_ACC(1, 2, t3 - t2);
+            DEC_ACC(1, 3, 1);
+        } while (false);
         wave_sync_d();
+        k += nwaves;
+        if (k >= a.nblocks) break;
+        gcur = gnx;
+        rp = rpn;
+        s = s1;
+        e = e1;
+        s1 = u64_at(gnx, 11);
+        e1 = u64_at(gnx, 13);
     }
 }
 

@@ -61,9 +61,71 @@ __global__ __launch_bounds__(256) void k_diag_copy(u32x4 *__restrict__ dst, cons
     for (; i < n16; i += stride) dst[i] = src[i];
 }
 
+// Copy-ceiling probes (mode): 1 plain loads / stores in the grid-stride pattern of k_diag_copy; 2 each wave
+// copies 4 KiB contiguous per step (4 x 16 B per lane, loads before stores); 3 read only (a xor-reduction
+// per thread, stored once); 4 write only.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_diag_bw(u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (MODE == 1) {
+        uint64_t i = t;
+        for (; i + 3 * stride < n16; i += 4 * stride) {
+            const u32x4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+            dst[i] = a;
+            dst[i + stride] = b;
+            dst[i + 2 * stride] = c;
+            dst[i + 3 * stride] = d;
+        }
+        for (; i < n16; i += stride) dst[i] = src[i];
+    } else if (MODE == 2) {
+        const uint64_t w = t >> 6, nw = stride >> 6, l = t & 63;
+        for (uint64_t b = w * 256; b + 256 <= n16; b += nw * 256) {
+            const u32x4 a = src[b + l], c = src[b + 64 + l], d = src[b + 128 + l], e = src[b + 192 + l];
+            dst[b + l] = a;
+            dst[b + 64 + l] = c;
+            dst[b + 128 + l] = d;
+            dst[b + 192 + l] = e;
+        }
+    } else if (MODE == 3) {
+        u32x4 x = {0, 0, 0, 0};
+        uint64_t i = t;
+        for (; i + 3 * stride < n16; i += 4 * stride) {
+            const u32x4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+            x ^= a ^ b ^ c ^ d;
+        }
+        for (; i < n16; i += stride) x ^= src[i];
+        if (t < n16) dst[t] = x;
+    } else {
+        const u32x4 v = {(uint32_t)t, 1u, 2u, 3u};
+        for (uint64_t i = t; i < n16; i += stride) dst[i] = v;
+    }
+}
+
 }  // namespace sdb
 
 using namespace sdb;
+
+extern "C" sdb_status sdb_diag_bw(void *dst, const void *src, uint64_t bytes, int mode, int wg_per_cu, void *stream) {
+    if (!dst || !src || (bytes & 4095) || (((uintptr_t)dst | (uintptr_t)src) & 15) || mode < 0 || mode > 4 || wg_per_cu < 1)
+        return SDB_INVALID_ARGUMENT;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const dim3 g((uint32_t)(wg_per_cu * cus)), b(256);
+    hipStream_t st = (hipStream_t)stream;
+    u32x4 *d = (u32x4 *)dst;
+    const u32x4 *s = (const u32x4 *)src;
+    const uint64_t n = bytes / 16;
+    switch (mode) {
+        case 0: hipLaunchKernelGGL(k_diag_copy, g, b, 0, st, d, s, n); break;
+        case 1: hipLaunchKernelGGL(k_diag_bw<1>, g, b, 0, st, d, s, n); break;
+        case 2: hipLaunchKernelGGL(k_diag_bw<2>, g, b, 0, st, d, s, n); break;
+        case 3: hipLaunchKernelGGL(k_diag_bw<3>, g, b, 0, st, d, s, n); break;
+        default: hipLaunchKernelGGL(k_diag_bw<4>, g, b, 0, st, d, s, n); break;
+    }
+    return hipGetLastError() == hipSuccess ? SDB_OK : SDB_DEVICE_ERROR;
+}
 
 extern "C" sdb_status sdb_diag_copy(void *dst, const void *src, uint64_t bytes, void *stream) {
     if (!dst || !src || (bytes & 15) || (((uintptr_t)dst | (uintptr_t)src) & 15)) return SDB_INVALID_ARGUMENT;

@@ -1721,10 +1721,6 @@ SDB_DEV uint32_t write_row_hdr_trailer(lu8 *dst, const RowInfo &r, uint64_t seq,
     return h;
 }
 
-// Everything one block needs from HBM, loaded into registers one block ahead (software pipeline):
-// the block's value / key granules (lane l holds granules l, 64 + l, ...) and the row metadata
-// (lane = row).  Plain loads only: the compute phase of the current block issues no global load,
-// so the compiler's in-order vmcnt waits never drain the prefetch early.
 // A block's prefetched data (16-byte granules of its values and keys, lane l holding granules l, l + 64,
 // ...) and row metadata (lane = row).
 struct EmitData {
