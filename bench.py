@@ -12,11 +12,12 @@ timing barrier and the max / sum of scalars.  `--job-ssts 64` runs configs[4] as
 scaling); `--batch 1` is the single-SST configs[1] shape.  The single-SST latency (sdb_encode_sst,
 one SST per launch sequence) is reported beside the headline as `single_sst`.
 
-`--streams S` (default 1) runs S such builders per GPU concurrently, each on its own HIP stream with its
-own workspace and outputs (step i on stream i mod S).  A kernel trace of two builders (DESIGN.md §5,
-profiles/r4_two_builders_trace.txt) shows why one is the default: k_emit takes every CU's VGPRs and most
-of its LDS, so nothing co-resides with it; the two builders fall into lock-step (both preps, then both
-emits one after the other) and lose to the same sequences back to back on one stream.
+`--streams S` (default 2) runs S such builders per GPU concurrently, each on its own HIP stream with its
+own workspace and outputs (step i on stream i mod S), after sdb_set_concurrent_builders(S): each builder's
+persistent block assembly (k_emit) then takes 1/S of the CUs, and the other builder's latency-bound
+segmentation kernels run on the rest.  With k_emit on every CU (round 4) nothing co-resided with it and two
+builders fell into lock-step (profiles/r4_two_builders_trace.txt); at 128 of 256 CUs two builders beat one
+by ~7 %.  The same sequences back to back on one stream are reported as `one_stream`.
 
   python bench.py [--gpus N --steps K --warmup W --batch B]   (N > 1: spawns N ranks itself)
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -48,8 +49,9 @@ def parse():
     p.add_argument("--steps", type=int, default=2200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch", type=int, default=8, help="SSTs per GPU per step (one sdb_encode_ssts call)")
-    p.add_argument("--streams", type=int, default=1,
-                   help="concurrent builders per GPU: step i runs on stream i mod S (its own workspace and outputs)")
+    p.add_argument("--streams", type=int, default=2,
+                   help="concurrent builders per GPU: step i runs on stream i mod S (its own workspace and outputs); "
+                        "sdb_set_concurrent_builders(S) gives each builder's block assembly 1/S of the CUs")
     p.add_argument("--job-ssts", type=int, default=0,
                    help="configs[4] fixed job: J distinct SSTs over all ranks (SST j -> rank j mod N), one pass per step")
     p.add_argument("--ssts", type=int, default=0, help="distinct resident input SSTs per rank (0: 2 x batch)")
@@ -301,6 +303,7 @@ def main():
     # the side measurements run BEFORE the warmup and the timed region, so the timed steps start on a GPU
     # that has been busy for a while (not straight after the idle of the host-side oracle check)
     # per-kernel pass: HIP events recorded around each kernel on the encode stream (sdb_diag_*)
+    lib.sdb_set_concurrent_builders(1)  # the side measurements: one builder on the whole chip
     lib.sdb_diag_enable_stage_timing(1)
     for i in range(args.stage_steps):
         step(i, one_stream=True)
@@ -350,6 +353,7 @@ def main():
 
     copy_gbs = measured_copy_gbs(dev)
 
+    lib.sdb_set_concurrent_builders(len(streams))  # the timed region: S builders in flight
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()

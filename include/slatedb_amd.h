@@ -191,6 +191,12 @@ uint64_t sdb_encode_ssts_workspace_bytes(uint32_t count, const sdb_kv_batch *bat
 sdb_status sdb_encode_ssts(uint32_t count, const sdb_kv_batch *batches, const sdb_sst_params *params,
                            const sdb_sst_out *outs, void *workspace, uint64_t workspace_bytes,
                            void *stream);
+/* Scheduling hint: the caller keeps `builders` encode launch sequences (sdb_encode_sst / _ssts on distinct
+ * streams, e.g. the concurrent SST writers of compactions and flushes) in flight on the current device.
+ * The block-assembly kernel then takes 1/builders of the CUs (at least 1 workgroup), so one sequence's
+ * segmentation kernels run on the CUs another sequence's assembly leaves free (1, the default: every
+ * CU).  Process-wide per device; results do not depend on it.  SDB_INVALID_ARGUMENT for 0. */
+sdb_status sdb_set_concurrent_builders(uint32_t builders);
 
 /* Bloom bitmap over n keys (BloomFilterBuilder with whole-key filtering, filter.rs:40-90).
  * bitmap must hold sdb_bloom_filter_bytes(n, bpk) bytes and be 4-byte aligned (the build stores

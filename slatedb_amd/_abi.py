@@ -281,6 +281,7 @@ SIGNATURES = {
     "sdb_diag_mfma_i8": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "sdb_diag_copy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
     "sdb_diag_bw": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_int, C.c_void_p]),
+    "sdb_set_concurrent_builders": (C.c_int, [C.c_uint32]),
     "sdb_compress_workspace_bytes": (C.c_uint64, [C.c_uint64, C.c_uint64]),
     "sdb_compress_blocks": (C.c_int, [C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
                                       C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
