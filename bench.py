@@ -39,7 +39,7 @@ sys.path.insert(0, ROOT)
 from slatedb_amd import _abi, datasets, job, runtime  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s); the box's STREAM copy: DESIGN.md §5
-PMC_FILES = ("r4_pmc_traffic.json", "r3_pmc_traffic.json", "r2_pmc_traffic.json")  # newest first
+PMC_FILES = ("r5_pmc_traffic.json", "r4_pmc_traffic.json", "r3_pmc_traffic.json", "r2_pmc_traffic.json")  # newest first
 PMC_FILE = PMC_FILES[0]
 
 
