@@ -1325,6 +1325,107 @@ __global__ __launch_bounds__(kAnchorThreads) void k_anchor(SstSet P) {
             }
             __syncthreads();
         }
+        // tables over the LDS (long SSTs: a 256 MiB compaction output has ~565 chunks): the group tables in
+        // LDS, and each group's chunk tables staged into one of kSW per-wave buffers when a wave composes
+        // that group, then again when it walks the group's anchors -- every chunk table is read twice, in
+        // bulk, instead of one dependent HBM load per chunk on a single lane
+        constexpr uint32_t kSW = 8;
+        const uint64_t s_gex = 0, s_gcn = (4 * ng + 15) & ~15ull, s_gby = s_gcn + ((4 * ng + 15) & ~15ull);
+        const uint64_t s_gent = s_gby + 8 * ng, s_gb64 = s_gent + 8ull * ngroups;
+        const uint64_t s_buf = (s_gb64 + 8ull * ngroups + 15) & ~15ull;
+        const uint64_t wcap = (uint64_t)G * W, wbytes = (wcap * 12 + 15) & ~15ull;
+        const bool streamed = !in_lds && s_buf + kSW * wbytes <= kAnchorLds;
+        if (streamed) {
+            uint32_t *sg_ex = (uint32_t *)(smem + s_gex), *sg_cn = (uint32_t *)(smem + s_gcn);
+            uint64_t *sg_by = (uint64_t *)(smem + s_gby), *sg_b64 = (uint64_t *)(smem + s_gb64);
+            uint32_t *sg_ent = (uint32_t *)(smem + s_gent);
+            const uint32_t wv = tid >> 6, ln = tid & 63;
+            uint8_t *wb = smem + s_buf + wv * wbytes;
+            uint64_t *bb = (uint64_t *)wb;
+            uint16_t *bx = (uint16_t *)(wb + 8 * wcap), *bc = bx + wcap;
+            // group q's chunk tables -> this wave's buffer (entry (k - qG) W + o), eight loads per lane in flight
+            auto stage_group = [&](uint32_t q) {
+                const uint32_t k0 = q * G, k1 = (q + 1) * G < K ? (q + 1) * G : K, ne = (k1 - k0) * W;
+                constexpr uint32_t kU = 8;
+                for (uint32_t i0 = 0; i0 < ne; i0 += 64 * kU) {
+                    uint32_t x[kU], c[kU];
+                    uint64_t b[kU];
+#pragma unroll
+                    for (uint32_t u = 0; u < kU; u++) {
+                        const uint32_t i = i0 + 64 * u + ln;
+                        x[u] = c[u] = 0;
+                        b[u] = 0;
+                        if (i < ne) tab_hbm(k0 + i / W, i % W, x[u], c[u], b[u]);
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < kU; u++) {
+                        const uint32_t i = i0 + 64 * u + ln;
+                        if (i < ne) {
+                            bx[i] = (uint16_t)x[u];
+                            bc[i] = (uint16_t)c[u];
+                            bb[i] = b[u];
+                        }
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the wave's LDS writes are done
+            };
+            if (wv < kSW) {
+                for (uint32_t q = wv; q < ngroups; q += kSW) {  // group tables: lane per candidate
+                    stage_group(q);
+                    const uint32_t nk = ((q + 1) * G < K ? (q + 1) * G : K) - q * G;
+                    for (uint32_t o = ln; o < W; o += 64) {
+                        uint32_t e = o, c = 0;
+                        uint64_t b = 0;
+                        for (uint32_t j = 0; j < nk; j++) {
+                            const uint32_t i = j * W + e;
+                            c += bc[i];
+                            b += bb[i];
+                            e = bx[i];
+                        }
+                        sg_ex[q * W + o] = e;
+                        sg_cn[q * W + o] = c;
+                        sg_by[q * W + o] = b;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_s_waitcnt(0xC07F);
+                }
+            }
+            __syncthreads();
+            if (tid == 0) {  // the groups from entry 0
+                uint32_t e = 0;
+                for (uint32_t q = 0; q < ngroups; q++) {
+                    sg_ent[2 * q] = e;
+                    sg_ent[2 * q + 1] = (uint32_t)tb;
+                    sg_b64[q] = ty;
+                    const uint32_t i = q * W + e;
+                    tb += sg_cn[i];
+                    ty += sg_by[i];
+                    e = sg_ex[i];
+                }
+            }
+            __syncthreads();
+            if (wv < kSW) {
+                for (uint32_t q = wv; q < ngroups; q += kSW) {  // each group's chunks from its entry
+                    stage_group(q);
+                    if (ln == 0) {
+                        uint32_t e = sg_ent[2 * q];
+                        uint64_t blk = sg_ent[2 * q + 1], by = sg_b64[q];
+                        const uint32_t k0 = q * G, k1 = (q + 1) * G < K ? (q + 1) * G : K;
+                        for (uint32_t k = k0; k < k1; k++) {
+                            a.anchor_e[k] = (uint32_t)((uint64_t)k * kChunk + e);
+                            a.anchor_blk[k] = (uint32_t)blk;
+                            a.anchor_byte[k] = by;
+                            const uint32_t i = (k - k0) * W + e;
+                            blk += bc[i];
+                            by += bb[i];
+                            e = bx[i];
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+        }
         // group tables: lane per (group, candidate)
         for (uint64_t i = tid; i < ng && in_lds; i += nt) {
             const uint32_t q = (uint32_t)(i / W), k1 = (q + 1) * G < K ? (q + 1) * G : K;
@@ -1343,7 +1444,7 @@ __global__ __launch_bounds__(kAnchorThreads) void k_anchor(SstSet P) {
             g_by[i] = b;
         }
         __syncthreads();
-        if (tid == 0) {  // the groups from entry 0
+        if (tid == 0 && !streamed) {  // the groups from entry 0
             uint32_t e = 0;
             for (uint32_t q = 0; q < ngroups; q++) {
                 if (in_lds) {
