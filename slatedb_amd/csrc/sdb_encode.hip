@@ -1329,72 +1329,90 @@ __global__ __launch_bounds__(kAnchorThreads) void k_anchor(SstSet P) {
         // LDS, and each group's chunk tables staged into one of kSW per-wave buffers when a wave composes
         // that group, then again when it walks the group's anchors -- every chunk table is read twice, in
         // bulk, instead of one dependent HBM load per chunk on a single lane
-        constexpr uint32_t kSW = 8;
-        const uint64_t s_gex = 0, s_gcn = (4 * ng + 15) & ~15ull, s_gby = s_gcn + ((4 * ng + 15) & ~15ull);
-        const uint64_t s_gent = s_gby + 8 * ng, s_gb64 = s_gent + 8ull * ngroups;
-        const uint64_t s_buf = (s_gb64 + 8ull * ngroups + 15) & ~15ull;
-        const uint64_t wcap = (uint64_t)G * W, wbytes = (wcap * 12 + 15) & ~15ull;
-        const bool streamed = !in_lds && s_buf + kSW * wbytes <= kAnchorLds;
+        // (its own group size Gs <= G, chosen so that the group tables and a buffer per wave fit beside each
+        // other: all 16 waves compose / walk groups at once)
+        constexpr uint32_t kSW = kAnchorThreads / 64;
+        uint32_t Gs = G, ngs = ngroups;
+        uint64_t s_gcn = 0, s_gby = 0, s_gent = 0, s_gb64 = 0, s_buf = 0, wcap = 0, wbytes = 0;
+        bool streamed = false;
+        for (; !in_lds && Gs >= 1; Gs--) {
+            ngs = (K + Gs - 1) / Gs;
+            const uint64_t ngw = (uint64_t)ngs * W;
+            s_gcn = (4 * ngw + 15) & ~15ull;
+            s_gby = s_gcn + ((4 * ngw + 15) & ~15ull);
+            s_gent = s_gby + 8 * ngw;
+            s_gb64 = s_gent + 8ull * ngs;
+            s_buf = (s_gb64 + 8ull * ngs + 15) & ~15ull;
+            wcap = (uint64_t)Gs * W;
+            wbytes = (wcap * 12 + 15) & ~15ull;
+            if (s_buf + kSW * wbytes <= kAnchorLds) {
+                streamed = true;
+                break;
+            }
+        }
         if (streamed) {
-            uint32_t *sg_ex = (uint32_t *)(smem + s_gex), *sg_cn = (uint32_t *)(smem + s_gcn);
+            uint32_t *sg_ex = (uint32_t *)smem, *sg_cn = (uint32_t *)(smem + s_gcn);
             uint64_t *sg_by = (uint64_t *)(smem + s_gby), *sg_b64 = (uint64_t *)(smem + s_gb64);
             uint32_t *sg_ent = (uint32_t *)(smem + s_gent);
             const uint32_t wv = tid >> 6, ln = tid & 63;
             uint8_t *wb = smem + s_buf + wv * wbytes;
             uint64_t *bb = (uint64_t *)wb;
             uint16_t *bx = (uint16_t *)(wb + 8 * wcap), *bc = bx + wcap;
-            // group q's chunk tables -> this wave's buffer (entry (k - qG) W + o), eight loads per lane in flight
+            // group q's chunk tables -> this wave's buffer (entry (k - q Gs) W + o), eight loads per lane in
+            // flight, unconditional (clamped to the group's last entry)
             auto stage_group = [&](uint32_t q) {
-                const uint32_t k0 = q * G, k1 = (q + 1) * G < K ? (q + 1) * G : K, ne = (k1 - k0) * W;
+                const uint32_t k0 = q * Gs, k1 = (q + 1) * Gs < K ? (q + 1) * Gs : K, ne = (k1 - k0) * W;
                 constexpr uint32_t kU = 8;
                 for (uint32_t i0 = 0; i0 < ne; i0 += 64 * kU) {
-                    uint32_t x[kU], c[kU];
-                    uint64_t b[kU];
+                    uint32_t te[kU], tc[kU];
+                    uint64_t tbv[kU];
 #pragma unroll
                     for (uint32_t u = 0; u < kU; u++) {
-                        const uint32_t i = i0 + 64 * u + ln;
-                        x[u] = c[u] = 0;
-                        b[u] = 0;
-                        if (i < ne) tab_hbm(k0 + i / W, i % W, x[u], c[u], b[u]);
+                        const uint32_t i = i0 + 64 * u + ln, ic = i < ne ? i : ne - 1;
+                        const uint32_t kq = ic / W, o = ic - kq * W;
+                        const uint64_t t = (uint64_t)(k0 + kq) * a.seg_look + o;
+                        te[u] = a.tab_exit[t];
+                        tc[u] = a.tab_cnt[t];
+                        tbv[u] = a.tab_bytes[t];
                     }
 #pragma unroll
                     for (uint32_t u = 0; u < kU; u++) {
                         const uint32_t i = i0 + 64 * u + ln;
-                        if (i < ne) {
-                            bx[i] = (uint16_t)x[u];
-                            bc[i] = (uint16_t)c[u];
-                            bb[i] = b[u];
-                        }
+                        if (i >= ne) continue;
+                        const uint32_t kq = i / W, o = i - kq * W;
+                        const uint64_t cs = (uint64_t)(k0 + kq) * kChunk, ce = cs + kChunk < a.n ? cs + kChunk : a.n;
+                        const bool in = cs + o < ce;  // as tab_hbm
+                        bx[i] = (uint16_t)(in ? (te[u] >= ce && te[u] - ce < W ? (uint32_t)(te[u] - ce) : W - 1) : 0u);
+                        bc[i] = (uint16_t)(in ? tc[u] : 0u);
+                        bb[i] = in ? tbv[u] : 0ull;
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the wave's LDS writes are done
             };
-            if (wv < kSW) {
-                for (uint32_t q = wv; q < ngroups; q += kSW) {  // group tables: lane per candidate
-                    stage_group(q);
-                    const uint32_t nk = ((q + 1) * G < K ? (q + 1) * G : K) - q * G;
-                    for (uint32_t o = ln; o < W; o += 64) {
-                        uint32_t e = o, c = 0;
-                        uint64_t b = 0;
-                        for (uint32_t j = 0; j < nk; j++) {
-                            const uint32_t i = j * W + e;
-                            c += bc[i];
-                            b += bb[i];
-                            e = bx[i];
-                        }
-                        sg_ex[q * W + o] = e;
-                        sg_cn[q * W + o] = c;
-                        sg_by[q * W + o] = b;
+            for (uint32_t q = wv; q < ngs; q += kSW) {  // group tables: lane per candidate
+                stage_group(q);
+                const uint32_t nk = ((q + 1) * Gs < K ? (q + 1) * Gs : K) - q * Gs;
+                for (uint32_t o = ln; o < W; o += 64) {
+                    uint32_t e = o, c = 0;
+                    uint64_t b = 0;
+                    for (uint32_t j = 0; j < nk; j++) {
+                        const uint32_t i = j * W + e;
+                        c += bc[i];
+                        b += bb[i];
+                        e = bx[i];
                     }
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_s_waitcnt(0xC07F);
+                    sg_ex[q * W + o] = e;
+                    sg_cn[q * W + o] = c;
+                    sg_by[q * W + o] = b;
                 }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_s_waitcnt(0xC07F);
             }
             __syncthreads();
             if (tid == 0) {  // the groups from entry 0
                 uint32_t e = 0;
-                for (uint32_t q = 0; q < ngroups; q++) {
+                for (uint32_t q = 0; q < ngs; q++) {
                     sg_ent[2 * q] = e;
                     sg_ent[2 * q + 1] = (uint32_t)tb;
                     sg_b64[q] = ty;
@@ -1405,25 +1423,23 @@ __global__ __launch_bounds__(kAnchorThreads) void k_anchor(SstSet P) {
                 }
             }
             __syncthreads();
-            if (wv < kSW) {
-                for (uint32_t q = wv; q < ngroups; q += kSW) {  // each group's chunks from its entry
-                    stage_group(q);
-                    if (ln == 0) {
-                        uint32_t e = sg_ent[2 * q];
-                        uint64_t blk = sg_ent[2 * q + 1], by = sg_b64[q];
-                        const uint32_t k0 = q * G, k1 = (q + 1) * G < K ? (q + 1) * G : K;
-                        for (uint32_t k = k0; k < k1; k++) {
-                            a.anchor_e[k] = (uint32_t)((uint64_t)k * kChunk + e);
-                            a.anchor_blk[k] = (uint32_t)blk;
-                            a.anchor_byte[k] = by;
-                            const uint32_t i = (k - k0) * W + e;
-                            blk += bc[i];
-                            by += bb[i];
-                            e = bx[i];
-                        }
+            for (uint32_t q = wv; q < ngs; q += kSW) {  // each group's chunks from its entry
+                stage_group(q);
+                if (ln == 0) {
+                    uint32_t e = sg_ent[2 * q];
+                    uint64_t blk = sg_ent[2 * q + 1], by = sg_b64[q];
+                    const uint32_t k0 = q * Gs, k1 = (q + 1) * Gs < K ? (q + 1) * Gs : K;
+                    for (uint32_t k = k0; k < k1; k++) {
+                        a.anchor_e[k] = (uint32_t)((uint64_t)k * kChunk + e);
+                        a.anchor_blk[k] = (uint32_t)blk;
+                        a.anchor_byte[k] = by;
+                        const uint32_t i = (k - k0) * W + e;
+                        blk += bc[i];
+                        by += bb[i];
+                        e = bx[i];
                     }
-                    __builtin_amdgcn_wave_barrier();
                 }
+                __builtin_amdgcn_wave_barrier();
             }
         }
         // group tables: lane per (group, candidate)
