@@ -333,6 +333,21 @@ sdb_status sdb_decompress_plan(uint32_t codec, const uint8_t *blocks, const uint
 sdb_status sdb_decompress_blocks(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
                                  uint8_t *out, uint64_t out_cap, const uint64_t *out_start, uint64_t *out_end,
                                  uint64_t *err, void *stream);
+/* Both steps without a host synchronisation between them (out sized by the caller up front).  For
+ * SDB_CODEC_ZLIB, whose plan is a whole inflate, each block is inflated once into a slot of slot_bytes
+ * (out_start[k] = k * slot_bytes, 8 <= slot_bytes <= 4 GiB, out_cap >= nblocks * slot_bytes); the blocks
+ * whose output + 4 does not fit their slot are planned and inflated again, packed from
+ * nblocks * slot_bytes on, and their out_start[k] rewritten — so out_start is not monotone and
+ * out_start[nblocks] = the bytes of out the call used.  A block past out_cap fails with
+ * SDB_INVALID_ARGUMENT as in step 2.  The other codecs ignore slot_bytes: the plan and the run back to
+ * back (out_start as step 1 writes it).  out_start / out_end / *err then mean what step 2 says, and
+ * sdb_decode_blocks_at(out, out_start, out_end, ...) decodes the run.  Workspace:
+ * sdb_decompress_once_workspace_bytes(nblocks). */
+uint64_t sdb_decompress_once_workspace_bytes(uint64_t nblocks);
+sdb_status sdb_decompress_blocks_once(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                                      uint64_t slot_bytes, uint8_t *out, uint64_t out_cap, uint64_t *out_start,
+                                      uint64_t *out_end, uint64_t *err, void *workspace, uint64_t workspace_bytes,
+                                      void *stream);
 
 /* The compressing write side: compress_and_transform (format/sst.rs:525-554) with SsTableFormat::compress
  * (format/sst.rs:557-594) for every block of an encoded data section (each Block::encode() ++ CRC32 BE, as

@@ -53,7 +53,7 @@ print('encx ${ENCX_ARGS:-}: value', d['value'], 'ms/SST', r['device_ms_per_sst']
          step compactprof 300 rocprofv3 --kernel-trace --stats -d $O/compactprof -o run --output-format csv -- python3 scripts/bench_configs.py --compact --reps 8 ;;
     codec) [ -z "$v" ] || step codectest$v 300 python3 -u -m pytest tests/test_gpu_codec.py -x -q --timeout 200 --timeout-method thread
          SDB_CODECS=${SDB_CODECS:-lz4,snappy,zlib,zstd} step codec$v 400 python3 scripts/bench_configs.py --codec --reps 3
-         grep '^{' $O/codec$v.log | cut -c1-300
+         grep "^{" $O/codec$v.log | cut -c1-520
          [ -n "$v" ] || step codecprof 400 rocprofv3 --kernel-trace --stats -d $O/codecprof -o run --output-format csv -- python3 scripts/bench_configs.py --codec --reps 3 ;;
   esac
 done

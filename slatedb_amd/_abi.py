@@ -241,6 +241,10 @@ SIGNATURES = {
                                       C.c_uint64, C.c_void_p]),
     "sdb_decompress_blocks": (C.c_int, [C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "sdb_decompress_once_workspace_bytes": (C.c_uint64, [C.c_uint64]),
+    "sdb_decompress_blocks_once": (C.c_int, [C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
+                                             C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                             C.c_void_p]),
     "sdb_sst_lookup_workspace_bytes": (C.c_uint64, [C.c_uint64, C.c_uint64]),
     "sdb_sst_lookup": (C.c_int, [C.POINTER(SstView), C.c_void_p, C.c_void_p, C.c_uint64, C.c_int32,
                                  C.POINTER(LookupOut), C.c_void_p, C.c_uint64, C.c_void_p]),

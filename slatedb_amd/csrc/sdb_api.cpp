@@ -455,6 +455,24 @@ sdb_status sdb_decompress_blocks(uint32_t codec, const uint8_t *blocks, const ui
                                  (unsigned long long *)err, S(stream)) == hipSuccess ? SDB_OK : SDB_DEVICE_ERROR;
 }
 
+uint64_t sdb_decompress_once_workspace_bytes(uint64_t nblocks) { return decompress_once_workspace_bytes(nblocks); }
+
+sdb_status sdb_decompress_blocks_once(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                                      uint64_t slot_bytes, uint8_t *out, uint64_t out_cap, uint64_t *out_start,
+                                      uint64_t *out_end, uint64_t *err, void *workspace, uint64_t workspace_bytes,
+                                      void *stream) {
+    if (!lz_codec(codec)) return SDB_INVALID_ARGUMENT;
+    if (!err || !out_start || (nblocks && (!blocks || !block_off || !out_end || (out_cap && !out)))) return SDB_INVALID_ARGUMENT;
+    if (!workspace || workspace_bytes < decompress_once_workspace_bytes(nblocks)) return SDB_INVALID_ARGUMENT;
+    if (codec == SDB_CODEC_ZLIB && (slot_bytes < 8 || slot_bytes > (1ull << 32) ||
+                                    (nblocks && out_cap / nblocks < slot_bytes)))
+        return SDB_INVALID_ARGUMENT;
+    if (!device_ok()) return SDB_DEVICE_ERROR;
+    return launch_decompress_once(codec, blocks, block_off, nblocks, slot_bytes, out, out_cap, out_start, out_end,
+                                  (unsigned long long *)err, workspace, S(stream)) == hipSuccess ? SDB_OK
+                                                                                                 : SDB_DEVICE_ERROR;
+}
+
 uint64_t sdb_compress_workspace_bytes(uint64_t nblocks, uint64_t in_bytes) {
     return compress_workspace_bytes(nblocks, in_bytes) + 256;
 }

@@ -516,4 +516,74 @@ hipError_t launch_decompress_run(uint32_t codec, const uint8_t *blocks, const ui
     return hipGetLastError();
 }
 
+// ---- decode once: no host synchronisation between sizing and decompressing --------------------------------
+// zlib's plan is a whole inflate (the stream does not record its length), so decode-once inflates every block
+// once into a fixed slot of slot_bytes (out_start[k] = k * slot_bytes), lists the blocks whose output overflowed
+// their slot, and only those are planned and inflated again, packed after the slots.  The other codecs' plans
+// read a length header, so for them it is the plan and the run back to back on the stream.
+bool zl_once_supported();
+hipError_t launch_zl_once_slots(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks, const uint32_t *list,
+                                const unsigned long long *nlist, uint64_t *slot, hipStream_t st);
+hipError_t launch_zl_once_run(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks, uint8_t *out,
+                              uint64_t out_cap, const uint64_t *out_start, uint64_t *out_end, unsigned long long *err,
+                              const uint32_t *list, const unsigned long long *nlist, uint32_t *ovf_list,
+                              unsigned long long *ovf_count, hipStream_t st);
+
+uint64_t decompress_once_workspace_bytes(uint64_t nblocks) {
+    return decompress_workspace_bytes(nblocks) + 8 * (nblocks + 2) + 4 * (nblocks + 2) + 512;
+}
+
+__global__ void k_zo_init(uint64_t *out_start, uint64_t nblocks, uint64_t slot_bytes, unsigned long long *err,
+                          unsigned long long *nlist) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= nblocks) out_start[i] = i * slot_bytes;
+    if (i == 0) {
+        *err = ~0ull;
+        *nlist = 0;
+    }
+}
+
+// pos: the overflow list's exclusive scan (nblocks + 1 values, zero past the list) -> absolute positions after
+// the slots; the listed blocks' out_start, and out_start[nblocks] = the bytes of out the call used
+__global__ void k_zo_fix(uint64_t *pos, uint64_t *out_start, uint64_t nblocks, uint64_t base, const uint32_t *list,
+                         const unsigned long long *nlist) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > nblocks) return;
+    const uint64_t n = *nlist < nblocks ? *nlist : nblocks;
+    const uint64_t p = base + pos[i];
+    pos[i] = p;
+    if (i < n) out_start[list[i]] = p;
+    if (i == nblocks) out_start[nblocks] = p;
+}
+
+hipError_t launch_decompress_once(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                                  uint64_t slot_bytes, uint8_t *out, uint64_t out_cap, uint64_t *out_start,
+                                  uint64_t *out_end, unsigned long long *err, void *ws, hipStream_t st) {
+    if (codec != SDB_CODEC_ZLIB || !zl_once_supported()) {
+        const hipError_t e = launch_decompress_plan(codec, blocks, block_off, nblocks, out_start, ws, st);
+        if (e != hipSuccess) return e;
+        return launch_decompress_run(codec, blocks, block_off, nblocks, out, out_cap, out_start, out_end, err, st);
+    }
+    uint8_t *w = (uint8_t *)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
+    const uint64_t nt = (nblocks + 1023) / 1024 + 1;
+    uint64_t *slot = (uint64_t *)w;
+    uint64_t *scratch = slot + (nblocks + 2);
+    uint64_t *tx = scratch + (nblocks + 2), *ty = tx + (nt + 1);
+    uint64_t *pos = ty + (nt + 1);
+    unsigned long long *nlist = (unsigned long long *)(pos + (nblocks + 2));
+    uint32_t *list = (uint32_t *)(nlist + 1);
+    const uint32_t g = (uint32_t)((nblocks + 256) / 256);
+    hipLaunchKernelGGL(k_zo_init, dim3(g), dim3(256), 0, st, out_start, nblocks, slot_bytes, err, nlist);
+    // 1. every block inflated once into its slot; the overflowed ones listed
+    hipError_t e = launch_zl_once_run(blocks, block_off, nblocks, out, out_cap, out_start, out_end, err, nullptr, nullptr,
+                                      list, nlist, st);
+    // 2. the listed blocks' exact sizes, packed after the slots, and their inflate
+    if (e == hipSuccess) e = launch_zl_once_slots(blocks, block_off, nblocks, list, nlist, slot, st);
+    if (e == hipSuccess) e = launch_excl_scan2(slot, slot, nblocks, tx, ty, pos, scratch, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_zo_fix, dim3(g), dim3(256), 0, st, pos, out_start, nblocks, nblocks * slot_bytes, list, nlist);
+    return launch_zl_once_run(blocks, block_off, nblocks, out, out_cap, pos, out_end, err, list, nlist, nullptr, nullptr,
+                              st);
+}
+
 }  // namespace sdb

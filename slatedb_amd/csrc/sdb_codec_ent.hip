@@ -49,6 +49,12 @@ struct EntArgs {
     const uint64_t *out_start;  // nblocks + 1
     uint64_t *out_end;
     unsigned long long *err;
+    // zlib decode-once (launch_zlib_once): slot i decodes block list[i] (i < *nlist) instead of block i; the
+    // optimistic run lists the blocks whose output overflowed their slot instead of failing them
+    const uint32_t *list;
+    const unsigned long long *nlist;
+    uint32_t *ovf_list;
+    unsigned long long *ovf_count;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -250,27 +256,42 @@ struct EntOutWC : EntOut {
 // ------------------------------------------------------------------------------------------------
 // zlib / deflate
 // ------------------------------------------------------------------------------------------------
-struct LsbBits {
+struct LsbBits {  // the 4 bytes after the stream (its block's CRC32 trailer) are readable
     const uint8_t *p;
     uint64_t n, pos;
     uint64_t buf;
     int cnt;
-    SDB_DEV void refill() {  // to >= 57 bits: one unaligned 8-byte load when 8 bytes remain
-        if (cnt <= 56 && pos + 8 <= n) {
-            // the load's bytes past the whole ones taken land above cnt; a later refill ORs the same
-            // bytes at the same bit positions, so they need no masking
-            uint64_t w;
-            __builtin_memcpy(&w, p + pos, 8);
-            buf |= w << cnt;
-            const uint32_t take = (63 - (uint32_t)cnt) >> 3;
-            pos += take;
-            cnt += 8 * (int)take;
+    uint64_t nw;   // the 8 bytes from pos, loaded one refill ahead (n >= 4): raw, then >> nsh bits at use
+    uint32_t nsh;
+    // the load for 8 bytes from `at` (<= n): it stays inside the stream and its trailer, at most 3 bytes
+    // back from the end (shifted out at use, so the load's wait comes at the next refill)
+    SDB_DEV void load_at(uint64_t at) {
+        const uint64_t q = at + 4 <= n ? at : n - 4;
+        __builtin_memcpy(&nw, p + q, 8);
+        nsh = 8 * (uint32_t)(at - q);
+    }
+    SDB_DEV void start() {
+        nw = 0;
+        nsh = 0;
+        if (n >= 4) load_at(pos);
+    }
+    SDB_DEV void refill() {  // to >= 56 bits (fewer at the stream's end)
+        if (cnt >= 56 || pos >= n) return;
+        if (n < 4) {  // (a stream too short to hold a header)
+            while (cnt <= 56 && pos < n) {
+                buf |= (uint64_t)p[pos++] << cnt;
+                cnt += 8;
+            }
             return;
         }
-        while (cnt <= 56 && pos < n) {
-            buf |= (uint64_t)p[pos++] << cnt;
-            cnt += 8;
-        }
+        // the bytes past the whole ones taken (or past the stream) land above cnt, where a later refill ORs
+        // the same bytes at the same bit positions, and nothing reads them as input
+        buf |= (nw >> nsh) << cnt;
+        uint64_t take = (63 - (uint32_t)cnt) >> 3;
+        if (take > n - pos) take = n - pos;
+        pos += take;
+        cnt += 8 * (int)take;
+        load_at(pos);  // in flight while this refill's bits are decoded
     }
     SDB_DEV bool get(int k, uint32_t &v) {  // k <= 16; false when the input ends first
         if (cnt < k) refill();
@@ -314,8 +335,7 @@ SDB_DEV void canon_fast(const CanonT<N> &h, uint16_t *fast) {
     int code = 0, index = 0;
     for (int l = 1; l <= K; l++) {
         for (int c = 0; c < h.count[l]; c++, code++, index++) {
-            int r = 0;
-            for (int b = 0; b < l; b++) r |= ((code >> b) & 1) << (l - 1 - b);
+            const int r = (int)(__builtin_bitreverse32((uint32_t)code) >> (32 - l));
             const uint16_t e = (uint16_t)(h.sym[index] | l << 12);
             for (int j = r; j < (1 << K); j += 1 << l) fast[j] = e;
         }
@@ -323,16 +343,21 @@ SDB_DEV void canon_fast(const CanonT<N> &h, uint16_t *fast) {
     }
 }
 
-// -1 input ended, -2 invalid code
+// -1 input ended, -2 invalid code: the code's bits MSB first from the buffer (one refill, no per-bit input)
 template <int N>
 SDB_DEV int canon_decode(LsbBits &s, const CanonT<N> &h) {
+    if (s.cnt < 15) s.refill();
     int code = 0, first = 0, index = 0;
+#pragma unroll 1
     for (int l = 1; l < 16; l++) {
-        uint32_t b;
-        if (!s.get(1, b)) return -1;
-        code |= (int)b;
+        if (l > s.cnt) return -1;
+        code |= (int)((s.buf >> (l - 1)) & 1);
         const int c = h.count[l];
-        if (code - first < c) return h.sym[index + code - first];
+        if (code - first < c) {
+            s.buf >>= l;
+            s.cnt -= l;
+            return h.sym[index + code - first];
+        }
         index += c;
         first += c;
         first <<= 1;
@@ -341,12 +366,13 @@ SDB_DEV int canon_decode(LsbBits &s, const CanonT<N> &h) {
     return -2;
 }
 
-__constant__ uint16_t c_len_base[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
-                                        35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t c_len_extra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t c_dist_base[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769,
-                                         1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t c_dist_extra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+// deflate's length symbols 257 + i and distance symbols ds: base and extra bits (RFC 1951 3.2.5)
+SDB_DEV uint32_t len_extra(int i) { return i < 8 || i == 28 ? 0u : (uint32_t)(i - 4) >> 2; }
+SDB_DEV uint32_t len_base(int i) {
+    return i < 8 ? 3u + i : i == 28 ? 258u : ((4u + (i & 3)) << ((uint32_t)(i - 4) >> 2)) + 3u;
+}
+SDB_DEV uint32_t dist_extra(int ds) { return ds < 4 ? 0u : (uint32_t)(ds >> 1) - 1u; }
+SDB_DEV uint32_t dist_base(int ds) { return ds < 4 ? 1u + ds : ((2u + (ds & 1)) << ((ds >> 1) - 1)) + 1u; }
 __constant__ uint8_t c_cl_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 enum { kZOk = 0, kZTrunc = 1, kZErr = -1 };
@@ -448,13 +474,13 @@ SDB_DEV int inflate_raw(LsbBits &s, Out &o, ZTab &t) {
             sym -= 257;
             if (sym >= 29) return kZErr;
             uint32_t v;
-            if (!s.get(c_len_extra[sym], v)) return kZTrunc;
-            const uint32_t len = c_len_base[sym] + v;
+            if (!s.get((int)len_extra(sym), v)) return kZTrunc;
+            const uint32_t len = len_base(sym) + v;
             const int ds = fast_decode(t.fast_dist, (1u << kFastDist) - 1, t.dist);
             if (ds == -1) return kZTrunc;
             if (ds < 0 || ds >= 30) return kZErr;
-            if (!s.get(c_dist_extra[ds], v)) return kZTrunc;
-            const uint32_t d = c_dist_base[ds] + v;
+            if (!s.get((int)dist_extra(ds), v)) return kZTrunc;
+            const uint32_t d = dist_base(ds) + v;
             if (d > o.len) return kZErr;
             if (!o.match(d, len)) return kZErr;
         }
@@ -468,7 +494,8 @@ SDB_DEV int zlib_decode(const uint8_t *in, uint64_t n, Out &o, ZTab &t) {
     if (n < 2) return 0;
     const uint32_t cmf = in[0], flg = in[1];
     if ((cmf & 0x0F) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 != 0 || (flg & 0x20)) return -1;
-    LsbBits s{in, n, 2, 0, 0};
+    LsbBits s{in, n, 2, 0, 0, 0, 0};
+    s.start();
     const int r = inflate_raw(s, o, t);
     if (r == kZErr) return -1;
     if (r == kZTrunc) return 0;
@@ -1310,13 +1337,17 @@ SDB_DEV int zstd_frames_size(const uint8_t *in, uint64_t n, uint64_t *total) {
     return 0;
 }
 
-SDB_DEV int ent_decode(uint32_t codec, const uint8_t *in, uint64_t n, EntOut &o, EntLds &t) {
-    return codec == SDB_CODEC_ZLIB ? zlib_decode(in, n, o, t.z) : zstd_decode(in, n, o, t);
+// one codec per kernel instance (ZL: zlib, else zstd), so neither decoder's registers weigh on the other's
+template <bool ZL>
+SDB_DEV int ent_decode(const uint8_t *in, uint64_t n, EntOut &o, EntLds &t) {
+    if constexpr (ZL) return zlib_decode(in, n, o, t.z);
+    else return zstd_decode(in, n, o, t);
 }
 
 // ------------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------------
+template <bool ZL>
 __global__ __launch_bounds__(kEntThreads) void k_ent_plan(EntArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t l = (uint32_t)lane_id(), wave = threadIdx.x >> 6;
@@ -1331,11 +1362,11 @@ __global__ __launch_bounds__(kEntThreads) void k_ent_plan(EntArgs a) {
             const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
             uint64_t fsz = 0;
             if (e >= s && e - s >= 4) {
-                if (a.codec != SDB_CODEC_ZLIB && !zstd_frames_size(a.blocks + s, e - s - 4, &fsz)) {
+                if (!ZL && !zstd_frames_size(a.blocks + s, e - s - 4, &fsz)) {
                     slot = fsz + 4;
                 } else {
                     EntOut o{nullptr, 0, kEntMaxOut, false, false};
-                    if (!ent_decode(a.codec, a.blocks + s, e - s - 4, o, t) && !o.bad) slot = o.len + 4;
+                    if (!ent_decode<ZL>(a.blocks + s, e - s - 4, o, t) && !o.bad) slot = o.len + 4;
                 }
             }
         }
@@ -1351,6 +1382,7 @@ SDB_DEV uint32_t ent_crc(const uint8_t *msg, uint64_t n, const uint32_t (*tab)[2
     return x ^ 0xFFFFFFFFu;
 }
 
+template <bool ZL>
 __global__ __launch_bounds__(kEntThreads) void k_ent_run(EntArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     crc_slice_tables_to_lds((lu32 *)smem);
@@ -1381,7 +1413,7 @@ __global__ __launch_bounds__(kEntThreads) void k_ent_run(EntArgs a) {
             } else {
                 // every lane runs the decoder (same state; the copies spread over the lanes, EntOut::wide)
                 EntOut out{a.out + o, 0, slot - 4, false, true};
-                const int r = ent_decode(a.codec, in, bl, out, t) || out.bad ? SDB_DECOMPRESSION_ERROR : 0;
+                const int r = ent_decode<ZL>(in, bl, out, t) || out.bad ? SDB_DECOMPRESSION_ERROR : 0;
                 st = __shfl(r, 0, 64);
                 ol = (uint64_t)__shfl((long long)out.len, 0, 64);
                 __threadfence_block();
@@ -1474,10 +1506,12 @@ __global__ __launch_bounds__(kZpThreads) void k_zl_plan_multi(EntArgs a) {
     if (l >= kZpD) return;
     ZTab &t = *(ZTab *)(smem + (wave * kZpD + l) * kZpTab);
     const uint64_t ndec = (uint64_t)gridDim.x * (blockDim.x >> 6) * kZpD;
+    const uint64_t n = a.nlist ? (*a.nlist < a.nblocks ? *a.nlist : a.nblocks) : a.nblocks;
     for (uint64_t k = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * kZpD + l; k <= a.nblocks; k += ndec) {
         uint64_t slot = 0;
-        if (k < a.nblocks) {
-            const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
+        if (k < n) {
+            const uint64_t b = a.list ? (uint64_t)a.list[k] : k;
+            const uint64_t s = a.block_off[b], e = a.block_off[b + 1];
             if (e >= s && e - s >= 4) {
                 EntOut o{nullptr, 0, kEntMaxOut, false, false};
                 if (!zlib_decode(a.blocks + s, e - s - 4, o, t) && !o.bad) slot = o.len + 4;
@@ -1520,13 +1554,18 @@ __global__ __launch_bounds__(kZpThreads) void k_zl_run_multi(EntArgs a) {
     const uint32_t l = (uint32_t)lane_id(), wave = threadIdx.x >> 6;
     ZTab &t = *(ZTab *)(smem + 8 * 1024 + (wave * kZpD + (l < kZpD ? l : 0)) * kZpTab);
     const uint64_t ndec = (uint64_t)gridDim.x * (blockDim.x >> 6) * kZpD;
-    for (uint64_t k0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * kZpD; k0 < a.nblocks; k0 += ndec) {
+    // slot i decodes block blk(i) (the identity, or a decode-once pass's list)
+    const uint64_t n = a.nlist ? (*a.nlist < a.nblocks ? *a.nlist : a.nblocks) : a.nblocks;
+    auto blk = [&](uint64_t i) { return a.list ? (uint64_t)a.list[i] : i; };
+    const bool optimistic = a.ovf_list != nullptr;
+    for (uint64_t k0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * kZpD; k0 < n; k0 += ndec) {
         // 1. the stored CRCs (validate_checksum, format/sst.rs:1029-1038): lane j keeps block k0 + j's status
         int st = 0;
         for (uint32_t j = 0; j < kZpD; j++) {
             const uint64_t k = k0 + j;
-            if (k >= a.nblocks) break;
-            const uint64_t s = a.block_off[k], e = a.block_off[k + 1], o = a.out_start[k];
+            if (k >= n) break;
+            const uint64_t b = blk(k);
+            const uint64_t s = a.block_off[b], e = a.block_off[b + 1], o = a.out_start[k];
             const uint64_t slot = a.out_start[k + 1] - o;
             int sj = 0;
             if (e < s || e - s < 4 || e - s > 0xFFFFFFFFull) {
@@ -1542,26 +1581,35 @@ __global__ __launch_bounds__(kZpThreads) void k_zl_run_multi(EntArgs a) {
             }
             if (l == j) st = sj;
         }
-        // 2. lane j decodes block k0 + j (its Adler-32 checked below by the whole wave)
+        // 2. lane j decodes block k0 + j (its Adler-32 checked below by the whole wave); optimistic slots: an
+        //    output over the slot is not an error, the block is listed for its exact-size pass
         uint64_t ol = 0;
-        uint32_t have = 0, want = 0;
+        uint32_t have = 0, want = 0, ovf = 0;
         const uint64_t kl = k0 + l;
-        if (l < kZpD && kl < a.nblocks && !st) {
-            const uint64_t s = a.block_off[kl], e = a.block_off[kl + 1], o = a.out_start[kl];
+        if (l < kZpD && kl < n && !st) {
+            const uint64_t b = blk(kl);
+            const uint64_t s = a.block_off[b], e = a.block_off[b + 1], o = a.out_start[kl];
             const uint64_t slot = a.out_start[kl + 1] - o;
+            bool bad = false;
             if (SDB_ZL_WC) {
                 EntOutWC out{{a.out + o, 0, slot - 4, false, false, true, false, 0}, 0, 0};
                 st = zlib_decode(a.blocks + s, e - s - 4, out, t) || out.bad ? SDB_DECOMPRESSION_ERROR : 0;
                 out.flush();
+                bad = out.bad;
                 ol = out.len;
                 have = out.have_adler ? 1u : 0u;
                 want = out.adler_want;
             } else {
                 EntOut out{a.out + o, 0, slot - 4, false, false, true, false, 0};
                 st = zlib_decode(a.blocks + s, e - s - 4, out, t) || out.bad ? SDB_DECOMPRESSION_ERROR : 0;
+                bad = out.bad;
                 ol = out.len;
                 have = out.have_adler ? 1u : 0u;
                 want = out.adler_want;
+            }
+            if (optimistic && bad) {
+                st = 0;
+                ovf = 1;
             }
         }
         __threadfence_block();
@@ -1569,10 +1617,18 @@ __global__ __launch_bounds__(kZpThreads) void k_zl_run_multi(EntArgs a) {
         // 3. the output CRCs, trailers and out_end
         for (uint32_t j = 0; j < kZpD; j++) {
             const uint64_t k = k0 + j;
-            if (k >= a.nblocks) break;
+            if (k >= n) break;
+            const uint64_t b = blk(k);
             int sj = __shfl(st, (int)j, 64);
             const uint64_t olj = (uint64_t)__shfl((long long)ol, (int)j, 64);
             const uint64_t o = a.out_start[k];
+            if (__shfl((int)ovf, (int)j, 64)) {  // decode-once: the exact-size pass takes it
+                if (l == 0) {
+                    a.out_end[b] = o;
+                    a.ovf_list[atomicAdd(a.ovf_count, 1ull)] = (uint32_t)b;
+                }
+                continue;
+            }
             if (!sj && __shfl((int)have, (int)j, 64) && wave_adler32(a.out + o, olj) != (uint32_t)__shfl((int)want, (int)j, 64))
                 sj = SDB_DECOMPRESSION_ERROR;
             if (!sj) {
@@ -1586,8 +1642,8 @@ __global__ __launch_bounds__(kZpThreads) void k_zl_run_multi(EntArgs a) {
                 }
             }
             if (l == 0) {
-                a.out_end[k] = sj ? o : o + olj + 4;
-                if (sj) atomicMin(a.err, (unsigned long long)((k << 8) | (uint64_t)sj));
+                a.out_end[b] = sj ? o : o + olj + 4;
+                if (sj) atomicMin(a.err, (unsigned long long)((b << 8) | (uint64_t)sj));
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -1653,9 +1709,10 @@ static std::once_flag g_ent_once;
 static hipError_t g_ent_attr = hipSuccess;
 static void ent_attrs() {
     std::call_once(g_ent_once, [] {
-        g_ent_attr = hipFuncSetAttribute((const void *)k_ent_plan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEntLds);
-        if (g_ent_attr == hipSuccess)
-            g_ent_attr = hipFuncSetAttribute((const void *)k_ent_run, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEntLds);
+        // (zlib takes its own kernels below; the <true> instances of the generic ones are never launched)
+        for (const void *f : {(const void *)k_ent_plan<false>, (const void *)k_ent_run<false>})
+            if (g_ent_attr == hipSuccess)
+                g_ent_attr = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEntLds);
         if (g_ent_attr == hipSuccess)
             g_ent_attr = hipFuncSetAttribute((const void *)k_zl_plan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kZLds);
         if (g_ent_attr == hipSuccess)
@@ -1694,7 +1751,7 @@ hipError_t launch_ent_slots(uint32_t codec, const uint8_t *blocks, const uint64_
     else if (codec == SDB_CODEC_ZLIB)
         hipLaunchKernelGGL(k_zl_plan, dim3(ent_grid(nblocks + 1, kZThreads)), dim3(kZThreads), kZLds, st, a);
     else
-        hipLaunchKernelGGL(k_ent_plan, dim3(ent_grid(nblocks + 1)), dim3(kEntThreads), kEntLds, st, a);
+        hipLaunchKernelGGL(k_ent_plan<false>, dim3(ent_grid(nblocks + 1)), dim3(kEntThreads), kEntLds, st, a);
     return hipGetLastError();
 }
 
@@ -1719,7 +1776,53 @@ hipError_t launch_ent_run(uint32_t codec, const uint8_t *blocks, const uint64_t 
     else if (nblocks && codec == SDB_CODEC_ZLIB)
         hipLaunchKernelGGL(k_zl_run, dim3(ent_grid(nblocks, kZThreads)), dim3(kZThreads), kZLds, st, a);
     else if (nblocks)
-        hipLaunchKernelGGL(k_ent_run, dim3(ent_grid(nblocks)), dim3(kEntThreads), kEntLds, st, a);
+        hipLaunchKernelGGL(k_ent_run<false>, dim3(ent_grid(nblocks)), dim3(kEntThreads), kEntLds, st, a);
+    return hipGetLastError();
+}
+
+// zlib decode-once (launch_decompress_once, sdb_codec.hip): the optimistic run over fixed slots, which lists
+// the blocks that overflowed theirs, and the exact plan + run over that list
+bool zl_once_supported() { return SDB_ZL_RUN_MULTI && kZpD > 1; }
+
+hipError_t launch_zl_once_slots(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks, const uint32_t *list,
+                                const unsigned long long *nlist, uint64_t *slot, hipStream_t st) {
+    ent_attrs();
+    if (g_ent_attr != hipSuccess) return g_ent_attr;
+    EntArgs a{};
+    a.codec = SDB_CODEC_ZLIB;
+    a.blocks = blocks;
+    a.block_off = block_off;
+    a.nblocks = nblocks;
+    a.slot = slot;
+    a.list = list;
+    a.nlist = nlist;
+    hipLaunchKernelGGL(k_zl_plan_multi, dim3(ent_grid((nblocks + kZpD) / kZpD, kZpThreads)), dim3(kZpThreads), kZpLds, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_zl_once_run(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks, uint8_t *out,
+                              uint64_t out_cap, const uint64_t *out_start, uint64_t *out_end, unsigned long long *err,
+                              const uint32_t *list, const unsigned long long *nlist, uint32_t *ovf_list,
+                              unsigned long long *ovf_count, hipStream_t st) {
+    ent_attrs();
+    if (g_ent_attr != hipSuccess) return g_ent_attr;
+    EntArgs a{};
+    a.codec = SDB_CODEC_ZLIB;
+    a.blocks = blocks;
+    a.block_off = block_off;
+    a.nblocks = nblocks;
+    a.out = out;
+    a.out_cap = out_cap;
+    a.out_start = out_start;
+    a.out_end = out_end;
+    a.err = err;
+    a.list = list;
+    a.nlist = nlist;
+    a.ovf_list = ovf_list;
+    a.ovf_count = ovf_count;
+    if (nblocks)
+        hipLaunchKernelGGL(k_zl_run_multi, dim3(ent_grid((nblocks + kZpD - 1) / kZpD, kZpThreads)), dim3(kZpThreads), kZrLds,
+                           st, a);
     return hipGetLastError();
 }
 

@@ -71,6 +71,10 @@ hipError_t launch_decompress_plan(uint32_t codec, const uint8_t *blocks, const u
 hipError_t launch_decompress_run(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
                                  uint8_t *out, uint64_t out_cap, const uint64_t *out_start, uint64_t *out_end,
                                  unsigned long long *err, hipStream_t st);
+uint64_t decompress_once_workspace_bytes(uint64_t nblocks);
+hipError_t launch_decompress_once(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
+                                  uint64_t slot_bytes, uint8_t *out, uint64_t out_cap, uint64_t *out_start,
+                                  uint64_t *out_end, unsigned long long *err, void *ws, hipStream_t st);
 // f3: per-block compression, the write side (sdb_codec_enc.hip)
 uint64_t compress_workspace_bytes(uint64_t nblocks, uint64_t in_bytes);
 hipError_t launch_compress(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,

@@ -619,6 +619,32 @@ def decompress_blocks_device(codec, blocks, block_off, stream=None):
     return out, out_start, out_end[:nb], err
 
 
+def decompress_blocks_once_device(codec, blocks, block_off, slot_bytes, out_cap=None, stream=None, out=None):
+    """sdb_decompress_blocks_once: decompress_blocks_device without the host synchronisation between the plan
+    and the run.  Zlib inflates every block once into a slot of slot_bytes and re-plans only the blocks that
+    overflowed theirs (packed after the slots; out_start then is not monotone, out_start[nblocks] = the bytes
+    used); the other codecs run plan + run back to back.  out_cap defaults to nblocks * slot_bytes plus the
+    compressed section's length * 8 for overflows.  Returns (out, out_start, out_end, err) as
+    decompress_blocks_device."""
+    import torch
+    dev = blocks.device
+    nb = block_off.numel() - 1
+    if out_cap is None:
+        out_cap = nb * slot_bytes + 8 * int(blocks.numel()) + 64
+    ws = torch.empty(int(lib().sdb_decompress_once_workspace_bytes(nb)), dtype=torch.uint8, device=dev)
+    if out is None:
+        out = torch.empty(max(out_cap, 1) + 16, dtype=torch.uint8, device=dev)
+    out_start = torch.empty(nb + 1, dtype=torch.int64, device=dev)
+    out_end = torch.empty(max(nb, 1), dtype=torch.int64, device=dev)
+    err = torch.empty(1, dtype=torch.int64, device=dev)
+    st = lib().sdb_decompress_blocks_once(codec, blocks.data_ptr(), block_off.data_ptr(), nb, slot_bytes,
+                                          out.data_ptr(), out_cap, out_start.data_ptr(), out_end.data_ptr(),
+                                          err.data_ptr(), ws.data_ptr(), ws.numel(), _sp(stream))
+    if st:
+        raise SdbError(st, "sdb_decompress_blocks_once")
+    return out, out_start, out_end[:nb], err
+
+
 def compress_blocks_device(codec, blocks, block_off, in_bytes=None, out_cap=None, stream=None):
     """An encoded data section -> the same blocks compressed (sdb_compress_blocks; compress_and_transform,
     format/sst.rs:525-594).  blocks: device u8 tensor, block_off: device int64 tensor of nblocks + 1.
