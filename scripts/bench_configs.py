@@ -575,6 +575,35 @@ def codec_bench(reps):
         ok_once = (int(r1.cpu().numpy().view(np.uint64)[0]) == 2**64 - 1 and
                    np.array_equal((e1 - s1[:nb]).cpu().numpy(), (end - start[:nb]).cpu().numpy()))
         del o1
+        dev_line = None
+        if codec == O.CODEC_ZLIB:
+            # the same blocks compressed by the device write side (sdb_compress_blocks: fixed-Huffman / stored
+            # deflate), decoded once: every lane of the wide pass decodes a block against shared tables
+            dd = torch.from_numpy(data).to(dev)
+            db = torch.from_numpy(block_off.view(np.int64)).to(dev)
+            cz, czoff, czerr = runtime.compress_blocks_device(codec, dd, db)
+            torch.cuda.synchronize()
+            czo = czoff[: nb + 1].contiguous()
+            ccap = nb * slot + 8 * int(czo[nb].item())
+            o2 = torch.empty(ccap + 16, dtype=torch.uint8, device=dev)
+
+            def once2():
+                if lib.sdb_decompress_blocks_once(codec, cz.data_ptr(), czo.data_ptr(), nb, slot, o2.data_ptr(), ccap,
+                                                  s1.data_ptr(), e1.data_ptr(), r1.data_ptr(), once_ws.data_ptr(),
+                                                  once_ws.numel(), s.cuda_stream):
+                    raise RuntimeError("sdb_decompress_blocks_once")
+
+            with torch.cuda.stream(s):
+                ms_once2 = timed(once2, reps, s)
+            torch.cuda.synchronize()
+            st2, en2 = s1.cpu().numpy().view(np.uint64), e1.cpu().numpy().view(np.uint64)
+            oh = o2.cpu().numpy()
+            ok2 = int(r1.cpu().numpy().view(np.uint64)[0]) == 2**64 - 1 and all(
+                np.array_equal(oh[int(st2[k]):int(en2[k])], data[int(block_off[k]):int(block_off[k + 1])])
+                for k in range(0, nb, 97))
+            dev_line = {"compressed_bytes": int(czo[nb].item()), "once_ms": round(ms_once2, 4),
+                        "GiB_per_s_decompressed": round(total / (ms_once2 * 1e-3) / 2**30, 2), "ok_sampled": bool(ok2)}
+            del o2, cz, dd
         dout = runtime.DeviceDecodeOutput(nb, nent + 16, kbytes + 4096, device=dev)
 
         def dec():
@@ -586,7 +615,8 @@ def codec_bench(reps):
                           "decompressed_bytes": total, "ratio": round(total / comp.size, 4), "ms": round(ms, 4),
                           "GiB_per_s_decompressed": round(total / (ms * 1e-3) / 2**30, 2),
                           "plan_ms": round(ms_plan, 4), "once_ms": round(ms_once, 4), "once_spilled_blocks": spilled,
-                          "once_ok": bool(ok_once), "decode_after_ms": round(ms_dec, 4), "bit_exact": bool(ok),
+                          "once_ok": bool(ok_once), "device_compressed_once": dev_line,
+                          "decode_after_ms": round(ms_dec, 4), "bit_exact": bool(ok),
                           "cpu_baseline": {"kind": "port", "GiB_per_s": round(cpu_bytes / cpu_s / 2**30, 3),
                                            "cores": 1, "sample": "first %d blocks, oracle orc_decompress_blocks" % ns,
                                            "canonical_lib_GiB_per_s_1_thread": canon}}), flush=True)

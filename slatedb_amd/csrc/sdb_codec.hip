@@ -524,22 +524,28 @@ hipError_t launch_decompress_run(uint32_t codec, const uint8_t *blocks, const ui
 bool zl_once_supported();
 hipError_t launch_zl_once_slots(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks, const uint32_t *list,
                                 const unsigned long long *nlist, uint64_t *slot, hipStream_t st);
-hipError_t launch_zl_once_run(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks, uint8_t *out,
+hipError_t launch_zl_once_run(int mode, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks, uint8_t *out,
                               uint64_t out_cap, const uint64_t *out_start, uint64_t *out_end, unsigned long long *err,
-                              const uint32_t *list, const unsigned long long *nlist, uint32_t *ovf_list,
-                              unsigned long long *ovf_count, hipStream_t st);
+                              const uint32_t *list, const unsigned long long *nlist, bool out_by_block, uint32_t *ovf_list,
+                              unsigned long long *ovf_count, uint32_t *dyn_list, unsigned long long *dyn_count,
+                              uint64_t *wres, hipStream_t st);
 
 uint64_t decompress_once_workspace_bytes(uint64_t nblocks) {
-    return decompress_workspace_bytes(nblocks) + 8 * (nblocks + 2) + 4 * (nblocks + 2) + 512;
+    return decompress_workspace_bytes(nblocks) + 8 * (nblocks + 2) + 8 * (nblocks + 2) + 16 * (nblocks + 2) + 1024;
 }
 
+#ifndef SDB_ZL_WIDE
+#define SDB_ZL_WIDE 1
+#endif
+
 __global__ void k_zo_init(uint64_t *out_start, uint64_t nblocks, uint64_t slot_bytes, unsigned long long *err,
-                          unsigned long long *nlist) {
+                          unsigned long long *nlist, unsigned long long *ndyn) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i <= nblocks) out_start[i] = i * slot_bytes;
     if (i == 0) {
         *err = ~0ull;
         *nlist = 0;
+        *ndyn = 0;
     }
 }
 
@@ -571,19 +577,34 @@ hipError_t launch_decompress_once(uint32_t codec, const uint8_t *blocks, const u
     uint64_t *tx = scratch + (nblocks + 2), *ty = tx + (nt + 1);
     uint64_t *pos = ty + (nt + 1);
     unsigned long long *nlist = (unsigned long long *)(pos + (nblocks + 2));
-    uint32_t *list = (uint32_t *)(nlist + 1);
+    unsigned long long *ndyn = nlist + 1;
+    uint32_t *list = (uint32_t *)(ndyn + 1);
+    uint32_t *dyn = list + (nblocks + 2);
+    uint64_t *wres = (uint64_t *)(((uintptr_t)(dyn + (nblocks + 2)) + 15) & ~(uintptr_t)15);
     const uint32_t g = (uint32_t)((nblocks + 256) / 256);
-    hipLaunchKernelGGL(k_zo_init, dim3(g), dim3(256), 0, st, out_start, nblocks, slot_bytes, err, nlist);
-    // 1. every block inflated once into its slot; the overflowed ones listed
-    hipError_t e = launch_zl_once_run(blocks, block_off, nblocks, out, out_cap, out_start, out_end, err, nullptr, nullptr,
-                                      list, nlist, st);
+    hipLaunchKernelGGL(k_zo_init, dim3(g), dim3(256), 0, st, out_start, nblocks, slot_bytes, err, nlist, ndyn);
+    hipError_t e;
+    if (SDB_ZL_WIDE) {
+        // 1. every block once into its slot, all 64 lanes decoding against the fixed code's shared tables;
+        //    blocks with dynamic-Huffman deflate blocks listed, then decoded by the per-decoder-table run into
+        //    their slots (out_start[block]); overflowed blocks listed by both
+        e = launch_zl_once_run(1, blocks, block_off, nblocks, out, out_cap, out_start, out_end, err, nullptr, nullptr,
+                               false, list, nlist, dyn, ndyn, wres, st);
+        if (e == hipSuccess)
+            e = launch_zl_once_run(0, blocks, block_off, nblocks, out, out_cap, out_start, out_end, err, dyn, ndyn, true,
+                                   list, nlist, nullptr, nullptr, nullptr, st);
+    } else {
+        // 1. every block once into its slot; the overflowed ones listed
+        e = launch_zl_once_run(0, blocks, block_off, nblocks, out, out_cap, out_start, out_end, err, nullptr, nullptr,
+                               false, list, nlist, nullptr, nullptr, nullptr, st);
+    }
     // 2. the listed blocks' exact sizes, packed after the slots, and their inflate
     if (e == hipSuccess) e = launch_zl_once_slots(blocks, block_off, nblocks, list, nlist, slot, st);
     if (e == hipSuccess) e = launch_excl_scan2(slot, slot, nblocks, tx, ty, pos, scratch, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_zo_fix, dim3(g), dim3(256), 0, st, pos, out_start, nblocks, nblocks * slot_bytes, list, nlist);
-    return launch_zl_once_run(blocks, block_off, nblocks, out, out_cap, pos, out_end, err, list, nlist, nullptr, nullptr,
-                              st);
+    return launch_zl_once_run(0, blocks, block_off, nblocks, out, out_cap, pos, out_end, err, list, nlist, false, nullptr,
+                              nullptr, nullptr, nullptr, nullptr, st);
 }
 
 }  // namespace sdb

@@ -21,6 +21,7 @@
 // decoded straight into the END of the block's own output slot: with o bytes written and lp of the
 // block's R literals consumed, the output still to come is at least R - lp, so o <= end - R + lp and
 // no store reaches a literal not yet copied.
+#include <atomic>
 #include <mutex>
 
 #include "sdb_crc.h"
@@ -49,12 +50,17 @@ struct EntArgs {
     const uint64_t *out_start;  // nblocks + 1
     uint64_t *out_end;
     unsigned long long *err;
-    // zlib decode-once (launch_zlib_once): slot i decodes block list[i] (i < *nlist) instead of block i; the
-    // optimistic run lists the blocks whose output overflowed their slot instead of failing them
+    // zlib decode-once (launch_decompress_once): slot i decodes block list[i] (i < *nlist) instead of block
+    // i; the optimistic run lists the blocks whose output overflowed their slot instead of failing them,
+    // the wide run those with dynamic-Huffman blocks; out_by_block: a list pass writes to out_start[list[i]]
     const uint32_t *list;
     const unsigned long long *nlist;
     uint32_t *ovf_list;
     unsigned long long *ovf_count;
+    uint32_t *dyn_list;
+    unsigned long long *dyn_count;
+    bool out_by_block;
+    uint64_t *wres;  // the wide pass's per-block results for k_zl_verify: 2 words per block
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -117,6 +123,7 @@ struct EntOut {
     bool adler_defer;     // zlib: leave the Adler-32 check to the caller (adler_want, have_adler)
     bool have_adler;
     uint32_t adler_want;
+    SDB_DEV void flush() {}  // (EntOutWC: its pending bytes)
     SDB_DEV uint32_t lane() const { return wide ? (uint32_t)lane_id() : 0u; }
     SDB_DEV uint32_t lanes() const { return wide ? 64u : 1u; }
     SDB_DEV bool put(uint8_t b) {
@@ -253,6 +260,41 @@ struct EntOutWC : EntOut {
     }
 };
 
+// EntOutWC for a wave of decoders (the wide zlib pass): each lane also keeps the last 256 bytes of its output
+// in an LDS column (byte i at ring[(i & 255) * 64]), so a match within 256 bytes copies from LDS instead of
+// loading the lane's own fresh stores back from memory (with 64 lanes decoding, some lane's match would
+// otherwise wait on memory at nearly every symbol).
+struct EntOutRing : EntOutWC {
+    lu8 *ring;
+    SDB_DEV bool put(uint8_t b) {
+        if (len >= cap) {
+            bad = true;
+            return false;
+        }
+        ring[(uint32_t)(len & 255) * 64] = b;
+        return EntOutWC::put(b);
+    }
+    SDB_DEV bool match(uint64_t d, uint64_t n) {
+        if (!room(n)) return false;
+        if (d <= 256) {
+            uint64_t i = 0;
+            if (d >= 8)  // eight reads in flight, then eight puts (no byte of a batch is one it reads)
+                for (; i + 8 <= n; i += 8) {
+                    uint8_t v[8];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) v[j] = ring[(uint32_t)((len - d + j) & 255) * 64];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) put(v[j]);
+                }
+            for (; i < n; i++) put(ring[(uint32_t)((len - d) & 255) * 64]);
+            return true;
+        }
+        flush();  // older bytes: from the lane's own stores, one at a time (rare: distances over 256)
+        for (uint64_t i = 0; i < n; i++) put(p[len - d]);
+        return true;
+    }
+};
+
 // ------------------------------------------------------------------------------------------------
 // zlib / deflate
 // ------------------------------------------------------------------------------------------------
@@ -375,9 +417,22 @@ SDB_DEV uint32_t dist_extra(int ds) { return ds < 4 ? 0u : (uint32_t)(ds >> 1) -
 SDB_DEV uint32_t dist_base(int ds) { return ds < 4 ? 1u + ds : ((2u + (ds & 1)) << ((ds >> 1) - 1)) + 1u; }
 __constant__ uint8_t c_cl_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-enum { kZOk = 0, kZTrunc = 1, kZErr = -1 };
+enum { kZOk = 0, kZTrunc = 1, kZErr = -1, kZDyn = 2 };
 
-template <class Out>
+// deflate's fixed code (RFC 1951 3.2.6) in t: the lengths, canonical tables and fast tables
+SDB_DEV void zl_fixed_tables(ZTab &t) {
+    uint8_t *lens = t.lens;
+    for (int i = 0; i < 288; i++) lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
+    for (int i = 0; i < 32; i++) lens[288 + i] = 5;
+    canon_build(t.lit, lens, 288);
+    canon_build(t.dist, lens + 288, 32);
+    canon_fast<kFastLit>(t.lit, t.fast_lit);
+    canon_fast<kFastDist>(t.dist, t.fast_dist);
+}
+
+// SHARED: t holds the fixed code's tables (zl_fixed_tables), read-only and shared by the decoders of a
+// workgroup; a dynamic-Huffman block returns kZDyn (its decoder has no tables of its own)
+template <bool SHARED = false, class Out>
 SDB_DEV int inflate_raw(LsbBits &s, Out &o, ZTab &t) {
     uint32_t last = 0;
     uint8_t *lens = t.lens;
@@ -389,16 +444,42 @@ SDB_DEV int inflate_raw(LsbBits &s, Out &o, ZTab &t) {
             uint32_t ln, nl;
             if (!s.get(16, ln) || !s.get(16, nl)) return kZTrunc;
             if ((ln ^ 0xFFFF) != nl) return kZErr;
-            for (uint32_t i = 0; i < ln; i++) {
-                uint32_t b;
-                if (!s.get(8, b)) return kZTrunc;
-                if (!o.put((uint8_t)b)) return kZErr;
+            // the whole bytes left in the bit buffer, then straight from the stream 32 bytes per step (four
+            // loads in flight instead of a refill every 7 bytes); the bit reader restarts after them
+            uint32_t i = 0;
+            for (; i < ln && s.cnt >= 8; i++) {
+                if (!o.put((uint8_t)s.buf)) return kZErr;
+                s.buf >>= 8;
+                s.cnt -= 8;
             }
+            const uint64_t avail = s.n - s.pos < (uint64_t)(ln - i) ? s.n - s.pos : (uint64_t)(ln - i);
+            const uint8_t *src = s.p + s.pos;
+            uint64_t c = 0;
+            for (; c + 32 <= avail; c += 32) {
+                uint64_t w[4];
+                __builtin_memcpy(w, src + c, 32);
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+#pragma unroll
+                    for (int j = 0; j < 8; j++)
+                        if (!o.put((uint8_t)(w[q] >> (8 * j)))) return kZErr;
+            }
+            for (; c < avail; c++)
+                if (!o.put(src[c])) return kZErr;
+            s.pos += avail;
+            s.buf = s.cnt ? s.buf & ((1ull << s.cnt) - 1) : 0;  // (cnt < 8 here: stale bits above it cleared)
+            if (s.n >= 4) s.load_at(s.pos);
+            if (i + avail < ln) return kZTrunc;
             continue;
         }
         if (type == 3) return kZErr;
+        if constexpr (SHARED) {
+            if (type == 2) return kZDyn;
+        }
         int nlen, ndist;
-        if (type == 1) {
+        if (SHARED) {
+            // the fixed code's tables are already in t
+        } else if (type == 1) {
             for (int i = 0; i < 288; i++) lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
             for (int i = 0; i < 32; i++) lens[288 + i] = 5;
             nlen = 288;
@@ -446,13 +527,25 @@ SDB_DEV int inflate_raw(LsbBits &s, Out &o, ZTab &t) {
             if (lens[256] == 0) return kZErr;
             for (int q = ndist - 1; q >= 0; q--) lens[288 + q] = lens[nlen + q];
         }
-        if (canon_build(t.lit, lens, nlen) || canon_build(t.dist, lens + 288, ndist)) return kZErr;
-        canon_fast<kFastLit>(t.lit, t.fast_lit);
-        canon_fast<kFastDist>(t.dist, t.fast_dist);
+        if (!SHARED) {
+            if (canon_build(t.lit, lens, nlen) || canon_build(t.dist, lens + 288, ndist)) return kZErr;
+            canon_fast<kFastLit>(t.lit, t.fast_lit);
+            canon_fast<kFastDist>(t.dist, t.fast_dist);
+        }
         // a symbol through the fast table (mask: its size - 1) when its code is short enough and the bits
         // are there
         auto fast_decode = [&](const uint16_t *fast, uint32_t mask, const auto &h) -> int {
-            if (s.cnt < 9) s.refill();
+            if constexpr (SHARED) {
+                // a wave of decoders: when any lane runs low, every lane here refills and stores its pending
+                // output bytes, so the loads and stores a refill's wait covers were issued a refill ago
+                // (lane by lane, some lane's fresh load or store would be waited on at every symbol)
+                if (__ballot(s.cnt < 9)) {
+                    s.refill();
+                    o.flush();
+                }
+            } else if (s.cnt < 9) {
+                s.refill();
+            }
             const uint16_t e = fast[s.buf & mask];
             const int L = e >> 12;
             if (L && L <= s.cnt) {
@@ -489,14 +582,16 @@ SDB_DEV int inflate_raw(LsbBits &s, Out &o, ZTab &t) {
 }
 
 // 0 or -1; Adler-32 checked when the bytes are kept
-template <class Out>
+// 0, -1, or (SHARED) 1: a dynamic-Huffman block, left to a decoder with its own tables
+template <bool SHARED = false, class Out>
 SDB_DEV int zlib_decode(const uint8_t *in, uint64_t n, Out &o, ZTab &t) {
     if (n < 2) return 0;
     const uint32_t cmf = in[0], flg = in[1];
     if ((cmf & 0x0F) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 != 0 || (flg & 0x20)) return -1;
     LsbBits s{in, n, 2, 0, 0, 0, 0};
     s.start();
-    const int r = inflate_raw(s, o, t);
+    const int r = inflate_raw<SHARED>(s, o, t);
+    if (r == kZDyn) return 1;
     if (r == kZErr) return -1;
     if (r == kZTrunc) return 0;
     s.align();
@@ -1534,6 +1629,50 @@ SDB_DEV uint32_t wave_adler32(const uint8_t *p, uint64_t n) {
     const uint32_t x = (uint32_t)((1 + sa) % 65521u), y = (uint32_t)((n % 65521u + sb % 65521u) % 65521u);
     return y << 16 | x;
 }
+// The same with lane l summing the 64-byte segments l, l + 64, ... from four 16-byte loads each, all in
+// flight before the sums (k_zl_verify: one latency per 4 KiB instead of one per 64 bytes; more VGPRs)
+SDB_DEV uint32_t wave_adler32_seg(const uint8_t *p, uint64_t n) {
+    uint64_t sa = 0, sb = 0;
+    for (uint64_t base = 64 * (uint64_t)lane_id(); base < n; base += 4096) {
+        uint32_t w[16];
+        if (base + 64 <= n && ((uintptr_t)(p + base) & 15) == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint4 v = *(const uint4 *)(p + base + 16 * q);
+                w[4 * q] = v.x;
+                w[4 * q + 1] = v.y;
+                w[4 * q + 2] = v.z;
+                w[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (base + 4 * q + j < n) x |= (uint32_t)p[base + 4 * q + j] << (8 * j);
+                w[q] = x;
+            }
+        }
+        // bytes past n are 0: they add nothing to either sum
+        uint32_t a32 = 0, b32 = 0;  // segment sums: sum b, sum (63 - i) b (< 2^23)
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t b = (w[q] >> (8 * j)) & 0xFF;
+                a32 += b;
+                b32 += (uint32_t)(63 - (4 * q + j)) * b;
+            }
+        // sum (n - i) b over the segment = (n - base - 63) * sum b + sum (63 - i) b
+        sa += a32;
+        sb += (uint64_t)(n - base - 63) * a32 + b32;
+    }
+    sa = wave_sum(sa);
+    sb = wave_sum(sb);
+    const uint32_t x = (uint32_t)((1 + sa) % 65521u), y = (uint32_t)((n % 65521u + sb % 65521u) % 65521u);
+    return y << 16 | x;
+}
 
 // The run the same way: each wave takes kZpD blocks, checks their stored CRCs one after the other with
 // the whole wave, lets lanes 0 .. kZpD - 1 decode one block each (copies and Adler-32 on that lane), then
@@ -1546,17 +1685,20 @@ SDB_DEV uint32_t wave_adler32(const uint8_t *p, uint64_t n) {
 #endif
 constexpr uint32_t kZrLds = 8 * 1024 + kZpLds;
 static_assert(kZrLds <= 160 * 1024, "zlib run LDS");
+template <bool>
 __global__ __launch_bounds__(kZpThreads) void k_zl_run_multi(EntArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     crc_slice_tables_to_lds((lu32 *)smem);
-    __syncthreads();
-    const uint32_t(*tab)[256] = (const uint32_t(*)[256])smem;
     const uint32_t l = (uint32_t)lane_id(), wave = threadIdx.x >> 6;
     ZTab &t = *(ZTab *)(smem + 8 * 1024 + (wave * kZpD + (l < kZpD ? l : 0)) * kZpTab);
+    __syncthreads();
+    const uint32_t(*tab)[256] = (const uint32_t(*)[256])smem;
     const uint64_t ndec = (uint64_t)gridDim.x * (blockDim.x >> 6) * kZpD;
-    // slot i decodes block blk(i) (the identity, or a decode-once pass's list)
+    // slot i decodes block blk(i) (the identity, or a decode-once pass's list); its output goes to
+    // out_start[i] (out_start[blk(i)] when a.out_by_block: a list pass over the fixed slots)
     const uint64_t n = a.nlist ? (*a.nlist < a.nblocks ? *a.nlist : a.nblocks) : a.nblocks;
     auto blk = [&](uint64_t i) { return a.list ? (uint64_t)a.list[i] : i; };
+    auto oix = [&](uint64_t i, uint64_t b) { return a.out_by_block ? b : i; };
     const bool optimistic = a.ovf_list != nullptr;
     for (uint64_t k0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * kZpD; k0 < n; k0 += ndec) {
         // 1. the stored CRCs (validate_checksum, format/sst.rs:1029-1038): lane j keeps block k0 + j's status
@@ -1565,8 +1707,8 @@ __global__ __launch_bounds__(kZpThreads) void k_zl_run_multi(EntArgs a) {
             const uint64_t k = k0 + j;
             if (k >= n) break;
             const uint64_t b = blk(k);
-            const uint64_t s = a.block_off[b], e = a.block_off[b + 1], o = a.out_start[k];
-            const uint64_t slot = a.out_start[k + 1] - o;
+            const uint64_t s = a.block_off[b], e = a.block_off[b + 1], o = a.out_start[oix(k, b)];
+            const uint64_t slot = a.out_start[oix(k, b) + 1] - o;
             int sj = 0;
             if (e < s || e - s < 4 || e - s > 0xFFFFFFFFull) {
                 sj = SDB_CORRUPT_BLOCK;
@@ -1588,12 +1730,13 @@ __global__ __launch_bounds__(kZpThreads) void k_zl_run_multi(EntArgs a) {
         const uint64_t kl = k0 + l;
         if (l < kZpD && kl < n && !st) {
             const uint64_t b = blk(kl);
-            const uint64_t s = a.block_off[b], e = a.block_off[b + 1], o = a.out_start[kl];
-            const uint64_t slot = a.out_start[kl + 1] - o;
+            const uint64_t s = a.block_off[b], e = a.block_off[b + 1], o = a.out_start[oix(kl, b)];
+            const uint64_t slot = a.out_start[oix(kl, b) + 1] - o;
             bool bad = false;
+            int r;
             if (SDB_ZL_WC) {
                 EntOutWC out{{a.out + o, 0, slot - 4, false, false, true, false, 0}, 0, 0};
-                st = zlib_decode(a.blocks + s, e - s - 4, out, t) || out.bad ? SDB_DECOMPRESSION_ERROR : 0;
+                r = zlib_decode(a.blocks + s, e - s - 4, out, t);
                 out.flush();
                 bad = out.bad;
                 ol = out.len;
@@ -1601,12 +1744,13 @@ __global__ __launch_bounds__(kZpThreads) void k_zl_run_multi(EntArgs a) {
                 want = out.adler_want;
             } else {
                 EntOut out{a.out + o, 0, slot - 4, false, false, true, false, 0};
-                st = zlib_decode(a.blocks + s, e - s - 4, out, t) || out.bad ? SDB_DECOMPRESSION_ERROR : 0;
+                r = zlib_decode(a.blocks + s, e - s - 4, out, t);
                 bad = out.bad;
                 ol = out.len;
                 have = out.have_adler ? 1u : 0u;
                 want = out.adler_want;
             }
+            st = r || bad ? SDB_DECOMPRESSION_ERROR : 0;
             if (optimistic && bad) {
                 st = 0;
                 ovf = 1;
@@ -1621,7 +1765,7 @@ __global__ __launch_bounds__(kZpThreads) void k_zl_run_multi(EntArgs a) {
             const uint64_t b = blk(k);
             int sj = __shfl(st, (int)j, 64);
             const uint64_t olj = (uint64_t)__shfl((long long)ol, (int)j, 64);
-            const uint64_t o = a.out_start[k];
+            const uint64_t o = a.out_start[oix(k, b)];
             if (__shfl((int)ovf, (int)j, 64)) {  // decode-once: the exact-size pass takes it
                 if (l == 0) {
                     a.out_end[b] = o;
@@ -1647,6 +1791,119 @@ __global__ __launch_bounds__(kZpThreads) void k_zl_run_multi(EntArgs a) {
             }
         }
         __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// The wide pass (decode-once's first): every lane of the wave inflates a block of its own against the
+// fixed code's tables, copied once per workgroup into LDS, so the decoders per CU are bounded by waves,
+// not by LDS (70 with a table set each).  It only decodes: each lane records its block's result in
+// a.wres, and k_zl_verify then checks the stored CRC and the Adler-32 and appends the output CRC with one
+// wave per block (the wave-wide checks of 64 blocks in a row would leave each wave waiting on memory
+// 64 times over).  Blocks whose first deflate block is dynamic (or that meet one later), and streams too
+// short for the bit reader's trailer rule, are listed (a.dyn_list) for k_zl_run_multi; blocks past their
+// slot, as there, for the exact-size pass (a.ovf_list).
+constexpr uint32_t kZwThreads = 256, kZwRing = 256 * 64;  // a wave's history rings (EntOutRing)
+constexpr uint32_t kZwLds = kZpTab + (kZwThreads / 64) * kZwRing;
+static_assert(kZpTab % 16 == 0, "ZTab copies as 16-byte words");
+__device__ ZTab g_zl_fixed;  // the fixed code's tables (k_zl_fixed_init, once per device)
+__global__ void k_zl_fixed_init() {
+    if (threadIdx.x == 0) zl_fixed_tables(g_zl_fixed);
+}
+// wres[2 b] = output length | code << 48 (kWrOk, kWrErr: the decode failed, kWrCap: the slot is past out_cap,
+// kWrOther: another pass owns the block); wres[2 b + 1] = Adler-32 wanted | have << 32
+enum : uint64_t { kWrOk = 0, kWrErr = 1, kWrCap = 2, kWrOther = 3 };
+__global__ __launch_bounds__(kZwThreads) void k_zl_wide(EntArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t l = (uint32_t)lane_id(), wave = threadIdx.x >> 6;
+    ZTab &t = *(ZTab *)smem;
+    for (uint32_t q = threadIdx.x; q < kZpTab / 16; q += blockDim.x) ((uint4 *)&t)[q] = ((const uint4 *)&g_zl_fixed)[q];
+    __syncthreads();
+    const uint64_t n = a.nblocks;
+    for (uint64_t b = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * 64 + l, bstep = (uint64_t)gridDim.x * blockDim.x;
+         b - l < n; b += bstep) {
+        bool dyn = false, ovf = false;
+        if (b < n) {
+            const uint64_t s = a.block_off[b], e = a.block_off[b + 1], o = a.out_start[b];
+            const uint64_t slot = a.out_start[b + 1] - o;
+            uint64_t code = kWrOk, ol = 0, adl = 0;
+            if (e < s + 7 || e - s > 0xFFFFFFFFull || ((a.blocks[s + 2] >> 1) & 3) == 2) {
+                dyn = true;
+            } else if (o + slot > a.out_cap) {
+                code = kWrCap;
+            } else {
+                EntOutRing out{{{a.out + o, 0, slot - 4, false, false, true, false, 0}, 0, 0},
+                               (lu8 *)smem + kZpTab + wave * kZwRing + l};
+                const int r = zlib_decode<true>(a.blocks + s, e - s - 4, out, t);
+                out.flush();
+                if (r == 1) dyn = true;                // a dynamic block further into the stream
+                else if (out.bad) ovf = true;          // past the slot: the exact-size pass
+                else if (r) code = kWrErr;
+                ol = out.len;
+                adl = out.have_adler ? (1ull << 32) | out.adler_want : 0;
+            }
+            if (dyn || ovf) {
+                code = kWrOther;
+                a.out_end[b] = o;
+            }
+            a.wres[2 * b] = ol | code << 48;
+            a.wres[2 * b + 1] = adl;
+        }
+        // the lists, one counter update per wave each
+        const uint64_t dm = (uint64_t)__ballot(dyn), om = (uint64_t)__ballot(ovf), below = (1ull << l) - 1;
+        if (dm) {
+            unsigned long long base = 0;
+            if (l == 0) base = atomicAdd(a.dyn_count, (unsigned long long)__builtin_popcountll(dm));
+            base = (unsigned long long)__shfl((long long)base, 0, 64);
+            if (dyn) a.dyn_list[base + __builtin_popcountll(dm & below)] = (uint32_t)b;
+        }
+        if (om) {
+            unsigned long long base = 0;
+            if (l == 0) base = atomicAdd(a.ovf_count, (unsigned long long)__builtin_popcountll(om));
+            base = (unsigned long long)__shfl((long long)base, 0, 64);
+            if (ovf) a.ovf_list[base + __builtin_popcountll(om & below)] = (uint32_t)b;
+        }
+    }
+}
+
+// One wave per block the wide pass decoded: the stored CRC (validate_checksum, format/sst.rs:1029-1038;
+// it outranks the decode's status), the Adler-32 trailer, then the output CRC, out_end and the error word.
+constexpr uint32_t kZvThreads = 256;
+__global__ __launch_bounds__(kZvThreads) void k_zl_verify(EntArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    crc_slice_tables_to_lds((lu32 *)smem);
+    __syncthreads();
+    const uint32_t(*tab)[256] = (const uint32_t(*)[256])smem;
+    const uint32_t l = (uint32_t)lane_id(), wave = threadIdx.x >> 6;
+    for (uint64_t b = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave; b < a.nblocks;
+         b += (uint64_t)gridDim.x * (blockDim.x >> 6)) {
+        const uint64_t w0 = a.wres[2 * b], code = w0 >> 48;
+        if (code == kWrOther) continue;
+        const uint64_t s = a.block_off[b], e = a.block_off[b + 1], o = a.out_start[b], ol = w0 & 0xFFFFFFFFFFFFull;
+        const uint64_t bl = e - s - 4;
+        const uint8_t *g = a.blocks + s;
+        const uint32_t stored = (uint32_t)g[bl] << 24 | (uint32_t)g[bl + 1] << 16 | (uint32_t)g[bl + 2] << 8 | (uint32_t)g[bl + 3];
+        int st = 0;
+        if (ent_crc(g, bl, tab) != stored) st = SDB_CHECKSUM_MISMATCH;
+        else if (code == kWrCap) st = SDB_INVALID_ARGUMENT;
+        else if (code == kWrErr) st = SDB_DECOMPRESSION_ERROR;
+        else {
+            const uint64_t w1 = a.wres[2 * b + 1];
+            if ((w1 >> 32) && wave_adler32_seg(a.out + o, ol) != (uint32_t)w1) st = SDB_DECOMPRESSION_ERROR;
+        }
+        if (!st) {
+            const uint32_t c = ent_crc(a.out + o, ol, tab);
+            if (l == 0) {
+                uint8_t *gw = a.out + o;
+                gw[ol] = (uint8_t)(c >> 24);
+                gw[ol + 1] = (uint8_t)(c >> 16);
+                gw[ol + 2] = (uint8_t)(c >> 8);
+                gw[ol + 3] = (uint8_t)c;
+            }
+        }
+        if (l == 0) {
+            a.out_end[b] = st ? o : o + ol + 4;
+            if (st) atomicMin(a.err, (unsigned long long)((b << 8) | (uint64_t)st));
+        }
     }
 }
 
@@ -1721,8 +1978,10 @@ static void ent_attrs() {
             g_ent_attr = hipFuncSetAttribute((const void *)k_zl_plan_multi, hipFuncAttributeMaxDynamicSharedMemorySize,
                                               (int)kZpLds);
         if (g_ent_attr == hipSuccess)
-            g_ent_attr = hipFuncSetAttribute((const void *)k_zl_run_multi, hipFuncAttributeMaxDynamicSharedMemorySize,
+            g_ent_attr = hipFuncSetAttribute((const void *)k_zl_run_multi<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                               (int)kZrLds);
+        if (g_ent_attr == hipSuccess)
+            g_ent_attr = hipFuncSetAttribute((const void *)k_zl_wide, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kZwLds);
     });
 }
 static uint32_t ent_grid(uint64_t nwaves, uint32_t threads = kEntThreads) {
@@ -1771,7 +2030,7 @@ hipError_t launch_ent_run(uint32_t codec, const uint8_t *blocks, const uint64_t 
     a.out_end = out_end;
     a.err = err;
     if (nblocks && codec == SDB_CODEC_ZLIB && SDB_ZL_RUN_MULTI)
-        hipLaunchKernelGGL(k_zl_run_multi, dim3(ent_grid((nblocks + kZpD - 1) / kZpD, kZpThreads)), dim3(kZpThreads), kZrLds,
+        hipLaunchKernelGGL(k_zl_run_multi<false>, dim3(ent_grid((nblocks + kZpD - 1) / kZpD, kZpThreads)), dim3(kZpThreads), kZrLds,
                            st, a);
     else if (nblocks && codec == SDB_CODEC_ZLIB)
         hipLaunchKernelGGL(k_zl_run, dim3(ent_grid(nblocks, kZThreads)), dim3(kZThreads), kZLds, st, a);
@@ -1800,10 +2059,12 @@ hipError_t launch_zl_once_slots(const uint8_t *blocks, const uint64_t *block_off
     return hipGetLastError();
 }
 
-hipError_t launch_zl_once_run(const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks, uint8_t *out,
+// mode 0: the per-decoder-table run; 1: the wide run (fixed-code blocks, the others to dyn_list)
+hipError_t launch_zl_once_run(int mode, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks, uint8_t *out,
                               uint64_t out_cap, const uint64_t *out_start, uint64_t *out_end, unsigned long long *err,
-                              const uint32_t *list, const unsigned long long *nlist, uint32_t *ovf_list,
-                              unsigned long long *ovf_count, hipStream_t st) {
+                              const uint32_t *list, const unsigned long long *nlist, bool out_by_block, uint32_t *ovf_list,
+                              unsigned long long *ovf_count, uint32_t *dyn_list, unsigned long long *dyn_count,
+                              uint64_t *wres, hipStream_t st) {
     ent_attrs();
     if (g_ent_attr != hipSuccess) return g_ent_attr;
     EntArgs a{};
@@ -1818,11 +2079,40 @@ hipError_t launch_zl_once_run(const uint8_t *blocks, const uint64_t *block_off, 
     a.err = err;
     a.list = list;
     a.nlist = nlist;
+    a.out_by_block = out_by_block;
     a.ovf_list = ovf_list;
     a.ovf_count = ovf_count;
-    if (nblocks)
-        hipLaunchKernelGGL(k_zl_run_multi, dim3(ent_grid((nblocks + kZpD - 1) / kZpD, kZpThreads)), dim3(kZpThreads), kZrLds,
-                           st, a);
+    a.dyn_list = dyn_list;
+    a.dyn_count = dyn_count;
+    a.wres = wres;
+    if (nblocks && mode == 1) {
+        int dev = 0, cus = 0;
+        (void)hipGetDevice(&dev);
+        static std::atomic<bool> fixed_ready[64];
+        const bool tracked = dev >= 0 && dev < 64;
+        if (!tracked) {
+            hipLaunchKernelGGL(k_zl_fixed_init, dim3(1), dim3(64), 0, st);  // (stream-ordered before the run)
+        } else if (!fixed_ready[dev].load()) {  // the shared tables, once per device
+            static std::mutex mu;
+            std::lock_guard<std::mutex> g(mu);
+            if (!fixed_ready[dev].load()) {
+                hipLaunchKernelGGL(k_zl_fixed_init, dim3(1), dim3(64), 0, st);
+                if (hipStreamSynchronize(st) != hipSuccess) return hipGetLastError();
+                fixed_ready[dev].store(true);
+            }
+        }
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const uint64_t most = 8ull * (cus > 0 ? cus : 256);
+        uint64_t wgs = (nblocks + kZwThreads - 1) / kZwThreads;
+        wgs = wgs < most ? wgs : most;
+        hipLaunchKernelGGL(k_zl_wide, dim3((uint32_t)wgs), dim3(kZwThreads), kZwLds, st, a);
+        uint64_t vgs = (nblocks + kZvThreads / 64 - 1) / (kZvThreads / 64);
+        vgs = vgs < most ? vgs : most;
+        hipLaunchKernelGGL(k_zl_verify, dim3((uint32_t)vgs), dim3(kZvThreads), 8 * 1024, st, a);
+    }
+    else if (nblocks)
+        hipLaunchKernelGGL(k_zl_run_multi<false>, dim3(ent_grid((nblocks + kZpD - 1) / kZpD, kZpThreads)), dim3(kZpThreads),
+                           kZrLds, st, a);
     return hipGetLastError();
 }
 

@@ -154,3 +154,44 @@ def test_once_capacity_and_arguments():
                                               None) == _abi.SDB_INVALID_ARGUMENT
     assert lib.sdb_decompress_blocks_once(O.CODEC_ZLIB, p, p, 4, 64, p, 4096, p, p, p, ws.data_ptr(), 16,
                                           None) == _abi.SDB_INVALID_ARGUMENT
+
+
+def _device_compressed(codec, data, block_off):
+    cz, czoff, err = runtime.compress_blocks_device(codec, _dev(data), _dev(block_off, np.int64))
+    torch.cuda.synchronize()
+    assert int(err.cpu().numpy().view(np.uint64)[0]) == NONE
+    nb = len(block_off) - 1
+    off = czoff.cpu().numpy().view(np.uint64)[: nb + 1].copy()
+    return cz.cpu().numpy()[: int(off[nb])].copy(), off
+
+
+@pytest.mark.parametrize("slot", [8, 2048, 4160])
+def test_once_zlib_wide_pass(slot):
+    """The wide pass (every lane a decoder against the fixed code's shared tables): blocks the device write
+    side compressed (fixed-Huffman / stored deflate), alone and interleaved with Python-zlib blocks (dynamic
+    Huffman, listed for the per-decoder-table pass), at slots every block, some blocks and no block
+    overflows: once == the oracle, and the bytes == the uncompressed blocks."""
+    b = datasets.d1(n=20000, sst_index=3)
+    enc = O.encode_sst(b, O.params(block_size=4096, bloom_bits_per_key=0))
+    nb = len(enc.block_off) - 1
+    fixed, foff = _device_compressed(O.CODEC_ZLIB, enc.data, enc.block_off)
+    dyn, doff = compress_run(O.CODEC_ZLIB, enc.data, enc.block_off)
+    parts = [(fixed[int(foff[k]):int(foff[k + 1])] if k % 3 else dyn[int(doff[k]):int(doff[k + 1])]).tobytes()
+             for k in range(nb)]
+    mixed = np.frombuffer(b"".join(parts), np.uint8).copy()
+    moff = np.cumsum([0] + [len(x) for x in parts]).astype(np.uint64)
+    for comp, coff in ((fixed, foff), (mixed, moff)):
+        out, start, end, err, _ = _check(O.CODEC_ZLIB, comp, coff, slot)
+        assert err == NONE
+        got = b"".join(out[int(start[k]):int(end[k])].tobytes() for k in range(nb))
+        assert got == enc.data.tobytes()
+    # a corrupt fixed-code block (CRC) and a truncated one among them
+    c2 = mixed.copy()
+    c2[int(moff[4]) + 5] ^= 0x40
+    assert _check(O.CODEC_ZLIB, c2, moff, slot)[3] == (4 << 8) | _abi.SDB_CHECKSUM_MISMATCH
+    p = parts[5][:-4]
+    parts2 = list(parts)
+    parts2[5] = frame(p[: len(p) // 2])
+    c3 = np.frombuffer(b"".join(parts2), np.uint8).copy()
+    o3 = np.cumsum([0] + [len(x) for x in parts2]).astype(np.uint64)
+    _check(O.CODEC_ZLIB, c3, o3, slot)
