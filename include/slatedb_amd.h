@@ -339,7 +339,10 @@ sdb_status sdb_decompress_blocks(uint32_t codec, const uint8_t *blocks, const ui
  * whose output + 4 does not fit their slot are planned and inflated again, packed from
  * nblocks * slot_bytes on, and their out_start[k] rewritten — so out_start is not monotone and
  * out_start[nblocks] = the bytes of out the call used.  A block past out_cap fails with
- * SDB_INVALID_ARGUMENT as in step 2.  The other codecs ignore slot_bytes: the plan and the run back to
+ * SDB_INVALID_ARGUMENT as in step 2.  Zlib blocks coded with deflate's fixed code or stored (what
+ * sdb_compress_blocks writes) are inflated one per lane against shared tables; dynamic-Huffman blocks (what
+ * flate2 at its default level writes) take the per-decoder-table kernel.  The other codecs ignore
+ * slot_bytes: the plan and the run back to
  * back (out_start as step 1 writes it).  out_start / out_end / *err then mean what step 2 says, and
  * sdb_decode_blocks_at(out, out_start, out_end, ...) decodes the run.  Workspace:
  * sdb_decompress_once_workspace_bytes(nblocks). */

@@ -13,11 +13,11 @@ step() {  # name timeout command...
 step tests 300 python -u -m pytest tests/test_gpu_codec.py tests/test_gpu_codec_once.py tests/test_gpu_codec_write.py -x -q --timeout 200 --timeout-method thread
 tail -1 $O/tests.log
 SDB_CODECS=${SDB_CODECS:-zlib} step codec 300 python3 scripts/bench_configs.py --codec --reps 3
-grep "^{" $O/codec.log | cut -c1-420
+grep "^{" $O/codec.log | cut -c1-420; grep -o '"device_compressed_once": {[^}]*}' $O/codec.log || true
 SDB_CODECS=${SDB_CODECS:-zlib} step prof 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 scripts/bench_configs.py --codec --reps 3
 grep -E "k_zl|k_ent" $O/prof/run_kernel_stats.csv | cut -c1-160
 for v in ${ZL_VARIANTS:-}; do  # variant libraries (make variant NAME=v) on the same bench line
   SDB_LIBRARY=libslatedb_amd_$v.so SDB_CODECS=zlib step codec_$v 300 python3 scripts/bench_configs.py --codec --reps 3
-  echo "[$v]"; grep "^{" $O/codec_$v.log | cut -c100-300
+  echo "[$v]"; grep -o '"once_ms": [0-9.]*\|"device_compressed_once": {[^}]*}' $O/codec_$v.log || true
 done
 echo done

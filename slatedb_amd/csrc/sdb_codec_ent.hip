@@ -274,6 +274,45 @@ struct EntOutRing : EntOutWC {
         ring[(uint32_t)(len & 255) * 64] = b;
         return EntOutWC::put(b);
     }
+    // c <= 8 bytes (the low bytes of w, the rest zero) at once: ring writes, then one merge with the
+    // pending bytes (an 8-byte store when they reach 8).  The caller has checked room(c).
+    SDB_DEV void put_n(uint64_t w, uint32_t c) {
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++)
+            if (j < c) ring[(uint32_t)((len + j) & 255) * 64] = (uint8_t)(w >> (8 * j));
+        if (pn + c < 8) {
+            pend |= w << (8 * pn);
+            pn += c;
+        } else {
+            const uint64_t out = pend | (w << (8 * pn));
+            __builtin_memcpy(p + len - pn, &out, 8);
+            const uint32_t rem = pn + c - 8;
+            pend = rem ? w >> (8 * (8 - pn)) : 0;
+            pn = rem;
+        }
+        len += c;
+    }
+    // the next c <= 8 bytes of a match at distance d (the step machine of zlib_decode_wide)
+    SDB_DEV bool copy_step(uint64_t d, uint32_t c) {
+        if (!room(c)) return false;
+        if (d > 256) {  // older bytes: from the lane's own stores, one at a time (rare)
+            flush();
+            for (uint32_t i = 0; i < c; i++) put(p[len - d]);
+            return true;
+        }
+        uint64_t w = 0;
+        const uint32_t dd = (uint32_t)d;
+        if (dd >= 8) {
+#pragma unroll
+            for (uint32_t j = 0; j < 8; j++) w |= (uint64_t)ring[(uint32_t)((len - dd + j) & 255) * 64] << (8 * j);
+        } else {  // an overlapping match: byte j repeats byte j mod d of the last d
+#pragma unroll
+            for (uint32_t j = 0; j < 8; j++) w |= (uint64_t)ring[(uint32_t)((len - dd + j % dd) & 255) * 64] << (8 * j);
+        }
+        if (c < 8) w &= (1ull << (8 * c)) - 1;
+        put_n(w, c);
+        return true;
+    }
     SDB_DEV bool match(uint64_t d, uint64_t n) {
         if (!room(n)) return false;
         if (d <= 256) {
@@ -629,6 +668,165 @@ SDB_DEV int zlib_decode(const uint8_t *in, uint64_t n, Out &o, ZTab &t) {
         }
         if ((y << 16 | x) != a) return -1;
     }
+    return 0;
+}
+
+// The wide pass's inflate (k_zl_wide: 64 decoders per wave on the fixed code's shared tables) as a step
+// machine: every iteration each lane does one short step — a block header, one symbol, or up to 8 bytes
+// of a pending match — so lanes that meet a match do not hold the others through its whole copy (the
+// divergent literal and match paths of inflate_raw ran one after the other for all 64 lanes).  Refills
+// and the pending output stores happen at wave-uniform points (any lane under 32 bits: every step needs
+// at most 9 + 5 + 5 + 13).  Returns what zlib_decode<true> returns: 0, -1, or 1 for a dynamic block.
+SDB_DEV int zlib_decode_wide(const uint8_t *in, uint64_t n, EntOutRing &o, const ZTab &t) {
+    if (n < 2) return 0;
+    const uint32_t cmf = in[0], flg = in[1];
+    if ((cmf & 0x0F) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 != 0 || (flg & 0x20)) return -1;
+    LsbBits s{in, n, 2, 0, 0, 0, 0};
+    s.start();
+    int r = kZOk;
+    uint32_t last = 0, mlen = 0, mdist = 0;
+    bool hdr = true, fin = false;
+    while (!fin) {
+        if (__ballot(s.cnt < 32)) {
+            s.refill();
+            o.flush();
+        }
+        if (mlen) {  // a pending match: up to 8 bytes this step
+            const uint32_t c = mlen < 8 ? mlen : 8;
+            if (!o.copy_step(mdist, c)) {
+                r = kZErr;
+                fin = true;
+            }
+            mlen -= c;
+            continue;
+        }
+        if (hdr) {  // the next deflate block's header, or the end of the last one
+            uint32_t type = 0;
+            if (last) {
+                fin = true;
+            } else if (!s.get(1, last) || !s.get(2, type)) {
+                r = kZTrunc;
+                fin = true;
+            } else if (type == 2 || type == 3) {
+                r = type == 2 ? kZDyn : kZErr;
+                fin = true;
+            } else if (type == 1) {
+                hdr = false;
+            } else {  // stored: the whole block in one step (bytes left in the buffer, then 32 per load)
+                s.align();
+                uint32_t ln, nl;
+                if (!s.get(16, ln) || !s.get(16, nl)) {
+                    r = kZTrunc;
+                    fin = true;
+                    continue;
+                }
+                if ((ln ^ 0xFFFF) != nl) {
+                    r = kZErr;
+                    fin = true;
+                    continue;
+                }
+                uint32_t i = 0;
+                bool ok = true;
+                for (; i < ln && s.cnt >= 8 && ok; i++) {
+                    ok = o.put((uint8_t)s.buf);
+                    s.buf >>= 8;
+                    s.cnt -= 8;
+                }
+                const uint64_t avail = s.n - s.pos < (uint64_t)(ln - i) ? s.n - s.pos : (uint64_t)(ln - i);
+                const uint8_t *src = s.p + s.pos;
+                for (uint64_t c = 0; c < avail && ok; c += 8) {
+                    const uint32_t k = avail - c < 8 ? (uint32_t)(avail - c) : 8;
+                    uint64_t w = 0;
+                    if (k == 8) __builtin_memcpy(&w, src + c, 8);
+                    else
+                        for (uint32_t j = 0; j < k; j++) w |= (uint64_t)src[c + j] << (8 * j);
+                    ok = o.room(k);
+                    if (ok) o.put_n(w, k);
+                }
+                s.pos += avail;
+                s.buf = s.cnt ? s.buf & ((1ull << s.cnt) - 1) : 0;
+                if (s.n >= 4) s.load_at(s.pos);
+                if (!ok) {
+                    r = kZErr;
+                    fin = true;
+                } else if (i + avail < ln) {
+                    r = kZTrunc;
+                    fin = true;
+                }
+            }
+            continue;
+        }
+        // one symbol of a fixed-code block (every fixed literal / length code is in the 9-bit table)
+        int sym;
+        {
+            const uint16_t e = t.fast_lit[s.buf & ((1u << kFastLit) - 1)];
+            const int L = e >> 12;
+            if (L && L <= s.cnt) {
+                s.buf >>= L;
+                s.cnt -= L;
+                sym = e & 0xFFF;
+            } else {
+                sym = canon_decode(s, t.lit);
+            }
+        }
+        if (sym < 0) {
+            r = sym == -1 ? kZTrunc : kZErr;
+            fin = true;
+        } else if (sym < 256) {
+            if (!o.put((uint8_t)sym)) {
+                r = kZErr;
+                fin = true;
+            }
+        } else if (sym == 256) {
+            hdr = true;
+        } else if (sym - 257 >= 29) {
+            r = kZErr;
+            fin = true;
+        } else {
+            uint32_t v;
+            const int ls = sym - 257;
+            if (!s.get((int)len_extra(ls), v)) {
+                r = kZTrunc;
+                fin = true;
+                continue;
+            }
+            const uint32_t len = len_base(ls) + v;
+            int ds;
+            {
+                const uint16_t e = t.fast_dist[s.buf & ((1u << kFastDist) - 1)];
+                const int L = e >> 12;
+                if (L && L <= s.cnt) {
+                    s.buf >>= L;
+                    s.cnt -= L;
+                    ds = e & 0xFFF;
+                } else {
+                    ds = canon_decode(s, t.dist);
+                }
+            }
+            if (ds == -1 || (ds >= 0 && ds < 30 && !s.get((int)dist_extra(ds), v))) {
+                r = kZTrunc;
+                fin = true;
+            } else if (ds < 0 || ds >= 30 || dist_base(ds) + v > o.len) {
+                r = kZErr;
+                fin = true;
+            } else {
+                mlen = len;
+                mdist = dist_base(ds) + v;
+            }
+        }
+    }
+    if (r == kZDyn) return 1;
+    if (r == kZErr) return -1;
+    if (r == kZTrunc) return 0;
+    s.align();
+    uint32_t a = 0;
+    for (int i = 0; i < 4; i++) {
+        uint32_t b;
+        if (!s.get(8, b)) return 0;
+        a = a << 8 | b;
+    }
+    o.have_adler = true;  // (k_zl_verify checks it)
+    o.adler_want = a;
     return 0;
 }
 
@@ -1802,6 +2000,10 @@ __global__ __launch_bounds__(kZpThreads) void k_zl_run_multi(EntArgs a) {
 // 64 times over).  Blocks whose first deflate block is dynamic (or that meet one later), and streams too
 // short for the bit reader's trailer rule, are listed (a.dyn_list) for k_zl_run_multi; blocks past their
 // slot, as there, for the exact-size pass (a.ovf_list).
+#ifndef SDB_ZL_WIDE_D
+#define SDB_ZL_WIDE_D 64
+#endif
+constexpr uint32_t kZwD = SDB_ZL_WIDE_D;
 constexpr uint32_t kZwThreads = 256, kZwRing = 256 * 64;  // a wave's history rings (EntOutRing)
 constexpr uint32_t kZwLds = kZpTab + (kZwThreads / 64) * kZwRing;
 static_assert(kZpTab % 16 == 0, "ZTab copies as 16-byte words");
@@ -1819,8 +2021,10 @@ __global__ __launch_bounds__(kZwThreads) void k_zl_wide(EntArgs a) {
     for (uint32_t q = threadIdx.x; q < kZpTab / 16; q += blockDim.x) ((uint4 *)&t)[q] = ((const uint4 *)&g_zl_fixed)[q];
     __syncthreads();
     const uint64_t n = a.nblocks;
-    for (uint64_t b = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * 64 + l, bstep = (uint64_t)gridDim.x * blockDim.x;
-         b - l < n; b += bstep) {
+    // kZwD decoding lanes per wave (the rest idle): fewer lanes, more waves to overlap the refill latency
+    const uint64_t bstep = (uint64_t)gridDim.x * (blockDim.x >> 6) * kZwD;
+    for (uint64_t b0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * kZwD; b0 < n; b0 += bstep) {
+        const uint64_t b = l < kZwD ? b0 + l : n;
         bool dyn = false, ovf = false;
         if (b < n) {
             const uint64_t s = a.block_off[b], e = a.block_off[b + 1], o = a.out_start[b];
@@ -1833,7 +2037,11 @@ __global__ __launch_bounds__(kZwThreads) void k_zl_wide(EntArgs a) {
             } else {
                 EntOutRing out{{{a.out + o, 0, slot - 4, false, false, true, false, 0}, 0, 0},
                                (lu8 *)smem + kZpTab + wave * kZwRing + l};
+#ifdef SDB_ZL_WIDE_INFLATE  // (diagnostic: inflate_raw's nested loops on the shared tables)
                 const int r = zlib_decode<true>(a.blocks + s, e - s - 4, out, t);
+#else
+                const int r = zlib_decode_wide(a.blocks + s, e - s - 4, out, t);
+#endif
                 out.flush();
                 if (r == 1) dyn = true;                // a dynamic block further into the stream
                 else if (out.bad) ovf = true;          // past the slot: the exact-size pass
@@ -2103,7 +2311,7 @@ hipError_t launch_zl_once_run(int mode, const uint8_t *blocks, const uint64_t *b
         }
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const uint64_t most = 8ull * (cus > 0 ? cus : 256);
-        uint64_t wgs = (nblocks + kZwThreads - 1) / kZwThreads;
+        uint64_t wgs = (nblocks + kZwD * (kZwThreads / 64) - 1) / (kZwD * (kZwThreads / 64));
         wgs = wgs < most ? wgs : most;
         hipLaunchKernelGGL(k_zl_wide, dim3((uint32_t)wgs), dim3(kZwThreads), kZwLds, st, a);
         uint64_t vgs = (nblocks + kZvThreads / 64 - 1) / (kZvThreads / 64);
