@@ -77,7 +77,8 @@ def main():
                          "write_bytes = 1024 * WRITE_SIZE",
            "per_dispatch": {}}
     for k in sorted(set(fetch) | set(write)):
-        if not k.startswith("k_"):
+        # (bench.py's own copy-ceiling probes, k_diag_*, run in the same process: not the encode)
+        if not k.startswith("k_") or k.startswith("k_diag"):
             continue
         rd, wr = 2048.0 * fetch.get(k, 0.0), 1024.0 * write.get(k, 0.0)
         out["per_dispatch"][k] = {"read_bytes": round(rd), "write_bytes": round(wr), "traffic_bytes": round(rd + wr)}
