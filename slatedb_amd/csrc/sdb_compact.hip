@@ -470,39 +470,93 @@ SDB_DEV void chunk_store(const Chunk &c, uint8_t *dst, uint32_t n) {
     if (b2) *(u16_u *)(dst + o + b4) = (uint16_t)(t >> (8 * b4));
     if (n & 1) dst[o + b4 + b2] = (uint8_t)(t >> (8 * (b4 + b2)));
 }
+// The unconditional form of a lane chunk (a load under a branch makes the compiler wait for every earlier
+// load at the join, so the chunks of eight entries went out one at a time): a range of >= 16 bytes reads
+// the 16 bytes at x, or for its tail the 16 ending at its end (shifted down at the store); a lane with no
+// chunk, or a range under 16 bytes, reads g_safe16 and (the latter) copies piecewise afterwards.
+__device__ uint4 g_safe16;
+SDB_DEV const uint8_t *chunk_src(const uint8_t *src, uint32_t len, uint32_t x) {
+    const bool live = x < len && len >= 16;
+    return live ? src + (x + 16 <= len ? x : len - 16) : (const uint8_t *)&g_safe16;
+}
+// global (not flat) accesses: a flat access also counts on lgkmcnt, so every LDS descriptor read after the
+// stores waited for all of them
+typedef __attribute__((address_space(1))) u32x4_u g_u32x4_u;
+typedef __attribute__((address_space(1))) u64_u g_u64_u;
+typedef __attribute__((address_space(1))) u32_u g_u32_u;
+typedef __attribute__((address_space(1))) u16_u g_u16_u;
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+SDB_DEV u32x4_u chunk_ld(const uint8_t *p) { return *(const g_u32x4_u *)(uintptr_t)p; }
+SDB_DEV void chunk_store_g(const Chunk &c, uint8_t *dst0, uint32_t n) {
+    const uintptr_t dst = (uintptr_t)dst0;
+    if (n >= 16) {
+        u32x4_u v;
+        v.x = (uint32_t)c.lo, v.y = (uint32_t)(c.lo >> 32), v.z = (uint32_t)c.hi, v.w = (uint32_t)(c.hi >> 32);
+        *(g_u32x4_u *)dst = v;
+        return;
+    }
+    const uint32_t o = n & 8, b4 = n & 4, b2 = n & 2;
+    if (o) *(g_u64_u *)dst = c.lo;
+    const uint64_t t = o ? c.hi : c.lo;
+    if (b4) *(g_u32_u *)(dst + o) = (uint32_t)t;
+    if (b2) *(g_u16_u *)(dst + o + b4) = (uint16_t)(t >> (8 * b4));
+    if (n & 1) *(g_u8 *)(dst + o + b4 + b2) = (uint8_t)(t >> (8 * (b4 + b2)));
+}
+// store bytes [x, min(len, x + 16)) of the range from the chunk_src window w
+SDB_DEV void chunk_put(const u32x4_u &w, const uint8_t *src, uint8_t *dst, uint32_t len, uint32_t x) {
+    if (x >= len) return;
+    const uint32_t n = len - x < 16 ? len - x : 16;
+    if (len < 16) {  // a short range: exact pieces (rare for keys and values)
+        Chunk c;
+        chunk_load(c, src + x, n);
+        chunk_store(c, dst + x, n);
+        return;
+    }
+    uint64_t lo = (uint64_t)w.x | ((uint64_t)w.y << 32), hi = (uint64_t)w.z | ((uint64_t)w.w << 32);
+    const uint32_t sh = 16 - n;  // bytes of the window before x (a tail window ends at len)
+    if (sh >= 8) {
+        lo = hi >> (8 * (sh - 8));
+        hi = 0;
+    } else if (sh) {
+        lo = (lo >> (8 * sh)) | (hi << (64 - 8 * sh));
+        hi >>= 8 * sh;
+    }
+    Chunk c;
+    c.lo = lo;
+    c.hi = hi;
+    chunk_store_g(c, dst + x, n);
+}
 // lane chunk x of every listed entry's key and value bytes: all sixteen loads, then the stores
 SDB_DEV void copy_group_chunks_kv(const CopyDesc *cd, uint32_t l, uint32_t x) {
-    Chunk ck[8], cv[8];
+    u32x4_u ck[8], cv[8];
 #pragma unroll
     for (uint32_t q = 0; q < 8; q++) {
         const CopyDesc &c = cd[8 * q + (l >> 3)];
-        if (x < c.kb) chunk_load(ck[q], c.ks + x, c.kb - x < 16 ? c.kb - x : 16);
-        if (x < c.vb) chunk_load(cv[q], c.vs + x, c.vb - x < 16 ? c.vb - x : 16);
+        ck[q] = chunk_ld(chunk_src(c.ks, c.kb, x));
+        cv[q] = chunk_ld(chunk_src(c.vs, c.vb, x));
     }
     asm volatile("" ::: "memory");  // re-read the descriptors from LDS rather than hold 8 of them
 #pragma unroll
     for (uint32_t q = 0; q < 8; q++) {
         const CopyDesc &c = cd[8 * q + (l >> 3)];
-        if (x < c.kb) chunk_store(ck[q], c.kd + x, c.kb - x < 16 ? c.kb - x : 16);
-        if (x < c.vb) chunk_store(cv[q], c.vd + x, c.vb - x < 16 ? c.vb - x : 16);
+        chunk_put(ck[q], c.ks, c.kd, c.kb, x);
+        chunk_put(cv[q], c.vs, c.vd, c.vb, x);
     }
 }
 // lane chunk x of every listed entry's key (K) or value bytes: all eight loads, then the stores
 template <bool K>
 SDB_DEV void copy_group_chunks(const CopyDesc *cd, uint32_t l, uint32_t x) {
-    Chunk ch[8];
+    u32x4_u ch[8];
 #pragma unroll
     for (uint32_t q = 0; q < 8; q++) {
         const CopyDesc &c = cd[8 * q + (l >> 3)];
-        const uint32_t len = K ? c.kb : c.vb;
-        if (x < len) chunk_load(ch[q], (K ? c.ks : c.vs) + x, len - x < 16 ? len - x : 16);
+        ch[q] = chunk_ld(chunk_src(K ? c.ks : c.vs, K ? c.kb : c.vb, x));
     }
     asm volatile("" ::: "memory");
 #pragma unroll
     for (uint32_t q = 0; q < 8; q++) {
         const CopyDesc &c = cd[8 * q + (l >> 3)];
-        const uint32_t len = K ? c.kb : c.vb;
-        if (x < len) chunk_store(ch[q], (K ? c.kd : c.vd) + x, len - x < 16 ? len - x : 16);
+        chunk_put(ch[q], K ? c.ks : c.vs, K ? c.kd : c.vd, K ? c.kb : c.vb, x);
     }
 }
 
