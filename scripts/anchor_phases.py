@@ -1,0 +1,31 @@
+"""Diagnostic: k_anchor's phase marks (row 1023 of the -DSDB_PHASE_TIMING build's phase table) for one SST
+of N D1 entries (env N, default 2,314,096: a 256 MiB compaction output).  SDB_LIBRARY=libslatedb_amd_pt.so."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from slatedb_amd import datasets, runtime  # noqa: E402
+
+n = int(os.environ.get("N", "2314096"))
+prm = runtime.params(block_size=4096, sst_version=2, restart_interval=16, bloom_bits_per_key=10)
+h = datasets.d1(sst_index=1, n=n)
+dev = torch.device("cuda", 0)
+db = h.to_device(dev)
+out = runtime.DeviceSstOutput(h.n, h.logical_bytes(), h.logical_bytes(), prm, device=dev)
+cdll = C.CDLL(runtime.LIB_PATH)
+cdll.sdb_diag_phase_times.argtypes = [C.c_void_p, C.c_int]
+buf = (C.c_uint64 * (8 * 1024))()
+rows = []
+for it in range(6):
+    runtime.encode_sst_device(db, out)
+    torch.cuda.synchronize()
+    assert cdll.sdb_diag_phase_times(C.addressof(buf), 1024) == 0
+    r = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 8)[1023].astype(np.int64)
+    rows.append(np.diff(r[:6]))
+rows = np.array(rows[1:])
+print({"entries": n, "chunks": (n + 2047) // 2048, "phase_ticks_median": [int(x) for x in np.median(rows, axis=0)],
+       "total_median": int(np.median(rows.sum(axis=1)))})

@@ -1222,6 +1222,7 @@ __global__ __launch_bounds__(kAnchorThreads) void k_anchor(SstSet P) {
         }
     }
     __syncthreads();
+    if (blockIdx.y == 0) PHASE_MARK_AT(1023, 0);
     const uint32_t W = s_W;
     const bool fast = W >= 1 && W <= a.seg_look;
     sdb_sst_summary *sm = a.summary;
@@ -1410,6 +1411,7 @@ __global__ __launch_bounds__(kAnchorThreads) void k_anchor(SstSet P) {
                 __builtin_amdgcn_s_waitcnt(0xC07F);
             }
             __syncthreads();
+            if (blockIdx.y == 0) PHASE_MARK_AT(1023, 1);
             if (tid == 0) {  // the groups from entry 0
                 uint32_t e = 0;
                 for (uint32_t q = 0; q < ngs; q++) {
@@ -1423,6 +1425,7 @@ __global__ __launch_bounds__(kAnchorThreads) void k_anchor(SstSet P) {
                 }
             }
             __syncthreads();
+            if (blockIdx.y == 0) PHASE_MARK_AT(1023, 2);
             for (uint32_t q = wv; q < ngs; q += kSW) {  // each group's chunks from its entry
                 stage_group(q);
                 if (ln == 0) {
@@ -1505,6 +1508,7 @@ __global__ __launch_bounds__(kAnchorThreads) void k_anchor(SstSet P) {
             }
         }
     }
+    if (blockIdx.y == 0) PHASE_MARK_AT(1023, 3);
     if (tid == 0) {
         a.anchor_e[K] = (uint32_t)a.n;
         a.anchor_blk[K] = (uint32_t)tb;
