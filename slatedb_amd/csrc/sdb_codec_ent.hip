@@ -458,15 +458,29 @@ __constant__ uint8_t c_cl_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 
 
 enum { kZOk = 0, kZTrunc = 1, kZErr = -1, kZDyn = 2 };
 
-// deflate's fixed code (RFC 1951 3.2.6) in t: the lengths, canonical tables and fast tables
-SDB_DEV void zl_fixed_tables(ZTab &t) {
-    uint8_t *lens = t.lens;
-    for (int i = 0; i < 288; i++) lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
-    for (int i = 0; i < 32; i++) lens[288 + i] = 5;
-    canon_build(t.lit, lens, 288);
-    canon_build(t.dist, lens + 288, 32);
-    canon_fast<kFastLit>(t.lit, t.fast_lit);
-    canon_fast<kFastDist>(t.dist, t.fast_dist);
+// deflate's fixed code (RFC 1951 3.2.6) in t, written by the whole workgroup (tid of nt) in closed form: the
+// canonical codes of the fixed lengths are 7-bit 0..23 (symbols 256..279), 8-bit 48..191 (0..143) and
+// 192..199 (280..287), 9-bit 400..511 (144..255), distances 5-bit 0..31; a fast-table index read LSB first
+// is the code's bits reversed
+SDB_DEV void zl_fixed_tables(ZTab &t, uint32_t tid, uint32_t nt) {
+    for (uint32_t i = tid; i < (1u << kFastLit); i += nt) {
+        const uint32_t r9 = __builtin_bitreverse32(i) >> 23, p8 = r9 >> 1;
+        uint32_t e;
+        if (r9 < 96) e = (256 + (r9 >> 2)) | 7u << 12;
+        else if (p8 < 192) e = (p8 - 48) | 8u << 12;
+        else if (p8 < 200) e = (280 + p8 - 192) | 8u << 12;
+        else e = (144 + r9 - 400) | 9u << 12;
+        t.fast_lit[i] = (uint16_t)e;
+    }
+    for (uint32_t i = tid; i < (1u << kFastDist); i += nt)
+        t.fast_dist[i] = (uint16_t)((__builtin_bitreverse32(i & 31) >> 27) | 5u << 12);
+    for (uint32_t j = tid; j < 288; j += nt)  // by length, then symbol
+        t.lit.sym[j] = (uint16_t)(j < 24 ? 256 + j : j < 168 ? j - 24 : j < 176 ? 280 + j - 168 : 144 + j - 176);
+    for (uint32_t j = tid; j < 32; j += nt) t.dist.sym[j] = (uint16_t)j;
+    for (uint32_t l = tid; l < 16; l += nt) {
+        t.lit.count[l] = (uint16_t)(l == 7 ? 24 : l == 8 ? 152 : l == 9 ? 112 : 0);
+        t.dist.count[l] = (uint16_t)(l == 5 ? 32 : 0);
+    }
 }
 
 // SHARED: t holds the fixed code's tables (zl_fixed_tables), read-only and shared by the decoders of a
@@ -1993,7 +2007,7 @@ __global__ __launch_bounds__(kZpThreads) void k_zl_run_multi(EntArgs a) {
 }
 
 // The wide pass (decode-once's first): every lane of the wave inflates a block of its own against the
-// fixed code's tables, copied once per workgroup into LDS, so the decoders per CU are bounded by waves,
+// fixed code's tables, written once per workgroup into LDS, so the decoders per CU are bounded by waves,
 // not by LDS (70 with a table set each).  It only decodes: each lane records its block's result in
 // a.wres, and k_zl_verify then checks the stored CRC and the Adler-32 and appends the output CRC with one
 // wave per block (the wave-wide checks of 64 blocks in a row would leave each wave waiting on memory
@@ -2007,10 +2021,6 @@ constexpr uint32_t kZwD = SDB_ZL_WIDE_D;
 constexpr uint32_t kZwThreads = 256, kZwRing = 256 * 64;  // a wave's history rings (EntOutRing)
 constexpr uint32_t kZwLds = kZpTab + (kZwThreads / 64) * kZwRing;
 static_assert(kZpTab % 16 == 0, "ZTab copies as 16-byte words");
-__device__ ZTab g_zl_fixed;  // the fixed code's tables (k_zl_fixed_init, once per device)
-__global__ void k_zl_fixed_init() {
-    if (threadIdx.x == 0) zl_fixed_tables(g_zl_fixed);
-}
 // wres[2 b] = output length | code << 48 (kWrOk, kWrErr: the decode failed, kWrCap: the slot is past out_cap,
 // kWrOther: another pass owns the block); wres[2 b + 1] = Adler-32 wanted | have << 32
 enum : uint64_t { kWrOk = 0, kWrErr = 1, kWrCap = 2, kWrOther = 3 };
@@ -2018,7 +2028,7 @@ __global__ __launch_bounds__(kZwThreads) void k_zl_wide(EntArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t l = (uint32_t)lane_id(), wave = threadIdx.x >> 6;
     ZTab &t = *(ZTab *)smem;
-    for (uint32_t q = threadIdx.x; q < kZpTab / 16; q += blockDim.x) ((uint4 *)&t)[q] = ((const uint4 *)&g_zl_fixed)[q];
+    zl_fixed_tables(t, threadIdx.x, blockDim.x);
     __syncthreads();
     const uint64_t n = a.nblocks;
     // kZwD decoding lanes per wave (the rest idle): fewer lanes, more waves to overlap the refill latency
@@ -2296,19 +2306,6 @@ hipError_t launch_zl_once_run(int mode, const uint8_t *blocks, const uint64_t *b
     if (nblocks && mode == 1) {
         int dev = 0, cus = 0;
         (void)hipGetDevice(&dev);
-        static std::atomic<bool> fixed_ready[64];
-        const bool tracked = dev >= 0 && dev < 64;
-        if (!tracked) {
-            hipLaunchKernelGGL(k_zl_fixed_init, dim3(1), dim3(64), 0, st);  // (stream-ordered before the run)
-        } else if (!fixed_ready[dev].load()) {  // the shared tables, once per device
-            static std::mutex mu;
-            std::lock_guard<std::mutex> g(mu);
-            if (!fixed_ready[dev].load()) {
-                hipLaunchKernelGGL(k_zl_fixed_init, dim3(1), dim3(64), 0, st);
-                if (hipStreamSynchronize(st) != hipSuccess) return hipGetLastError();
-                fixed_ready[dev].store(true);
-            }
-        }
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const uint64_t most = 8ull * (cus > 0 ? cus : 256);
         uint64_t wgs = (nblocks + kZwD * (kZwThreads / 64) - 1) / (kZwD * (kZwThreads / 64));
