@@ -44,6 +44,7 @@ struct MergeArgs {
     uint8_t *start;              // merged position: first version of its key
     uint8_t *dec;                // merged position: 0 drop, 1 keep, 2 keep as a tombstone
     uint64_t *tile_sum;          // per tile: kept entries, key bytes, value bytes (exclusive offsets after k_mg_scan)
+    uint64_t *bound;             // per 256 entries (k_mg_rank workgroup) and side: the first / last entry's count in each run
     unsigned long long *err;     // run order violations: min (global entry << 8 | code)
     unsigned long long *err_merge;  // merge operands (MergeOperatorRequiredIterator): min merged position << 8 | code
     unsigned long long *metric;  // expired values, expired merges
@@ -53,7 +54,7 @@ struct MergeArgs {
 static_assert(sizeof(MergeArgs) < 4000, "MergeArgs is passed as kernel arguments");
 
 struct MergeWorkspace {
-    uint64_t pfx, perm, start, dec, tile_sum, err, err_merge, metric, lcp0, total;
+    uint64_t pfx, perm, start, dec, tile_sum, bound, err, err_merge, metric, lcp0, total;
 };
 inline MergeWorkspace merge_workspace_layout(uint64_t total) {
     MergeWorkspace w{};
@@ -69,6 +70,7 @@ inline MergeWorkspace merge_workspace_layout(uint64_t total) {
     w.start = take(total + 1);
     w.dec = take(total + 1);
     w.tile_sum = take(24 * (ntiles + 1));
+    w.bound = take(16 * (uint64_t)kMaxRuns * ((total + 255) / 256 + 1));  // k_mg_bounds: 2 x runs per 256 entries
     w.err = take(8);
     w.err_merge = take(8);
     w.metric = take(16);

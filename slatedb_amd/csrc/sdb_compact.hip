@@ -159,11 +159,66 @@ SDB_DEV uint64_t rank_in(const MergeArgs &a, uint32_t r2, uint32_t r, uint64_t p
     return lo;
 }
 
+// rank_in over a window whose prefixes are staged in LDS (w: the window's a.pfx values, from run index lo):
+// a step whose prefix differs from the key's is decided in LDS, a tie compares the full keys and seqs in
+// HBM as rank_in does
+SDB_DEV uint64_t rank_in_lds(const MergeArgs &a, uint32_t r2, uint32_t r, uint64_t pk, const KeyAt &k, uint64_t sq,
+                             uint32_t L0, uint64_t lo, uint64_t hi, const uint64_t *w) {
+    const RunDesc &Q = a.r[r2];
+    const uint64_t base = lo;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        const uint64_t pm = w[mid - base];
+        bool before;
+        if (pm != pk) {
+            before = pm < pk;
+        } else {
+            const KeyAt f = key_at(Q, mid);
+            const int c = cmp_key(pm, f.p, f.n, pk, k.p, k.n, L0);
+            before = c < 0;
+            if (c == 0) {
+                const uint64_t s2 = Q.seq[mid];
+                before = s2 > sq || (s2 == sq && r2 < r);
+            }
+        }
+        if (before) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
 // Merged position = own index + the entries of every other run that come before.  A workgroup's
 // entries are consecutive in one run, so their counts in run r2 lie between those of its first and
-// last entry: two full binary searches per workgroup and run, then each entry searches that window.
+// last entry: two full binary searches per workgroup and run, then each entry searches that window —
+// in LDS when the windows' prefixes fit (kRankLds; staged with coalesced loads), so a search step is an
+// LDS read instead of a dependent HBM gather.
+constexpr uint32_t kRankLds = 16 * 1024;
+// The two full searches of every k_mg_rank workgroup and run, one thread each, all in flight at once (inside
+// the rank workgroups each one was a 20-step chain of dependent gathers in front of the workgroup's work):
+// bound[(b * 2 + side) * nruns + r2] = the count in run r2 of workgroup b's first (side 0) / last entry.
+__global__ __launch_bounds__(256) void k_mg_bounds(MergeArgs a) {
+    if (*a.err != ~0ull) return;
+    const uint64_t gb = (a.total + kPfxThreads - 1) / kPfxThreads, nr = a.nruns;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, q = t / nr;
+    const uint32_t r2 = (uint32_t)(t - q * nr), side = (uint32_t)(q & 1);
+    const uint64_t b = q >> 1;
+    if (b >= gb) return;
+    const uint64_t g0 = b * kPfxThreads, gl = (g0 + kPfxThreads < a.total ? g0 + kPfxThreads : a.total) - 1;
+    const uint64_t ge = side ? gl : g0;
+    const uint32_t r = run_of(a, ge);
+    uint64_t v = 0;
+    if (r2 != r) {
+        const RunDesc &R = a.r[r];
+        const uint64_t i = ge - R.base;
+        v = rank_in(a, r2, r, a.pfx[ge], key_at(R, i), R.seq[i], *a.lcp0, 0, a.r[r2].n);
+    }
+    a.bound[t] = v;
+}
+
 __global__ __launch_bounds__(kPfxThreads) void k_mg_rank(MergeArgs a) {
     __shared__ uint64_t s_win[2][kMaxRuns];
+    __shared__ uint64_t s_pf[kRankLds / 8];
+    __shared__ uint32_t s_woff[kMaxRuns];  // window r2's offset in s_pf (~0: searched in HBM)
     if (*a.err != ~0ull) return;
     const uint64_t g0 = (uint64_t)blockIdx.x * kPfxThreads;
     const uint64_t gl = (g0 + kPfxThreads < a.total ? g0 + kPfxThreads : a.total) - 1;
@@ -171,13 +226,27 @@ __global__ __launch_bounds__(kPfxThreads) void k_mg_rank(MergeArgs a) {
     const bool one_run = run_of(a, gl) == r;  // uniform
     const uint32_t L0 = *a.lcp0;
     if (one_run) {
-        // thread t < nruns: the first entry's count in run t; thread 64 + t: the last entry's
+        // thread t < nruns: the first entry's count in run t; thread 64 + t: the last entry's (k_mg_bounds)
         const uint32_t side = tid >> 6, r2 = tid & 63;
-        if (side < 2 && r2 < a.nruns && r2 != r) {
-            const uint64_t ge = side ? gl : g0;
-            const RunDesc &R = a.r[r];
-            const uint64_t i = ge - R.base;
-            s_win[side][r2] = rank_in(a, r2, r, a.pfx[ge], key_at(R, i), R.seq[i], L0, 0, a.r[r2].n);
+        if (side < 2 && r2 < a.nruns && r2 != r) s_win[side][r2] = a.bound[((uint64_t)blockIdx.x * 2 + side) * a.nruns + r2];
+        __syncthreads();
+        if (tid == 0) {  // pack the windows that fit
+            uint32_t off = 0;
+            for (uint32_t r2 = 0; r2 < a.nruns; r2++) {
+                const uint64_t c = r2 == r ? 0 : s_win[1][r2] - s_win[0][r2];
+                s_woff[r2] = ~0u;
+                if (r2 != r && off + c <= kRankLds / 8) {
+                    s_woff[r2] = off;
+                    off += (uint32_t)c;
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t r2 = 0; r2 < a.nruns; r2++) {  // (uniform)
+            const uint32_t off = s_woff[r2];
+            if (off == ~0u) continue;
+            const uint64_t lo = s_win[0][r2], c = s_win[1][r2] - lo, b = a.r[r2].base + lo;
+            for (uint64_t x = tid; x < c; x += kPfxThreads) s_pf[off + x] = a.pfx[b + x];
         }
         __syncthreads();
     }
@@ -192,7 +261,9 @@ __global__ __launch_bounds__(kPfxThreads) void k_mg_rank(MergeArgs a) {
     for (uint32_t r2 = 0; r2 < a.nruns; r2++) {
         if (r2 == rg) continue;
         const uint64_t lo = one_run ? s_win[0][r2] : 0, hi = one_run ? s_win[1][r2] : a.r[r2].n;
-        pos += rank_in(a, r2, rg, pk, k, sq, L0, lo, hi);
+        const uint32_t off = one_run ? s_woff[r2] : ~0u;
+        pos += off != ~0u ? rank_in_lds(a, r2, rg, pk, k, sq, L0, lo, hi, s_pf + off)
+                          : rank_in(a, r2, rg, pk, k, sq, L0, lo, hi);
     }
     a.perm[pos] = g;
 }
@@ -986,6 +1057,7 @@ sdb_status build_merge_args(const sdb_run *runs, uint32_t nruns, const sdb_reten
     a.start = ws + w.start;
     a.dec = ws + w.dec;
     a.tile_sum = (uint64_t *)(ws + w.tile_sum);
+    a.bound = (uint64_t *)(ws + w.bound);
     a.err = (unsigned long long *)(ws + w.err);
     a.err_merge = (unsigned long long *)(ws + w.err_merge);
     a.metric = (unsigned long long *)(ws + w.metric);
@@ -1001,6 +1073,8 @@ hipError_t launch_merge(const MergeArgs &a, bool emit, hipStream_t st) {
     if (gb) {
         hipLaunchKernelGGL(k_mg_lcp0, dim3(1), dim3(256), 0, st, a);
         hipLaunchKernelGGL(k_mg_prefix, dim3(gb), dim3(kPfxThreads), 0, st, a);
+        const uint64_t nb = (uint64_t)gb * 2 * a.nruns;
+        hipLaunchKernelGGL(k_mg_bounds, dim3((uint32_t)((nb + 255) / 256)), dim3(256), 0, st, a);
         hipLaunchKernelGGL(k_mg_rank, dim3(gb), dim3(kPfxThreads), 0, st, a);
         hipLaunchKernelGGL(k_mg_keys, dim3(gb), dim3(kPfxThreads), 0, st, a);
     }
