@@ -483,6 +483,9 @@ SDB_DEV void zl_fixed_tables(ZTab &t, uint32_t tid, uint32_t nt) {
     }
 }
 
+#ifndef SDB_ZL_UNIFORM_REFILL
+#define SDB_ZL_UNIFORM_REFILL 1
+#endif
 // SHARED: t holds the fixed code's tables (zl_fixed_tables), read-only and shared by the decoders of a
 // workgroup; a dynamic-Huffman block returns kZDyn (its decoder has no tables of its own)
 template <bool SHARED = false, class Out>
@@ -588,7 +591,7 @@ SDB_DEV int inflate_raw(LsbBits &s, Out &o, ZTab &t) {
         // a symbol through the fast table (mask: its size - 1) when its code is short enough and the bits
         // are there
         auto fast_decode = [&](const uint16_t *fast, uint32_t mask, const auto &h) -> int {
-            if constexpr (SHARED) {
+            if constexpr (SHARED || SDB_ZL_UNIFORM_REFILL) {
                 // a wave of decoders: when any lane runs low, every lane here refills and stores its pending
                 // output bytes, so the loads and stores a refill's wait covers were issued a refill ago
                 // (lane by lane, some lane's fresh load or store would be waited on at every symbol)
