@@ -486,6 +486,9 @@ SDB_DEV void zl_fixed_tables(ZTab &t, uint32_t tid, uint32_t nt) {
 #ifndef SDB_ZL_UNIFORM_REFILL
 #define SDB_ZL_UNIFORM_REFILL 1
 #endif
+#ifndef SDB_ZL_REFILL_AT
+#define SDB_ZL_REFILL_AT 9  // (bits under which a wave refills: a literal / length code needs at most 9 here)
+#endif
 // SHARED: t holds the fixed code's tables (zl_fixed_tables), read-only and shared by the decoders of a
 // workgroup; a dynamic-Huffman block returns kZDyn (its decoder has no tables of its own)
 template <bool SHARED = false, class Out>
@@ -595,7 +598,7 @@ SDB_DEV int inflate_raw(LsbBits &s, Out &o, ZTab &t) {
                 // a wave of decoders: when any lane runs low, every lane here refills and stores its pending
                 // output bytes, so the loads and stores a refill's wait covers were issued a refill ago
                 // (lane by lane, some lane's fresh load or store would be waited on at every symbol)
-                if (__ballot(s.cnt < 9)) {
+                if (__ballot(s.cnt < SDB_ZL_REFILL_AT)) {
                     s.refill();
                     o.flush();
                 }
