@@ -622,6 +622,109 @@ def codec_bench(reps):
                                            "canonical_lib_GiB_per_s_1_thread": canon}}), flush=True)
 
 
+def _encoded_blocks(batches, dev):
+    """Encode batches on the device (4 KiB V2 blocks, no filter); returns the concatenated data section and
+    the block offsets (one run of blocks)."""
+    prm = runtime.params(block_size=4096, sst_version=2, bloom_bits_per_key=0)
+    datas, offs, base = [], [], 0
+    for j, h in enumerate(batches):
+        db = h.to_device(dev)
+        out = runtime.DeviceSstOutput(h.n, h.logical_bytes(), h.logical_bytes(), prm, device=dev)
+        runtime.encode_sst_device(db, out)
+        torch.cuda.synchronize()
+        r = out.to_host()
+        datas.append(r["data"])
+        bo = r["block_off"].astype(np.uint64)
+        offs.append((bo[:-1] if j < len(batches) - 1 else bo) + np.uint64(base))
+        base += int(r["data"].size)
+        del db, out
+    return np.concatenate(datas), np.concatenate(offs)
+
+
+def compress_bench(reps, sets=("d1", "text")):
+    """f3 write side: sdb_compress_blocks over 4 D1 SSTs (random values) and over a compressible set
+    (datasets.text_kv: JSON documents, ~60 MiB), every codec.  Device bytes and ratio beside the canonical
+    library's on the same blocks (zstd level 3 = zstd::bulk::compress(data, 3); zlib level 6 = flate2's
+    default; pyarrow LZ4 raw / Snappy), sampled every 4th block; device GB/s by HIP events; the canonical
+    library's one-thread speed as the CPU baseline.  Validity: every block of the device output decompresses
+    (device decompressor) to the input."""
+    import zlib
+    import pyarrow as pa
+    from oracle import oracle as O
+    lib = runtime.lib()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(device=dev)
+    canon = {O.CODEC_LZ4: pa.Codec("lz4_raw"), O.CODEC_SNAPPY: pa.Codec("snappy"),
+             O.CODEC_ZSTD: pa.Codec("zstd", compression_level=3)}
+    only = os.environ.get("SDB_CODECS", "lz4,snappy,zlib,zstd").split(",")
+    sets = os.environ.get("SDB_SETS", ",".join(sets)).split(",")
+    for name in sets:
+        if name == "d1":
+            batches = [datasets.d1(sst_index=j) for j in range(4)]
+        else:
+            batches = [datasets.text_kv(n=200_000, seed=11 + j) for j in range(2)]
+        data, block_off = _encoded_blocks(batches, dev)
+        del batches
+        nb = len(block_off) - 1
+        in_bytes = int(block_off[-1] - block_off[0])
+        dd = torch.from_numpy(np.concatenate([data, np.zeros(64, np.uint8)])).to(dev)
+        db = torch.from_numpy(block_off.view(np.int64)).to(dev)
+        sample = range(0, nb, 4)
+        raws = [data[int(block_off[k]):int(block_off[k + 1]) - 4].tobytes() for k in sample]
+        for codec, cname in ((O.CODEC_LZ4, "lz4"), (O.CODEC_SNAPPY, "snappy"), (O.CODEC_ZLIB, "zlib"), (O.CODEC_ZSTD, "zstd")):
+            if cname not in only:
+                continue
+            with torch.cuda.stream(s):
+                out, out_off, err = runtime.compress_blocks_device(codec, dd, db, stream=s)
+            torch.cuda.synchronize()
+            ok_err = int(err.item()) == -1
+            ws = torch.empty(int(lib.sdb_compress_workspace_bytes(nb, in_bytes)), dtype=torch.uint8, device=dev)
+            cap = out.numel() - 16
+
+            def run():
+                if lib.sdb_compress_blocks(codec, dd.data_ptr(), db.data_ptr(), nb, in_bytes, out.data_ptr(), cap,
+                                           out_off.data_ptr(), err.data_ptr(), ws.data_ptr(), ws.numel(), s.cuda_stream):
+                    raise RuntimeError("sdb_compress_blocks")
+
+            with torch.cuda.stream(s):
+                ms = timed(run, reps, s)
+            coff = out_off.cpu().numpy().view(np.uint64)
+            total = int(coff[nb])
+            # validity: the device decompressor restores every block
+            with torch.cuda.stream(s):
+                o, st, en, derr = runtime.decompress_blocks_device(codec, out[:total + 64].contiguous(), out_off, stream=s)
+            torch.cuda.synchronize()
+            ok = ok_err and int(derr.item()) == -1 and int(st[nb].item()) == data.size and \
+                np.array_equal(o[:data.size].cpu().numpy(), data)
+            # the canonical library on the sampled blocks (+ the same framing: lz4 size prefix, CRC)
+            t0 = time.perf_counter()
+            lib_bytes = 0
+            for x in raws:
+                if codec == O.CODEC_ZLIB:
+                    c = zlib.compress(x, 6)
+                else:
+                    c = canon[codec].compress(x, asbytes=True)
+                lib_bytes += len(c) + 4 + (4 if codec == O.CODEC_LZ4 else 0)
+            cpu_s = time.perf_counter() - t0
+            raw_bytes = sum(len(x) + 4 for x in raws)
+            dev_bytes = int(sum(int(coff[k + 1] - coff[k]) for k in sample))
+            print(json.dumps({
+                "what": "f3 compress (%s) of %s" % (cname, "4 D1 SSTs" if name == "d1" else "text_kv (JSON values)"),
+                "blocks": nb, "input_bytes": in_bytes, "compressed_bytes": total, "ratio_device": round(in_bytes / total, 4),
+                "sample_blocks": len(raws), "sample_ratio_device": round(raw_bytes / dev_bytes, 4),
+                "sample_ratio_library": round(raw_bytes / lib_bytes, 4),
+                "device_over_library_bytes": round(dev_bytes / lib_bytes, 4),
+                "library": {O.CODEC_ZLIB: "zlib level 6", O.CODEC_ZSTD: "zstd level 3 (pyarrow)",
+                            O.CODEC_LZ4: "lz4 raw (pyarrow)", O.CODEC_SNAPPY: "snappy (pyarrow)"}[codec],
+                "ms": round(ms, 4), "GB_per_s": round(in_bytes / (ms * 1e-3) / 1e9, 2),
+                "frac_hbm": round((in_bytes + total) / (ms * 1e-3) / 1e9 / PEAK * 1000 / 1000, 5),
+                "valid_device_roundtrip": bool(ok),
+                "cpu_baseline": {"kind": "canonical library", "GiB_per_s": round(raw_bytes / cpu_s / 2**30, 3), "cores": 1,
+                                 "sample": "every 4th block, %d blocks" % len(raws)}}), flush=True)
+            del out, ws, o
+        del dd, db
+
+
 def lookup_bench(reps):
     """Point lookups (sdb_sst_lookup: bloom -> index partition -> block CRC -> restart search -> seek) of
     1 M keys into one D1 SST (configs[1] shape): half present, half absent (bloom-filtered or seeking past),
@@ -775,6 +878,7 @@ def main():
     p.add_argument("--compact", action="store_true")
     p.add_argument("--hbm", action="store_true")
     p.add_argument("--codec", action="store_true")
+    p.add_argument("--compress", action="store_true", help="f3 write side: device vs canonical library ratio and speed")
     p.add_argument("--lookup", action="store_true")
     p.add_argument("--encode", action="store_true", help="encode D2 and D1-L0 (headline shape)")
     p.add_argument("--footer", action="store_true", help="host footer of one D1 SST (no device)")
@@ -782,7 +886,8 @@ def main():
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--no-granular", action="store_true", help="decode: skip the 2 MiB granularity run")
     a = p.parse_args()
-    allp = not (a.decode or a.bloom or a.e2e or a.compact or a.hbm or a.codec or a.lookup or a.encode or a.footer)
+    allp = not (a.decode or a.bloom or a.e2e or a.compact or a.hbm or a.codec or a.compress or a.lookup or a.encode or
+                a.footer)
     if a.footer or allp:
         footer_bench(max(a.reps, 20))
     if a.footer and not allp:
@@ -799,6 +904,8 @@ def main():
         hbm_bench(a.reps)
     if a.codec or allp:
         codec_bench(max(3, a.reps // 2))
+    if a.compress or allp:
+        compress_bench(max(3, a.reps // 4))
     if a.compact or allp:
         compact_bench(max(3, a.reps // 4))
     if a.lookup or allp:

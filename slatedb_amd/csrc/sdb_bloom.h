@@ -214,7 +214,7 @@ SDB_DEV void bloom_bin_core(uint32_t tile, const uint32_t (&hh)[KPT], const uint
                 const uint32_t c0 = sl < S ? cnt[sc] : 0;
                 c[u] = c0 < cap ? c0 : cap;
                 const uint32_t *src = (const uint32_t *)(bkt + sc * cap);
-                v0[u] = src[l];  // (the granule's tail beyond the run: stale bucket words)
+                v0[u] = 2 * l < cap ? src[l] : 0;  // (the granule's tail beyond the run: stale bucket words)
                 v1[u] = 2 * l + 128 < cap ? src[l + 64] : 0;
             }
 #pragma unroll

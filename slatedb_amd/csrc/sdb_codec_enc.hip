@@ -5,28 +5,35 @@
 // Block::encode(), then the CRC32 (BE) of those compressed bytes:
 //   Lz4    lz4_flex 0.11.6 block::compress_prepend_size: u32 LE length ++ one LZ4 block;
 //   Snappy snap 1.1.1 raw::Encoder::compress_vec: varint length ++ Snappy raw elements;
-//   Zlib   flate2 1.1.9 ZlibEncoder (default level): 78 9C ++ deflate ++ Adler-32 BE;
+//   Zlib   flate2 1.1.9 ZlibEncoder (default level 6): 78 9C ++ deflate ++ Adler-32 BE;
 //   Zstd   zstd 0.13.3 bulk::compress(data, 3): one frame with Frame_Content_Size (single segment).
-// A compressor's output bytes are a choice of its match finder, not of the format: these streams are
-// valid for the formats (they decode through the reference's decompressors — and sdb_decompress_blocks,
-// the oracle, pyarrow / zlib in the tests — to the same block bytes) but are not the crates' bytes.
+// A compressor's output bytes are a choice of its match finder and entropy coder, not of the format:
+// these streams are valid for the formats (they decode through the reference's decompressors — and
+// sdb_decompress_blocks, the oracle, pyarrow / zlib in the tests — to the same block bytes) and compress
+// to within a few per cent of the canonical libraries, but they are not the crates' bytes.
 //
-//   C1 compress  one wave per block (four per workgroup, the block in the wave's LDS):
-//                a. every position's match: a 4-byte hash into a 2048-entry table of the latest earlier
-//                   position (built 64 positions at a time: each lane reads its bucket, then the batch
-//                   stores its positions with ds_max_u32), verified and extended bytewise (<= 258);
-//                b. the greedy parse: one wave-uniform walk over the chosen matches only (lane w holds the
-//                   match bitmap of positions [64 w, 64 w + 64): the next match is one ballot away), the
-//                   sequences (literal run, offset, length) listed in LDS;
-//                c. the codec's elements: lanes size their sequence's elements, a wave scan places them,
-//                   each lane writes its headers / match codes and the wave copies the literal runs;
-//                   deflate as fixed-Huffman codes (bit positions from a prefix count of the literals
-//                   that take 9 bits) or a stored block when that is shorter; zstd as one raw (or RLE)
-//                   block;
-//                d. the wave CRC32 of the compressed bytes (two windows past 4 KiB), the slot written to
-//                   the workspace, its length recorded.
-//                Blocks over 4 KiB (SstBlockSize 8-64 KiB) are written by one lane as literal-only
-//                streams (stored deflate, raw zstd).
+// One wave per block; a block is processed in windows of <= 4 KiB staged in the wave's LDS (one window for
+// the default SstBlockSize):
+//   a. matches: every position's longest match among the earlier positions with the same 4-byte hash
+//      (hash heads and chains built 64 positions at a time with LDS exchanges; zlib / zstd walk a 16-deep chain of
+//      earlier positions, lz4 / snappy take the latest one like lz4_flex / snap), extended 4 bytes a step;
+//   b. the parse: one wave-uniform walk over the match bitmap (lane w holds positions [64 w, 64 w + 64):
+//      the next match is one ballot away), lazy by one position, the sequences (literal run, length,
+//      offset) listed in LDS;
+//   c. the codec's elements:
+//      lz4 / snappy  lanes size their sequence's elements, a wave scan places them, the wave copies the
+//                    literal runs;
+//      zlib          one deflate block per window — dynamic Huffman (wave histograms, code lengths by a
+//                    bitonic sort + Moffat–Katajainen + a Kraft-sum length limit, the code-length code's
+//                    run-length items), fixed Huffman or stored, whichever is shortest; every code's bit
+//                    position from prefix sums of code lengths, ORed into the LDS bitstream;
+//      zstd          one compressed block per window: Huffman literals (direct weights, 1 or 4 streams
+//                    written backwards at suffix-sum bit positions) or raw / RLE literals; sequences with
+//                    repeat offsets, each of the LL / OF / ML codes predefined, RLE or FSE_Compressed
+//                    (normalised counts + the NCount description) by estimated cost, the three FSE state
+//                    machines run side by side on lanes 0-2, their bits placed by a suffix scan;
+//                    a raw or RLE block when that is shorter;
+//   d. the wave CRC32 of the compressed bytes (chained across windows), the slot written, its length.
 //   C2 scan      exclusive scan of the lengths -> out_off (the compressed BlockMeta offsets).
 //   C3 pack      one wave per block: slot -> out[out_off[k], out_off[k+1]).
 #include <mutex>
@@ -38,25 +45,35 @@
 namespace sdb {
 
 typedef __attribute__((address_space(3))) uint16_t lu16;
+typedef __attribute__((address_space(3))) int16_t li16;
+typedef __attribute__((address_space(3))) int32_t li32;
 
-constexpr uint32_t kCzWaves = 4, kCzThreads = 64 * kCzWaves;
-constexpr uint32_t kCzMax = 4096;              // fast path: blocks of at most 4 KiB
+constexpr uint32_t kCzWin = 4096;                   // window: a block of <= 4 KiB is one window
 constexpr uint32_t kCzHashBits = 11;
-constexpr uint32_t kCzIn = kCzMax + 64;        // the block (+ zeros for reads past its end)
-constexpr uint32_t kCzHt = 4u << kCzHashBits;  // hash table (u32 position + 1), then the sequence list
-constexpr uint32_t kCzMm = 4 * kCzMax;         // per position off << 16 | len; then the output (at +64) and
-                                               // zlib's prefix count of 9-bit literals (at +8 KiB)
-constexpr uint32_t kCzWaveLds = kCzIn + kCzHt + kCzMm + 64 * 8;
-constexpr uint32_t kCzLds = kCrcTablesLds + kCzWaves * kCzWaveLds;
-static_assert(kCzLds <= 160 * 1024, "compress LDS");
-constexpr uint32_t kCzMaxSeq = kCzHt / 8 - 8;  // sequences listed per block (the rest stays literal)
-constexpr uint32_t kCzOutOff = 64;             // the output at mm + 64: the CRC's 64 zero lead-in bytes before it
-constexpr uint32_t kCzP9Off = 8192;
+constexpr uint32_t kCzIn = kCzWin + 64;             // the window (+ zeros for reads past its end)
+constexpr uint32_t kCzHead = 4u << kCzHashBits;     // u32 hash heads; after the parse: the sequence list
+constexpr uint32_t kCzPrev = 2 * kCzWin;            // u16 chain (zlib / zstd); after the parse: entropy scratch
+constexpr uint32_t kCzMm = 4 * kCzWin + 128;        // u32 per position; after the parse: out | aux
+constexpr uint32_t kCzOutOff = 64;                  // out at mm + 64 (the CRC's 64 zero lead-in bytes before it)
+constexpr uint32_t kCzAuxOff = 8192;                // aux at mm + 8 KiB: literal mask, code-length prefix sums, FSE records
+constexpr uint32_t kCzOutCap = kCzAuxOff - kCzOutOff;
+constexpr uint32_t kCzMaxSeq = kCzHead / 8;         // a match is >= 4 bytes: a window has <= 1024 sequences
 constexpr uint32_t kCzMaxMatch = 258;
+constexpr uint32_t kCzNice = 128;                   // a chain walk stops at a match this long (zlib level 6)
+
+template <uint32_t C>
+struct CzCfg {
+    static constexpr bool kDeep = C == SDB_CODEC_ZLIB || C == SDB_CODEC_ZSTD;
+    static constexpr uint32_t kWaves = kDeep ? 3 : 4;
+    static constexpr uint32_t kDepth = kDeep ? 16 : 1;
+    static constexpr uint32_t kWaveLds = kCzIn + kCzHead + (kDeep ? kCzPrev : 0) + kCzMm;
+    static constexpr uint32_t kLds = kCrcTablesLds + kWaves * kWaveLds;
+    static_assert(kLds <= 160 * 1024, "compress LDS");
+};
 
 // block k's slot in the workspace (rel = block_off[k] - block_off[0]): compressed bytes + CRC stay under
 // n + n/8 + 48 for every codec here (literal-only worst cases: lz4 n + n/255 + 10, snappy n + 14, stored
-// deflate n + 15, raw zstd n + 16)
+// deflate n + 5 per window + 6, raw zstd n + 3 per window + 12)
 __host__ __device__ inline uint64_t cz_slot(uint64_t rel, uint64_t k) { return (rel + rel / 8 + 64 * k + 15) & ~15ull; }
 
 struct CzArgs {
@@ -64,6 +81,7 @@ struct CzArgs {
     const uint8_t *blocks;
     const uint64_t *block_off;  // nblocks + 1
     uint64_t nblocks;
+    uint64_t in_bytes;          // block_off[nblocks] - block_off[0] may not exceed it (the slots are sized by it)
     uint8_t *slots;             // workspace
     uint64_t *len;              // nblocks + 1: compressed bytes + CRC per block
     uint8_t *out;
@@ -78,69 +96,11 @@ SDB_DEV uint32_t lds_u32u(const lu8 *p, uint32_t i) {  // 4 bytes at any LDS byt
     return __builtin_amdgcn_alignbyte(w[1], w[0], a & 3);
 }
 SDB_DEV uint32_t cz_hash(uint32_t v) { return (v * 2654435761u) >> (32 - kCzHashBits); }
-
-// deflate's fixed Huffman code (RFC 1951 3.2.6) of a literal / length symbol, bit-reversed for the
-// LSB-first stream: value in the low `*nb` bits
-SDB_DEV uint32_t rev_bits(uint32_t v, uint32_t n) { return __builtin_bitreverse32(v) >> (32 - n); }
-SDB_DEV uint32_t fixed_code(uint32_t sym, uint32_t *nb) {
-    if (sym < 144) { *nb = 8; return rev_bits(0x30 + sym, 8); }
-    if (sym < 256) { *nb = 9; return rev_bits(0x190 + sym - 144, 9); }
-    if (sym < 280) { *nb = 7; return rev_bits(sym - 256, 7); }
-    *nb = 8;
-    return rev_bits(0xC0 + sym - 280, 8);
+SDB_DEV uint32_t hibit(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }  // v > 0
+SDB_DEV uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
-__constant__ uint16_t c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                                        31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t c_len_extra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t c_dist_base[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,   65,    97,    129,
-                                         193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t c_dist_extra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
-// a match (len 3..258, dist 1..32768) as fixed-Huffman bits: up to 7 + 5 + 5 + 13 = 30 bits (one u32)
-SDB_DEV uint32_t deflate_match(uint32_t len, uint32_t dist, uint32_t *nb) {
-    uint32_t lc = 0;
-    while (lc < 28 && c_len_base[lc + 1] <= len) lc++;
-    uint32_t dc = 0;
-    while (dc < 29 && c_dist_base[dc + 1] <= dist) dc++;
-    uint32_t n0;
-    uint32_t v = fixed_code(257 + lc, &n0), n = n0;
-    v |= (len - c_len_base[lc]) << n;
-    n += c_len_extra[lc];
-    v |= rev_bits(dc, 5) << n;
-    n += 5;
-    v |= (dist - c_dist_base[dc]) << n;
-    n += c_dist_extra[dc];
-    *nb = n;
-    return v;
-}
-
-// OR `nb` (<= 32) bits `v` into the LDS bitstream `w` (u32 words, zeroed) at bit position `pos`
-SDB_DEV void put_bits(lu32 *w, uint32_t pos, uint32_t v, uint32_t nb) {
-    if (!nb) return;
-    const uint32_t q = pos >> 5, r = pos & 31;
-    __hip_atomic_fetch_or(&w[q], v << r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    if (r + nb > 32) __hip_atomic_fetch_or(&w[q + 1], v >> (32 - r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-}
-
-// crc32fast::hash of out[0, m), m <= 4096 + 1024, by the wave (out 16-byte aligned, the 64 bytes before it
-// zero): [0, min(m, 4096)) in place, the rest (when m > 4096) copied to `sc` (16-byte aligned, 64 free bytes
-// before it), combined by x^(8 (m - 4096))
-SDB_DEV void wsync();
-SDB_DEV uint32_t cz_crc(lu8 *out, uint32_t m, lu8 *sc) {
-    const uint32_t l = (uint32_t)lane_id();
-    const uint32_t head = m > 4096 ? 4096 : m, tail = m - head;
-    if (tail) {
-        if (l < 16) ((lu32 *)(sc - 64))[l] = 0;
-        for (uint32_t i = l; i < tail; i += 64) sc[i] = out[4096 + i];
-    }
-    if (l == 0) ((lu32 *)out)[0] = ~((const lu32 *)out)[0];  // crc32fast's init, folded into bytes [0, 4)
-    wsync();
-    uint32_t raw = wave_crc_image_ra(out, head) ^ 0xFFFFFFFFu;
-    if (tail) raw = crc_shift_bytes(raw, tail) ^ wave_crc_image_ra(sc, tail) ^ 0xFFFFFFFFu;
-    wsync();
-    if (l == 0) ((lu32 *)out)[0] = ~((const lu32 *)out)[0];
-    wsync();
-    return raw ^ 0xFFFFFFFFu;
-}
+SDB_DEV uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
 SDB_DEV void wsync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -148,9 +108,107 @@ SDB_DEV void wsync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// RFC 1951 3.2.5: length / distance code bases and extra bits
+__constant__ uint16_t c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                                        31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t c_len_extra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t c_dist_base[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,   65,    97,    129,
+                                         193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t c_dist_extra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t c_cl_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+// RFC 8878 3.1.1.3.2.1: literal / match length codes, and the predefined distributions (3.1.1.3.2.2)
+__constant__ uint32_t c_zll_base[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,   9,   10,  11,   12,   13,   14,   15,    16,    18,
+                                        20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
+__constant__ uint8_t c_zll_bits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1,
+                                       1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__constant__ uint32_t c_zml_base[53] = {3,  4,  5,  6,  7,  8,  9,  10, 11, 12,  13,  14,  15,   16,   17,   18,   19,    20,
+                                        21, 22, 23, 24, 25, 26, 27, 28, 29, 30,  31,  32,  33,   34,   35,   37,   39,    41,
+                                        43, 47, 51, 59, 67, 83, 99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
+__constant__ uint8_t c_zml_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                       0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__constant__ int16_t c_zdef[3][53] = {
+    {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1},
+    {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+     1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1},
+    {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1}};
+// zstd tables in lane order t: 0 literal lengths, 1 match lengths, 2 offsets
+__constant__ uint8_t c_zdef_n[3] = {36, 53, 29};
+__constant__ uint8_t c_zdef_al[3] = {6, 6, 5};
+
+SDB_DEV uint32_t rev_bits(uint32_t v, uint32_t n) { return __builtin_bitreverse32(v) >> (32 - n); }
+// deflate's fixed Huffman code (RFC 1951 3.2.6) of a literal / length symbol: length, and the code
+// bit-reversed for the LSB-first stream
+SDB_DEV uint32_t fixed_len(uint32_t sym) { return sym < 144 ? 8 : sym < 256 ? 9 : sym < 280 ? 7 : 8; }
+SDB_DEV uint32_t fixed_code(uint32_t sym) {
+    if (sym < 144) return rev_bits(0x30 + sym, 8);
+    if (sym < 256) return rev_bits(0x190 + sym - 144, 9);
+    if (sym < 280) return rev_bits(sym - 256, 7);
+    return rev_bits(0xC0 + sym - 280, 8);
+}
+SDB_DEV uint32_t len_code(uint32_t len) {  // 3..258 -> 0..28
+    uint32_t c = 0;
+    while (c < 28 && c_len_base[c + 1] <= len) c++;
+    return c;
+}
+SDB_DEV uint32_t dist_code(uint32_t d) {  // 1..32768 -> 0..29
+    uint32_t c = 0;
+    while (c < 29 && c_dist_base[c + 1] <= d) c++;
+    return c;
+}
+SDB_DEV uint32_t zll_code(uint32_t v) {
+    if (v < 16) return v;
+    uint32_t c = 16;
+    while (c < 35 && c_zll_base[c + 1] <= v) c++;
+    return c;
+}
+SDB_DEV uint32_t zml_code(uint32_t len) {  // match length >= 3
+    if (len < 35) return len - 3;
+    uint32_t c = 32;
+    while (c < 52 && c_zml_base[c + 1] <= len) c++;
+    return c;
+}
+
+// OR `nb` (<= 32) bits `v` into the LDS bitstream `w` (u32 words, zeroed) at bit position `pos`
+SDB_DEV void put_bits(lu32 *w, uint32_t pos, uint32_t v, uint32_t nb) {
+    if (!nb) return;
+    if (nb < 32) v &= (1u << nb) - 1;
+    const uint32_t q = pos >> 5, r = pos & 31;
+    __hip_atomic_fetch_or(&w[q], v << r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if (r + nb > 32) __hip_atomic_fetch_or(&w[q + 1], v >> (32 - r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+// Raw CRC register (init folded in when `first`, no final inversion) of out[0, m) by the wave: out is 16-byte
+// aligned with 64 zero bytes before it; bytes past 4096 are copied to `sc` (16-byte aligned, 64 free bytes
+// before it).  m <= 4096 + 1024.
+SDB_DEV uint32_t cz_crc_raw(lu8 *out, uint32_t m, lu8 *sc, bool first) {
+    const uint32_t l = (uint32_t)lane_id();
+    if (m < 16) {  // short: lane 0 through the byte table (LDS tables at address 0)
+        uint32_t c = 0;
+        if (l == 0) {
+            const lu32 *t0 = (const lu32 *)(uintptr_t)0;
+            c = first ? 0xFFFFFFFFu : 0u;
+            for (uint32_t i = 0; i < m; i++) c = (c >> 8) ^ t0[(c ^ out[i]) & 0xFF];
+        }
+        return uni(c);
+    }
+    const uint32_t head = m > 4096 ? 4096 : m, tail = m - head;
+    if (tail) {
+        if (l < 16) ((lu32 *)(sc - 64))[l] = 0;
+        for (uint32_t i = l; i < tail; i += 64) sc[i] = out[4096 + i];
+    }
+    if (first && l == 0) ((lu32 *)out)[0] = ~((const lu32 *)out)[0];  // crc32fast's init, folded into bytes [0, 4)
+    wsync();
+    uint32_t raw = wave_crc_image_ra(out, head) ^ 0xFFFFFFFFu;
+    if (tail) raw = crc_shift_bytes(raw, tail) ^ wave_crc_image_ra(sc, tail) ^ 0xFFFFFFFFu;
+    wsync();
+    if (first && l == 0) ((lu32 *)out)[0] = ~((const lu32 *)out)[0];
+    wsync();
+    return raw;
+}
+
 // ------------------------------------------------------------------------------------------------
-// One lane, any size: a literal-only stream of the codec straight into the global slot (blocks over
-// the wave's LDS).  Returns the bytes written (without the CRC).
+// One lane, any size: a literal-only stream of the codec straight into the global slot (lz4 blocks
+// over 4 KiB whose windows find no match to end a sequence).  Returns the bytes written (no CRC).
 // ------------------------------------------------------------------------------------------------
 SDB_DEV uint32_t cz_literal_only(uint32_t codec, const uint8_t *in, uint32_t n, uint8_t *o) {
     uint32_t p = 0;
@@ -168,64 +226,1171 @@ SDB_DEV uint32_t cz_literal_only(uint32_t codec, const uint8_t *in, uint32_t n, 
             o[p++] = (uint8_t)x;
         }
         lit_copy(in, n);
-    } else if (codec == SDB_CODEC_SNAPPY) {
-        for (uint32_t x = n;; x >>= 7) {
-            o[p++] = (uint8_t)(x >= 0x80 ? (x & 0x7F) | 0x80 : x);
-            if (x < 0x80) break;
-        }
-        if (n) {
-            const uint32_t v = n - 1;
-            if (v < 60) o[p++] = (uint8_t)(v << 2);
-            else if (v < 256) { o[p++] = 60 << 2; o[p++] = (uint8_t)v; }
-            else if (v < 65536) { o[p++] = 61 << 2; o[p++] = (uint8_t)v; o[p++] = (uint8_t)(v >> 8); }
-            else if (v < (1u << 24)) { o[p++] = 62 << 2; o[p++] = (uint8_t)v; o[p++] = (uint8_t)(v >> 8); o[p++] = (uint8_t)(v >> 16); }
-            else { o[p++] = 63 << 2; o[p++] = (uint8_t)v; o[p++] = (uint8_t)(v >> 8); o[p++] = (uint8_t)(v >> 16); o[p++] = (uint8_t)(v >> 24); }
-            lit_copy(in, n);
-        }
-    } else if (codec == SDB_CODEC_ZLIB) {
-        o[p++] = 0x78;
-        o[p++] = 0x9C;
-        uint32_t a = 1, b = 0;
-        for (uint32_t i = 0; i < n; i++) {
-            a += in[i];
-            if (a >= 65521) a -= 65521;
-            b += a;
-            if (b >= 65521) b -= 65521;
-        }
-        uint32_t done = 0;
-        do {  // stored blocks of <= 65535 bytes
-            const uint32_t c = n - done < 65535 ? n - done : 65535;
-            o[p++] = done + c == n ? 1 : 0;
-            o[p++] = (uint8_t)c; o[p++] = (uint8_t)(c >> 8);
-            o[p++] = (uint8_t)~c; o[p++] = (uint8_t)(~c >> 8);
-            lit_copy(in + done, c);
-            done += c;
-        } while (done < n);
-        o[p++] = (uint8_t)(b >> 8); o[p++] = (uint8_t)b; o[p++] = (uint8_t)(a >> 8); o[p++] = (uint8_t)a;
-    } else {  // zstd: one frame, raw blocks of <= 128 KiB
-        o[0] = 0x28; o[1] = 0xB5; o[2] = 0x2F; o[3] = 0xFD;
-        p = 4;
-        if (n < 256) { o[p++] = 0x20; o[p++] = (uint8_t)n; }
-        else if (n < 65536 + 256) { o[p++] = 0x60; o[p++] = (uint8_t)(n - 256); o[p++] = (uint8_t)((n - 256) >> 8); }
-        else { o[p++] = 0xA0; o[p++] = (uint8_t)n; o[p++] = (uint8_t)(n >> 8); o[p++] = (uint8_t)(n >> 16); o[p++] = (uint8_t)(n >> 24); }
-        uint32_t done = 0;
-        do {
-            const uint32_t c = n - done < (128u << 10) ? n - done : (128u << 10);
-            const uint32_t bh = (done + c == n ? 1u : 0u) | (c << 3);  // Raw_Block
-            o[p++] = (uint8_t)bh; o[p++] = (uint8_t)(bh >> 8); o[p++] = (uint8_t)(bh >> 16);
-            lit_copy(in + done, c);
-            done += c;
-        } while (done < n);
     }
     return p;
 }
 
 // ------------------------------------------------------------------------------------------------
-// C1: compress.  Lane l of a wave owns: positions l, l + 64, ... in the match pass; sequence l of each
-// 64-sequence chunk in the element pass.
+// a. matches over the staged window [0, wn): mm[p] = off << 16 | len (len >= 4 or 0); the returned
+//    register is lane w's 64-bit match bitmap of positions [64 w, 64 w + 64).  `room` = bytes from the
+//    window start to the block end (lz4's end rules).
 // ------------------------------------------------------------------------------------------------
 template <uint32_t CODEC>
-__global__ __launch_bounds__(kCzThreads) void k_cz(CzArgs a) {
+SDB_DEV uint64_t cz_matches(const lu8 *in, uint32_t wn, uint32_t room, lu32 *head, lu16 *prev, lu32 *mm) {
+    constexpr uint32_t kDepth = CzCfg<CODEC>::kDepth;
+    const uint32_t l = (uint32_t)lane_id();
+    for (uint32_t q = l; q < (1u << kCzHashBits); q += 64) head[q] = 0;
+    wsync();
+    uint64_t vmask = 0;
+    if (wn < 4) return 0;
+    const uint32_t last = wn - 4;  // positions with 4 bytes to hash: [0, last]
+    for (uint32_t b0 = 0; b0 <= last; b0 += 64) {
+        const uint32_t p = b0 + l;
+        const bool live = p <= last;
+        const uint32_t v = live ? lds_u32u(in, p) : 0, h = cz_hash(v);
+        // the latest earlier position + 1 with this hash: the exchange returns the previous holder, which for
+        // lanes of one batch sharing a hash is the lane before (same-address LDS atomics of one instruction
+        // are applied in lane order; a candidate not before p is never used, so any other order only loses
+        // matches)
+        const uint32_t cand = live ? __hip_atomic_exchange(&head[h], p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : 0;
+        if constexpr (kDepth > 1) {
+            if (live) prev[p] = (uint16_t)cand;
+        }
+        wsync();
+        const uint32_t lim = live ? (wn - p < kCzMaxMatch ? wn - p : kCzMaxMatch) : 0;
+        uint32_t blen = 0, boff = 0, c = cand;
+        for (uint32_t d = 0; d < kDepth && c && c <= p; d++) {
+            const uint32_t q = c - 1;
+            if (lds_u32u(in, q) == v) {
+                uint32_t len = 4;
+                while (len < lim) {
+                    const uint32_t x = lds_u32u(in, q + len) ^ lds_u32u(in, p + len);
+                    if (x) {
+                        len += (uint32_t)__builtin_ctz(x) >> 3;
+                        break;
+                    }
+                    len += 4;
+                }
+                if (len > lim) len = lim;
+                if (len > blen) {
+                    blen = len;
+                    boff = p - q;
+                    if (len >= kCzNice) break;
+                }
+            }
+            if constexpr (kDepth > 1) c = prev[q];
+            else c = 0;
+        }
+        if (CODEC == SDB_CODEC_LZ4) {  // LZ4: a match starts 12+ bytes before the end, ends 5+ before it
+            if (p + 12 > room) blen = 0;
+            else if (blen > room - 5 - p) blen = room - 5 - p;
+        }
+        if (blen < 4) blen = 0;
+        if (live) mm[p] = (boff << 16) | blen;
+        const uint64_t bits = __ballot(blen >= 4);
+        if (l == (b0 >> 6)) vmask = bits;
+        wsync();
+    }
+    return vmask;
+}
+
+// b. the greedy parse with one position of lazy evaluation: seq[2 i] = lit | len << 16, seq[2 i + 1] = off
+//    (window coordinates).  Returns the sequence count; *tail = the end of the last match.
+SDB_DEV uint32_t cz_parse(uint64_t vmask, uint32_t wn, const lu32 *mm, lu32 *seq, uint32_t *tail) {
+    const uint32_t l = (uint32_t)lane_id();
+    const uint32_t last = wn >= 4 ? wn - 4 : 0;
+    uint32_t nseq = 0, ls = 0, cur = 0;
+    while (nseq < kCzMaxSeq && cur < wn && wn >= 4) {
+        const uint32_t w0 = cur >> 6;
+        const uint64_t mine = l < w0 ? 0 : (l == w0 ? (vmask & (~0ull << (cur & 63))) : vmask);
+        const uint64_t any = __ballot(mine != 0);
+        if (!any) break;
+        const uint32_t ww = (uint32_t)__builtin_ctzll(any);
+        const uint64_t mw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mine >> 32), (int)ww) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mine, (int)ww);
+        const uint32_t q = 64 * ww + (uint32_t)__builtin_ctzll(mw);
+        const uint32_t mq = mm[q];
+        const uint32_t len = mq & 0xFFFF, off = mq >> 16;
+        if (q + 1 <= last && (mm[q + 1] & 0xFFFF) > len) {  // lazy: the next position's match is longer
+            cur = q + 1;
+            continue;
+        }
+        if (l == 0) {
+            seq[2 * nseq] = (q - ls) | (len << 16);
+            seq[2 * nseq + 1] = off;
+        }
+        nseq++;
+        ls = cur = q + len;
+    }
+    *tail = ls;
+    wsync();
+    return nseq;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Huffman code lengths of the symbols with nonzero f[0, ns) (ns <= 512, at least two of them), each
+// <= maxlen, by the wave: nonzero (freq << 9 | sym) keys compacted and bitonic-sorted in `work` (>= the
+// next power of two of their count), lengths of the sorted run by Moffat & Katajainen's in-place method on
+// lane 0 (A: >= ns words), the Kraft-sum limit on the per-length counts, then lengths handed out longest
+// first to the least frequent symbols.  len[0, ns) written (0 for absent symbols).  Returns max length.
+// ------------------------------------------------------------------------------------------------
+SDB_DEV uint32_t wave_huff_lengths(const lu32 *f, uint32_t ns, uint32_t maxlen, lu8 *len, lu32 *work, lu32 *A) {
+    const uint32_t l = (uint32_t)lane_id();
+    uint32_t m = 0;
+    for (uint32_t i0 = 0; i0 < ns; i0 += 64) {
+        const uint32_t i = i0 + l;
+        const uint32_t fr = i < ns ? f[i] : 0;
+        const uint64_t b = __ballot(fr != 0);
+        if (fr) work[m + lanes_below(b)] = (fr << 9) | i;
+        if (i < ns) len[i] = 0;
+        m += (uint32_t)__builtin_popcountll(b);
+    }
+    uint32_t P = 1;
+    while (P < m) P <<= 1;
+    for (uint32_t i = m + l; i < P; i += 64) work[i] = 0xFFFFFFFFu;
+    wsync();
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = l; t < P / 2; t += 64) {
+                const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), p = i + j;
+                const uint32_t a = work[i], b = work[p];
+                if ((a > b) == ((i & k) == 0)) {
+                    work[i] = b;
+                    work[p] = a;
+                }
+            }
+            wsync();
+        }
+    }
+    uint32_t mx = 0;
+    if (l == 0) {
+        const int n = (int)m;
+        for (int i = 0; i < n; i++) A[i] = work[i] >> 9;
+        if (n == 1) A[0] = 1;
+        else if (n > 1) {
+            A[0] += A[1];
+            int root = 0, leaf = 2, next;
+            for (next = 1; next < n - 1; next++) {
+                if (leaf >= n || A[root] < A[leaf]) {
+                    A[next] = A[root];
+                    A[root++] = next;
+                } else {
+                    A[next] = A[leaf++];
+                }
+                if (leaf >= n || (root < next && A[root] < A[leaf])) {
+                    A[next] += A[root];
+                    A[root++] = next;
+                } else {
+                    A[next] += A[leaf++];
+                }
+            }
+            A[n - 2] = 0;
+            for (next = n - 3; next >= 0; next--) A[next] = A[A[next]] + 1;
+            int avbl = 1, used = 0, dpth = 0;
+            root = n - 2;
+            next = n - 1;
+            while (avbl > 0) {
+                while (root >= 0 && (int)A[root] == dpth) {
+                    used++;
+                    root--;
+                }
+                while (avbl > used) {
+                    A[next--] = (uint32_t)dpth;
+                    avbl--;
+                }
+                avbl = 2 * used;
+                dpth++;
+                used = 0;
+            }
+        }
+        // A[i]: length of the i-th least frequent symbol (non-increasing in i)
+        if (A[0] > maxlen) {
+            uint32_t cnt[16];
+            for (uint32_t b = 0; b <= 15; b++) cnt[b] = 0;
+            for (int i = 0; i < n; i++) cnt[A[i] > maxlen ? maxlen : A[i]]++;
+            uint32_t total = 0;
+            for (uint32_t b = 1; b <= maxlen; b++) total += cnt[b] << (maxlen - b);
+            while (total != (1u << maxlen)) {
+                cnt[maxlen]--;
+                for (uint32_t b = maxlen - 1; b > 0; b--)
+                    if (cnt[b]) {
+                        cnt[b]--;
+                        cnt[b + 1] += 2;
+                        break;
+                    }
+                total--;
+            }
+            int i = 0;
+            for (uint32_t b = maxlen; b >= 1; b--)
+                for (uint32_t c = 0; c < cnt[b]; c++) A[i++] = b;
+        }
+        mx = n ? A[0] : 0;
+        for (int i = 0; i < n; i++) len[work[i] & 511] = (uint8_t)A[i];
+    }
+    wsync();
+    return uni(mx);
+}
+
+// deflate's canonical codes (RFC 1951 3.2.2), bit-reversed for the LSB-first stream.  One lane.
+SDB_DEV void deflate_codes(const lu8 *len, uint32_t ns, lu16 *code) {
+    uint32_t cnt[16], next[16];
+    for (uint32_t b = 0; b < 16; b++) cnt[b] = 0;
+    for (uint32_t s = 0; s < ns; s++) cnt[len[s]]++;
+    cnt[0] = 0;
+    uint32_t c = 0;
+    for (uint32_t b = 1; b < 16; b++) {
+        c = (c + cnt[b - 1]) << 1;
+        next[b] = c;
+    }
+    for (uint32_t s = 0; s < ns; s++) {
+        const uint32_t b = len[s];
+        code[s] = b ? (uint16_t)rev_bits(next[b]++, b) : 0;
+    }
+}
+
+// The mask of literal positions of the window (bit p: not inside a match), the sequence starts from a
+// scan.  lmask: 128 words.
+SDB_DEV void cz_lit_mask(const lu32 *seq, uint32_t nseq, uint32_t wn, lu32 *lmask) {
+    const uint32_t l = (uint32_t)lane_id();
+    for (uint32_t q = l; q < 128; q += 64) {
+        const uint32_t b0 = 32 * q;
+        lmask[q] = b0 + 32 <= wn ? 0xFFFFFFFFu : (b0 >= wn ? 0u : (1u << (wn - b0)) - 1);
+    }
+    wsync();
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < nseq; c0 += 64) {
+        const uint32_t i = c0 + l;
+        const bool v = i < nseq;
+        const uint32_t s0 = v ? seq[2 * i] : 0;
+        const uint32_t lit = s0 & 0xFFFF, len = s0 >> 16, span = lit + len;
+        const uint32_t inc = wave_incl_scan(span);
+        const uint32_t ms = carry + inc - span + lit;  // the match's first position
+        for (uint32_t p = ms; p < ms + len;) {
+            const uint32_t q = p >> 5, r = p & 31, k = (ms + len - p) < (32 - r) ? (ms + len - p) : (32 - r);
+            const uint32_t bits = (k == 32 ? 0xFFFFFFFFu : ((1u << k) - 1)) << r;
+            __hip_atomic_fetch_and(&lmask[q], ~bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            p += k;
+        }
+        carry += wave_readlane(inc, 63);
+    }
+    wsync();
+}
+
+// ------------------------------------------------------------------------------------------------
+// zlib: one deflate block for the window, written at bit `origin` of `out` (zeroed past the origin).
+// Returns the end bit.  HZ layout (entropy scratch, 8 KiB).
+// ------------------------------------------------------------------------------------------------
+struct ZlHz {
+    lu32 *fq;      // [320]: literal / length 0..285, distances at 288..317
+    lu32 *fcl;     // [20]
+    lu8 *lens;     // [320]
+    lu8 *cll;      // [20]
+    lu16 *codes;   // [320]
+    lu16 *clc;     // [20]
+    lu32 *work;    // [512]
+    lu32 *A;       // [320]
+    lu16 *rle;     // [320]: sym | extra << 5
+    lu32 *misc;    // [32]
+    __device__ ZlHz(lu8 *hz)
+        : fq((lu32 *)hz), fcl((lu32 *)(hz + 1280)), lens(hz + 1360), cll(hz + 1680), codes((lu16 *)(hz + 1712)),
+          clc((lu16 *)(hz + 2352)), work((lu32 *)(hz + 2400)), A((lu32 *)(hz + 4448)), rle((lu16 *)(hz + 5728)),
+          misc((lu32 *)(hz + 6368)) {}
+};
+
+SDB_DEV uint32_t cz_deflate_window(const lu8 *in, uint32_t wn, const lu32 *seq, uint32_t nseq, lu8 *out,
+                                   uint32_t origin, bool final, lu8 *hz_base, lu8 *aux) {
+    const uint32_t l = (uint32_t)lane_id();
+    ZlHz hz(hz_base);
+    lu32 *lmask = (lu32 *)aux;
+    lu16 *plen = (lu16 *)aux;
+    lu32 *bw = (lu32 *)out;
+    for (uint32_t q = l; q < 340; q += 64) hz.fq[q] = 0;  // fq + fcl
+    cz_lit_mask(seq, nseq, wn, lmask);
+    // histograms: each sequence's length and distance codes, then the literals
+    for (uint32_t c0 = 0; c0 < nseq; c0 += 64) {
+        const uint32_t i = c0 + l;
+        if (i < nseq) {
+            const uint32_t s0 = seq[2 * i], off = seq[2 * i + 1];
+            __hip_atomic_fetch_add(&hz.fq[257 + len_code(s0 >> 16)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            __hip_atomic_fetch_add(&hz.fq[288 + dist_code(off)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
+    }
+    for (uint32_t p = l; p < wn; p += 64)
+        if ((lmask[p >> 5] >> (p & 31)) & 1)
+            __hip_atomic_fetch_add(&hz.fq[in[p]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if (l == 0) hz.fq[256] = 1;
+    wsync();
+    // extra bits (both codes) and the fixed code's size; then >= 2 used symbols per alphabet (the distance
+    // alphabet may be unused: two placeholder codes of length 1 keep every code complete)
+    uint32_t xb = 0, fixb = 0;
+    for (uint32_t s = l; s < 318; s += 64) {
+        const uint32_t f = hz.fq[s];
+        if (s < 286) fixb += f * fixed_len(s);
+        else if (s >= 288) fixb += f * 5;
+        if (s >= 257 && s < 286) xb += f * c_len_extra[s - 257];
+        if (s >= 288) xb += f * c_dist_extra[s - 288];
+    }
+    xb = wave_sum(xb);
+    fixb = wave_sum(fixb) + xb;
+    {
+        const uint64_t b = __ballot(l < 30 && hz.fq[288 + l] != 0);
+        uint32_t nzl = 0;
+        for (uint32_t s = l; s < 286; s += 64) nzl += hz.fq[s] != 0;
+        nzl = wave_sum(nzl);
+        if (l == 0) {
+            uint32_t nz = (uint32_t)__builtin_popcountll(b);
+            for (uint32_t t = 0; t < 2 && nz < 2; t++)
+                if (!hz.fq[288 + t]) {
+                    hz.fq[288 + t] = 1;
+                    nz++;
+                }
+            for (uint32_t t = 0; t < 2 && nzl < 2; t++)  // an empty window: EOB and a placeholder literal
+                if (!hz.fq[t]) {
+                    hz.fq[t] = 1;
+                    nzl++;
+                }
+        }
+        wsync();
+    }
+    wave_huff_lengths(hz.fq, 286, 15, hz.lens, hz.work, hz.A);
+    wave_huff_lengths(hz.fq + 288, 30, 15, hz.lens + 288, hz.work, hz.A);
+    // the code-length sequence (HLIT literal / length lengths, then HDIST distance lengths) run-length coded
+    uint32_t hlit = 257, hdist = 1;
+    for (uint32_t s = l; s < 286; s += 64)
+        if (hz.lens[s]) hlit = hlit > s + 1 ? hlit : s + 1;
+    if (l < 30 && hz.lens[288 + l]) hdist = l + 1;
+    hlit = wave_max(hlit);
+    hdist = wave_max(hdist);
+    uint32_t nitem = 0;
+    if (l == 0) {
+        const uint32_t N = hlit + hdist;
+        auto L = [&](uint32_t i) -> uint32_t { return i < hlit ? hz.lens[i] : hz.lens[288 + i - hlit]; };
+        auto emit = [&](uint32_t sym, uint32_t x) {
+            hz.rle[nitem++] = (uint16_t)(sym | (x << 5));
+            hz.fcl[sym]++;
+        };
+        uint32_t i = 0;
+        while (i < N) {
+            const uint32_t v = L(i);
+            uint32_t run = 1;
+            while (i + run < N && L(i + run) == v) run++;
+            if (v == 0) {
+                while (run >= 11) {
+                    const uint32_t k = run < 138 ? run : 138;
+                    emit(18, k - 11);
+                    run -= k;
+                    i += k;
+                }
+                if (run >= 3) {
+                    emit(17, run - 3);
+                    i += run;
+                    run = 0;
+                }
+                for (; run; run--, i++) emit(0, 0);
+            } else {
+                emit(v, 0);
+                i++;
+                run--;
+                while (run >= 3) {
+                    const uint32_t k = run < 6 ? run : 6;
+                    emit(16, k - 3);
+                    run -= k;
+                    i += k;
+                }
+                for (; run; run--, i++) emit(v, 0);
+            }
+        }
+        uint32_t nz = 0;
+        for (uint32_t s = 0; s < 19; s++) nz += hz.fcl[s] != 0;
+        for (uint32_t s = 0; s < 19 && nz < 2; s++)
+            if (!hz.fcl[s]) {
+                hz.fcl[s] = 1;
+                nz++;
+            }
+        hz.misc[0] = nitem;
+    }
+    wsync();
+    nitem = hz.misc[0];
+    wave_huff_lengths(hz.fcl, 19, 7, hz.cll, hz.work, hz.A);
+    uint32_t hclen = 19;
+    {
+        // the dynamic block's size: header + items + codes + extra bits
+        uint32_t db = 0;
+        for (uint32_t s = l; s < 318; s += 64)
+            if (s < 286 || s >= 288) db += hz.fq[s] * hz.lens[s];
+        for (uint32_t i = l; i < nitem; i += 64) {
+            const uint32_t it = hz.rle[i], sym = it & 31;
+            db += hz.cll[sym] + (sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0);
+        }
+        db = wave_sum(db);
+        const uint64_t nzo = __ballot(l < 19 && hz.cll[c_cl_order[l < 19 ? l : 0]] != 0);
+        hclen = nzo ? 64 - (uint32_t)__builtin_clzll(nzo) : 4;
+        if (hclen < 4) hclen = 4;
+        const uint32_t dynb = 3 + 14 + 3 * hclen + db + xb;
+        const uint32_t fb = 3 + fixb;
+        const uint32_t sb = ((origin + 3 + 7) & ~7u) - origin + 32 + 8 * wn;
+        uint32_t kind = dynb < fb ? 2 : 1;
+        if ((kind == 2 ? dynb : fb) >= sb) kind = 0;
+        if (kind == 0) {
+            // stored: BFINAL / 00, byte-aligned LEN / NLEN and the window's bytes
+            if (l == 0) put_bits(bw, origin, final ? 1u : 0u, 3);
+            const uint32_t b = (origin + 3 + 7) >> 3;
+            wsync();
+            if (l == 0) {
+                out[b] = (uint8_t)wn; out[b + 1] = (uint8_t)(wn >> 8);
+                out[b + 2] = (uint8_t)~wn; out[b + 3] = (uint8_t)(~wn >> 8);
+            }
+            for (uint32_t i = l; i < wn; i += 64) out[b + 4 + i] = in[i];
+            wsync();
+            return 8 * (b + 4 + wn);
+        }
+        if (kind == 1) {
+            for (uint32_t s = l; s < 318; s += 64) {
+                const bool d = s >= 288;
+                hz.lens[s] = (uint8_t)(d ? 5 : (s < 286 ? fixed_len(s) : 0));
+                hz.codes[s] = (uint16_t)(d ? rev_bits(s - 288, 5) : (s < 286 ? fixed_code(s) : 0));
+            }
+            if (l == 0) put_bits(bw, origin, (final ? 1u : 0u) | (1u << 1), 3);
+            origin += 3;
+        } else {
+            if (l == 0) {
+                deflate_codes(hz.lens, 286, hz.codes);
+                deflate_codes(hz.lens + 288, 30, hz.codes + 288);
+                deflate_codes(hz.cll, 19, hz.clc);
+                uint32_t pos = origin;
+                put_bits(bw, pos, (final ? 1u : 0u) | (2u << 1), 3);
+                put_bits(bw, pos + 3, (hlit - 257) | ((hdist - 1) << 5) | ((hclen - 4) << 10), 14);
+                pos += 17;
+                for (uint32_t i = 0; i < hclen; i++, pos += 3) put_bits(bw, pos, hz.cll[c_cl_order[i]], 3);
+                for (uint32_t i = 0; i < nitem; i++) {
+                    const uint32_t it = hz.rle[i], sym = it & 31, x = it >> 5;
+                    put_bits(bw, pos, hz.clc[sym], hz.cll[sym]);
+                    pos += hz.cll[sym];
+                    const uint32_t xn = sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0;
+                    put_bits(bw, pos, x, xn);
+                    pos += xn;
+                }
+                hz.misc[1] = pos;
+            }
+            wsync();
+            origin = hz.misc[1];
+        }
+    }
+    wsync();
+    // plen[i] = sum of the literal code lengths of bytes [0, i)
+    {
+        uint32_t carry = 0;
+        for (uint32_t c0 = 0; c0 < wn + 1; c0 += 64) {
+            const uint32_t i = c0 + l;
+            const uint32_t v = i < wn ? hz.lens[in[i]] : 0u;
+            const uint32_t inc = wave_incl_scan(v);
+            if (i <= wn) plen[i] = (uint16_t)(carry + inc - v);
+            carry += wave_readlane(inc, 63);
+        }
+    }
+    wsync();
+    uint32_t carry_bits = origin, carry_pos = 0;
+    for (uint32_t c0 = 0; c0 < nseq; c0 += 64) {
+        const uint32_t i = c0 + l;
+        const bool v = i < nseq;
+        const uint32_t s0 = v ? seq[2 * i] : 0, off = v ? seq[2 * i + 1] : 0;
+        const uint32_t lit = s0 & 0xFFFF, len = s0 >> 16, span = lit + len;
+        const uint32_t pinc = wave_incl_scan(span);
+        const uint32_t lstart = carry_pos + pinc - span;
+        uint32_t lbits = 0, dbits = 0, lval = 0, dval = 0;
+        if (v) {
+            const uint32_t lc = len_code(len), dc = dist_code(off);
+            lval = hz.codes[257 + lc] | ((len - c_len_base[lc]) << hz.lens[257 + lc]);
+            lbits = hz.lens[257 + lc] + c_len_extra[lc];
+            dval = hz.codes[288 + dc] | ((off - c_dist_base[dc]) << hz.lens[288 + dc]);
+            dbits = hz.lens[288 + dc] + c_dist_extra[dc];
+        }
+        const uint32_t litb = v ? (uint32_t)(plen[lstart + lit] - plen[lstart]) : 0;
+        const uint32_t bits = litb + lbits + dbits;
+        const uint32_t binc = wave_incl_scan(bits);
+        const uint32_t bstart = carry_bits + binc - bits;
+        if (v) {
+            put_bits(bw, bstart + litb, lval, lbits);
+            put_bits(bw, bstart + litb + lbits, dval, dbits);
+        }
+        const uint32_t ncur = nseq - c0 < 64 ? nseq - c0 : 64;
+        for (uint32_t j = 0; j < ncur; j++) {
+            const uint32_t ls_j = (uint32_t)__builtin_amdgcn_readlane((int)lstart, (int)j);
+            const uint32_t lit_j = (uint32_t)__builtin_amdgcn_readlane((int)lit, (int)j);
+            const uint32_t b_j = (uint32_t)__builtin_amdgcn_readlane((int)bstart, (int)j);
+            for (uint32_t x = l; x < lit_j; x += 64) {
+                const uint32_t c = in[ls_j + x];
+                put_bits(bw, b_j + (plen[ls_j + x] - plen[ls_j]), hz.codes[c], hz.lens[c]);
+            }
+        }
+        carry_bits += wave_readlane(binc, 63);
+        carry_pos += wave_readlane(pinc, 63);
+    }
+    // final literals [carry_pos, wn), then end-of-block
+    for (uint32_t x = l; x < wn - carry_pos; x += 64) {
+        const uint32_t c = in[carry_pos + x];
+        put_bits(bw, carry_bits + (plen[carry_pos + x] - plen[carry_pos]), hz.codes[c], hz.lens[c]);
+    }
+    carry_bits += plen[wn] - plen[carry_pos];
+    if (l == 0) put_bits(bw, carry_bits, hz.codes[256], hz.lens[256]);
+    carry_bits += hz.lens[256];
+    wsync();
+    return carry_bits;
+}
+
+// ------------------------------------------------------------------------------------------------
+// zstd: one block for the window, its content written at out[ob, ...) (zeroed).  Returns the content size
+// (0: not smaller than the window — the caller writes a raw block).  rep: the repeat offsets, carried.
+// HZ layout (8 KiB): lit [0, 4096) then the FSE tables; fq / code histograms + norms [4096, 5120);
+// Huffman lens [5120, 5376), codes [5376, 5888); work [5888, 7936); misc [7936, 8192).
+// ------------------------------------------------------------------------------------------------
+SDB_DEV void fse_build_ct(const li16 *norm, uint32_t ns, uint32_t al, lu16 *stab, li32 *tt, lu8 *spread, lu16 *cumul) {
+    const uint32_t size = 1u << al, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+    uint32_t high = size - 1;
+    cumul[0] = 0;
+    for (uint32_t u = 1; u <= ns; u++) {
+        const int nc = norm[u - 1];
+        if (nc == -1) {
+            cumul[u] = cumul[u - 1] + 1;
+            spread[high--] = (uint8_t)(u - 1);
+        } else {
+            cumul[u] = cumul[u - 1] + (uint32_t)nc;
+        }
+    }
+    uint32_t pos = 0;
+    for (uint32_t s = 0; s < ns; s++) {
+        const int nc = norm[s];
+        for (int i = 0; i < nc; i++) {
+            spread[pos] = (uint8_t)s;
+            pos = (pos + step) & mask;
+            while (pos > high) pos = (pos + step) & mask;
+        }
+    }
+    for (uint32_t u = 0; u < size; u++) {
+        const uint32_t s = spread[u];
+        stab[cumul[s]] = (uint16_t)(size + u);
+        cumul[s] = cumul[s] + 1;
+    }
+    int total = 0;
+    for (uint32_t s = 0; s < ns; s++) {
+        const int nc = norm[s];
+        if (nc == 0) {
+            tt[2 * s] = (int32_t)(((al + 1) << 16) - size);
+            tt[2 * s + 1] = 0;
+        } else if (nc == -1 || nc == 1) {
+            tt[2 * s] = (int32_t)((al << 16) - size);
+            tt[2 * s + 1] = total - 1;
+            total++;
+        } else {
+            const uint32_t mbo = al - hibit((uint32_t)nc - 1), msp = (uint32_t)nc << mbo;
+            tt[2 * s] = (int32_t)((mbo << 16) - msp);
+            tt[2 * s + 1] = total - nc;
+            total += nc;
+        }
+    }
+}
+
+// FSE table description (RFC 8878 4.1.1) of norm[0, ns) at accuracy log al into o; returns its bytes.
+SDB_DEV uint32_t fse_ncount(const li16 *norm, uint32_t ns, uint32_t al, lu8 *o) {
+    uint64_t bs = al - 5;
+    uint32_t bc = 4, op = 0;
+    int remaining = (1 << al) + 1, threshold = 1 << al, nb = (int)al + 1;
+    uint32_t sym = 0;
+    bool prev0 = false;
+    auto flush = [&]() {
+        while (bc >= 8) {
+            o[op++] = (uint8_t)bs;
+            bs >>= 8;
+            bc -= 8;
+        }
+    };
+    while (sym < ns && remaining > 1) {
+        if (prev0) {
+            uint32_t start = sym;
+            while (sym < ns && !norm[sym]) sym++;
+            while (sym >= start + 24) {
+                start += 24;
+                bs |= 0xFFFFull << bc;
+                bc += 16;
+                flush();
+            }
+            while (sym >= start + 3) {
+                start += 3;
+                bs |= 3ull << bc;
+                bc += 2;
+            }
+            bs |= (uint64_t)(sym - start) << bc;
+            bc += 2;
+            flush();
+        }
+        int count = norm[sym++];
+        const int mx = 2 * threshold - 1 - remaining;
+        remaining -= count < 0 ? -count : count;
+        count++;
+        if (count >= threshold) count += mx;
+        bs |= (uint64_t)(uint32_t)count << bc;
+        bc += (uint32_t)nb;
+        bc -= count < mx ? 1u : 0u;
+        prev0 = count == 1;
+        while (remaining < threshold) {
+            nb--;
+            threshold >>= 1;
+        }
+        flush();
+    }
+    if (bc) o[op++] = (uint8_t)bs;
+    return op;
+}
+
+// A serial forward bitstream (one lane) into LDS bytes: BIT_addBits / BIT_closeCStream.
+struct SerBits {
+    lu8 *o;
+    uint32_t op = 0, bc = 0;
+    uint64_t acc = 0;
+    __device__ explicit SerBits(lu8 *out) : o(out) {}
+    __device__ void add(uint32_t v, uint32_t nb) {
+        if (nb < 32) v &= (1u << nb) - 1;
+        acc |= (uint64_t)v << bc;
+        bc += nb;
+        while (bc >= 8) {
+            o[op++] = (uint8_t)acc;
+            acc >>= 8;
+            bc -= 8;
+        }
+    }
+    __device__ uint32_t close() {  // the end mark, then the partial byte
+        add(1u, 1);
+        if (bc) o[op++] = (uint8_t)acc;
+        return op;
+    }
+};
+
+// Huffman weights wt[0, N) (N >= 2, values 0..11) as an FSE-compressed tree description (RFC 8878 4.2.1.2:
+// NCount at accuracy log <= 6, then two interleaved states sharing the table — HUF_compressWeights /
+// FSE_compress_usingCTable): bytes into o, or 0 when the weights do not compress that way (one value, every
+// value once, or >= 128 bytes).  One lane; scratch: 640 bytes.
+SDB_DEV uint32_t huf_weights_fse(const lu8 *wt, uint32_t N, lu8 *o, lu8 *scratch) {
+    li16 *norm = (li16 *)scratch;                 // [16]
+    lu16 *stab = (lu16 *)(scratch + 32);          // [64]
+    li32 *tt = (li32 *)(scratch + 160);           // [16][2]
+    lu8 *spread = scratch + 288;                  // [64]
+    lu16 *cumul = (lu16 *)(scratch + 352);        // [17]
+    uint32_t cnt[12];
+    for (uint32_t w = 0; w < 12; w++) cnt[w] = 0;
+    for (uint32_t i = 0; i < N; i++) cnt[wt[i]]++;
+    uint32_t maxw = 0, maxc = 0, best = 0;
+    for (uint32_t w = 0; w < 12; w++)
+        if (cnt[w]) {
+            maxw = w;
+            if (cnt[w] > maxc) {
+                maxc = cnt[w];
+                best = w;
+            }
+        }
+    if (maxc == N || maxc == 1) return 0;
+    uint32_t al = hibit(N - 1);
+    al = al > 2 ? al - 2 : 0;
+    if (al > 6) al = 6;
+    const uint32_t a1 = hibit(N) + 1, a2 = hibit(maxw ? maxw : 1) + 2, minb = a1 < a2 ? a1 : a2;
+    if (al < minb) al = minb;
+    if (al < 5) al = 5;
+    if (al > 6) al = 6;
+    const int scale = 1 << al;
+    int sum = 0;
+    for (uint32_t w = 0; w <= maxw; w++) {
+        int v = 0;
+        if (cnt[w]) {
+            v = (int)(((uint32_t)cnt[w] * (uint32_t)scale + N / 2) / N);
+            if (v < 1) v = 1;
+        }
+        norm[w] = (int16_t)v;
+        sum += v;
+    }
+    int diff = scale - sum;
+    if (diff >= 0 || norm[best] + diff >= 1) {
+        norm[best] = (int16_t)(norm[best] + diff);
+    } else {
+        while (diff < 0) {
+            uint32_t m = 0;
+            for (uint32_t w = 0; w <= maxw; w++)
+                if (norm[w] > norm[m]) m = w;
+            norm[m] = (int16_t)(norm[m] - 1);
+            diff++;
+        }
+    }
+    const uint32_t hs = fse_ncount(norm, maxw + 1, al, o);
+    fse_build_ct(norm, maxw + 1, al, stab, tt, spread, cumul);
+    SerBits bs(o + hs);
+    uint32_t st[2];  // st[0]: even indices (state 1), st[1]: odd (state 2)
+    auto init = [&](uint32_t sym) -> uint32_t {
+        const int dnb = tt[2 * sym], dfs = tt[2 * sym + 1];
+        const uint32_t nbo = (uint32_t)((dnb + (1 << 15)) >> 16);
+        const uint32_t v = (nbo << 16) - (uint32_t)dnb;
+        return stab[(int)(v >> nbo) + dfs];
+    };
+    st[(N - 1) & 1] = init(wt[N - 1]);
+    st[(N - 2) & 1] = init(wt[N - 2]);
+    for (int i = (int)N - 3; i >= 0; i--) {
+        const uint32_t sym = wt[i], k = (uint32_t)i & 1;
+        const int dnb = tt[2 * sym], dfs = tt[2 * sym + 1];
+        const uint32_t nb = (uint32_t)((int)st[k] + dnb) >> 16;
+        bs.add(st[k], nb);
+        st[k] = stab[(int)(st[k] >> nb) + dfs];
+        if (hs + bs.op > 120) return 0;
+    }
+    bs.add(st[1] - (uint32_t)scale, al);
+    bs.add(st[0] - (uint32_t)scale, al);
+    const uint32_t total = hs + bs.close();
+    return total < 128 ? total : 0;
+}
+
+struct ZsHz {
+    lu8 *lit;      // [4096]
+    lu16 *stab;    // [3][256] (over lit, after the literals section)
+    li32 *tt;      // [3][64][2]
+    lu8 *spread;   // [3][256]
+    lu8 *nc;       // [3][64]: NCount descriptions
+    lu32 *fq;      // [256] literal histogram; then [3][64] code histograms
+    li16 *norm;    // [3][64] (at fq + 768 B)
+    lu8 *lens;     // [256]
+    lu16 *codes;   // [256]
+    lu32 *work;    // [512]: sort + MK; then cumul [3][66] u16
+    lu32 *misc;    // [64]: scalars, then (byte 64 on) the FSE tree description
+    __device__ ZsHz(lu8 *hz)
+        : lit(hz), stab((lu16 *)hz), tt((li32 *)(hz + 1536)), spread(hz + 3072), nc(hz + 3840), fq((lu32 *)(hz + 4096)),
+          norm((li16 *)(hz + 4096 + 768)), lens(hz + 5120), codes((lu16 *)(hz + 5376)), work((lu32 *)(hz + 5888)),
+          misc((lu32 *)(hz + 7936)) {}
+};
+
+// The per-table work of lane t (0 LL, 1 ML, 2 OF): the mode by estimated cost, the table description,
+// the encoding table.  Returns mode | al << 8 | ncount bytes << 16.
+SDB_DEV uint32_t zs_table(ZsHz &hz, uint32_t t, uint32_t nseq) {
+    lu32 *f = hz.fq + 64 * t;
+    li16 *norm = hz.norm + 64 * t;
+    const uint32_t ns_max = c_zdef_n[t];
+    uint32_t maxsym = 0, nz = 0, best = 0;
+    for (uint32_t s = 0; s < ns_max; s++)
+        if (f[s]) {
+            maxsym = s;
+            nz++;
+            if (f[s] > f[best] || !f[best]) best = s;
+        }
+    lu16 *cumul = (lu16 *)hz.work + 66 * t;
+    if (nz == 1) {  // RLE: the one code as the description, no state bits
+        hz.nc[64 * t] = (uint8_t)maxsym;
+        return 1u | (0u << 8) | (1u << 16);
+    }
+    // predefined cost (bits, fixed point 1/256)
+    const uint32_t dal = c_zdef_al[t];
+    float pre = 0.f;
+    for (uint32_t s = 0; s <= maxsym; s++)
+        if (f[s]) {
+            const int d = c_zdef[t][s];
+            pre += (float)f[s] * ((float)dal - __log2f((float)(d < 0 ? 1 : d)));
+        }
+    // custom: the accuracy log as zstd's FSE_optimalTableLog, counts normalised to 2^al, every used code >= 1
+    const uint32_t maxal = t == 2 ? 8 : 9;
+    uint32_t al = nseq > 1 ? hibit(nseq - 1) : 0;
+    al = al > 2 ? al - 2 : 0;
+    if (al > maxal) al = maxal;
+    const uint32_t a1 = hibit(nseq) + 1, a2 = hibit(maxsym ? maxsym : 1) + 2, minb = a1 < a2 ? a1 : a2;
+    if (al < minb) al = minb;
+    if (al < 5) al = 5;
+    if (al > 8) al = 8;
+    const int scale = 1 << al;
+    int sum = 0;
+    for (uint32_t s = 0; s <= maxsym; s++) {
+        int v = 0;
+        if (f[s]) {
+            v = (int)(((uint64_t)f[s] * (uint32_t)scale + nseq / 2) / nseq);
+            if (v < 1) v = 1;
+        }
+        norm[s] = (int16_t)v;
+        sum += v;
+    }
+    int diff = scale - sum;
+    if (diff >= 0 || norm[best] + diff >= 1) {
+        norm[best] = (int16_t)(norm[best] + diff);
+    } else {
+        while (diff < 0) {
+            uint32_t m = 0;
+            for (uint32_t s = 0; s <= maxsym; s++)
+                if (norm[s] > norm[m]) m = s;
+            norm[m] = (int16_t)(norm[m] - 1);
+            diff++;
+        }
+    }
+    float cus = 0.f;
+    for (uint32_t s = 0; s <= maxsym; s++)
+        if (f[s]) cus += (float)f[s] * ((float)al - __log2f((float)norm[s]));
+    const uint32_t ncb = fse_ncount(norm, maxsym + 1, al, hz.nc + 64 * t);
+    cus += 8.f * (float)ncb;
+    if (pre <= cus) {
+        for (uint32_t s = 0; s < ns_max; s++) norm[s] = c_zdef[t][s];
+        fse_build_ct(norm, ns_max, dal, hz.stab + 256 * t, hz.tt + 128 * t, hz.spread + 256 * t, cumul);
+        return 0u | (dal << 8);
+    }
+    fse_build_ct(norm, maxsym + 1, al, hz.stab + 256 * t, hz.tt + 128 * t, hz.spread + 256 * t, cumul);
+    return 2u | (al << 8) | (ncb << 16);
+}
+
+SDB_DEV uint32_t cz_zstd_window(const lu8 *in, uint32_t wn, lu32 *seq, uint32_t nseq, lu8 *out, uint32_t ob,
+                                uint32_t (&rep)[3], lu8 *hz_base, lu8 *aux) {
+    const uint32_t l = (uint32_t)lane_id();
+    ZsHz hz(hz_base);
+    lu32 *lmask = (lu32 *)aux;
+    lu16 *plen = (lu16 *)aux;
+    lu16 *fsei = (lu16 *)aux;  // [3][1024]
+    lu32 *bw = (lu32 *)out;
+    for (uint32_t q = l; q < 256; q += 64) hz.fq[q] = 0;
+    cz_lit_mask(seq, nseq, wn, lmask);
+    // literals gathered in order, their histogram
+    uint32_t nlit = 0;
+    for (uint32_t c0 = 0; c0 < wn; c0 += 64) {
+        const uint32_t p = c0 + l;
+        const bool isl = p < wn && ((lmask[p >> 5] >> (p & 31)) & 1);
+        const uint64_t b = __ballot(isl);
+        if (isl) {
+            const uint32_t c = in[p];
+            hz.lit[nlit + lanes_below(b)] = (uint8_t)c;
+            __hip_atomic_fetch_add(&hz.fq[c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
+        nlit += (uint32_t)__builtin_popcountll(b);
+    }
+    wsync();
+    // ---- literals section
+    uint32_t nz = 0, maxsym = 0;
+    for (uint32_t s = l; s < 256; s += 64)
+        if (hz.fq[s]) {
+            nz++;
+            maxsym = s;
+        }
+    nz = wave_sum(nz);
+    maxsym = wave_max(maxsym);
+    const uint32_t raw_hdr = nlit < 32 ? 1 : (nlit < 4096 ? 2 : 3);
+    uint32_t p = ob;  // output byte position
+    bool huf = false;
+    uint32_t maxbits = 0;
+    uint32_t td = 0;  // the tree description's bytes: direct weights, or FSE-compressed (hz.misc byte 16 on)
+    bool tfse = false;
+    if (nz >= 2 && nlit >= 64) {
+        maxbits = wave_huff_lengths(hz.fq, maxsym + 1, 11, hz.lens, hz.work, hz.work + 256);
+        uint32_t bits = 0;
+        for (uint32_t s = l; s <= maxsym; s += 64) bits += hz.fq[s] * hz.lens[s];
+        bits = wave_sum(bits);
+        // weights of symbols 0 .. maxsym - 1 (the last one's is implied) into work, then the FSE description
+        lu8 *wt = (lu8 *)hz.work;
+        for (uint32_t s = l; s < maxsym; s += 64) wt[s] = hz.lens[s] ? (uint8_t)(maxbits + 1 - hz.lens[s]) : 0;
+        wsync();
+        if (l == 0) {
+            const uint32_t f = huf_weights_fse(wt, maxsym, (lu8 *)hz.misc + 64, (lu8 *)hz.work + 256);
+            const uint32_t direct = maxsym <= 128 ? 1 + (maxsym + 1) / 2 : 0;
+            uint32_t r = 0;
+            if (f && (!direct || f + 1 < direct)) r = (f + 1) | (1u << 16);
+            else if (direct) r = direct;
+            hz.misc[0] = r;
+        }
+        wsync();
+        td = hz.misc[0] & 0xFFFF;
+        tfse = (hz.misc[0] >> 16) != 0;
+        const uint32_t est = 3 + td + (nlit < 256 ? 0 : 6 + 4) + bits / 8 + 1;
+        huf = td && est + 8 < raw_hdr + nlit;
+    }
+    if (nlit == 0 || nz == 1) {
+        const uint32_t type = nz == 1 ? 1u : 0u;
+        if (l == 0) {
+            if (raw_hdr == 1) out[p] = (uint8_t)(type | (nlit << 3));
+            else if (raw_hdr == 2) {
+                const uint32_t h = type | (1u << 2) | (nlit << 4);
+                out[p] = (uint8_t)h; out[p + 1] = (uint8_t)(h >> 8);
+            } else {
+                const uint32_t h = type | (3u << 2) | (nlit << 4);
+                out[p] = (uint8_t)h; out[p + 1] = (uint8_t)(h >> 8); out[p + 2] = (uint8_t)(h >> 16);
+            }
+            if (nz == 1) out[p + raw_hdr] = hz.lit[0];
+        }
+        p += raw_hdr + (nz == 1 ? 1 : 0);
+    } else if (!huf) {
+        if (l == 0) {
+            if (raw_hdr == 1) out[p] = (uint8_t)(nlit << 3);
+            else if (raw_hdr == 2) {
+                const uint32_t h = (1u << 2) | (nlit << 4);
+                out[p] = (uint8_t)h; out[p + 1] = (uint8_t)(h >> 8);
+            } else {
+                const uint32_t h = (3u << 2) | (nlit << 4);
+                out[p] = (uint8_t)h; out[p + 1] = (uint8_t)(h >> 8); out[p + 2] = (uint8_t)(h >> 16);
+            }
+        }
+        for (uint32_t i = l; i < nlit; i += 64) out[p + raw_hdr + i] = hz.lit[i];
+        p += raw_hdr + nlit;
+    } else {
+        // zstd's canonical codes: weight w = maxbits + 1 - len; within the index space, weight-1 symbols
+        // first (in symbol order), then weight 2, ...; code = start >> (w - 1) (HUF_readDTableX1)
+        if (l == 0) {
+            uint32_t cnt[13], start[13];
+            for (uint32_t w = 0; w < 13; w++) cnt[w] = 0;
+            for (uint32_t s = 0; s <= maxsym; s++)
+                if (hz.lens[s]) cnt[maxbits + 1 - hz.lens[s]]++;
+            uint32_t acc = 0;
+            for (uint32_t w = 1; w <= maxbits; w++) {
+                start[w] = acc;
+                acc += cnt[w] << (w - 1);
+            }
+            for (uint32_t s = 0; s <= maxsym; s++) {
+                const uint32_t b = hz.lens[s];
+                if (!b) {
+                    hz.codes[s] = 0;
+                    continue;
+                }
+                const uint32_t w = maxbits + 1 - b;
+                hz.codes[s] = (uint16_t)(start[w] >> (w - 1));
+                start[w] += 1u << (w - 1);
+            }
+        }
+        wsync();
+        // plen over the literals
+        {
+            uint32_t carry = 0;
+            for (uint32_t c0 = 0; c0 < nlit + 1; c0 += 64) {
+                const uint32_t i = c0 + l;
+                const uint32_t v = i < nlit ? hz.lens[hz.lit[i]] : 0u;
+                const uint32_t inc = wave_incl_scan(v);
+                if (i <= nlit) plen[i] = (uint16_t)(carry + inc - v);
+                carry += wave_readlane(inc, 63);
+            }
+        }
+        wsync();
+        const uint32_t ns = nlit < 256 ? 1 : 4, seg = ns == 1 ? nlit : (nlit + 3) / 4;
+        uint32_t sbytes[4] = {0, 0, 0, 0}, sa[4], sb[4], comp = td + (ns == 4 ? 6 : 0);
+        for (uint32_t k = 0; k < ns; k++) {
+            sa[k] = k * seg;
+            sb[k] = k + 1 == ns ? nlit : (k + 1) * seg;
+            sbytes[k] = (plen[sb[k]] - plen[sa[k]]) / 8 + 1;
+            comp += sbytes[k];
+        }
+        const uint32_t sf = ns == 1 ? 0 : (nlit <= 1023 && comp <= 1023 ? 1 : 2);
+        const uint32_t lh = sf == 2 ? 4 : 3;
+        if (l == 0) {
+            if (sf == 2) {
+                const uint32_t h = 2u | (2u << 2) | (nlit << 4) | (comp << 18);
+                out[p] = (uint8_t)h; out[p + 1] = (uint8_t)(h >> 8); out[p + 2] = (uint8_t)(h >> 16); out[p + 3] = (uint8_t)(h >> 24);
+            } else {
+                const uint32_t h = 2u | (sf << 2) | (nlit << 4) | (comp << 14);
+                out[p] = (uint8_t)h; out[p + 1] = (uint8_t)(h >> 8); out[p + 2] = (uint8_t)(h >> 16);
+            }
+            out[p + lh] = (uint8_t)(tfse ? td - 1 : 127 + maxsym);
+        }
+        if (tfse) {  // FSE-compressed weights: the header byte is their size
+            for (uint32_t i = l; i + 1 < td; i += 64) out[p + lh + 1 + i] = ((lu8 *)hz.misc)[64 + i];
+        } else {
+            // direct weights: symbols 0 .. maxsym - 1, two per byte (the first in the high nibble)
+            for (uint32_t i = l; i < (maxsym + 1) / 2; i += 64) {
+                const uint32_t s0 = 2 * i, s1 = 2 * i + 1;
+                const uint32_t w0 = hz.lens[s0] ? maxbits + 1 - hz.lens[s0] : 0;
+                const uint32_t w1 = s1 < maxsym && hz.lens[s1] ? maxbits + 1 - hz.lens[s1] : 0;
+                out[p + lh + 1 + i] = (uint8_t)((w0 << 4) | w1);
+            }
+        }
+        uint32_t s0 = p + lh + td;
+        if (ns == 4 && l == 0) {
+            out[s0] = (uint8_t)sbytes[0]; out[s0 + 1] = (uint8_t)(sbytes[0] >> 8);
+            out[s0 + 2] = (uint8_t)sbytes[1]; out[s0 + 3] = (uint8_t)(sbytes[1] >> 8);
+            out[s0 + 4] = (uint8_t)sbytes[2]; out[s0 + 5] = (uint8_t)(sbytes[2] >> 8);
+        }
+        if (ns == 4) s0 += 6;
+        wsync();
+        uint32_t sbase[4];
+        sbase[0] = s0;
+        for (uint32_t k = 1; k < ns; k++) sbase[k] = sbase[k - 1] + sbytes[k - 1];
+        // symbol j of stream k at bit plen[b_k] - plen[j + 1] (written last to first), the end mark after
+        for (uint32_t j = l; j < nlit; j += 64) {
+            const uint32_t k = ns == 1 ? 0 : (j / seg < 3 ? j / seg : 3);
+            const uint32_t kb = k == 0 ? sb[0] : k == 1 ? sb[1] : k == 2 ? sb[2] : sb[3];
+            const uint32_t kbase = k == 0 ? sbase[0] : k == 1 ? sbase[1] : k == 2 ? sbase[2] : sbase[3];
+            const uint32_t c = hz.lit[j];
+            put_bits(bw, 8 * kbase + (plen[kb] - plen[j + 1]), hz.codes[c], hz.lens[c]);
+        }
+        if (l < ns) {
+            const uint32_t kb = l == 0 ? sb[0] : l == 1 ? sb[1] : l == 2 ? sb[2] : sb[3];
+            const uint32_t ka = l == 0 ? sa[0] : l == 1 ? sa[1] : l == 2 ? sa[2] : sa[3];
+            const uint32_t kbase = l == 0 ? sbase[0] : l == 1 ? sbase[1] : l == 2 ? sbase[2] : sbase[3];
+            put_bits(bw, 8 * kbase + (plen[kb] - plen[ka]), 1u, 1);
+        }
+        wsync();
+        p = s0 + comp - (td + (ns == 4 ? 6 : 0));
+    }
+    // ---- sequences section
+    if (l == 0) {
+        if (nseq < 128) out[p] = (uint8_t)nseq;
+        else {
+            out[p] = (uint8_t)((nseq >> 8) + 128);
+            out[p + 1] = (uint8_t)nseq;
+        }
+    }
+    p += nseq < 128 ? 1 : 2;
+    if (nseq) {
+        // repeat offsets (RFC 8878 3.1.2.5), serial: seq[2 i + 1] = offBase | llc << 16 | mlc << 22
+        if (l == 0) {
+            uint32_t r0 = rep[0], r1 = rep[1], r2 = rep[2];
+            for (uint32_t i = 0; i < nseq; i++) {
+                const uint32_t s0 = seq[2 * i], lit = s0 & 0xFFFF, off = seq[2 * i + 1];
+                uint32_t obase;
+                if (lit) obase = off == r0 ? 1 : off == r1 ? 2 : off == r2 ? 3 : off + 3;
+                else obase = off == r1 ? 1 : off == r2 ? 2 : off == r0 - 1 ? 3 : off + 3;
+                if (obase > 3) {
+                    r2 = r1;
+                    r1 = r0;
+                    r0 = off;
+                } else {
+                    const uint32_t idx = lit ? obase - 1 : obase;
+                    if (idx == 1) {
+                        r1 = r0;
+                        r0 = off;
+                    } else if (idx == 2) {
+                        r2 = r1;
+                        r1 = r0;
+                        r0 = off;
+                    } else if (idx == 3) {
+                        r2 = r1;
+                        r1 = r0;
+                        r0 = off;
+                    }
+                }
+                seq[2 * i + 1] = obase;
+            }
+            hz.misc[0] = r0;
+            hz.misc[1] = r1;
+            hz.misc[2] = r2;
+        }
+        for (uint32_t q = l; q < 3 * 64; q += 64) hz.fq[q] = 0;
+        wsync();
+        rep[0] = hz.misc[0];
+        rep[1] = hz.misc[1];
+        rep[2] = hz.misc[2];
+        for (uint32_t i = l; i < nseq; i += 64) {
+            const uint32_t s0 = seq[2 * i], obase = seq[2 * i + 1];
+            const uint32_t llc = zll_code(s0 & 0xFFFF), mlc = zml_code(s0 >> 16), ofc = hibit(obase);
+            seq[2 * i + 1] = obase | (llc << 16) | (mlc << 22);
+            __hip_atomic_fetch_add(&hz.fq[llc], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            __hip_atomic_fetch_add(&hz.fq[64 + mlc], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            __hip_atomic_fetch_add(&hz.fq[128 + ofc], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
+        wsync();
+        // the three tables side by side on lanes 0-2, then their state machines (last sequence first)
+        if (l < 3) {
+            const uint32_t r = zs_table(hz, l, nseq);
+            hz.misc[4 + l] = r;
+            const uint32_t mode = r & 0xFF, al = (r >> 8) & 0xFF;
+            uint32_t fin = 0;
+            if (mode != 1) {
+                const lu16 *stab = hz.stab + 256 * l;
+                const li32 *tt = hz.tt + 128 * l;
+                auto code_of = [&](uint32_t n) -> uint32_t {
+                    const uint32_t w = seq[2 * n + 1];
+                    return l == 0 ? (w >> 16) & 63 : l == 1 ? (w >> 22) & 63 : hibit(w & 0xFFFF);
+                };
+                uint32_t c = code_of(nseq - 1);
+                int dnb = tt[2 * c], dfs = tt[2 * c + 1];
+                const uint32_t nbo = (uint32_t)((dnb + (1 << 15)) >> 16);
+                uint32_t value = (nbo << 16) - (uint32_t)dnb;
+                value = stab[(int)(value >> nbo) + dfs];
+                for (int n = (int)nseq - 2; n >= 0; n--) {
+                    c = code_of((uint32_t)n);
+                    dnb = tt[2 * c];
+                    dfs = tt[2 * c + 1];
+                    const uint32_t nb = (uint32_t)((int)value + dnb) >> 16;
+                    fsei[1024 * l + n] = (uint16_t)((nb << 12) | (value & ((1u << nb) - 1)));
+                    value = stab[(int)(value >> nb) + dfs];
+                }
+                fin = value - (1u << al);
+            } else {
+                for (uint32_t n = 0; n + 1 < nseq; n++) fsei[1024 * l + n] = 0;
+            }
+            hz.misc[8 + l] = fin;
+        }
+        wsync();
+        const uint32_t r_ll = hz.misc[4], r_ml = hz.misc[5], r_of = hz.misc[6];
+        const uint32_t m_ll = r_ll & 0xFF, m_ml = r_ml & 0xFF, m_of = r_of & 0xFF;
+        const uint32_t al_ll = m_ll == 1 ? 0 : (r_ll >> 8) & 0xFF, al_ml = m_ml == 1 ? 0 : (r_ml >> 8) & 0xFF,
+                       al_of = m_of == 1 ? 0 : (r_of >> 8) & 0xFF;
+        const uint32_t n_ll = r_ll >> 16, n_ml = r_ml >> 16, n_of = r_of >> 16;
+        // modes byte, then the descriptions in the order LL, OF, ML
+        if (l == 0) out[p] = (uint8_t)((m_ll << 6) | (m_of << 4) | (m_ml << 2));
+        for (uint32_t i = l; i < n_ll + n_of + n_ml; i += 64) {
+            uint8_t v;
+            if (i < n_ll) v = hz.nc[i];
+            else if (i < n_ll + n_of) v = hz.nc[128 + i - n_ll];
+            else v = hz.nc[64 + i - n_ll - n_of];
+            out[p + 1 + i] = v;
+        }
+        p += 1 + n_ll + n_of + n_ml;
+        wsync();
+        // the bitstream: sequence nseq - 1 first; per sequence [OF st][ML st][LL st][LL x][ML x][OF x]
+        const uint32_t base = 8 * p;
+        uint32_t carry = 0;
+        for (int c0 = (int)((nseq - 1) & ~63u); c0 >= 0; c0 -= 64) {
+            const uint32_t n = (uint32_t)c0 + l;
+            const bool v = n < nseq;
+            uint32_t lit = 0, len = 0, obase = 1, llc = 0, mlc = 0;
+            if (v) {
+                const uint32_t s0 = seq[2 * n], w = seq[2 * n + 1];
+                lit = s0 & 0xFFFF;
+                len = s0 >> 16;
+                obase = w & 0xFFFF;
+                llc = (w >> 16) & 63;
+                mlc = (w >> 22) & 63;
+            }
+            const uint32_t ofc = hibit(obase);
+            const uint32_t llb = c_zll_bits[llc], mlb = c_zml_bits[mlc];
+            uint32_t e_of = 0, e_ml = 0, e_ll = 0;
+            if (v && n + 1 < nseq) {
+                e_ll = fsei[n];
+                e_ml = fsei[1024 + n];
+                e_of = fsei[2048 + n];
+            }
+            const uint32_t nb_of = e_of >> 12, nb_ml = e_ml >> 12, nb_ll = e_ll >> 12;
+            const uint32_t b = v ? nb_of + nb_ml + nb_ll + llb + mlb + ofc : 0;
+            const uint32_t inc = wave_incl_scan(b), tot = wave_readlane(inc, 63);
+            uint32_t pos = base + carry + (tot - inc);
+            if (v) {
+                put_bits(bw, pos, e_of & 0xFFF, nb_of);
+                pos += nb_of;
+                put_bits(bw, pos, e_ml & 0xFFF, nb_ml);
+                pos += nb_ml;
+                put_bits(bw, pos, e_ll & 0xFFF, nb_ll);
+                pos += nb_ll;
+                put_bits(bw, pos, lit - c_zll_base[llc], llb);
+                pos += llb;
+                put_bits(bw, pos, len - c_zml_base[mlc], mlb);
+                pos += mlb;
+                put_bits(bw, pos, obase - (1u << ofc), ofc);
+            }
+            carry += tot;
+        }
+        if (l == 0) {
+            uint32_t pos = base + carry;
+            put_bits(bw, pos, hz.misc[9], al_ml);
+            pos += al_ml;
+            put_bits(bw, pos, hz.misc[10], al_of);
+            pos += al_of;
+            put_bits(bw, pos, hz.misc[8], al_ll);
+            pos += al_ll;
+            put_bits(bw, pos, 1u, 1);
+        }
+        wsync();
+        p += (carry + al_ml + al_of + al_ll) / 8 + 1;
+    }
+    wsync();
+    const uint32_t content = p - ob;
+    return content < wn ? content : 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// C1: compress.  One wave per block, windows of <= 4 KiB.
+// ------------------------------------------------------------------------------------------------
+template <uint32_t CODEC>
+__global__ __launch_bounds__(64 * CzCfg<CODEC>::kWaves) void k_cz(CzArgs a) {
+    using Cfg = CzCfg<CODEC>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if (lds_addr((const void *)smem) != 0) {
         if (threadIdx.x == 0) atomicMin(a.err, (unsigned long long)SDB_DEVICE_ERROR);
@@ -234,375 +1399,301 @@ __global__ __launch_bounds__(kCzThreads) void k_cz(CzArgs a) {
     crc_tables_to_lds((lu32 *)smem);
     __syncthreads();
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    lu8 *wb = (lu8 *)smem + kCrcTablesLds + w * kCzWaveLds;
+    lu8 *wb = (lu8 *)smem + kCrcTablesLds + w * Cfg::kWaveLds;
     lu8 *in = wb;
-    lu32 *ht = (lu32 *)(wb + kCzIn);
-    lu32 *seq = ht;  // after the match pass: 2 dwords per sequence (lit | mlen << 16, off)
-    lu32 *mm = (lu32 *)(wb + kCzIn + kCzHt);
+    lu32 *head = (lu32 *)(wb + kCzIn);
+    lu32 *seq = head;  // after the match pass: 2 dwords per sequence
+    lu16 *prev = (lu16 *)(wb + kCzIn + kCzHead);
+    lu8 *hz = (lu8 *)prev;  // after the match pass: the entropy coders' scratch (zlib / zstd)
+    lu32 *mm = (lu32 *)(wb + kCzIn + kCzHead + (Cfg::kDeep ? kCzPrev : 0));
     lu8 *out = (lu8 *)mm + kCzOutOff;
-    lu16 *p9 = (lu16 *)((lu8 *)mm + kCzP9Off);
+    lu8 *aux = (lu8 *)mm + kCzAuxOff;
     const uint64_t base = a.block_off[0];
-    for (uint64_t k = (uint64_t)blockIdx.x * kCzWaves + w; k < a.nblocks; k += (uint64_t)gridDim.x * kCzWaves) {
+    for (uint64_t k = (uint64_t)blockIdx.x * Cfg::kWaves + w; k < a.nblocks; k += (uint64_t)gridDim.x * Cfg::kWaves) {
         const uint64_t s = a.block_off[k], e = a.block_off[k + 1];
-        uint8_t *slot = a.slots + cz_slot(s - base, k);
-        if (e < s + 4) {  // no block (Block::encode() ++ CRC is at least 8 bytes): the caller's error
+        if (e < s + 4 || e - base > a.in_bytes) {  // no block (Block::encode() ++ CRC is >= 8 bytes), or past in_bytes
             if (l == 0) {
-                atomicMin(a.err, (unsigned long long)((k << 8) | SDB_CORRUPT_BLOCK));
+                atomicMin(a.err, (unsigned long long)((k << 8) | (e < s + 4 ? SDB_CORRUPT_BLOCK : SDB_INVALID_ARGUMENT)));
                 a.len[k] = 0;
             }
             continue;
         }
+        uint8_t *slot = a.slots + cz_slot(s - base, k);
         const uint32_t n = (uint32_t)(e - 4 - s);  // Block::encode() bytes (the stored CRC is not compressed)
-        if (n > kCzMax) {
-            uint32_t m = 0;
-            if (l == 0) {
-                m = cz_literal_only(CODEC, a.blocks + s, n, slot);
-                uint32_t c = 0xFFFFFFFFu;
-                for (uint32_t i = 0; i < m; i++) c = (c >> 8) ^ c_crc.t[0][(c ^ slot[i]) & 0xFF];
-                c = ~c;
-                slot[m] = (uint8_t)(c >> 24); slot[m + 1] = (uint8_t)(c >> 16); slot[m + 2] = (uint8_t)(c >> 8); slot[m + 3] = (uint8_t)c;
-                a.len[k] = m + 4;
-            }
-            continue;
-        }
-        // stage the block (16-byte granules) and zero the 64 bytes past it
-        {
-            const uint64_t g0 = s & ~15ull;
-            const uint32_t lead = (uint32_t)(s - g0), ng = (lead + n + 15) >> 4;
-            for (uint32_t q = l; q < ng; q += 64) {
-                const uint4 v = ((const uint4 *)(a.blocks + g0))[q];
-                const uint32_t d0 = 16 * q;  // byte d0 - lead of the block
-                const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+        const uint8_t *src = a.blocks + s;
+        // window state (wave-uniform)
+        uint32_t w0 = 0, opos = 0, crc = 0;
+        uint32_t zcarry = 0, zbyte = 0;  // zlib: bits of a partial byte carried into the next window
+        uint64_t sa = 0, sb = 0;         // zlib: Adler-32 sums
+        uint32_t rep[3] = {1, 4, 8};     // zstd: repeat offsets
+        bool fallback = false;
+        for (;;) {
+            const uint32_t wn = n - w0 < kCzWin ? n - w0 : kCzWin;
+            const bool first = w0 == 0, last = w0 + wn == n;
+            // stage the window (16-byte granules) and zero the 64 bytes past it
+            {
+                const uint64_t g0 = (s + w0) & ~15ull;
+                const uint32_t lead = (uint32_t)(s + w0 - g0), ng = (lead + wn + 15) >> 4;
+                for (uint32_t q = l; q < ng; q += 64) {
+                    const uint4 v = ((const uint4 *)(a.blocks + g0))[q];
+                    const uint32_t d0 = 16 * q;
+                    const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-                for (int b = 0; b < 16; b++) {
-                    const int64_t x = (int64_t)d0 + b - lead;
-                    if (x >= 0 && x < (int64_t)n) in[x] = (uint8_t)(vv[b >> 2] >> (8 * (b & 3)));
-                }
-            }
-            in[n + l] = 0;
-            for (uint32_t q = l; q < (1u << kCzHashBits); q += 64) ht[q] = 0;
-        }
-        wsync();
-        // a. matches: batches of 64 positions, lane = position
-        uint64_t vmask = 0;
-        const uint32_t last = n >= 4 ? n - 4 : 0;  // positions with 4 bytes to hash: [0, last]
-        for (uint32_t b0 = 0; b0 <= last && n >= 4; b0 += 64) {
-            const uint32_t p = b0 + l;
-            const bool live = p <= last;
-            const uint32_t v = live ? lds_u32u(in, p) : 0, h = cz_hash(v);
-            const uint32_t cand = live ? ht[h] : 0;  // latest position + 1 of an earlier batch
-            wsync();
-            if (live) __hip_atomic_fetch_max(&ht[h], p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-            uint32_t len = 0;
-            const uint32_t q = cand - 1;
-            if (live && cand && lds_u32u(in, q) == v) {
-                len = 4;
-                const uint32_t lim = n - p < kCzMaxMatch ? n - p : kCzMaxMatch;
-                while (len < lim && in[q + len] == in[p + len]) len++;
-            }
-            if (CODEC == SDB_CODEC_LZ4) {  // LZ4: a match starts 12+ bytes before the end, ends 5+ before it
-                if (p + 12 > n) len = 0;
-                else if (len > n - 5 - p) len = n - 5 - p;
-            }
-            if (len < 4) len = 0;
-            if (live) mm[p] = ((p - q) << 16) | len;
-            const uint64_t bits = __ballot(len >= 4);
-            if (l == (b0 >> 6)) vmask = bits;
-            wsync();
-        }
-        // b. the greedy parse: lit_start / cur wave-uniform, the next match = first set bit >= cur
-        uint32_t nseq = 0, ls = 0;
-        {
-            uint32_t cur = 0;
-            while (nseq < kCzMaxSeq && cur < n) {
-                const uint32_t w0 = cur >> 6;
-                const uint64_t mine = l < w0 ? 0 : (l == w0 ? (vmask & (~0ull << (cur & 63))) : vmask);
-                const uint64_t any = __ballot(mine != 0);
-                if (!any) break;
-                const uint32_t ww = (uint32_t)__builtin_ctzll(any);
-                const uint64_t mw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mine >> 32), (int)ww) << 32) |
-                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mine, (int)ww);
-                const uint32_t q = 64 * ww + (uint32_t)__builtin_ctzll(mw);
-                const uint32_t mq = mm[q];
-                const uint32_t len = mq & 0xFFFF, off = mq >> 16;
-                if (l == 0) {
-                    seq[2 * nseq] = (q - ls) | (len << 16);
-                    seq[2 * nseq + 1] = off;
-                }
-                nseq++;
-                ls = cur = q + len;
-            }
-        }
-        wsync();
-        // c. the codec's elements into out (the mm region: its match words are no longer needed)
-        uint32_t m = 0;  // output bytes
-        if (CODEC == SDB_CODEC_ZSTD) {
-            // one frame, Single_Segment, Frame_Content_Size; one raw block (RLE when every byte is equal)
-            const uint8_t b0 = in[0];
-            bool same = true;
-            for (uint32_t i = l; i < n; i += 64) same &= in[i] == b0;
-            same = __ballot(!same) == 0 && n > 0;
-            if (l == 0) {
-                out[0] = 0x28; out[1] = 0xB5; out[2] = 0x2F; out[3] = 0xFD;
-                uint32_t p = 4;
-                if (n < 256) { out[p++] = 0x20; out[p++] = (uint8_t)n; }
-                else { out[p++] = 0x60; out[p++] = (uint8_t)(n - 256); out[p++] = (uint8_t)((n - 256) >> 8); }
-                const uint32_t bh = 1u | ((same ? 1u : 0u) << 1) | (n << 3);
-                out[p++] = (uint8_t)bh; out[p++] = (uint8_t)(bh >> 8); out[p++] = (uint8_t)(bh >> 16);
-                ((lu32 *)mm)[0] = p;  // (scratch: the header length, in the lead-in, re-zeroed below)
-            }
-            wsync();
-            const uint32_t hdr = ((lu32 *)mm)[0];
-            wsync();
-            if (same) {
-                if (l == 0) out[hdr] = b0;
-                m = hdr + 1;
-            } else {
-                for (uint32_t i = l; i < n; i += 64) out[hdr + i] = in[i];
-                m = hdr + n;
-            }
-        } else if (CODEC == SDB_CODEC_ZLIB) {
-            // P9 = prefix count of literals >= 144 (9-bit codes), by 64-byte chunks with a carry
-            {
-                uint32_t carry = 0;
-                for (uint32_t c0 = 0; c0 < n + 1; c0 += 64) {
-                    const uint32_t i = c0 + l;
-                    const uint32_t v = (i < n && in[i] >= 144) ? 1u : 0u;
-                    const uint32_t inc = wave_incl_scan(v);
-                    if (i <= n) p9[i] = (uint16_t)(carry + inc - v);
-                    carry += wave_readlane(inc, 63);
-                }
-            }
-            wsync();
-            // sizes in bits: per sequence its literals + its match; the final literals after them
-            const uint32_t nchunk = (nseq + 63) / 64;
-            uint32_t carry_bits = 3, carry_pos = 0;  // after BFINAL / BTYPE
-            lu32 *bw = (lu32 *)(out + 4);  // the deflate stream: 16-byte aligned words past the 2 header bytes + 2 pad
-            // (out[2..4) pad: deflate bytes are gathered to out + 2 after the stream is complete)
-            const uint32_t cap_words = (kCzP9Off - kCzOutOff - 8) / 4;
-            for (uint32_t q = l; q < cap_words; q += 64) bw[q] = 0;
-            wsync();
-            if (l == 0) put_bits(bw, 0, 3, 3);  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
-            for (uint32_t ch = 0; ch < nchunk; ch++) {
-                const uint32_t i = 64 * ch + l;
-                const bool v = i < nseq;
-                const uint32_t s0 = v ? seq[2 * i] : 0, off = v ? seq[2 * i + 1] : 0;
-                const uint32_t lit = s0 & 0xFFFF, len = s0 >> 16;
-                const uint32_t span = lit + len;
-                const uint32_t pinc = wave_incl_scan(span);
-                const uint32_t lstart = carry_pos + pinc - span;
-                uint32_t mb = 0, mbits = 0;
-                if (v) mbits = deflate_match(len, off, &mb);
-                const uint32_t bits = v ? 8 * lit + (p9[lstart + lit] - p9[lstart]) + mb : 0;
-                const uint32_t binc = wave_incl_scan(bits);
-                const uint32_t bstart = carry_bits + binc - bits;
-                if (v) put_bits(bw, bstart + bits - mb, mbits, mb);
-                // the chunk's literals, a sequence at a time, by the wave
-                for (uint32_t j = 0; j < 64 && 64 * ch + j < nseq; j++) {
-                    const uint32_t ls_j = (uint32_t)__builtin_amdgcn_readlane((int)lstart, (int)j);
-                    const uint32_t lit_j = (uint32_t)__builtin_amdgcn_readlane((int)lit, (int)j);
-                    const uint32_t b_j = (uint32_t)__builtin_amdgcn_readlane((int)bstart, (int)j);
-                    for (uint32_t x = l; x < lit_j; x += 64) {
-                        const uint32_t c = in[ls_j + x];
-                        uint32_t nb;
-                        const uint32_t code = fixed_code(c, &nb);
-                        put_bits(bw, b_j + 8 * x + (p9[ls_j + x] - p9[ls_j]), code, nb);
+                    for (int b = 0; b < 16; b++) {
+                        const int64_t x = (int64_t)d0 + b - lead;
+                        if (x >= 0 && x < (int64_t)wn) in[x] = (uint8_t)(vv[b >> 2] >> (8 * (b & 3)));
                     }
                 }
-                carry_bits += wave_readlane(binc, 63);
-                carry_pos += wave_readlane(pinc, 63);
-            }
-            // final literals [carry_pos, n), then end-of-block
-            {
-                const uint32_t ls_f = carry_pos, lit_f = n - carry_pos;
-                for (uint32_t x = l; x < lit_f; x += 64) {
-                    const uint32_t c = in[ls_f + x];
-                    uint32_t nb;
-                    const uint32_t code = fixed_code(c, &nb);
-                    put_bits(bw, carry_bits + 8 * x + (p9[ls_f + x] - p9[ls_f]), code, nb);
-                }
-                carry_bits += 8 * lit_f + (p9[n] - p9[ls_f]);
-                if (l == 0) put_bits(bw, carry_bits, 0, 7);  // 256 = seven zero bits
-                carry_bits += 7;
+                in[wn + l] = 0;
             }
             wsync();
-            const uint32_t fixed_bytes = (carry_bits + 7) >> 3, stored_bytes = 5 + n;
-            // Adler-32 of the block: A = 1 + sum b, B = n + sum (n - i) b (mod 65521)
-            uint64_t sa = 0, sb = 0;
-            for (uint32_t i = l; i < n; i += 64) {
-                sa += in[i];
-                sb += (uint64_t)(n - i) * in[i];
+            const uint64_t vmask = cz_matches<CODEC>(in, wn, n - w0, head, prev, mm);
+            uint32_t tail = 0;
+            const uint32_t nseq = cz_parse(vmask, wn, mm, seq, &tail);
+            if (CODEC == SDB_CODEC_LZ4 && !last && nseq == 0) {  // no sequence can end this window
+                fallback = true;
+                break;
             }
-            sa = wave_sum(sa);
-            sb = wave_sum(sb);
-            const uint32_t A = (uint32_t)((1 + sa) % 65521), B = (uint32_t)((n + sb) % 65521);
-            uint32_t p;
-            if (fixed_bytes <= stored_bytes) {
-                // move the stream from out + 4 down to out + 2 (bytes, ascending: the source is ahead)
-                for (uint32_t c0 = 0; c0 < fixed_bytes; c0 += 64) {
-                    const uint32_t i = c0 + l;
-                    const uint8_t v = i < fixed_bytes ? out[4 + i] : 0;
-                    wsync();
-                    if (i < fixed_bytes) out[2 + i] = v;
-                    wsync();
+            // c. the codec's elements into out (the mm region: its match words are no longer needed)
+            for (uint32_t q = l; q < kCzOutCap / 4 + 16; q += 64) ((lu32 *)mm)[q] = 0;  // lead-in + out
+            wsync();
+            uint32_t m = 0;        // output bytes of this window
+            uint32_t next_w0 = w0 + wn;
+            if constexpr (CODEC == SDB_CODEC_ZSTD) {
+                uint32_t hb = 0;
+                if (first && l == 0) {
+                    out[0] = 0x28; out[1] = 0xB5; out[2] = 0x2F; out[3] = 0xFD;
+                    uint32_t p = 4;
+                    if (n < 256) { out[p++] = 0x20; out[p++] = (uint8_t)n; }
+                    else if (n < 65536 + 256) { out[p++] = 0x60; out[p++] = (uint8_t)(n - 256); out[p++] = (uint8_t)((n - 256) >> 8); }
+                    else { out[p++] = 0xA0; out[p++] = (uint8_t)n; out[p++] = (uint8_t)(n >> 8); out[p++] = (uint8_t)(n >> 16); out[p++] = (uint8_t)(n >> 24); }
                 }
-                p = 2 + fixed_bytes;
-            } else {
-                for (uint32_t i = l; i < n; i += 64) out[7 + i] = in[i];
+                if (first) hb = n < 256 ? 6 : (n < 65536 + 256 ? 7 : 9);
+                const uint8_t b0 = in[0];
+                bool same = true;
+                for (uint32_t i = l; i < wn; i += 64) same &= in[i] == b0;
+                same = __ballot(!same) == 0 && wn > 0;
+                uint32_t content = 0, btype = 0;
+                if (!same && wn >= 16) {
+                    content = cz_zstd_window(in, wn, seq, nseq, out, hb + 3, rep, hz, aux);
+                    btype = content ? 2 : 0;
+                } else if (same) {
+                    btype = 1;
+                }
+                if (btype == 0) {  // raw block: the window's bytes (the bit region may hold a discarded attempt)
+                    for (uint32_t i = l; i < wn; i += 64) out[hb + 3 + i] = in[i];
+                    content = wn;
+                } else if (btype == 1) {
+                    if (l == 0) out[hb + 3] = b0;
+                    content = 1;
+                }
                 if (l == 0) {
-                    out[2] = 1;
-                    out[3] = (uint8_t)n; out[4] = (uint8_t)(n >> 8);
-                    out[5] = (uint8_t)~n; out[6] = (uint8_t)(~n >> 8);
+                    const uint32_t bh = (last ? 1u : 0u) | (btype << 1) | ((btype == 1 ? wn : content) << 3);
+                    out[hb] = (uint8_t)bh; out[hb + 1] = (uint8_t)(bh >> 8); out[hb + 2] = (uint8_t)(bh >> 16);
                 }
-                p = 7 + n;
-            }
-            if (l == 0) {
-                out[0] = 0x78;
-                out[1] = 0x9C;
-                out[p] = (uint8_t)(B >> 8); out[p + 1] = (uint8_t)B; out[p + 2] = (uint8_t)(A >> 8); out[p + 3] = (uint8_t)A;
-            }
-            m = p + 4;
-        } else {
-            // LZ4 / Snappy: byte elements.  Header: lz4 u32 LE length; snappy varint length.
-            uint32_t hdr = 4;
-            if (CODEC == SDB_CODEC_SNAPPY) hdr = n < 128 ? 1 : (n < 16384 ? 2 : 3);
-            if (l == 0) {
-                if (CODEC == SDB_CODEC_LZ4) {
-                    out[0] = (uint8_t)n; out[1] = (uint8_t)(n >> 8); out[2] = (uint8_t)(n >> 16); out[3] = (uint8_t)(n >> 24);
+                m = hb + 3 + content;
+                // the rest of the bit region past m is never read: the slot copy takes [0, m)
+            } else if constexpr (CODEC == SDB_CODEC_ZLIB) {
+                uint32_t hb = 0;
+                if (first && l == 0) {
+                    out[0] = 0x78;
+                    out[1] = 0x9C;
+                }
+                if (first) hb = 2;
+                else if (l == 0 && zcarry) out[0] = (uint8_t)zbyte;
+                wsync();
+                {
+                    uint64_t xa = 0, xb = 0;
+                    for (uint32_t i = l; i < wn; i += 64) {
+                        xa += in[i];
+                        xb += (uint64_t)(n - (w0 + i)) * in[i];
+                    }
+                    sa += wave_sum(xa);
+                    sb += wave_sum(xb);
+                }
+                const uint32_t endb = cz_deflate_window(in, wn, seq, nseq, out, 8 * hb + zcarry, last, hz, aux);
+                if (last) {
+                    m = (endb + 7) >> 3;
+                    const uint32_t A = (uint32_t)((1 + sa) % 65521), B = (uint32_t)((n + sb) % 65521);
+                    if (l == 0) {
+                        out[m] = (uint8_t)(B >> 8); out[m + 1] = (uint8_t)B; out[m + 2] = (uint8_t)(A >> 8); out[m + 3] = (uint8_t)A;
+                    }
+                    m += 4;
                 } else {
-                    uint32_t x = n, p = 0;
-                    for (;; x >>= 7) {
-                        out[p++] = (uint8_t)(x >= 0x80 ? (x & 0x7F) | 0x80 : x);
-                        if (x < 0x80) break;
+                    m = endb >> 3;
+                    zcarry = endb & 7;
+                    zbyte = zcarry ? out[m] : 0;
+                }
+            } else {
+                // LZ4 / Snappy: byte elements.  Header: lz4 u32 LE length; snappy varint length.
+                uint32_t hdr = 0;
+                if (first) hdr = CODEC == SDB_CODEC_LZ4 ? 4 : (n < 128 ? 1 : (n < 16384 ? 2 : (n < (1u << 21) ? 3 : 4)));
+                if (first && l == 0) {
+                    if (CODEC == SDB_CODEC_LZ4) {
+                        out[0] = (uint8_t)n; out[1] = (uint8_t)(n >> 8); out[2] = (uint8_t)(n >> 16); out[3] = (uint8_t)(n >> 24);
+                    } else {
+                        uint32_t x = n, p = 0;
+                        for (;; x >>= 7) {
+                            out[p++] = (uint8_t)(x >= 0x80 ? (x & 0x7F) | 0x80 : x);
+                            if (x < 0x80) break;
+                        }
                     }
                 }
-            }
-            // element sizes: literal header + literals + match element(s)
-            auto lit_hdr = [](uint32_t lit) -> uint32_t {
-                if (CODEC == SDB_CODEC_LZ4) return lit >= 15 ? (lit - 15) / 255 + 1 : 0;  // (the token counted with the match)
-                if (!lit) return 0;
-                const uint32_t v = lit - 1;
-                return v < 60 ? 1 : v < 256 ? 2 : 3;
-            };
-            auto match_bytes = [](uint32_t len, uint32_t off) -> uint32_t {
-                if (CODEC == SDB_CODEC_LZ4) return 2 + (len - 4 >= 15 ? (len - 4 - 15) / 255 + 1 : 0);
-                uint32_t b = 0;  // snappy: copy-2 elements of 64 (60 before a short tail), then the rest
-                while (len >= 68) { b += 3; len -= 64; }
-                if (len > 64) { b += 3; len -= 60; }
-                return b + ((len < 12 && off < 2048) ? 2 : 3);
-            };
-            const uint32_t nchunk = (nseq + 63) / 64;
-            uint32_t carry_out = hdr, carry_pos = 0;
-            for (uint32_t ch = 0; ch < nchunk; ch++) {
-                const uint32_t i = 64 * ch + l;
-                const bool v = i < nseq;
-                const uint32_t s0 = v ? seq[2 * i] : 0, off = v ? seq[2 * i + 1] : 0;
-                const uint32_t lit = s0 & 0xFFFF, len = s0 >> 16;
-                const uint32_t span = lit + len, pinc = wave_incl_scan(span);
-                const uint32_t lstart = carry_pos + pinc - span;
-                const uint32_t lh = v ? lit_hdr(lit) : 0, mb = v ? match_bytes(len, off) : 0;
-                const uint32_t sz = v ? (CODEC == SDB_CODEC_LZ4 ? 1 : 0) + lh + lit + mb : 0;
-                const uint32_t oinc = wave_incl_scan(sz);
-                const uint32_t o0 = carry_out + oinc - sz;
-                if (v) {
-                    uint32_t p = o0;
-                    if (CODEC == SDB_CODEC_LZ4) {
-                        const uint32_t ml = len - 4;
-                        out[p++] = (uint8_t)(((lit >= 15 ? 15 : lit) << 4) | (ml >= 15 ? 15 : ml));
-                        if (lit >= 15) {
-                            uint32_t x = lit - 15;
-                            for (; x >= 255; x -= 255) out[p++] = 255;
-                            out[p++] = (uint8_t)x;
-                        }
-                        p += lit;
-                        out[p++] = (uint8_t)off;
-                        out[p++] = (uint8_t)(off >> 8);
-                        if (ml >= 15) {
-                            uint32_t x = ml - 15;
-                            for (; x >= 255; x -= 255) out[p++] = 255;
-                            out[p++] = (uint8_t)x;
-                        }
-                    } else {
-                        if (lit) {
-                            const uint32_t x = lit - 1;
-                            if (x < 60) out[p++] = (uint8_t)(x << 2);
-                            else if (x < 256) { out[p++] = 60 << 2; out[p++] = (uint8_t)x; }
-                            else { out[p++] = 61 << 2; out[p++] = (uint8_t)x; out[p++] = (uint8_t)(x >> 8); }
-                        }
-                        p += lit;
-                        uint32_t r = len;
-                        auto copy2 = [&](uint32_t c) {
-                            out[p++] = (uint8_t)(2 | ((c - 1) << 2));
+                auto lit_hdr = [](uint32_t lit) -> uint32_t {
+                    if (CODEC == SDB_CODEC_LZ4) return lit >= 15 ? (lit - 15) / 255 + 1 : 0;  // (the token counted with the match)
+                    if (!lit) return 0;
+                    const uint32_t v = lit - 1;
+                    return v < 60 ? 1 : v < 256 ? 2 : 3;
+                };
+                auto match_bytes = [](uint32_t len, uint32_t off) -> uint32_t {
+                    if (CODEC == SDB_CODEC_LZ4) return 2 + (len - 4 >= 15 ? (len - 4 - 15) / 255 + 1 : 0);
+                    uint32_t b = 0;  // snappy: copy-2 elements of 64 (60 before a short tail), then the rest
+                    while (len >= 68) { b += 3; len -= 64; }
+                    if (len > 64) { b += 3; len -= 60; }
+                    return b + ((len < 12 && off < 2048) ? 2 : 3);
+                };
+                const uint32_t nchunk = (nseq + 63) / 64;
+                uint32_t carry_out = hdr, carry_pos = 0;
+                for (uint32_t ch = 0; ch < nchunk; ch++) {
+                    const uint32_t i = 64 * ch + l;
+                    const bool v = i < nseq;
+                    const uint32_t s0 = v ? seq[2 * i] : 0, off = v ? seq[2 * i + 1] : 0;
+                    const uint32_t lit = s0 & 0xFFFF, len = s0 >> 16;
+                    const uint32_t span = lit + len, pinc = wave_incl_scan(span);
+                    const uint32_t lstart = carry_pos + pinc - span;
+                    const uint32_t lh = v ? lit_hdr(lit) : 0, mb = v ? match_bytes(len, off) : 0;
+                    const uint32_t sz = v ? (CODEC == SDB_CODEC_LZ4 ? 1 : 0) + lh + lit + mb : 0;
+                    const uint32_t oinc = wave_incl_scan(sz);
+                    const uint32_t o0 = carry_out + oinc - sz;
+                    if (v) {
+                        uint32_t p = o0;
+                        if (CODEC == SDB_CODEC_LZ4) {
+                            const uint32_t ml = len - 4;
+                            out[p++] = (uint8_t)(((lit >= 15 ? 15 : lit) << 4) | (ml >= 15 ? 15 : ml));
+                            if (lit >= 15) {
+                                uint32_t x = lit - 15;
+                                for (; x >= 255; x -= 255) out[p++] = 255;
+                                out[p++] = (uint8_t)x;
+                            }
+                            p += lit;
                             out[p++] = (uint8_t)off;
                             out[p++] = (uint8_t)(off >> 8);
-                        };
-                        while (r >= 68) { copy2(64); r -= 64; }
-                        if (r > 64) { copy2(60); r -= 60; }
-                        if (r < 12 && off < 2048) {
-                            out[p++] = (uint8_t)(1 | ((r - 4) << 2) | ((off >> 8) << 5));
-                            out[p++] = (uint8_t)off;
+                            if (ml >= 15) {
+                                uint32_t x = ml - 15;
+                                for (; x >= 255; x -= 255) out[p++] = 255;
+                                out[p++] = (uint8_t)x;
+                            }
                         } else {
-                            copy2(r);
+                            if (lit) {
+                                const uint32_t x = lit - 1;
+                                if (x < 60) out[p++] = (uint8_t)(x << 2);
+                                else if (x < 256) { out[p++] = 60 << 2; out[p++] = (uint8_t)x; }
+                                else { out[p++] = 61 << 2; out[p++] = (uint8_t)x; out[p++] = (uint8_t)(x >> 8); }
+                            }
+                            p += lit;
+                            uint32_t r = len;
+                            auto copy2 = [&](uint32_t c) {
+                                out[p++] = (uint8_t)(2 | ((c - 1) << 2));
+                                out[p++] = (uint8_t)off;
+                                out[p++] = (uint8_t)(off >> 8);
+                            };
+                            while (r >= 68) { copy2(64); r -= 64; }
+                            if (r > 64) { copy2(60); r -= 60; }
+                            if (r < 12 && off < 2048) {
+                                out[p++] = (uint8_t)(1 | ((r - 4) << 2) | ((off >> 8) << 5));
+                                out[p++] = (uint8_t)off;
+                            } else {
+                                copy2(r);
+                            }
                         }
                     }
+                    // the chunk's literal runs, by the wave
+                    const uint32_t lpos = o0 + (CODEC == SDB_CODEC_LZ4 ? 1 : 0) + lh;
+                    const uint32_t ncur = nseq - 64 * ch < 64 ? nseq - 64 * ch : 64;
+                    for (uint32_t j = 0; j < ncur; j++) {
+                        const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)lstart, (int)j);
+                        const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane((int)lit, (int)j);
+                        const uint32_t dst = (uint32_t)__builtin_amdgcn_readlane((int)lpos, (int)j);
+                        for (uint32_t x = l; x < cnt; x += 64) out[dst + x] = in[sj + x];
+                    }
+                    carry_out += wave_readlane(oinc, 63);
+                    carry_pos += wave_readlane(pinc, 63);
                 }
-                // the chunk's literal runs, by the wave
-                const uint32_t lpos = o0 + (CODEC == SDB_CODEC_LZ4 ? 1 : 0) + lh;
-                for (uint32_t j = 0; j < 64 && 64 * ch + j < nseq; j++) {
-                    const uint32_t src = (uint32_t)__builtin_amdgcn_readlane((int)lstart, (int)j);
-                    const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane((int)lit, (int)j);
-                    const uint32_t dst = (uint32_t)__builtin_amdgcn_readlane((int)lpos, (int)j);
-                    for (uint32_t x = l; x < cnt; x += 64) out[dst + x] = in[src + x];
-                }
-                carry_out += wave_readlane(oinc, 63);
-                carry_pos += wave_readlane(pinc, 63);
-            }
-            // the final literals (lz4: a last sequence of literals only)
-            {
-                const uint32_t lit = n - carry_pos;
-                uint32_t p = carry_out;
-                if (CODEC == SDB_CODEC_LZ4) {
-                    if (l == 0) {
-                        out[p] = (uint8_t)((lit >= 15 ? 15 : lit) << 4);
-                        if (lit >= 15) {
-                            uint32_t x = lit - 15, q = p + 1;
-                            for (; x >= 255; x -= 255) out[q++] = 255;
-                            out[q] = (uint8_t)x;
+                // the window's final literals (lz4: only in the last window, as its last sequence; the
+                // other windows end at their last match and the next window starts there)
+                if (CODEC == SDB_CODEC_LZ4 && !last) {
+                    m = carry_out;
+                    next_w0 = w0 + tail;
+                } else {
+                    const uint32_t lit = wn - carry_pos;
+                    uint32_t p = carry_out;
+                    if (CODEC == SDB_CODEC_LZ4) {
+                        if (l == 0) {
+                            out[p] = (uint8_t)((lit >= 15 ? 15 : lit) << 4);
+                            if (lit >= 15) {
+                                uint32_t x = lit - 15, q = p + 1;
+                                for (; x >= 255; x -= 255) out[q++] = 255;
+                                out[q] = (uint8_t)x;
+                            }
                         }
+                        p += 1 + lit_hdr(lit);
+                    } else if (lit) {
+                        if (l == 0) {
+                            const uint32_t x = lit - 1;
+                            if (x < 60) out[p] = (uint8_t)(x << 2);
+                            else if (x < 256) { out[p] = 60 << 2; out[p + 1] = (uint8_t)x; }
+                            else { out[p] = 61 << 2; out[p + 1] = (uint8_t)x; out[p + 2] = (uint8_t)(x >> 8); }
+                        }
+                        p += lit_hdr(lit);
                     }
-                    p += 1 + lit_hdr(lit);
-                } else if (lit) {
-                    if (l == 0) {
-                        const uint32_t x = lit - 1;
-                        if (x < 60) out[p] = (uint8_t)(x << 2);
-                        else if (x < 256) { out[p] = 60 << 2; out[p + 1] = (uint8_t)x; }
-                        else { out[p] = 61 << 2; out[p + 1] = (uint8_t)x; out[p + 2] = (uint8_t)(x >> 8); }
-                    }
-                    p += lit_hdr(lit);
+                    for (uint32_t x = l; x < lit; x += 64) out[p + x] = in[carry_pos + x];
+                    m = p + lit;
                 }
-                for (uint32_t x = l; x < lit; x += 64) out[p + x] = in[carry_pos + x];
-                m = p + lit;
             }
+            wsync();
+            // d. CRC32 of the window's bytes (chained), then the slot
+            if (l < 16) ((lu32 *)mm)[l] = 0;  // the lead-in (scratch above may have used it)
+            wsync();
+            const uint32_t raw = cz_crc_raw(out, m, aux + 64, first);
+            crc = crc_shift_bytes(crc, m) ^ raw;
+            if (first && last) {  // one window: the CRC after the bytes, 16-byte stores into the aligned slot
+                const uint32_t c = ~crc;
+                if (l == 0) {
+                    out[m] = (uint8_t)(c >> 24); out[m + 1] = (uint8_t)(c >> 16); out[m + 2] = (uint8_t)(c >> 8); out[m + 3] = (uint8_t)c;
+                    a.len[k] = m + 4;
+                }
+                wsync();
+                const uint32_t n16 = (m + 4 + 15) >> 4;
+                for (uint32_t q = l; q < n16; q += 64) {
+                    const u32x4 v = ((const lu128 *)out)[q];
+                    uint4 g;
+                    g.x = v.x;
+                    g.y = v.y;
+                    g.z = v.z;
+                    g.w = v.w;
+                    ((uint4 *)slot)[q] = g;
+                }
+                wsync();
+                break;
+            }
+            for (uint32_t i = l; i < m; i += 64) slot[opos + i] = out[i];
+            opos += m;
+            wsync();
+            if (last) {
+                const uint32_t c = ~crc;
+                if (l < 4) slot[opos + l] = (uint8_t)(c >> (24 - 8 * l));
+                if (l == 0) a.len[k] = opos + 4;
+                break;
+            }
+            w0 = next_w0;
         }
-        wsync();
-        // d. CRC32 of the compressed bytes (lead-in zeroed: the scratch above may have used it), then the slot
-        if (l < 16) ((lu32 *)mm)[l] = 0;
-        wsync();
-        const uint32_t crc = cz_crc(out, m, (lu8 *)mm + kCzP9Off + 64);
-        if (l == 0) {
-            out[m] = (uint8_t)(crc >> 24); out[m + 1] = (uint8_t)(crc >> 16); out[m + 2] = (uint8_t)(crc >> 8); out[m + 3] = (uint8_t)crc;
+        if (fallback && l == 0) {  // lz4 only: one literal-only sequence, by one lane
+            const uint32_t m = cz_literal_only(CODEC, src, n, slot);
+            uint32_t c = 0xFFFFFFFFu;
+            for (uint32_t i = 0; i < m; i++) c = (c >> 8) ^ c_crc.t[0][(c ^ slot[i]) & 0xFF];
+            c = ~c;
+            slot[m] = (uint8_t)(c >> 24); slot[m + 1] = (uint8_t)(c >> 16); slot[m + 2] = (uint8_t)(c >> 8); slot[m + 3] = (uint8_t)c;
             a.len[k] = m + 4;
-        }
-        wsync();
-        const uint32_t tot = m + 4, n16 = (tot + 15) >> 4;  // slots are 16-byte aligned; out is too
-        for (uint32_t q = l; q < n16; q += 64) {
-            const u32x4 v = ((const lu128 *)out)[q];
-            uint4 g;
-            g.x = v.x;
-            g.y = v.y;
-            g.z = v.z;
-            g.w = v.w;
-            ((uint4 *)slot)[q] = g;
         }
         wsync();
     }
@@ -644,14 +1735,22 @@ uint64_t compress_workspace_bytes(uint64_t nblocks, uint64_t in_bytes) {
     return slots + 8 * (nblocks + 2) * 2 + 16 * (nt + 1) + 512;
 }
 
+template <uint32_t C>
+static void cz_launch(const CzArgs &a, hipStream_t st) {
+    using Cfg = CzCfg<C>;
+    const uint64_t wgs = (a.nblocks + Cfg::kWaves - 1) / Cfg::kWaves;
+    const uint32_t grid = (uint32_t)(wgs < 4096 ? wgs : 4096);
+    hipLaunchKernelGGL(k_cz<C>, dim3(grid), dim3(64 * Cfg::kWaves), Cfg::kLds, st, a);
+}
+
 hipError_t launch_compress(uint32_t codec, const uint8_t *blocks, const uint64_t *block_off, uint64_t nblocks,
                            uint64_t in_bytes, uint8_t *out, uint64_t out_cap, uint64_t *out_off,
                            unsigned long long *err, void *ws, hipStream_t st) {
     std::call_once(g_cz_once, [] {
-        (void)hipFuncSetAttribute((const void *)k_cz<SDB_CODEC_LZ4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCzLds);
-        (void)hipFuncSetAttribute((const void *)k_cz<SDB_CODEC_SNAPPY>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCzLds);
-        (void)hipFuncSetAttribute((const void *)k_cz<SDB_CODEC_ZLIB>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCzLds);
-        (void)hipFuncSetAttribute((const void *)k_cz<SDB_CODEC_ZSTD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCzLds);
+        (void)hipFuncSetAttribute((const void *)k_cz<SDB_CODEC_LZ4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CzCfg<SDB_CODEC_LZ4>::kLds);
+        (void)hipFuncSetAttribute((const void *)k_cz<SDB_CODEC_SNAPPY>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CzCfg<SDB_CODEC_SNAPPY>::kLds);
+        (void)hipFuncSetAttribute((const void *)k_cz<SDB_CODEC_ZLIB>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CzCfg<SDB_CODEC_ZLIB>::kLds);
+        (void)hipFuncSetAttribute((const void *)k_cz<SDB_CODEC_ZSTD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CzCfg<SDB_CODEC_ZSTD>::kLds);
         (void)hipGetLastError();
     });
     uint8_t *w = (uint8_t *)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
@@ -660,6 +1759,7 @@ hipError_t launch_compress(uint32_t codec, const uint8_t *blocks, const uint64_t
     a.blocks = blocks;
     a.block_off = block_off;
     a.nblocks = nblocks;
+    a.in_bytes = in_bytes;
     a.slots = w;
     uint8_t *tail = w + ((cz_slot(in_bytes, nblocks) + 255) & ~255ull);
     a.len = (uint64_t *)tail;
@@ -672,12 +1772,11 @@ hipError_t launch_compress(uint32_t codec, const uint8_t *blocks, const uint64_t
     a.err = err;
     if (hipMemsetAsync(err, 0xFF, 8, st) != hipSuccess) return hipErrorUnknown;
     if (!nblocks) return hipMemsetAsync(out_off, 0, 8, st);
-    const uint32_t grid = (uint32_t)((nblocks + kCzWaves - 1) / kCzWaves < 4096 ? (nblocks + kCzWaves - 1) / kCzWaves : 4096);
     switch (codec) {
-        case SDB_CODEC_LZ4: hipLaunchKernelGGL(k_cz<SDB_CODEC_LZ4>, dim3(grid), dim3(kCzThreads), kCzLds, st, a); break;
-        case SDB_CODEC_SNAPPY: hipLaunchKernelGGL(k_cz<SDB_CODEC_SNAPPY>, dim3(grid), dim3(kCzThreads), kCzLds, st, a); break;
-        case SDB_CODEC_ZLIB: hipLaunchKernelGGL(k_cz<SDB_CODEC_ZLIB>, dim3(grid), dim3(kCzThreads), kCzLds, st, a); break;
-        default: hipLaunchKernelGGL(k_cz<SDB_CODEC_ZSTD>, dim3(grid), dim3(kCzThreads), kCzLds, st, a); break;
+        case SDB_CODEC_LZ4: cz_launch<SDB_CODEC_LZ4>(a, st); break;
+        case SDB_CODEC_SNAPPY: cz_launch<SDB_CODEC_SNAPPY>(a, st); break;
+        case SDB_CODEC_ZLIB: cz_launch<SDB_CODEC_ZLIB>(a, st); break;
+        default: cz_launch<SDB_CODEC_ZSTD>(a, st); break;
     }
     hipError_t e = launch_excl_scan2(a.len, a.len, nblocks, tx, ty, out_off, scratch, st);
     if (e != hipSuccess) return e;

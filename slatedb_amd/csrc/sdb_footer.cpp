@@ -444,7 +444,10 @@ extern "C" sdb_status sdb_sst_footer(const sdb_footer_in *in, uint8_t *out, uint
         if (in->first_key_off[k + 1] < in->first_key_off[k]) return SDB_INVALID_ARGUMENT;
     const HostCrc &crc = host_crc();
     const uint64_t base = in->data_len;
-    thread_local FooterScratch sc;
+    // the caller's thread-local scratch, bound by reference: the stats lambda may run on a worker thread,
+    // and a lambda names a thread_local directly (it is not captured), so it must see this reference
+    thread_local FooterScratch tl_sc;
+    FooterScratch &sc = tl_sc;
 
     // 1. composite filter block [u16 count][u16 name_len]["_bf"][u64 len][Filter::encode]
     //    (format/sst.rs:394-421; Filter::encode = u16 BE num_probes ++ bitmap, filter.rs:177-180)

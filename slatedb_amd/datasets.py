@@ -162,3 +162,31 @@ def overwrite_runs(nruns=4, n=D1_N, value_len=100, overlap=0.75, tomb_frac=0.1, 
         runs.append(Batch(keys.reshape(-1), np.arange(n + 1, dtype=np.uint64) * np.uint64(16), vals, val_off,
                           kind, seq))
     return runs
+
+
+_FIRST = ["alice", "bob", "carol", "dave", "erin", "frank", "grace", "heidi", "ivan", "judy", "mallory",
+          "niaj", "olivia", "peggy", "rupert", "sybil", "trent", "victor", "walter", "yolanda"]
+_LAST = ["smith", "jones", "garcia", "miller", "davis", "lopez", "wilson", "taylor", "thomas", "moore",
+         "martin", "lee", "walker", "hall", "young", "king", "wright", "scott", "green", "baker"]
+_CITY = ["amsterdam", "berlin", "chicago", "denver", "edinburgh", "florence", "geneva", "houston",
+         "istanbul", "jakarta", "kyoto", "lisbon", "madrid", "nairobi", "oslo", "paris"]
+_TAGS = ["admin", "beta", "churned", "trial", "premium", "verified", "mobile", "eu", "us", "apac"]
+
+
+def text_kv(n=200_000, seed=11):
+    """A compressible set for the codec write side (f3): ASCII keys "user:%010d" (sorted, gaps) and JSON
+    documents of 90-200 bytes drawn from small vocabularies — the kind of values a KV store actually
+    compresses, unlike D1's random bytes."""
+    rng = np.random.default_rng(seed)
+    ids = np.cumsum(rng.integers(1, 50, n))
+    f, l, c = rng.integers(0, len(_FIRST), n), rng.integers(0, len(_LAST), n), rng.integers(0, len(_CITY), n)
+    age, score = rng.integers(18, 90, n), rng.integers(0, 100000, n)
+    nt = rng.integers(0, 4, n)
+    tg = rng.integers(0, len(_TAGS), (n, 3))
+    entries = []
+    for i in range(n):
+        tags = ",".join('"%s"' % _TAGS[t] for t in tg[i, :nt[i]])
+        v = ('{"name":"%s %s","email":"%s.%s@example.com","city":"%s","age":%d,"score":%d,"tags":[%s]}' %
+             (_FIRST[f[i]], _LAST[l[i]], _FIRST[f[i]], _LAST[l[i]], _CITY[c[i]], age[i], score[i], tags))
+        entries.append((b"user:%010d" % ids[i], 0, v.encode(), 0, None, None))
+    return Batch.from_entries(entries)

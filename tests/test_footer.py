@@ -224,3 +224,23 @@ def test_compressed_footer_blocks(codec):
     assert i1["compression"] == codec and i0["compression"] == 0
     assert (v1, x1, s1, f1) == (v0, x0, s0, f0)
     assert i1["first_entry"] == i0["first_entry"] and i1["last_entry"] == i0["last_entry"]
+
+
+def test_footer_threaded_stats_do_not_leak():
+    """nb >= 2048 builds the stats vector on a second thread; its scratch must be the caller's
+    (bound by reference), so repeated footers reuse it instead of leaking a fresh one per call."""
+    b = datasets.d1(n=80000, sst_index=3)
+    r = O.encode_sst(b, O.params())
+    assert r.summary.num_blocks >= 2048
+    want = runtime.sst_footer(b, r)
+
+    def rss():
+        with open("/proc/self/statm") as f:
+            return int(f.read().split()[1]) * 4096
+
+    for _ in range(20):
+        assert runtime.sst_footer(b, r) == want
+    r0 = rss()
+    for _ in range(300):
+        runtime.sst_footer(b, r)
+    assert rss() - r0 < 8 << 20, (rss() - r0)
