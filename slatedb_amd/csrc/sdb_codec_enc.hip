@@ -44,6 +44,26 @@
 
 namespace sdb {
 
+// Phase ticks (diagnostic builds with -DSDB_CZ_PT): s_memtime between marks, summed over waves.
+#ifdef SDB_CZ_PT
+__device__ unsigned long long g_cz_pt[16];
+#define CZ_T0(prev) uint64_t prev = __builtin_amdgcn_s_memtime()
+#define CZ_MARK(i, prev)                                                                              \
+    do {                                                                                              \
+        __builtin_amdgcn_s_waitcnt(0);                                                                \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                                             \
+        if (lane_id() == 0) atomicAdd(&g_cz_pt[i], (unsigned long long)(t_ - prev));                  \
+        prev = t_;                                                                                    \
+    } while (0)
+#else
+#define CZ_T0(prev) \
+    do {            \
+    } while (0)
+#define CZ_MARK(i, prev) \
+    do {                 \
+    } while (0)
+#endif
+
 typedef __attribute__((address_space(3))) uint16_t lu16;
 typedef __attribute__((address_space(3))) int16_t li16;
 typedef __attribute__((address_space(3))) int32_t li32;
@@ -60,12 +80,17 @@ constexpr uint32_t kCzOutCap = kCzAuxOff - kCzOutOff;
 constexpr uint32_t kCzMaxSeq = kCzHead / 8;         // a match is >= 4 bytes: a window has <= 1024 sequences
 constexpr uint32_t kCzMaxMatch = 258;
 constexpr uint32_t kCzNice = 128;                   // a chain walk stops at a match this long (zlib level 6)
+constexpr uint32_t kCzGood = 16;                    // ... and takes half of its remaining steps past this one
 
 template <uint32_t C>
 struct CzCfg {
     static constexpr bool kDeep = C == SDB_CODEC_ZLIB || C == SDB_CODEC_ZSTD;
     static constexpr uint32_t kWaves = kDeep ? 3 : 4;
+#ifdef SDB_CZ_DEPTH  // diagnostic: chain depth of zlib / zstd
+    static constexpr uint32_t kDepth = kDeep ? SDB_CZ_DEPTH : 1;
+#else
     static constexpr uint32_t kDepth = kDeep ? 16 : 1;
+#endif
     static constexpr uint32_t kWaveLds = kCzIn + kCzHead + (kDeep ? kCzPrev : 0) + kCzMm;
     static constexpr uint32_t kLds = kCrcTablesLds + kWaves * kWaveLds;
     static_assert(kLds <= 160 * 1024, "compress LDS");
@@ -94,6 +119,12 @@ SDB_DEV uint32_t lds_u32u(const lu8 *p, uint32_t i) {  // 4 bytes at any LDS byt
     const uint32_t a = lds_addr((const void *)(p + i));
     const lu32 *w = (const lu32 *)(uintptr_t)(a & ~3u);
     return __builtin_amdgcn_alignbyte(w[1], w[0], a & 3);
+}
+SDB_DEV uint64_t lds_u64u(const lu8 *p, uint32_t i) {  // 8 bytes at any LDS byte offset
+    const uint32_t a = lds_addr((const void *)(p + i));
+    const lu32 *w = (const lu32 *)(uintptr_t)(a & ~3u);
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, a & 3) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, a & 3) << 32);
 }
 SDB_DEV uint32_t cz_hash(uint32_t v) { return (v * 2654435761u) >> (32 - kCzHashBits); }
 SDB_DEV uint32_t hibit(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }  // v > 0
@@ -244,51 +275,84 @@ SDB_DEV uint64_t cz_matches(const lu8 *in, uint32_t wn, uint32_t room, lu32 *hea
     uint64_t vmask = 0;
     if (wn < 4) return 0;
     const uint32_t last = wn - 4;  // positions with 4 bytes to hash: [0, last]
-    for (uint32_t b0 = 0; b0 <= last; b0 += 64) {
-        const uint32_t p = b0 + l;
-        const bool live = p <= last;
-        const uint32_t v = live ? lds_u32u(in, p) : 0, h = cz_hash(v);
+    // two batches of 64 positions per step: both insert (the second batch after the first, so it sees it),
+    // then each lane walks its two chains interleaved (two independent LDS round trips in flight)
+    for (uint32_t b0 = 0; b0 <= last; b0 += 128) {
+        const uint32_t p0 = b0 + l, p1 = b0 + 64 + l;
+        const bool live0 = p0 <= last, live1 = p1 <= last;
+        const uint32_t v0 = live0 ? lds_u32u(in, p0) : 0, v1 = live1 ? lds_u32u(in, p1) : 0;
         // the latest earlier position + 1 with this hash: the exchange returns the previous holder, which for
         // lanes of one batch sharing a hash is the lane before (same-address LDS atomics of one instruction
         // are applied in lane order; a candidate not before p is never used, so any other order only loses
         // matches)
-        const uint32_t cand = live ? __hip_atomic_exchange(&head[h], p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : 0;
+        const uint32_t cand0 = live0 ? __hip_atomic_exchange(&head[cz_hash(v0)], p0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : 0;
+        const uint32_t cand1 = live1 ? __hip_atomic_exchange(&head[cz_hash(v1)], p1 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : 0;
         if constexpr (kDepth > 1) {
-            if (live) prev[p] = (uint16_t)cand;
+            if (live0) prev[p0] = (uint16_t)cand0;
+            if (live1) prev[p1] = (uint16_t)cand1;
         }
         wsync();
-        const uint32_t lim = live ? (wn - p < kCzMaxMatch ? wn - p : kCzMaxMatch) : 0;
-        uint32_t blen = 0, boff = 0, c = cand;
-        for (uint32_t d = 0; d < kDepth && c && c <= p; d++) {
-            const uint32_t q = c - 1;
-            if (lds_u32u(in, q) == v) {
-                uint32_t len = 4;
-                while (len < lim) {
-                    const uint32_t x = lds_u32u(in, q + len) ^ lds_u32u(in, p + len);
-                    if (x) {
-                        len += (uint32_t)__builtin_ctz(x) >> 3;
-                        break;
-                    }
-                    len += 4;
+        const uint32_t lim0 = live0 ? (wn - p0 < kCzMaxMatch ? wn - p0 : kCzMaxMatch) : 0;
+        const uint32_t lim1 = live1 ? (wn - p1 < kCzMaxMatch ? wn - p1 : kCzMaxMatch) : 0;
+        uint32_t bl0 = 0, bo0 = 0, c0 = cand0 <= p0 ? cand0 : 0;
+        uint32_t bl1 = 0, bo1 = 0, c1 = cand1 <= p1 ? cand1 : 0;
+        auto extend = [&](uint32_t q, uint32_t p, uint32_t lim) -> uint32_t {
+            uint32_t len = 4;
+            while (len < lim) {
+                const uint64_t x = lds_u64u(in, q + len) ^ lds_u64u(in, p + len);
+                if (x) {
+                    len += (uint32_t)__builtin_ctzll(x) >> 3;
+                    break;
                 }
-                if (len > lim) len = lim;
-                if (len > blen) {
-                    blen = len;
-                    boff = p - q;
-                    if (len >= kCzNice) break;
+                len += 8;
+            }
+            return len < lim ? len : lim;
+        };
+        // zlib's good / nice lengths: a match of kCzGood bytes cuts the rest of the chain to a half, one of
+        // kCzNice ends it
+        uint32_t dl0 = kDepth, dl1 = kDepth;
+        for (uint32_t d = 0; d < kDepth; d++) {
+            if (!c0 && !c1) break;
+            const uint32_t q0 = c0 ? c0 - 1 : 0, q1 = c1 ? c1 - 1 : 0;
+            const uint32_t w0 = lds_u32u(in, q0), w1 = lds_u32u(in, q1);
+            uint32_t n0 = 0, n1 = 0;
+            if constexpr (kDepth > 1) {
+                n0 = prev[q0];
+                n1 = prev[q1];
+            }
+            if (c0 && w0 == v0) {
+                const uint32_t len = extend(q0, p0, lim0);
+                if (len > bl0) {
+                    if (bl0 < kCzGood && len >= kCzGood) dl0 = d + 1 + (kDepth - d - 1) / 2;
+                    bl0 = len;
+                    bo0 = p0 - q0;
+                    if (len >= kCzNice) n0 = 0;
                 }
             }
-            if constexpr (kDepth > 1) c = prev[q];
-            else c = 0;
+            if (c1 && w1 == v1) {
+                const uint32_t len = extend(q1, p1, lim1);
+                if (len > bl1) {
+                    if (bl1 < kCzGood && len >= kCzGood) dl1 = d + 1 + (kDepth - d - 1) / 2;
+                    bl1 = len;
+                    bo1 = p1 - q1;
+                    if (len >= kCzNice) n1 = 0;
+                }
+            }
+            c0 = c0 && d + 1 < dl0 ? n0 : 0;
+            c1 = c1 && d + 1 < dl1 ? n1 : 0;
         }
-        if (CODEC == SDB_CODEC_LZ4) {  // LZ4: a match starts 12+ bytes before the end, ends 5+ before it
-            if (p + 12 > room) blen = 0;
-            else if (blen > room - 5 - p) blen = room - 5 - p;
-        }
-        if (blen < 4) blen = 0;
-        if (live) mm[p] = (boff << 16) | blen;
-        const uint64_t bits = __ballot(blen >= 4);
-        if (l == (b0 >> 6)) vmask = bits;
+        auto finish = [&](uint32_t p, bool live, uint32_t blen, uint32_t boff, uint32_t bsel) {
+            if (CODEC == SDB_CODEC_LZ4) {  // LZ4: a match starts 12+ bytes before the end, ends 5+ before it
+                if (p + 12 > room) blen = 0;
+                else if (blen > room - 5 - p) blen = room - 5 - p;
+            }
+            if (blen < 4) blen = 0;
+            if (live) mm[p] = (boff << 16) | blen;
+            const uint64_t bits = __ballot(blen >= 4);
+            if (l == bsel) vmask = bits;
+        };
+        finish(p0, live0, bl0, bo0, b0 >> 6);
+        finish(p1, live1, bl1, bo1, (b0 >> 6) + 1);
         wsync();
     }
     return vmask;
@@ -330,11 +394,42 @@ SDB_DEV uint32_t cz_parse(uint64_t vmask, uint32_t wn, const lu32 *mm, lu32 *seq
 // ------------------------------------------------------------------------------------------------
 // Huffman code lengths of the symbols with nonzero f[0, ns) (ns <= 512, at least two of them), each
 // <= maxlen, by the wave: nonzero (freq << 9 | sym) keys compacted and bitonic-sorted in `work` (>= the
-// next power of two of their count), lengths of the sorted run by Moffat & Katajainen's in-place method on
-// lane 0 (A: >= ns words), the Kraft-sum limit on the per-length counts, then lengths handed out longest
-// first to the least frequent symbols.  len[0, ns) written (0 for absent symbols).  Returns max length.
+// next power of two of their count); Moffat & Katajainen's in-place method over the sorted run on lane 0
+// (Al: >= ns LDS words; an array held in VGPRs and accessed by readlane at wave-uniform indices measured
+// four times slower: SGPR spills); then the lengths lane-interleaved in eight VGPRs for the Kraft-sum
+// length limit on the per-length counts (ballots), handed out longest first to the least frequent symbols.  len[0, ns) written (0 for absent symbols).  Returns the max length.
 // ------------------------------------------------------------------------------------------------
-SDB_DEV uint32_t wave_huff_lengths(const lu32 *f, uint32_t ns, uint32_t maxlen, lu8 *len, lu32 *work, lu32 *A) {
+struct WArr {  // 512 wave-uniform-indexed entries (a switch on the register: a dynamic index would spill to scratch)
+    uint32_t r[8];
+    SDB_DEV uint32_t get(uint32_t x) const {
+        const int ln = (int)(x & 63);
+        switch (x >> 6) {
+            case 0: return (uint32_t)__builtin_amdgcn_readlane((int)r[0], ln);
+            case 1: return (uint32_t)__builtin_amdgcn_readlane((int)r[1], ln);
+            case 2: return (uint32_t)__builtin_amdgcn_readlane((int)r[2], ln);
+            case 3: return (uint32_t)__builtin_amdgcn_readlane((int)r[3], ln);
+            case 4: return (uint32_t)__builtin_amdgcn_readlane((int)r[4], ln);
+            case 5: return (uint32_t)__builtin_amdgcn_readlane((int)r[5], ln);
+            case 6: return (uint32_t)__builtin_amdgcn_readlane((int)r[6], ln);
+            default: return (uint32_t)__builtin_amdgcn_readlane((int)r[7], ln);
+        }
+    }
+    SDB_DEV void set(uint32_t x, uint32_t v) {
+        const bool me = (uint32_t)lane_id() == (x & 63);
+        switch (x >> 6) {
+            case 0: r[0] = me ? v : r[0]; break;
+            case 1: r[1] = me ? v : r[1]; break;
+            case 2: r[2] = me ? v : r[2]; break;
+            case 3: r[3] = me ? v : r[3]; break;
+            case 4: r[4] = me ? v : r[4]; break;
+            case 5: r[5] = me ? v : r[5]; break;
+            case 6: r[6] = me ? v : r[6]; break;
+            default: r[7] = me ? v : r[7]; break;
+        }
+    }
+};
+
+SDB_DEV uint32_t wave_huff_lengths(const lu32 *f, uint32_t ns, uint32_t maxlen, lu8 *len, lu32 *work, lu32 *Al) {
     const uint32_t l = (uint32_t)lane_id();
     uint32_t m = 0;
     for (uint32_t i0 = 0; i0 < ns; i0 += 64) {
@@ -362,40 +457,41 @@ SDB_DEV uint32_t wave_huff_lengths(const lu32 *f, uint32_t ns, uint32_t maxlen, 
             wsync();
         }
     }
-    uint32_t mx = 0;
-    if (l == 0) {
+    if (m == 0) return 0;
+    if (l == 0) {  // Moffat & Katajainen on one lane, the array in LDS
         const int n = (int)m;
-        for (int i = 0; i < n; i++) A[i] = work[i] >> 9;
-        if (n == 1) A[0] = 1;
-        else if (n > 1) {
-            A[0] += A[1];
+        for (int i = 0; i < n; i++) Al[i] = work[i] >> 9;
+        if (n == 1) {
+            Al[0] = 1;
+        } else {
+            Al[0] += Al[1];
             int root = 0, leaf = 2, next;
             for (next = 1; next < n - 1; next++) {
-                if (leaf >= n || A[root] < A[leaf]) {
-                    A[next] = A[root];
-                    A[root++] = next;
+                if (leaf >= n || Al[root] < Al[leaf]) {
+                    Al[next] = Al[root];
+                    Al[root++] = next;
                 } else {
-                    A[next] = A[leaf++];
+                    Al[next] = Al[leaf++];
                 }
-                if (leaf >= n || (root < next && A[root] < A[leaf])) {
-                    A[next] += A[root];
-                    A[root++] = next;
+                if (leaf >= n || (root < next && Al[root] < Al[leaf])) {
+                    Al[next] += Al[root];
+                    Al[root++] = next;
                 } else {
-                    A[next] += A[leaf++];
+                    Al[next] += Al[leaf++];
                 }
             }
-            A[n - 2] = 0;
-            for (next = n - 3; next >= 0; next--) A[next] = A[A[next]] + 1;
+            Al[n - 2] = 0;
+            for (next = n - 3; next >= 0; next--) Al[next] = Al[Al[next]] + 1;
             int avbl = 1, used = 0, dpth = 0;
             root = n - 2;
             next = n - 1;
             while (avbl > 0) {
-                while (root >= 0 && (int)A[root] == dpth) {
+                while (root >= 0 && (int)Al[root] == dpth) {
                     used++;
                     root--;
                 }
                 while (avbl > used) {
-                    A[next--] = (uint32_t)dpth;
+                    Al[next--] = (uint32_t)dpth;
                     avbl--;
                 }
                 avbl = 2 * used;
@@ -403,49 +499,97 @@ SDB_DEV uint32_t wave_huff_lengths(const lu32 *f, uint32_t ns, uint32_t maxlen, 
                 used = 0;
             }
         }
-        // A[i]: length of the i-th least frequent symbol (non-increasing in i)
-        if (A[0] > maxlen) {
-            uint32_t cnt[16];
-            for (uint32_t b = 0; b <= 15; b++) cnt[b] = 0;
-            for (int i = 0; i < n; i++) cnt[A[i] > maxlen ? maxlen : A[i]]++;
-            uint32_t total = 0;
-            for (uint32_t b = 1; b <= maxlen; b++) total += cnt[b] << (maxlen - b);
-            while (total != (1u << maxlen)) {
-                cnt[maxlen]--;
-                for (uint32_t b = maxlen - 1; b > 0; b--)
-                    if (cnt[b]) {
-                        cnt[b]--;
-                        cnt[b + 1] += 2;
-                        break;
-                    }
-                total--;
-            }
-            int i = 0;
-            for (uint32_t b = maxlen; b >= 1; b--)
-                for (uint32_t c = 0; c < cnt[b]; c++) A[i++] = b;
-        }
-        mx = n ? A[0] : 0;
-        for (int i = 0; i < n; i++) len[work[i] & 511] = (uint8_t)A[i];
     }
     wsync();
-    return uni(mx);
+    WArr A;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) A.r[k] = 64 * k + l < m ? Al[64 * k + l] : 0;
+    // A[i]: length of the i-th least frequent symbol (non-increasing in i)
+    uint32_t mx = uni(A.r[0]);  // lane 0: the least frequent symbol's length, the longest
+    if (mx > maxlen) {
+        uint32_t cnt[16];
+        cnt[0] = 0;
+#pragma unroll
+        for (uint32_t b = 1; b < 16; b++) {
+            uint32_t c = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 8; k++) {
+                const bool in = 64 * k + l < m;
+                const uint32_t a = A.r[k] > maxlen ? maxlen : A.r[k];
+                c += (uint32_t)__builtin_popcountll(__ballot(in && a == b));
+            }
+            cnt[b] = c;
+        }
+        uint32_t total = 0;
+        for (uint32_t b = 1; b <= maxlen; b++) total += cnt[b] << (maxlen - b);
+        while (total != (1u << maxlen)) {
+            cnt[maxlen]--;
+            for (uint32_t b = maxlen - 1; b > 0; b--)
+                if (cnt[b]) {
+                    cnt[b]--;
+                    cnt[b + 1] += 2;
+                    break;
+                }
+            total--;
+        }
+        // entries [0, cnt[maxlen]) get maxlen, the next cnt[maxlen - 1] entries maxlen - 1, ...
+        uint32_t end[16];
+        uint32_t acc = 0;
+        for (int b = 15; b >= 1; b--) {
+            if ((uint32_t)b <= maxlen) acc += cnt[b];
+            end[b] = acc;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) {
+            const uint32_t i = 64 * k + l;
+            uint32_t b = maxlen;
+            while (b > 1 && i >= end[b]) b--;
+            A.r[k] = b;
+        }
+        mx = maxlen;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+        const uint32_t i = 64 * k + l;
+        if (i < m) len[work[i] & 511] = (uint8_t)A.r[k];
+    }
+    wsync();
+    return mx;
 }
 
-// deflate's canonical codes (RFC 1951 3.2.2), bit-reversed for the LSB-first stream.  One lane.
-SDB_DEV void deflate_codes(const lu8 *len, uint32_t ns, lu16 *code) {
-    uint32_t cnt[16], next[16];
+// deflate's canonical codes (RFC 1951 3.2.2), bit-reversed for the LSB-first stream, by the wave: the
+// per-length counts and each symbol's rank among the symbols of its length from ballots.
+SDB_DEV void wave_deflate_codes(const lu8 *len, uint32_t ns, lu16 *code) {
+    const uint32_t l = (uint32_t)lane_id();
+    uint32_t cnt[16];
+#pragma unroll
     for (uint32_t b = 0; b < 16; b++) cnt[b] = 0;
-    for (uint32_t s = 0; s < ns; s++) cnt[len[s]]++;
-    cnt[0] = 0;
+    for (uint32_t c0 = 0; c0 < ns; c0 += 64) {
+        const uint32_t b = c0 + l < ns ? len[c0 + l] : 0;
+#pragma unroll
+        for (uint32_t bl = 1; bl < 16; bl++) cnt[bl] += (uint32_t)__builtin_popcountll(__ballot(b == bl));
+    }
+    uint32_t next[16];
     uint32_t c = 0;
+    next[0] = 0;
+#pragma unroll
     for (uint32_t b = 1; b < 16; b++) {
-        c = (c + cnt[b - 1]) << 1;
+        c = (c + (b > 1 ? cnt[b - 1] : 0)) << 1;
         next[b] = c;
     }
-    for (uint32_t s = 0; s < ns; s++) {
-        const uint32_t b = len[s];
-        code[s] = b ? (uint16_t)rev_bits(next[b]++, b) : 0;
+    for (uint32_t c0 = 0; c0 < ns; c0 += 64) {
+        const uint32_t i = c0 + l;
+        const uint32_t b = i < ns ? len[i] : 0;
+        uint32_t cv = 0;
+#pragma unroll
+        for (uint32_t bl = 1; bl < 16; bl++) {
+            const uint64_t m = __ballot(b == bl);
+            if (b == bl) cv = next[bl] + lanes_below(m);
+            next[bl] += (uint32_t)__builtin_popcountll(m);
+        }
+        if (i < ns) code[i] = b ? (uint16_t)rev_bits(cv, b) : 0;
     }
+    wsync();
 }
 
 // The mask of literal positions of the window (bit p: not inside a match), the sequence starts from a
@@ -504,6 +648,7 @@ SDB_DEV uint32_t cz_deflate_window(const lu8 *in, uint32_t wn, const lu32 *seq, 
     lu32 *lmask = (lu32 *)aux;
     lu16 *plen = (lu16 *)aux;
     lu32 *bw = (lu32 *)out;
+    CZ_T0(pt);
     for (uint32_t q = l; q < 340; q += 64) hz.fq[q] = 0;  // fq + fcl
     cz_lit_mask(seq, nseq, wn, lmask);
     // histograms: each sequence's length and distance codes, then the literals
@@ -552,8 +697,10 @@ SDB_DEV uint32_t cz_deflate_window(const lu8 *in, uint32_t wn, const lu32 *seq, 
         }
         wsync();
     }
+    CZ_MARK(5, pt);
     wave_huff_lengths(hz.fq, 286, 15, hz.lens, hz.work, hz.A);
     wave_huff_lengths(hz.fq + 288, 30, 15, hz.lens + 288, hz.work, hz.A);
+    CZ_MARK(6, pt);
     // the code-length sequence (HLIT literal / length lengths, then HDIST distance lengths) run-length coded
     uint32_t hlit = 257, hdist = 1;
     for (uint32_t s = l; s < 286; s += 64)
@@ -561,57 +708,91 @@ SDB_DEV uint32_t cz_deflate_window(const lu8 *in, uint32_t wn, const lu32 *seq, 
     if (l < 30 && hz.lens[288 + l]) hdist = l + 1;
     hlit = wave_max(hlit);
     hdist = wave_max(hdist);
+    // run-length items (sym | extra << 5) by the wave: run starts from ballots, each start lane sizes and then
+    // writes its run's items (16 / 17 / 18 as zlib's send_tree) at a scanned position
     uint32_t nitem = 0;
-    if (l == 0) {
+    {
         const uint32_t N = hlit + hdist;
         auto L = [&](uint32_t i) -> uint32_t { return i < hlit ? hz.lens[i] : hz.lens[288 + i - hlit]; };
-        auto emit = [&](uint32_t sym, uint32_t x) {
-            hz.rle[nitem++] = (uint16_t)(sym | (x << 5));
-            hz.fcl[sym]++;
-        };
-        uint32_t i = 0;
-        while (i < N) {
-            const uint32_t v = L(i);
-            uint32_t run = 1;
-            while (i + run < N && L(i + run) == v) run++;
-            if (v == 0) {
-                while (run >= 11) {
-                    const uint32_t k = run < 138 ? run : 138;
-                    emit(18, k - 11);
-                    run -= k;
-                    i += k;
-                }
-                if (run >= 3) {
-                    emit(17, run - 3);
-                    i += run;
-                    run = 0;
-                }
-                for (; run; run--, i++) emit(0, 0);
-            } else {
-                emit(v, 0);
-                i++;
-                run--;
-                while (run >= 3) {
-                    const uint32_t k = run < 6 ? run : 6;
-                    emit(16, k - 3);
-                    run -= k;
-                    i += k;
-                }
-                for (; run; run--, i++) emit(v, 0);
-            }
+        for (uint32_t c0 = 0; c0 < N; c0 += 64) {
+            const uint32_t i = c0 + l;
+            const bool st = i < N && (i == 0 || L(i) != L(i - 1));
+            const uint64_t m = __ballot(st);
+            if (l == 0) ((__attribute__((address_space(3))) uint64_t *)(void *)hz.A)[c0 >> 6] = m;  // run-start bitmap
         }
-        uint32_t nz = 0;
-        for (uint32_t s = 0; s < 19; s++) nz += hz.fcl[s] != 0;
-        for (uint32_t s = 0; s < 19 && nz < 2; s++)
-            if (!hz.fcl[s]) {
-                hz.fcl[s] = 1;
-                nz++;
+        wsync();
+        const __attribute__((address_space(3))) uint64_t *sm = (const __attribute__((address_space(3))) uint64_t *)(void *)hz.A;
+        const uint32_t nw = (N + 63) >> 6;
+        for (uint32_t c0 = 0; c0 < N; c0 += 64) {
+            const uint32_t i = c0 + l;
+            const bool st = i < N && ((sm[c0 >> 6] >> l) & 1);
+            uint32_t v = 0, run = 0, ni = 0;
+            if (st) {
+                v = L(i);
+                uint32_t w = (i + 1) >> 6, nx = N;
+                uint64_t bits = w < nw ? sm[w] & (~0ull << ((i + 1) & 63)) : 0;
+                while (!bits && ++w < nw) bits = sm[w];
+                if (bits) nx = 64 * w + (uint32_t)__builtin_ctzll(bits);
+                run = nx - i;
+                uint32_t r = run;
+                if (v == 0) {
+                    while (r >= 11) { r -= r < 138 ? r : 138; ni++; }
+                    if (r >= 3) { ni++; r = 0; }
+                    ni += r;
+                } else {
+                    ni++;
+                    r--;
+                    while (r >= 3) { r -= r < 6 ? r : 6; ni++; }
+                    ni += r;
+                }
             }
-        hz.misc[0] = nitem;
+            const uint32_t inc = wave_incl_scan(ni);
+            uint32_t at = nitem + inc - ni;
+            if (st) {
+                auto emit = [&](uint32_t sym, uint32_t x) {
+                    hz.rle[at++] = (uint16_t)(sym | (x << 5));
+                    __hip_atomic_fetch_add(&hz.fcl[sym], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                };
+                uint32_t r = run;
+                if (v == 0) {
+                    while (r >= 11) {
+                        const uint32_t k = r < 138 ? r : 138;
+                        emit(18, k - 11);
+                        r -= k;
+                    }
+                    if (r >= 3) {
+                        emit(17, r - 3);
+                        r = 0;
+                    }
+                    for (; r; r--) emit(0, 0);
+                } else {
+                    emit(v, 0);
+                    r--;
+                    while (r >= 3) {
+                        const uint32_t k = r < 6 ? r : 6;
+                        emit(16, k - 3);
+                        r -= k;
+                    }
+                    for (; r; r--) emit(v, 0);
+                }
+            }
+            nitem += wave_readlane(inc, 63);
+        }
+        wsync();
+        if (l == 0) {
+            uint32_t nz = 0;
+            for (uint32_t s = 0; s < 19; s++) nz += hz.fcl[s] != 0;
+            for (uint32_t s = 0; s < 19 && nz < 2; s++)
+                if (!hz.fcl[s]) {
+                    hz.fcl[s] = 1;
+                    nz++;
+                }
+        }
+        wsync();
     }
-    wsync();
-    nitem = hz.misc[0];
+    CZ_MARK(7, pt);
     wave_huff_lengths(hz.fcl, 19, 7, hz.cll, hz.work, hz.A);
+    CZ_MARK(8, pt);
     uint32_t hclen = 19;
     {
         // the dynamic block's size: header + items + codes + extra bits
@@ -653,30 +834,33 @@ SDB_DEV uint32_t cz_deflate_window(const lu8 *in, uint32_t wn, const lu32 *seq, 
             if (l == 0) put_bits(bw, origin, (final ? 1u : 0u) | (1u << 1), 3);
             origin += 3;
         } else {
+            wave_deflate_codes(hz.lens, 286, hz.codes);
+            wave_deflate_codes(hz.lens + 288, 30, hz.codes + 288);
+            wave_deflate_codes(hz.cll, 19, hz.clc);
             if (l == 0) {
-                deflate_codes(hz.lens, 286, hz.codes);
-                deflate_codes(hz.lens + 288, 30, hz.codes + 288);
-                deflate_codes(hz.cll, 19, hz.clc);
-                uint32_t pos = origin;
-                put_bits(bw, pos, (final ? 1u : 0u) | (2u << 1), 3);
-                put_bits(bw, pos + 3, (hlit - 257) | ((hdist - 1) << 5) | ((hclen - 4) << 10), 14);
-                pos += 17;
-                for (uint32_t i = 0; i < hclen; i++, pos += 3) put_bits(bw, pos, hz.cll[c_cl_order[i]], 3);
-                for (uint32_t i = 0; i < nitem; i++) {
-                    const uint32_t it = hz.rle[i], sym = it & 31, x = it >> 5;
-                    put_bits(bw, pos, hz.clc[sym], hz.cll[sym]);
-                    pos += hz.cll[sym];
-                    const uint32_t xn = sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0;
-                    put_bits(bw, pos, x, xn);
-                    pos += xn;
-                }
-                hz.misc[1] = pos;
+                put_bits(bw, origin, (final ? 1u : 0u) | (2u << 1), 3);
+                put_bits(bw, origin + 3, (hlit - 257) | ((hdist - 1) << 5) | ((hclen - 4) << 10), 14);
             }
-            wsync();
-            origin = hz.misc[1];
+            if (l < hclen) put_bits(bw, origin + 17 + 3 * l, hz.cll[c_cl_order[l]], 3);
+            uint32_t pos = origin + 17 + 3 * hclen;
+            for (uint32_t c0 = 0; c0 < nitem; c0 += 64) {
+                const uint32_t i = c0 + l;
+                const uint32_t it = i < nitem ? hz.rle[i] : 0, sym = it & 31, x = it >> 5;
+                const uint32_t xn = sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0;
+                const uint32_t nb = i < nitem ? hz.cll[sym] + xn : 0;
+                const uint32_t inc = wave_incl_scan(nb);
+                const uint32_t at = pos + inc - nb;
+                if (i < nitem) {
+                    put_bits(bw, at, hz.clc[sym], hz.cll[sym]);
+                    put_bits(bw, at + hz.cll[sym], x, xn);
+                }
+                pos += wave_readlane(inc, 63);
+            }
+            origin = pos;
         }
     }
     wsync();
+    CZ_MARK(9, pt);
     // plen[i] = sum of the literal code lengths of bytes [0, i)
     {
         uint32_t carry = 0;
@@ -735,6 +919,7 @@ SDB_DEV uint32_t cz_deflate_window(const lu8 *in, uint32_t wn, const lu32 *seq, 
     if (l == 0) put_bits(bw, carry_bits, hz.codes[256], hz.lens[256]);
     carry_bits += hz.lens[256];
     wsync();
+    CZ_MARK(10, pt);
     return carry_bits;
 }
 
@@ -1073,7 +1258,15 @@ SDB_DEV uint32_t cz_zstd_window(const lu8 *in, uint32_t wn, lu32 *seq, uint32_t 
     uint32_t maxbits = 0;
     uint32_t td = 0;  // the tree description's bytes: direct weights, or FSE-compressed (hz.misc byte 16 on)
     bool tfse = false;
-    if (nz >= 2 && nlit >= 64) {
+    // the literals' order-0 entropy (bits, x16) bounds what a Huffman code can save: skip the code when even
+    // the entropy plus a tree description would not beat raw literals (random bytes, D1's values)
+    uint32_t hfx = 0;
+    for (uint32_t s = l; s < 256; s += 64) {
+        const uint32_t f = hz.fq[s];
+        if (f) hfx += (uint32_t)(16.f * (float)f * __log2f((float)nlit / (float)f));
+    }
+    hfx = wave_sum(hfx);
+    if (nz >= 2 && nlit >= 64 && hfx / 128 + 40 < nlit) {
         maxbits = wave_huff_lengths(hz.fq, maxsym + 1, 11, hz.lens, hz.work, hz.work + 256);
         uint32_t bits = 0;
         for (uint32_t s = l; s <= maxsym; s += 64) bits += hz.fq[s] * hz.lens[s];
@@ -1427,6 +1620,7 @@ __global__ __launch_bounds__(64 * CzCfg<CODEC>::kWaves) void k_cz(CzArgs a) {
         uint64_t sa = 0, sb = 0;         // zlib: Adler-32 sums
         uint32_t rep[3] = {1, 4, 8};     // zstd: repeat offsets
         bool fallback = false;
+        CZ_T0(kt);
         for (;;) {
             const uint32_t wn = n - w0 < kCzWin ? n - w0 : kCzWin;
             const bool first = w0 == 0, last = w0 + wn == n;
@@ -1447,9 +1641,12 @@ __global__ __launch_bounds__(64 * CzCfg<CODEC>::kWaves) void k_cz(CzArgs a) {
                 in[wn + l] = 0;
             }
             wsync();
+            CZ_MARK(0, kt);
             const uint64_t vmask = cz_matches<CODEC>(in, wn, n - w0, head, prev, mm);
+            CZ_MARK(1, kt);
             uint32_t tail = 0;
             const uint32_t nseq = cz_parse(vmask, wn, mm, seq, &tail);
+            CZ_MARK(2, kt);
             if (CODEC == SDB_CODEC_LZ4 && !last && nseq == 0) {  // no sequence can end this window
                 fallback = true;
                 break;
@@ -1474,7 +1671,11 @@ __global__ __launch_bounds__(64 * CzCfg<CODEC>::kWaves) void k_cz(CzArgs a) {
                 for (uint32_t i = l; i < wn; i += 64) same &= in[i] == b0;
                 same = __ballot(!same) == 0 && wn > 0;
                 uint32_t content = 0, btype = 0;
+#ifdef SDB_CZ_NOENT  // diagnostic: raw blocks (the match pass and parse only)
+                if (false) {
+#else
                 if (!same && wn >= 16) {
+#endif
                     content = cz_zstd_window(in, wn, seq, nseq, out, hb + 3, rep, hz, aux);
                     btype = content ? 2 : 0;
                 } else if (same) {
@@ -1651,6 +1852,7 @@ __global__ __launch_bounds__(64 * CzCfg<CODEC>::kWaves) void k_cz(CzArgs a) {
                 }
             }
             wsync();
+            CZ_MARK(3, kt);
             // d. CRC32 of the window's bytes (chained), then the slot
             if (l < 16) ((lu32 *)mm)[l] = 0;  // the lead-in (scratch above may have used it)
             wsync();
@@ -1674,8 +1876,10 @@ __global__ __launch_bounds__(64 * CzCfg<CODEC>::kWaves) void k_cz(CzArgs a) {
                     ((uint4 *)slot)[q] = g;
                 }
                 wsync();
+                CZ_MARK(4, kt);
                 break;
             }
+            CZ_MARK(4, kt);
             for (uint32_t i = l; i < m; i += 64) slot[opos + i] = out[i];
             opos += m;
             wsync();
@@ -1725,6 +1929,20 @@ __global__ __launch_bounds__(256) void k_cz_pack(CzArgs a) {
         }
         for (uint64_t i = head + body + l; i < len; i += 64) dst[i] = src[i];
     }
+}
+
+extern "C" int sdb_diag_cz_phase(uint64_t *out, int reset) {  // -DSDB_CZ_PT builds: ticks per phase
+#ifdef SDB_CZ_PT
+    if (reset) {
+        static const unsigned long long z[16] = {};
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_cz_pt), z, sizeof(z)) == hipSuccess ? 0 : -1;
+    }
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cz_pt), 16 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+#else
+    (void)out;
+    (void)reset;
+    return -1;
+#endif
 }
 
 static std::once_flag g_cz_once;
