@@ -294,7 +294,7 @@ SIGNATURES = {
 }
 
 
-STAGES = ["bloom", "facts", "seg", "group", "enum", "emit", "emit_slow", "bloom_fill"]
+STAGES = ["bloom", "facts", "seg", "anchor", "blocks", "emit", "emit_slow", "bloom_fill"]  # k_anchor, k_blocks (round 5 on)
 
 
 def bind(lib, partial=False):

@@ -2886,12 +2886,12 @@ hipError_t launch_encode_set(const SstSet &P, size_t bin_lds, size_t fill_lds, h
     hipLaunchKernelGGL(k_seg, dim3(P.max_chunks + P.max_slices, P.count), dim3(kSegThreads), seg_lds, st, P);
     stage_mark(st, kStSeg, false);
     // the chain: every chunk's anchor (one workgroup per SST), then each chunk's blocks
-    stage_mark(st, kStGroup, true);
+    stage_mark(st, kStAnchor, true);
     hipLaunchKernelGGL(k_anchor, dim3(1, P.count), dim3(kAnchorThreads), kAnchorLds, st, P);
-    stage_mark(st, kStGroup, false);
-    stage_mark(st, kStEnum, true);
+    stage_mark(st, kStAnchor, false);
+    stage_mark(st, kStBlocks, true);
     hipLaunchKernelGGL(k_blocks, dim3(P.max_chunks, P.count), dim3(kBlkThreads), 0, st, P);
-    stage_mark(st, kStEnum, false);
+    stage_mark(st, kStBlocks, false);
     stage_mark(st, kStEmit, true);
     // blocks over one wave image: every block at SstBlockSize 8 - 64 KiB, only blocks of > 64 tiny rows
     // at 4 KiB and below (a small grid: a full grid of 137 KB workgroups that find nothing to do costs
