@@ -12,8 +12,8 @@
 // sdb_decompress_blocks, the oracle, pyarrow / zlib in the tests — to the same block bytes) and compress
 // to within a few per cent of the canonical libraries, but they are not the crates' bytes.
 //
-// One wave per block; a block is processed in windows of <= 4 KiB staged in the wave's LDS (one window for
-// the default SstBlockSize):
+// One wave per block (four zlib / zstd or five lz4 / snappy waves per CU); a block is processed in windows of
+// <= 4 KiB staged in the wave's LDS (one window for the default SstBlockSize):
 //   a. matches: every position's longest match among the earlier positions with the same 4-byte hash
 //      (hash heads and chains built 64 positions at a time with LDS exchanges; zlib / zstd walk a 16-deep chain of
 //      earlier positions, lz4 / snappy take the latest one like lz4_flex / snap), extended 4 bytes a step;
@@ -82,17 +82,22 @@ constexpr uint32_t kCzMaxMatch = 258;
 constexpr uint32_t kCzNice = 128;                   // a chain walk stops at a match this long (zlib level 6)
 constexpr uint32_t kCzGood = 16;                    // ... and takes half of its remaining steps past this one
 
+// CRC tables: slicing-by-8 and x^256 only (12 KiB at LDS 0); the six tree-combine steps multiply by their
+// constant in registers (gf_mul) instead of reading 24 KiB of tables, which buys a wave per CU (one CRC per
+// window, ~600 VALU)
+constexpr uint32_t kCzCrcLds = 12 * 1024;
+
 template <uint32_t C>
 struct CzCfg {
     static constexpr bool kDeep = C == SDB_CODEC_ZLIB || C == SDB_CODEC_ZSTD;
-    static constexpr uint32_t kWaves = kDeep ? 3 : 4;
+    static constexpr uint32_t kWaves = kDeep ? 4 : 5;
 #ifdef SDB_CZ_DEPTH  // diagnostic: chain depth of zlib / zstd
     static constexpr uint32_t kDepth = kDeep ? SDB_CZ_DEPTH : 1;
 #else
     static constexpr uint32_t kDepth = kDeep ? 16 : 1;
 #endif
     static constexpr uint32_t kWaveLds = kCzIn + kCzHead + (kDeep ? kCzPrev : 0) + kCzMm;
-    static constexpr uint32_t kLds = kCrcTablesLds + kWaves * kWaveLds;
+    static constexpr uint32_t kLds = kCzCrcLds + kWaves * kWaveLds;
     static_assert(kLds <= 160 * 1024, "compress LDS");
 };
 
@@ -208,6 +213,58 @@ SDB_DEV void put_bits(lu32 *w, uint32_t pos, uint32_t v, uint32_t nb) {
     if (r + nb > 32) __hip_atomic_fetch_or(&w[q + 1], v >> (32 - r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
+SDB_DEV void cz_crc_tables_to_lds(lu32 *crc) {
+    for (uint32_t q = threadIdx.x; q < 8 * 256; q += blockDim.x) crc[q] = (&c_crc.t[0][0])[q];
+    for (uint32_t q = threadIdx.x; q < 4 * 256; q += blockDim.x) crc[8 * 256 + q] = (&c_mul256.t[0][0])[q];
+}
+template <int S>
+SDB_DEV uint32_t cz_tree_mul(uint32_t c) {
+    constexpr uint32_t K = x8n_c(64ull << S);
+    return gf_mul(K, c);
+}
+// crc_tree_combine with the step multipliers in registers
+SDB_DEV uint32_t cz_tree_combine(uint32_t c) {
+    const uint32_t l = (uint32_t)lane_id();
+    uint32_t p = dpp32<0x101>(c);
+    if ((l & 1) == 0) c = cz_tree_mul<0>(c) ^ p;
+    p = dpp32<0x102>(c);
+    if ((l & 3) == 0) c = cz_tree_mul<1>(c) ^ p;
+    p = dpp32<0x104>(c);
+    if ((l & 7) == 0) c = cz_tree_mul<2>(c) ^ p;
+    p = dpp32<0x108>(c);
+    if ((l & 15) == 0) c = cz_tree_mul<3>(c) ^ p;
+    p = (uint32_t)__builtin_amdgcn_permlane16_swap(c, c, false, false)[1];
+    if ((l & 31) == 0) c = cz_tree_mul<4>(c) ^ p;
+    p = (uint32_t)__builtin_amdgcn_permlane32_swap(c, c, false, false)[1];
+    if (l == 0) c = cz_tree_mul<5>(c) ^ p;
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+}
+// wave_crc_image_ra (sdb_crc.h) over the 12 KiB table set
+SDB_DEV uint32_t cz_crc_image_ra(const lu8 *img, uint32_t Lc) {
+    const uint32_t l = (uint32_t)lane_id();
+    const int s = (int)Lc - 64 * (64 - (int)l);
+    uint32_t c = 0;
+    if (s > -64) {
+        const lu128 *w = (const lu128 *)(uintptr_t)(lds_addr((const void *)img) + (uint32_t)(s - (int)(Lc & 15)));
+        uint32_t x[20], m[16];
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            const u32x4 v = w[i];
+            x[4 * i] = v.x;
+            x[4 * i + 1] = v.y;
+            x[4 * i + 2] = v.z;
+            x[4 * i + 3] = v.w;
+        }
+        const uint32_t q = (Lc >> 2) & 3, r = Lc & 3;
+        if (q == 0) realign16<0>(x, r, m);
+        else if (q == 1) realign16<1>(x, r, m);
+        else if (q == 2) realign16<2>(x, r, m);
+        else realign16<3>(x, r, m);
+        c = crc_seg64_lds(m);
+    }
+    return cz_tree_combine(c) ^ 0xFFFFFFFFu;
+}
+
 // Raw CRC register (init folded in when `first`, no final inversion) of out[0, m) by the wave: out is 16-byte
 // aligned with 64 zero bytes before it; bytes past 4096 are copied to `sc` (16-byte aligned, 64 free bytes
 // before it).  m <= 4096 + 1024.
@@ -229,8 +286,8 @@ SDB_DEV uint32_t cz_crc_raw(lu8 *out, uint32_t m, lu8 *sc, bool first) {
     }
     if (first && l == 0) ((lu32 *)out)[0] = ~((const lu32 *)out)[0];  // crc32fast's init, folded into bytes [0, 4)
     wsync();
-    uint32_t raw = wave_crc_image_ra(out, head) ^ 0xFFFFFFFFu;
-    if (tail) raw = crc_shift_bytes(raw, tail) ^ wave_crc_image_ra(sc, tail) ^ 0xFFFFFFFFu;
+    uint32_t raw = cz_crc_image_ra(out, head) ^ 0xFFFFFFFFu;
+    if (tail) raw = crc_shift_bytes(raw, tail) ^ cz_crc_image_ra(sc, tail) ^ 0xFFFFFFFFu;
     wsync();
     if (first && l == 0) ((lu32 *)out)[0] = ~((const lu32 *)out)[0];
     wsync();
@@ -1589,10 +1646,10 @@ __global__ __launch_bounds__(64 * CzCfg<CODEC>::kWaves) void k_cz(CzArgs a) {
         if (threadIdx.x == 0) atomicMin(a.err, (unsigned long long)SDB_DEVICE_ERROR);
         return;
     }
-    crc_tables_to_lds((lu32 *)smem);
+    cz_crc_tables_to_lds((lu32 *)smem);
     __syncthreads();
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    lu8 *wb = (lu8 *)smem + kCrcTablesLds + w * Cfg::kWaveLds;
+    lu8 *wb = (lu8 *)smem + kCzCrcLds + w * Cfg::kWaveLds;
     lu8 *in = wb;
     lu32 *head = (lu32 *)(wb + kCzIn);
     lu32 *seq = head;  // after the match pass: 2 dwords per sequence
