@@ -583,8 +583,10 @@ typedef struct sdb_footer_in {
     const char *filter_name;          /* FilterPolicy::name: NULL = "_bf"; a prefix / no-whole-key policy
                                          is "_bf:p=<extractor>[:wh=0]" (filter_policy.rs:237-250) */
     uint32_t compression;             /* SsTableInfo.compression_format (SDB_CODEC_*): the filter, index and
-                                         stats blocks go through compress_and_transform with that codec, as
-                                         literal-only streams of the format (the data blocks: sdb_compress_blocks) */
+                                         stats blocks go through compress_and_transform with that codec: zlib
+                                         level 6, hash-chain LZ4 / Snappy, zstd with predefined FSE sequences,
+                                         each kept only when shorter than the literal-only stream (host code,
+                                         sdb_host_codec.cpp; the data blocks: sdb_compress_blocks) */
     uint32_t pad;
 } sdb_footer_in;
 /* Writes the footer into out[0..cap) and its length into *len.  out == NULL: size query only.

@@ -25,6 +25,10 @@
 
 #include "../../include/slatedb_amd.h"
 
+namespace sdb {
+void host_compress(uint32_t codec, const uint8_t *in, uint64_t n, std::vector<uint8_t> &o);  // sdb_host_codec.cpp
+}
+
 namespace {
 
 // crc32fast::hash (IEEE, reflected, init/xorout 0xFFFFFFFF) on the host: carry-less multiply folding
@@ -527,15 +531,18 @@ extern "C" sdb_status sdb_sst_footer(const sdb_footer_in *in, uint8_t *out, uint
             std::vector<uint8_t> composite(fh);
             composite.insert(composite.end(), in->bloom, in->bloom + in->bloom_len);
             literal_stream(codec, composite.data(), composite.size(), zf);
+            sdb::host_compress(codec, composite.data(), composite.size(), zf);
             filter_crc = crc(zf.data(), zf.size());
             filter_len = zf.size() + 4;
         }
         literal_stream(codec, idx_p, idx_n, zi);
+        sdb::host_compress(codec, idx_p, idx_n, zi);
         idx_p = zi.data();
         idx_n = zi.size();
         idx_crc = crc(idx_p, idx_n);
         if (in->stats) {
             literal_stream(codec, st_p, st_n, zs);
+            sdb::host_compress(codec, st_p, st_n, zs);
             st_p = zs.data();
             st_n = zs.size();
             st_crc = crc(st_p, st_n);
