@@ -40,6 +40,7 @@ sys.path.insert(0, ROOT)
 from slatedb_amd import _abi, datasets, job, runtime  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s); the box's STREAM copy: DESIGN.md §5
+GUIDE_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: 6.29 TB/s measured float4 copy (79 % of spec)
 PMC_FILES = ("r5_pmc_traffic.json", "r4_pmc_traffic.json", "r3_pmc_traffic.json", "r2_pmc_traffic.json")  # newest first
 PMC_FILE = PMC_FILES[0]
 
@@ -456,6 +457,7 @@ def main():
                      "frac": round(pipe_gbs / PEAK_HBM_GBS, 4),
                      "measured_copy_GBps": round(copy_gbs, 1) if copy_gbs else None,
                      "frac_of_measured_copy": round(pipe_gbs / copy_gbs, 4) if copy_gbs else None,
+                     "frac_of_guide_copy": round(pipe_gbs / GUIDE_COPY_GBS, 4),
                      "traffic": traffic_sst * batch if traffic_sst else None,
                      "traffic_source": ("committed PMC passes profiles/%s (same command, per SST x batch)" % PMC_FILE)
                      if traffic_sst else None,
@@ -463,6 +465,7 @@ def main():
                      "device_ms_per_step": round(set_ms, 5), "device_ms_per_sst": round(set_ms / batch, 5),
                      "k_emit": {"achieved": round(emit_gbs, 1), "frac": round(emit_gbs / PEAK_HBM_GBS, 4),
                                 "frac_of_measured_copy": round(emit_gbs / copy_gbs, 4) if copy_gbs else None,
+                                "frac_of_guide_copy": round(emit_gbs / GUIDE_COPY_GBS, 4),
                                 "avg_launch_ms": round(emit_ms, 5), "algorithmic_bytes_per_launch": emit_bytes,
                                 "traffic_per_sst": traffic_kernels.get("k_emit")},
                      "stage_ms_per_step": {k: round(v, 5) for k, v in stage_ms.items()}},

@@ -447,3 +447,26 @@ def test_compactor_many_runs_order_error(rt):
     ents = [(b"zz", 0, b"x", 5, None, None), (b"aa", 0, b"y", 4, None, None)]  # descending keys
     runs[35] = Run.from_entries(ents)
     compact_both(rt, runs, O.retention(), dict(), 10 ** 9)
+
+
+def test_compactor_subcompactions(rt):
+    """RFC-0028 subcompactions on the device: the planner's key ranges (slatedb_amd/subcompaction.py over
+    the inputs' block indexes), each range compacted by its own sdb_compactor job from the input runs cut to
+    the range — every range bit-exact vs the oracle (merged stream, cut list, every output SST), and the
+    ranges' merged streams concatenate to the unsplit job's."""
+    from slatedb_amd import subcompaction as S
+
+    from .test_subcompaction import _job, merged_entries
+    _, runs, metas, _ = _job(n=20000)
+    ranges = S.plan_subcompaction_ranges(metas, 4)
+    assert len(ranges) >= 2
+    ret = O.retention(filter_tombstone=True)
+    got = []
+    for x in ranges:
+        part = [S.slice_run(r, x) for r in runs]
+        comp, ssts = compact_both(rt, part, ret, dict(block_size=4096, bloom_bits_per_key=10), 2 << 20)
+        gm, _ = comp.merged()
+        got += merged_entries(gm)
+        comp.close()
+    whole, wsm, _, _ = O.compact(runs, ret, O.params(block_size=4096, bloom_bits_per_key=10), 2 << 20)
+    assert got == merged_entries(whole)
