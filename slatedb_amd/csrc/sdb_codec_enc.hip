@@ -368,8 +368,20 @@ SDB_DEV uint64_t cz_matches(const lu8 *in, uint32_t wn, uint32_t room, lu32 *hea
         // zlib's good / nice lengths: a match of kCzGood bytes cuts the rest of the chain to a half, one of
         // kCzNice ends it
         uint32_t dl0 = kDepth, dl1 = kDepth;
+        // inside a run of one byte value (the 4 bytes at p - 1 equal those at p) a match of the run is met at
+        // every step of the chain: two steps, as the parse takes such positions only past a match's end
+        if (kDepth > 2) {
+            if (p0 > 0 && live0 && lds_u32u(in, p0 - 1) == v0) dl0 = 2;
+            if (live1 && lds_u32u(in, p1 - 1) == v1) dl1 = 2;
+        }
+#ifdef SDB_CZ_PT
+        uint32_t pt_steps = 0;
+#endif
         for (uint32_t d = 0; d < kDepth; d++) {
             if (!c0 && !c1) break;
+#ifdef SDB_CZ_PT
+            pt_steps++;
+#endif
             const uint32_t q0 = c0 ? c0 - 1 : 0, q1 = c1 ? c1 - 1 : 0;
             const uint32_t w0 = lds_u32u(in, q0), w1 = lds_u32u(in, q1);
             uint32_t n0 = 0, n1 = 0;
@@ -410,6 +422,16 @@ SDB_DEV uint64_t cz_matches(const lu8 *in, uint32_t wn, uint32_t room, lu32 *hea
         };
         finish(p0, live0, bl0, bo0, b0 >> 6);
         finish(p1, live1, bl1, bo1, (b0 >> 6) + 1);
+#ifdef SDB_CZ_PT
+        {  // 11: wave steps of the chain walks (the slowest lane's), 12: lanes' steps summed
+            const uint32_t ws = wave_max(pt_steps);
+            const uint32_t ls = wave_sum(pt_steps);
+            if (l == 0) {
+                atomicAdd(&g_cz_pt[11], (unsigned long long)ws);
+                atomicAdd(&g_cz_pt[12], (unsigned long long)ls);
+            }
+        }
+#endif
         wsync();
     }
     return vmask;
@@ -451,41 +473,12 @@ SDB_DEV uint32_t cz_parse(uint64_t vmask, uint32_t wn, const lu32 *mm, lu32 *seq
 // ------------------------------------------------------------------------------------------------
 // Huffman code lengths of the symbols with nonzero f[0, ns) (ns <= 512, at least two of them), each
 // <= maxlen, by the wave: nonzero (freq << 9 | sym) keys compacted and bitonic-sorted in `work` (>= the
-// next power of two of their count); Moffat & Katajainen's in-place method over the sorted run on lane 0
-// (Al: >= ns LDS words; an array held in VGPRs and accessed by readlane at wave-uniform indices measured
-// four times slower: SGPR spills); then the lengths lane-interleaved in eight VGPRs for the Kraft-sum
-// length limit on the per-length counts (ballots), handed out longest first to the least frequent symbols.  len[0, ns) written (0 for absent symbols).  Returns the max length.
+// next power of two of their count); Moffat & Katajainen's method over the sorted run — its first pass on
+// lane 0 with the queue heads in registers (Al: >= ns LDS words; the array itself in VGPRs, read by readlane
+// at wave-uniform indices, measured four times slower: SGPR spills), its second and third passes as
+// wave-parallel pointer jumping and ballot counts — and the Kraft-sum length limit on the per-length
+// counts, lengths handed out longest first to the least frequent symbols.  len[0, ns) written (0 for absent symbols).  Returns the max length.
 // ------------------------------------------------------------------------------------------------
-struct WArr {  // 512 wave-uniform-indexed entries (a switch on the register: a dynamic index would spill to scratch)
-    uint32_t r[8];
-    SDB_DEV uint32_t get(uint32_t x) const {
-        const int ln = (int)(x & 63);
-        switch (x >> 6) {
-            case 0: return (uint32_t)__builtin_amdgcn_readlane((int)r[0], ln);
-            case 1: return (uint32_t)__builtin_amdgcn_readlane((int)r[1], ln);
-            case 2: return (uint32_t)__builtin_amdgcn_readlane((int)r[2], ln);
-            case 3: return (uint32_t)__builtin_amdgcn_readlane((int)r[3], ln);
-            case 4: return (uint32_t)__builtin_amdgcn_readlane((int)r[4], ln);
-            case 5: return (uint32_t)__builtin_amdgcn_readlane((int)r[5], ln);
-            case 6: return (uint32_t)__builtin_amdgcn_readlane((int)r[6], ln);
-            default: return (uint32_t)__builtin_amdgcn_readlane((int)r[7], ln);
-        }
-    }
-    SDB_DEV void set(uint32_t x, uint32_t v) {
-        const bool me = (uint32_t)lane_id() == (x & 63);
-        switch (x >> 6) {
-            case 0: r[0] = me ? v : r[0]; break;
-            case 1: r[1] = me ? v : r[1]; break;
-            case 2: r[2] = me ? v : r[2]; break;
-            case 3: r[3] = me ? v : r[3]; break;
-            case 4: r[4] = me ? v : r[4]; break;
-            case 5: r[5] = me ? v : r[5]; break;
-            case 6: r[6] = me ? v : r[6]; break;
-            default: r[7] = me ? v : r[7]; break;
-        }
-    }
-};
-
 SDB_DEV uint32_t wave_huff_lengths(const lu32 *f, uint32_t ns, uint32_t maxlen, lu8 *len, lu32 *work, lu32 *Al) {
     const uint32_t l = (uint32_t)lane_id();
     uint32_t m = 0;
@@ -515,100 +508,150 @@ SDB_DEV uint32_t wave_huff_lengths(const lu32 *f, uint32_t ns, uint32_t maxlen, 
         }
     }
     if (m == 0) return 0;
-    if (l == 0) {  // Moffat & Katajainen on one lane, the array in LDS
-        const int n = (int)m;
-        for (int i = 0; i < n; i++) Al[i] = work[i] >> 9;
-        if (n == 1) {
-            Al[0] = 1;
-        } else {
-            Al[0] += Al[1];
-            int root = 0, leaf = 2, next;
-            for (next = 1; next < n - 1; next++) {
-                if (leaf >= n || Al[root] < Al[leaf]) {
-                    Al[next] = Al[root];
-                    Al[root++] = next;
-                } else {
-                    Al[next] = Al[leaf++];
-                }
-                if (leaf >= n || (root < next && Al[root] < Al[leaf])) {
-                    Al[next] += Al[root];
-                    Al[root++] = next;
-                } else {
-                    Al[next] += Al[leaf++];
-                }
+    const int n = (int)m;
+    if (n == 1) {
+        if (l == 0) len[work[0] & 511] = 1;
+        wsync();
+        return 1;
+    }
+    // 1. Moffat & Katajainen's first pass on lane 0: the internal nodes' weights, then (once consumed) their
+    //    parent indices, in Al[0, n - 1).  The leaves are read from the sorted keys (never written), and the
+    //    heads of both queues are kept in registers with the next values loaded ahead, so a pick waits on no
+    //    LDS round trip: the head after an internal node is the node behind it (Al, loaded when it became
+    //    second) or, when the queue ran dry, the node this step creates.
+    if (l == 0) {
+        auto LV = [&](int i) -> uint32_t { return i < n ? work[i] >> 9 : 0xFFFFFFFFu; };
+        uint32_t l0 = LV(2), l1 = LV(3), l2 = LV(4);
+        uint32_t i0 = (work[0] >> 9) + (work[1] >> 9), i1 = 0;
+        Al[0] = i0;
+        int root = 0, leaf = 2;
+        for (int next = 1; next < n - 1; next++) {
+            uint32_t w;
+            if (leaf >= n || i0 < l0) {
+                w = i0;
+                Al[root] = (uint32_t)next;
+                root++;
+                i0 = i1;
+                i1 = root + 1 < next ? Al[root + 1] : 0u;
+            } else {
+                w = l0;
+                leaf++;
+                l0 = l1;
+                l1 = l2;
+                l2 = LV(leaf + 2);
             }
-            Al[n - 2] = 0;
-            for (next = n - 3; next >= 0; next--) Al[next] = Al[Al[next]] + 1;
-            int avbl = 1, used = 0, dpth = 0;
-            root = n - 2;
-            next = n - 1;
-            while (avbl > 0) {
-                while (root >= 0 && (int)Al[root] == dpth) {
-                    used++;
-                    root--;
-                }
-                while (avbl > used) {
-                    Al[next--] = (uint32_t)dpth;
-                    avbl--;
-                }
-                avbl = 2 * used;
-                dpth++;
-                used = 0;
+            if (leaf >= n || (root < next && i0 < l0)) {
+                w += i0;
+                Al[root] = (uint32_t)next;
+                root++;
+                i0 = i1;
+                i1 = root + 1 < next ? Al[root + 1] : 0u;
+            } else {
+                w += l0;
+                leaf++;
+                l0 = l1;
+                l1 = l2;
+                l2 = LV(leaf + 2);
             }
+            Al[next] = w;
+            if (root == next) i0 = w;
+            else if (root + 1 == next) i1 = w;
         }
     }
     wsync();
-    WArr A;
+    uint32_t sym[8];
 #pragma unroll
-    for (uint32_t k = 0; k < 8; k++) A.r[k] = 64 * k + l < m ? Al[64 * k + l] : 0;
-    // A[i]: length of the i-th least frequent symbol (non-increasing in i)
-    uint32_t mx = uni(A.r[0]);  // lane 0: the least frequent symbol's length, the longest
-    if (mx > maxlen) {
-        uint32_t cnt[16];
-        cnt[0] = 0;
+    for (uint32_t k = 0; k < 8; k++) sym[k] = 64 * k + l < m ? work[64 * k + l] & 511 : 0;
+    wsync();
+    // 2. the internal nodes' depths by pointer jumping (the second pass as log2(n) wave-parallel rounds):
+    //    D = work, P = Al (the root, node n - 2, is its own parent at depth 0)
+    const uint32_t ni = m - 1;
+    for (uint32_t i = l; i < ni; i += 64) {
+        work[i] = i == ni - 1 ? 0u : 1u;
+        if (i == ni - 1) Al[i] = i;
+    }
+    wsync();
+    for (uint32_t r = 1; r < ni; r <<= 1) {
+        uint32_t nd[8], np[8];
 #pragma unroll
-        for (uint32_t b = 1; b < 16; b++) {
+        for (uint32_t k = 0; k < 8; k++) {
+            const uint32_t i = 64 * k + l;
+            nd[k] = np[k] = 0;
+            if (i < ni) {
+                const uint32_t pa = Al[i];
+                nd[k] = work[i] + work[pa];
+                np[k] = Al[pa];
+            }
+        }
+        wsync();
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) {
+            const uint32_t i = 64 * k + l;
+            if (i < ni) {
+                work[i] = nd[k];
+                Al[i] = np[k];
+            }
+        }
+        wsync();
+    }
+    // 3. leaves per depth from the internal nodes' (third pass): with C(d) = internal nodes of depth >= d,
+    //    the leaves of depth >= d number 2 C(d - 1) - C(d); the least frequent leaves are the deepest.  Depths
+    //    past maxlen are counted at maxlen, then the Kraft-sum fix.
+    uint32_t C[17];
+    {
+        uint32_t dep[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) dep[k] = 64 * k + l < ni ? work[64 * k + l] : 0;
+#pragma unroll
+        for (uint32_t d = 0; d <= 16; d++) {
             uint32_t c = 0;
 #pragma unroll
-            for (uint32_t k = 0; k < 8; k++) {
-                const bool in = 64 * k + l < m;
-                const uint32_t a = A.r[k] > maxlen ? maxlen : A.r[k];
-                c += (uint32_t)__builtin_popcountll(__ballot(in && a == b));
+            for (uint32_t k = 0; k < 8; k++) c += (uint32_t)__builtin_popcountll(__ballot(64 * k + l < ni && dep[k] >= d));
+            C[d] = c;
+        }
+    }
+    uint32_t cnt[16], mx = 0;
+    {
+        auto Lge = [&](uint32_t d) -> uint32_t { return 2 * C[d - 1] - C[d]; };  // 1 <= d <= 16
+        cnt[0] = 0;
+        for (uint32_t d = 1; d < 16; d++) cnt[d] = 0;
+        for (uint32_t d = 1; d < maxlen; d++) cnt[d] = Lge(d) - Lge(d + 1);
+        cnt[maxlen] = Lge(maxlen);
+        for (uint32_t d = 1; d <= maxlen; d++)
+            if (cnt[d]) mx = d;
+        if (Lge(maxlen + 1) > 0) {  // deeper leaves: the Kraft-sum limit
+            uint32_t total = 0;
+            for (uint32_t b = 1; b <= maxlen; b++) total += cnt[b] << (maxlen - b);
+            while (total != (1u << maxlen)) {
+                cnt[maxlen]--;
+                for (uint32_t b = maxlen - 1; b > 0; b--)
+                    if (cnt[b]) {
+                        cnt[b]--;
+                        cnt[b + 1] += 2;
+                        break;
+                    }
+                total--;
             }
-            cnt[b] = c;
+            mx = maxlen;
         }
-        uint32_t total = 0;
-        for (uint32_t b = 1; b <= maxlen; b++) total += cnt[b] << (maxlen - b);
-        while (total != (1u << maxlen)) {
-            cnt[maxlen]--;
-            for (uint32_t b = maxlen - 1; b > 0; b--)
-                if (cnt[b]) {
-                    cnt[b]--;
-                    cnt[b + 1] += 2;
-                    break;
-                }
-            total--;
-        }
-        // entries [0, cnt[maxlen]) get maxlen, the next cnt[maxlen - 1] entries maxlen - 1, ...
-        uint32_t end[16];
+    }
+    // leaf j (ascending frequency) -> its length: [0, cnt[maxlen]) maxlen, the next cnt[maxlen - 1] maxlen - 1, ...
+    uint32_t end[16];
+    {
         uint32_t acc = 0;
         for (int b = 15; b >= 1; b--) {
             if ((uint32_t)b <= maxlen) acc += cnt[b];
             end[b] = acc;
         }
-#pragma unroll
-        for (uint32_t k = 0; k < 8; k++) {
-            const uint32_t i = 64 * k + l;
-            uint32_t b = maxlen;
-            while (b > 1 && i >= end[b]) b--;
-            A.r[k] = b;
-        }
-        mx = maxlen;
     }
 #pragma unroll
     for (uint32_t k = 0; k < 8; k++) {
-        const uint32_t i = 64 * k + l;
-        if (i < m) len[work[i] & 511] = (uint8_t)A.r[k];
+        const uint32_t j = 64 * k + l;
+        if (j < m) {
+            uint32_t b = maxlen;
+            while (b > 1 && j >= end[b]) b--;
+            len[sym[k]] = (uint8_t)b;
+        }
     }
     wsync();
     return mx;
