@@ -50,7 +50,7 @@ def main():
     shutil.copy(one("bench.json"), os.path.join(PROF, tag + "_bench.json"))
     shutil.copy(one("configs.jsonl"), os.path.join(PROF, tag + "_configs.jsonl"))
     for d, name in (("enc", "encode"), ("dec", "decode"), ("bloom", "bloom"), ("compact", "compact"),
-                    ("codec", "codec"), ("lookup", "lookup")):
+                    ("codec", "codec"), ("lookup", "lookup"), ("compress", "compress"), ("single", "single_sst")):
         m = glob.glob(os.path.join(RP, d, "**", "run_kernel_stats.csv"), recursive=True)
         if m:
             shutil.copy(m[0], os.path.join(PROF, "%s_%s_kernel_stats.csv" % (tag, name)))

@@ -4,7 +4,8 @@
 #   2. rocprofv3 --kernel-trace --stats over the bench, one stream        -> rp/enc/
 #   3. PMC passes FETCH_SIZE, WRITE_SIZE over the bench                    -> rp/pmc_*/
 #   4. scripts/bench_configs.py (every config, CPU baselines)             -> rp/configs.jsonl
-#   5. kernel traces: configs[2] decode, configs[3] bloom, compaction, codecs, lookups -> rp/{dec,bloom,compact,codec,lookup}/
+#   5. kernel traces: configs[2] decode, configs[3] bloom, compaction, codecs, lookups, the compressors,
+#      the single-SST (configs[1]) sequence -> rp/{dec,bloom,compact,codec,lookup,compress,single}/
 #   6. PMC FETCH / WRITE of the bloom, the compaction and the decode      -> rp/pmc_{bloom,compact,dec}_*/
 #   7. SQ counter passes over the encode and the decode                   -> rp/sq_{enc,dec}/
 # Then on the host: python3 scripts/collect_profiles.py $TAG
@@ -37,6 +38,8 @@ step bloom 200 rocprofv3 --kernel-trace --stats -d $O/bloom -o run --output-form
 step compact 300 rocprofv3 --kernel-trace --stats -d $O/compact -o run --output-format csv -- python3 scripts/bench_configs.py --compact --reps 8
 step codec 400 rocprofv3 --kernel-trace --stats -d $O/codec -o run --output-format csv -- python3 scripts/bench_configs.py --codec --reps 3
 step lookup 200 rocprofv3 --kernel-trace --stats -d $O/lookup -o run --output-format csv -- python3 scripts/bench_configs.py --lookup --reps 10
+step compress 400 rocprofv3 --kernel-trace --stats -d $O/compress -o run --output-format csv -- python3 scripts/bench_configs.py --compress --reps 3
+step single 200 rocprofv3 --kernel-trace --stats -d $O/single -o run --output-format csv -- python3 scripts/single_sst.py
 for w in bloom:--bloom compact:--compact dec:--decode; do
   n=${w%%:*}; f=${w#*:}
   for c in FETCH_SIZE WRITE_SIZE; do
