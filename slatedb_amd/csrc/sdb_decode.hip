@@ -1551,6 +1551,11 @@ SDB_DEV void dec_finish(const DecodeArgs &a) {
 // k_dec_emit_gen writes the summary (no k_dec_finish launch).
 // DESC: the order as a compile-time constant of the local copy, so the ascending instance carries none
 // of the mirroring
+#ifndef SDB_DEC_EMIT_REV
+#define SDB_DEC_EMIT_REV 1
+#endif
+constexpr bool kEmitRev = SDB_DEC_EMIT_REV != 0;
+
 template <bool DESC>
 __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmEu))) void k_dec_emit(DecodeArgs a0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1644,10 +1649,14 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)g, lane + 1) << 32);
     };
     auto rowpos_load = [&](uint64_t kk) -> uint32_t { return ((const uint32_t *)(a.rowpos + 128 * kk))[l]; };
-    uint64_t k = gwave;
-    uint64_t s = a.block_off[k], e = block_end_of(a, k);
-    uint32_t gcur = gather(k, clampk(k + nwaves));
-    uint32_t rp = rowpos_load(k);
+    // wave step k takes block B(k): descending block order when SDB_DEC_EMIT_REV, so the emit starts on the
+    // blocks the count pass read last (still in the Infinity Cache)
+    const bool rev = kEmitRev && !small;  // (small: each wave's scan results above are for block gwave)
+    auto B = [&](uint64_t x) -> uint64_t { return rev ? lastk - x : x; };
+    uint64_t k = gwave, kb = B(k);
+    uint64_t s = a.block_off[kb], e = block_end_of(a, kb);
+    uint32_t gcur = gather(kb, B(clampk(k + nwaves)));
+    uint32_t rp = rowpos_load(kb);
     Granules cur;
     gran_load_u(a, s, e, cur);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the pipeline starts with nothing in flight
@@ -1655,7 +1664,7 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
     for (;;) {
         // block k's granules -> its LDS image first, so their registers take the next block's
         if (dec_fast(s, e)) gran_store(s, e, cur, img);
-        const uint64_t kn = clampk(k + nwaves), k2 = clampk(k + 2 * nwaves);
+        const uint64_t kn = B(clampk(k + nwaves)), k2 = B(clampk(k + 2 * nwaves));
         gran_load_u(a, s1, e1, cur);
         const uint32_t gnx = gather(kn, k2);
         const uint32_t rpn = rowpos_load(kn);
@@ -1664,8 +1673,8 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
             const uint64_t kb0 = small ? s_kb0 : u64_at(gcur, 4), kb1 = small ? s_kb1 : u64_at(gcur, 6);
             const uint64_t rcw = u64_at(gcur, 8);
             const uint32_t fw = (uint32_t)__builtin_amdgcn_readlane((int)gcur, 10);
-            if (run && l == 0) a.out.block_entry_start[k] = ent0;
-            const uint32_t fb = (fw >> (8 * (k & 3))) & 0xFF;
+            if (run && l == 0) a.out.block_entry_start[kb] = ent0;
+            const uint32_t fb = (fw >> (8 * (kb & 3))) & 0xFF;
             const bool skip = ent1 == ent0 || (fb & kFlagGen);  // nothing to emit, or k_dec_emit_gen's
             // fail-fast: every block of one wave image the count pass did not reject is checked here
             if ((skip || !run) && !(ff && !(fb & kFlagBad) && dec_fast(s, e))) break;
@@ -1673,9 +1682,9 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
             const LdsBlockView v = stage_lds(a, s, e, img, ff, nullptr, true);
             if (v.status) {  // fail-fast: a checksum mismatch (the count pass accepted the rest)
                 if (l == 0) {
-                    atomicMin(a.err, (unsigned long long)((k << 8) | (uint64_t)v.status));
+                    atomicMin(a.err, (unsigned long long)((kb << 8) | (uint64_t)v.status));
                     const unsigned long long slot = atomicAdd(a.nbad, 1ull);
-                    if (slot < a.bad_cap) a.bad_block[slot] = (uint32_t)k;
+                    if (slot < a.bad_cap) a.bad_block[slot] = (uint32_t)kb;
                 }
                 break;
             }
@@ -1698,6 +1707,7 @@ __global__ __launch_bounds__(kEmThreads) __attribute__((amdgpu_waves_per_eu(kEmE
         wave_sync_d();
         k += nwaves;
         if (k >= a.nblocks) break;
+        kb = B(k);
         gcur = gnx;
         rp = rpn;
         s = s1;
