@@ -163,6 +163,46 @@ SDB_DEV void probes_hd(uint32_t h, uint32_t d, uint32_t k, uint32_t m, F f) {
     }
 }
 
+// The probes of the lane's keys (probes_hd's fast path: m > K, m <= 2^31) binned into the slices' LDS buckets:
+// every probe first, then all their bucket reservations in flight together, then the offsets -- instead of
+// one LDS round trip per probe (bloom_bin_core's one-pass plan)
+template <uint32_t KPT, uint32_t K>
+SDB_DEV void bin_probes_batched(const uint32_t (&hh)[KPT], const uint32_t (&dd)[KPT], uint32_t nk, const BloomPlan &pl,
+                                uint32_t cap, uint32_t *cnt, uint16_t *bkt) {
+    const uint32_t tid = threadIdx.x, nt = blockDim.x, mask = (1u << pl.sb) - 1;
+    uint32_t pp[KPT][K], pos[KPT][K];
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; j++) {
+        uint32_t h = hh[j], d = dd[j];
+#pragma unroll
+        for (uint32_t i = 0; i < K; i++) {
+            d += i;
+            const uint32_t dm = d - pl.m;
+            d = dm < d ? dm : d;
+            pp[j][i] = h;
+            h += d;
+            const uint32_t hm = h - pl.m;
+            h = hm < h ? hm : h;
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; j++) {
+#pragma unroll
+        for (uint32_t i = 0; i < K; i++) pos[j][i] = cap;
+        if (tid + j * nt < nk) {
+#pragma unroll
+            for (uint32_t i = 0; i < K; i++) pos[j][i] = atomicAdd(&cnt[pp[j][i] >> pl.sb], 1u);
+        }
+    }
+#ifndef SDB_EXP_BIN_NOWRITE
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; j++)
+#pragma unroll
+        for (uint32_t i = 0; i < K; i++)
+            if (pos[j][i] < cap) bkt[__umul24(pp[j][i] >> pl.sb, cap) + pos[j][i]] = (uint16_t)(pp[j][i] & mask);
+#endif
+}
+
 // Bin one tile whose keys' (h0, d0) are held in registers: key tid + j * blockDim.x of the tile in
 // (hh[j], dd[j]), nk keys.  An LDS counting sort by slice (histogram, scan, scatter), then every
 // slice's run is written to the tile's slot with consecutive lanes on consecutive words (coalesced;
@@ -175,20 +215,29 @@ SDB_DEV void bloom_bin_core(uint32_t tile, const uint32_t (&hh)[KPT], const uint
     if (pl.one_pass) {
         // every probe takes the next place of its slice's LDS bucket (cap u16 offsets, the slot's own
         // capacity: a longer run is an overflow either way), then each bucket is copied to its slot
-        uint32_t *cnt = lds;                           // S
-        uint16_t *bkt = (uint16_t *)(lds + S);         // S x cap
+        uint32_t *cnt = lds;                                   // S
+        uint16_t *bkt = (uint16_t *)(lds + ((S + 3) & ~3u));   // S x cap, 16-byte aligned (cap: multiple of 32)
         const uint32_t tid = threadIdx.x, nt = blockDim.x, cap = q.cap, mask = (1u << pl.sb) - 1;
         for (uint32_t x = tid; x < S; x += nt) cnt[x] = 0;
         __syncthreads();
+        const bool fast = pl.m > pl.k && pl.m <= 0x80000000u;
+        if (fast && pl.k == 6) {  // the default plan: 10 bits per key -> (u16)(10 * 0.69) = 6 probes
+            bin_probes_batched<KPT, 6>(hh, dd, nk, pl, cap, cnt, bkt);
+        } else if (fast && pl.k == 7) {
+            bin_probes_batched<KPT, 7>(hh, dd, nk, pl, cap, cnt, bkt);
+        } else if (fast && pl.k == 5) {
+            bin_probes_batched<KPT, 5>(hh, dd, nk, pl, cap, cnt, bkt);
+        } else {
 #pragma unroll
-        for (uint32_t j = 0; j < KPT; j++)
-            if (tid + j * nt < nk)
-                probes_hd(hh[j], dd[j], pl.k, pl.m, [&](uint32_t p) {
-                    const uint32_t sl = p >> pl.sb, pos = atomicAdd(&cnt[sl], 1u);
+            for (uint32_t j = 0; j < KPT; j++)
+                if (tid + j * nt < nk)
+                    probes_hd(hh[j], dd[j], pl.k, pl.m, [&](uint32_t p) {
+                        const uint32_t sl = p >> pl.sb, pos = atomicAdd(&cnt[sl], 1u);
 #ifndef SDB_EXP_BIN_NOWRITE  // diagnostic: the atomics alone
-                    if (pos < cap) bkt[__umul24(sl, cap) + pos] = (uint16_t)(p & mask);  // sl < 256: full-rate mul
+                        if (pos < cap) bkt[__umul24(sl, cap) + pos] = (uint16_t)(p & mask);  // sl < 256: full-rate mul
 #endif
-                });
+                    });
+        }
         __syncthreads();
 #if defined(SDB_EXP_BIN_NOWRITE) || defined(SDB_EXP_BIN_NOCOPY)  // diagnostic: no slot copy-out (empty runs)
         for (uint32_t x = tid; x < S; x += nt) q.count[(uint64_t)tile * S + x] = cnt[x] == 0x7FFFFFFF ? 1 : 0;
@@ -198,37 +247,38 @@ SDB_DEV void bloom_bin_core(uint32_t tile, const uint32_t (&hh)[KPT], const uint
             const uint32_t c = cnt[x];
             q.count[(uint64_t)tile * S + x] = c <= cap ? c : kSlotOverflow;
         }
-        // wave w copies buckets w, w + nw, ...: two offsets per lane per step (cap is a multiple of 4).  The
-        // first 256 offsets of kU buckets are read from LDS before any of them is stored (one LDS round trip
-        // for the wave's buckets instead of one per bucket and step: the copy-out was 3 us of k_facts' 12.7
-        // per SST, r5)
+        // each half-wave copies one bucket per step, 16 bytes (eight offsets) per lane: a wave moves two runs
+        // of up to 256 offsets per load / store pair; kU steps' loads are issued before any store.  Whole
+        // 64-byte granules (cap is a multiple of 32): the words past the run carry stale bucket bytes, which
+        // the fill never reads
         const uint64_t stride = (uint64_t)pl.tiles * cap;
         uint16_t *slots = (uint16_t *)q.slot + (uint64_t)tile * cap;
-        const uint32_t w = tid >> 6, nw = nt >> 6, l = tid & 63;
-        constexpr uint32_t kU = 6;
-        for (uint32_t sl0 = w; sl0 < S; sl0 += nw * kU) {
-            uint32_t c[kU], v0[kU], v1[kU];
+        const uint32_t w = tid >> 6, nw = nt >> 6, l = tid & 63, hl = l & 31;
+        const uint32_t o8 = 8 * hl < cap ? 8 * hl : 0;  // (inside the bucket)
+        constexpr uint32_t kU = 3;
+        for (uint32_t sl0 = 2 * w + (l >> 5); sl0 < S; sl0 += 2 * nw * kU) {
+            uint32_t c[kU];
+            uint4 v[kU];
 #pragma unroll
             for (uint32_t u = 0; u < kU; u++) {
-                const uint32_t sl = sl0 + u * nw, sc = sl < S ? sl : 0;
+                const uint32_t sl = sl0 + u * 2 * nw, sc = sl < S ? sl : 0;
                 const uint32_t c0 = sl < S ? cnt[sc] : 0;
                 c[u] = c0 < cap ? c0 : cap;
-                const uint32_t *src = (const uint32_t *)(bkt + sc * cap);
-                v0[u] = 2 * l < cap ? src[l] : 0;  // (the granule's tail beyond the run: stale bucket words)
-                v1[u] = 2 * l + 128 < cap ? src[l + 64] : 0;
+                v[u] = *(const uint4 *)(bkt + __umul24(sc, cap) + o8);
             }
 #pragma unroll
             for (uint32_t u = 0; u < kU; u++) {
-                const uint32_t sl = sl0 + u * nw;
-                if (sl >= S) continue;
-                // whole 64-byte granules (32 offsets; cap is a multiple of 32): the words past the run carry
-                // stale bucket bytes, which the fill never reads
-                uint32_t *dst = (uint32_t *)(slots + sl * stride);
+                const uint32_t sl = sl0 + u * 2 * nw;
                 const uint32_t cg = (c[u] + 31) & ~31u;
-                if (2 * l < cg) dst[l] = v0[u];
-                if (2 * l + 128 < cg) dst[l + 64] = v1[u];
+                if (sl < S && 8 * hl < cg) *(uint4 *)(slots + sl * stride + 8 * hl) = v[u];
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kU; u++) {  // runs over 256 offsets (cap > 256)
+                const uint32_t sl = sl0 + u * 2 * nw;
+                if (sl >= S || c[u] <= 256) continue;
                 const uint32_t *src = (const uint32_t *)(bkt + sl * cap);
-                for (uint32_t i = 2 * l + 256; i < c[u]; i += 128) {  // runs over 256 offsets (cap > 256)
+                uint32_t *dst = (uint32_t *)(slots + sl * stride);
+                for (uint32_t i = 2 * hl + 256; i < c[u]; i += 64) {
                     if (i + 1 < c[u]) dst[i >> 1] = src[i >> 1];
                     else ((uint16_t *)dst)[i] = (uint16_t)src[i >> 1];
                 }
@@ -243,9 +293,34 @@ SDB_DEV void bloom_bin_core(uint32_t tile, const uint32_t (&hh)[KPT], const uint
     const uint32_t tid = threadIdx.x, nt = blockDim.x, np = nk * pl.k;
     for (uint32_t x = tid; x < S; x += nt) hist[x] = 0;
     __syncthreads();
+    const bool fast = pl.k == 6 && pl.m > pl.k && pl.m <= 0x80000000u;  // the default plan (10 bits per key)
+    uint32_t pp[KPT][6];  // (fast) the probes of the lane's keys, generated once for both passes
+    if (fast) {
 #pragma unroll
-    for (uint32_t j = 0; j < KPT; j++)
-        if (tid + j * nt < nk) probes_hd(hh[j], dd[j], pl.k, pl.m, [&](uint32_t p) { atomicAdd(&hist[p >> pl.sb], 1u); });
+        for (uint32_t j = 0; j < KPT; j++) {
+            uint32_t h = hh[j], d = dd[j];
+#pragma unroll
+            for (uint32_t i = 0; i < 6; i++) {  // probes_hd's fast path
+                d += i;
+                const uint32_t dm = d - pl.m;
+                d = dm < d ? dm : d;
+                pp[j][i] = h;
+                h += d;
+                const uint32_t hm = h - pl.m;
+                h = hm < h ? hm : h;
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; j++)
+            if (tid + j * nt < nk) {
+#pragma unroll
+                for (uint32_t i = 0; i < 6; i++) atomicAdd(&hist[pp[j][i] >> pl.sb], 1u);
+            }
+    } else {
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; j++)
+            if (tid + j * nt < nk) probes_hd(hh[j], dd[j], pl.k, pl.m, [&](uint32_t p) { atomicAdd(&hist[p >> pl.sb], 1u); });
+    }
     __syncthreads();
     // local run starts (exclusive scan); run lengths -> count[tile][s]
     uint64_t carry = 0;
@@ -262,10 +337,28 @@ SDB_DEV void bloom_bin_core(uint32_t tile, const uint32_t (&hh)[KPT], const uint
         carry += tot;
     }
     __syncthreads();
+    if (fast) {  // every cursor reservation of the lane in flight together, then the stores
+        uint32_t pos[KPT][6];
 #pragma unroll
-    for (uint32_t j = 0; j < KPT; j++)
-        if (tid + j * nt < nk)
-            probes_hd(hh[j], dd[j], pl.k, pl.m, [&](uint32_t p) { sorted[atomicAdd(&cur[p >> pl.sb], 1u)] = p; });
+        for (uint32_t j = 0; j < KPT; j++) {
+#pragma unroll
+            for (uint32_t i = 0; i < 6; i++) pos[j][i] = ~0u;
+            if (tid + j * nt < nk) {
+#pragma unroll
+                for (uint32_t i = 0; i < 6; i++) pos[j][i] = atomicAdd(&cur[pp[j][i] >> pl.sb], 1u);
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; j++)
+#pragma unroll
+            for (uint32_t i = 0; i < 6; i++)
+                if (pos[j][i] != ~0u) sorted[pos[j][i]] = pp[j][i];
+    } else {
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; j++)
+            if (tid + j * nt < nk)
+                probes_hd(hh[j], dd[j], pl.k, pl.m, [&](uint32_t p) { sorted[atomicAdd(&cur[p >> pl.sb], 1u)] = p; });
+    }
     __syncthreads();
     // write the runs: sorted[x] belongs to slice sl = p >> sb at run position x - hist[sl]
     const uint64_t stride = (uint64_t)pl.tiles * q.cap;

@@ -383,6 +383,13 @@ static hipError_t launch_bloom_dense(const uint8_t *key_bytes, const uint64_t *k
     return hipGetLastError();
 }
 
+// one pass also when its buckets take more LDS than the counting sort but no more than this (two binning
+// workgroups per CU either way)
+#ifndef SDB_BIN_ONEPASS_LDS
+#define SDB_BIN_ONEPASS_LDS (64 * 1024)
+#endif
+constexpr uint64_t kBinOnePassLds = SDB_BIN_ONEPASS_LDS;
+
 BloomPlan bloom_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes, uint32_t tile_keys) {
     BloomPlan pl{};
     pl.k = k ? k : 1;
@@ -403,8 +410,8 @@ BloomPlan bloom_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes, uint32_t til
     pl.mmod = pl.m ? ~0ull / pl.m + 1 : 0;
     // one pass (probes straight into per-slice LDS buckets of the slot capacity) when the offsets are
     // u16 and the buckets take no more LDS than the two-pass counting sort
-    const uint64_t bk = 4ull * pl.nslices + 2ull * pl.nslices * bloom_slot_cap(pl);
-    pl.one_pass = pl.sb <= 16 && bk <= 4ull * (2ull * pl.nslices + (uint64_t)pl.T * pl.k) ? 1u : 0u;
+    const uint64_t bk = 4ull * ((pl.nslices + 3) & ~3u) + 2ull * pl.nslices * bloom_slot_cap(pl);
+    pl.one_pass = pl.sb <= 16 && (bk <= 4ull * (2ull * pl.nslices + (uint64_t)pl.T * pl.k) || bk <= kBinOnePassLds) ? 1u : 0u;
     return pl;
 }
 
@@ -449,7 +456,8 @@ BloomSlots bloom_slots(void *ws, const BloomPlan &pl) {
 }
 
 size_t bloom_bin_lds(const BloomPlan &pl) {
-    if (pl.one_pass) return 4 * (size_t)pl.nslices + 2 * (size_t)pl.nslices * bloom_slot_cap(pl);
+    // counts (padded to 16 bytes), then the buckets
+    if (pl.one_pass) return 4 * (size_t)((pl.nslices + 3) & ~3u) + 2 * (size_t)pl.nslices * bloom_slot_cap(pl);
     return 4 * (2 * (size_t)pl.nslices + (size_t)pl.T * pl.k);
 }
 size_t bloom_fill_lds(const BloomPlan &pl) { return 4 * ((size_t)(1u << (pl.sb - 5)) + pl.tiles); }
