@@ -433,7 +433,8 @@ SDB_DEV void bloom_fill_slice(uint32_t s, const uint8_t *__restrict__ key_bytes,
             for (uint32_t u = 0; u < kU; u++) {  // unconditional loads (a clamped in-bounds slot when idle)
                 const uint32_t t = t0 + u * 4 * nw + g;
                 c[u] = t < T ? cnt[t] : 0;
-                const uint32_t tc = t < T ? t : 0, o = 8 * gl < q.cap ? 8 * gl : 0;  // inside the slot
+                // lanes past the run read its first granule again (a line the group fetches anyway)
+                const uint32_t tc = t < T ? t : 0, o = 8 * gl < c[u] && 8 * gl < q.cap ? 8 * gl : 0;
                 v[u] = *(const uint4 *)(base + (uint64_t)tc * q.cap + o);
             }
 #pragma unroll

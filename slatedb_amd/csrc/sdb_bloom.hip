@@ -120,7 +120,9 @@ static DensePlan dense_plan(uint64_t n, uint32_t k, uint64_t bitmap_bytes) {
     d.mmod = d.m ? ~0ull / d.m + 1 : 0;
     return d;
 }
-static size_t dense_sort_lds(const DensePlan &d) { return 4 * (size_t)d.S + 2 * (size_t)d.rec_stride; }
+// k_bloom_sort's LDS: S + 1 counts, then the sorted records 16-byte aligned
+__host__ __device__ inline uint32_t dense_sorted_at(uint32_t S) { return (S + 1 + 3) & ~3u; }
+static size_t dense_sort_lds(const DensePlan &d) { return 4 * (size_t)dense_sorted_at(d.S) + 2 * (size_t)d.rec_stride; }
 static size_t dense_or_lds(const DensePlan &d);
 static bool dense_fits(const DensePlan &d) {
     return d.k >= 1 && d.k <= 15 && d.m >= 2 && d.S <= kDenseMaxSlices && (uint64_t)d.T * d.k < 65536 &&
@@ -170,19 +172,18 @@ SDB_DEV void dense_hash_keys(const uint8_t *__restrict__ key_bytes, const uint64
     }
 }
 
-// KMAX: probes per key the registers hold (k <= KMAX); KPT keys per thread.
-template <uint32_t KMAX, uint32_t KPT>
-__global__ __launch_bounds__(kDenseThreads) void k_bloom_sort(const uint8_t *__restrict__ key_bytes,
-                                                              const uint64_t *__restrict__ key_off, uint64_t n,
-                                                              DensePlan d) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    uint32_t *hist = lds;                          // S: counts, then run starts
-    uint16_t *sorted = (uint16_t *)(lds + d.S);    // T * k offsets, slice order
+// KMAX: probes per key the registers hold (k <= KMAX; EXACT: k == KMAX, the loops fully unrolled with no
+// uniform branches between the probes); KPT keys per thread.
+template <uint32_t KMAX, uint32_t KPT, bool EXACT>
+SDB_DEV void bloom_sort_tile(const uint8_t *__restrict__ key_bytes, const uint64_t *__restrict__ key_off, uint64_t n,
+                             const DensePlan &d, uint32_t *lds) {
+    uint32_t *hist = lds;  // S: counts, then run starts; hist[S]: the count of dead lanes' probes (unused)
+    uint16_t *sorted = (uint16_t *)(lds + dense_sorted_at(d.S));  // T * k offsets, slice order
     __shared__ uint64_t s_w[17];
-    const uint32_t tid = threadIdx.x, tile = blockIdx.x, S = d.S, k = d.k;
+    const uint32_t tid = threadIdx.x, tile = blockIdx.x, S = d.S, k = EXACT ? KMAX : d.k;
     const uint64_t k0 = (uint64_t)tile * d.T;
     const uint32_t nk = (uint32_t)((k0 + d.T < n ? k0 + d.T : n) - k0);
-    for (uint32_t x = tid; x < S; x += kDenseThreads) hist[x] = 0;
+    for (uint32_t x = tid; x <= S; x += kDenseThreads) hist[x] = 0;
     // hash: key tid + j * 1024 of the tile (consecutive lanes read consecutive keys)
     BloomPlan pl{};
     pl.m = d.m;
@@ -191,27 +192,56 @@ __global__ __launch_bounds__(kDenseThreads) void k_bloom_sort(const uint8_t *__r
     dense_hash_keys<KPT>(key_bytes, key_off, k0, nk, pl, hh, dd);
     __syncthreads();
     // every probe (u32) and its rank inside its slice (u16: T * k < 2^16, two per register) stay in
-    // registers from the counting pass to the scatter
+    // registers from the counting pass to the scatter.  The probes are generated first, then each key's
+    // rank reservations are issued back to back (a dead lane counts into hist[S]), so a wave has many LDS
+    // adds in flight instead of one round trip per probe
     uint32_t pr[KPT * KMAX], rk[(KPT * KMAX + 1) / 2];
 #pragma unroll
     for (uint32_t x = 0; x < (KPT * KMAX + 1) / 2; x++) rk[x] = 0;
+    if constexpr (EXACT) {
 #pragma unroll
-    for (uint32_t j = 0; j < KPT; j++) {
-        const bool live = tid + j * kDenseThreads < nk;
-        uint32_t h = hh[j], dl = dd[j];
-        const uint32_t m = d.m;
+        for (uint32_t j = 0; j < KPT; j++) {
+            uint32_t h = hh[j], dl = dd[j];
+            const uint32_t m = d.m;
 #pragma unroll
-        for (uint32_t i = 0; i < KMAX; i++) {
-            pr[j * KMAX + i] = h;
-            if (live && i < k) {
+            for (uint32_t i = 0; i < KMAX; i++) {
                 dl += i;
                 const uint32_t dm = dl - m;
                 dl = dm < dl ? dm : dl;
-                const uint32_t r = atomicAdd(&hist[h >> kDenseSliceBits], 1u);
-                rk[(j * KMAX + i) / 2] |= r << (16 * ((j * KMAX + i) & 1));
+                pr[j * KMAX + i] = h;
                 h += dl;
                 const uint32_t hm = h - m;
                 h = hm < h ? hm : h;
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; j++) {
+            const bool live = tid + j * kDenseThreads < nk;
+            uint32_t r[KMAX];
+#pragma unroll
+            for (uint32_t i = 0; i < KMAX; i++) r[i] = atomicAdd(&hist[live ? pr[j * KMAX + i] >> kDenseSliceBits : S], 1u);
+#pragma unroll
+            for (uint32_t i = 0; i < KMAX; i++) rk[(j * KMAX + i) / 2] |= r[i] << (16 * ((j * KMAX + i) & 1));
+        }
+    } else {  // one LDS round trip per probe, in fewer registers
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; j++) {
+            const bool live = tid + j * kDenseThreads < nk;
+            uint32_t h = hh[j], dl = dd[j];
+            const uint32_t m = d.m;
+#pragma unroll
+            for (uint32_t i = 0; i < KMAX; i++) {
+                pr[j * KMAX + i] = h;
+                if (live && i < k) {
+                    dl += i;
+                    const uint32_t dm = dl - m;
+                    dl = dm < dl ? dm : dl;
+                    const uint32_t r = atomicAdd(&hist[h >> kDenseSliceBits], 1u);
+                    rk[(j * KMAX + i) / 2] |= r << (16 * ((j * KMAX + i) & 1));
+                    h += dl;
+                    const uint32_t hm = h - m;
+                    h = hm < h ? hm : h;
+                }
             }
         }
     }
@@ -253,6 +283,20 @@ __global__ __launch_bounds__(kDenseThreads) void k_bloom_sort(const uint8_t *__r
     const uint4 *src = (const uint4 *)sorted;
     uint4 *dst = (uint4 *)(d.rec + (uint64_t)tile * d.rec_stride);
     for (uint32_t x = tid; x < n16; x += kDenseThreads) dst[x] = src[x];
+}
+
+// the default plan (k = 6) at two workgroups per CU: its 48 probes' rank reservations in flight fit 128 VGPRs
+__global__ __launch_bounds__(kDenseThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_bloom_sort6(
+    const uint8_t *__restrict__ key_bytes, const uint64_t *__restrict__ key_off, uint64_t n, DensePlan d) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    bloom_sort_tile<6, 8, true>(key_bytes, key_off, n, d, lds);
+}
+template <uint32_t KMAX, uint32_t KPT>
+__global__ __launch_bounds__(kDenseThreads) void k_bloom_sort(const uint8_t *__restrict__ key_bytes,
+                                                              const uint64_t *__restrict__ key_off, uint64_t n,
+                                                              DensePlan d) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    bloom_sort_tile<KMAX, KPT, false>(key_bytes, key_off, n, d, lds);
 }
 
 // Workgroup b -> its run of slices, XCD-aware: the dispatcher places workgroup b on XCD b mod 8, so
@@ -363,7 +407,8 @@ static hipError_t launch_bloom_dense(const uint8_t *key_bytes, const uint64_t *k
     static std::once_flag attrs;
     static hipError_t attr_err = hipSuccess;
     std::call_once(attrs, [] {
-        const void *f[] = {(const void *)k_bloom_sort<7, 8>, (const void *)k_bloom_sort<15, 4>};
+        const void *f[] = {(const void *)k_bloom_sort6, (const void *)k_bloom_sort<7, 8>,
+                           (const void *)k_bloom_sort<15, 4>};
         for (const void *x : f)
             if (attr_err == hipSuccess)
                 attr_err = hipFuncSetAttribute(x, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLds);
@@ -373,7 +418,10 @@ static hipError_t launch_bloom_dense(const uint8_t *key_bytes, const uint64_t *k
     });
     if (attr_err != hipSuccess) return attr_err;
     dense_carve(d, ws);
-    if (d.k <= 7)
+    if (d.k == 6)  // 10 bits per key
+        hipLaunchKernelGGL(k_bloom_sort6, dim3(d.tiles), dim3(kDenseThreads), dense_sort_lds(d), st, key_bytes,
+                           key_off, n, d);
+    else if (d.k <= 7)
         hipLaunchKernelGGL((k_bloom_sort<7, 8>), dim3(d.tiles), dim3(kDenseThreads), dense_sort_lds(d), st, key_bytes,
                            key_off, n, d);
     else
