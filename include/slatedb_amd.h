@@ -358,9 +358,13 @@ sdb_status sdb_decompress_blocks_once(uint32_t codec, const uint8_t *blocks, con
  * (BE) of those compressed bytes, at out[out_off[k], out_off[k + 1]):
  *   SDB_CODEC_LZ4     u32 LE length ++ one LZ4 block (lz4_flex block::compress_prepend_size);
  *   SDB_CODEC_SNAPPY  varint length ++ Snappy raw elements (snap raw::Encoder::compress_vec);
- *   SDB_CODEC_ZLIB    78 9C ++ deflate (fixed-Huffman or stored) ++ Adler-32 BE (flate2 ZlibEncoder);
- *   SDB_CODEC_ZSTD    one zstd frame with Frame_Content_Size (zstd::bulk::compress).
- * One wave per block, a greedy LZ77 parse in the wave's LDS.  The streams are valid for their formats and
+ *   SDB_CODEC_ZLIB    78 9C ++ deflate (a dynamic-Huffman, fixed-Huffman or stored block per 4 KiB window,
+ *                     whichever is shortest) ++ Adler-32 BE (flate2 ZlibEncoder, default level 6);
+ *   SDB_CODEC_ZSTD    one zstd frame with Frame_Content_Size, a compressed block per 4 KiB window (Huffman
+ *                     or raw / RLE literals, sequences with predefined / RLE / FSE-compressed tables) or a
+ *                     raw / RLE block when shorter (zstd::bulk::compress at level 3).
+ * One wave per block: hash-chain LZ77 with lazy matching in the wave's LDS, entropy codes built by the wave
+ * (compression ratio within a few per cent of the canonical libraries).  The streams are valid for their formats and
  * decode (the crates' decompressors, sdb_decompress_blocks) to the block; they are not the crates' own
  * bytes (a match finder's choices are its own).  in_bytes = block_off[nblocks] - block_off[0];
  * out_off (device, nblocks + 1) = the compressed blocks' offsets from out (BlockMeta.offset when the data
