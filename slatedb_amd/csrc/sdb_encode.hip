@@ -624,6 +624,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_group(SstSet P) {
     const uint32_t K = a.nchunks, g = blockIdx.x, G = a.group, ngroups = (K + G - 1) / G;
     if (g >= ngroups) return;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    if (blockIdx.y == 0) PHASE_MARK_AT(1023, 5);
     if (tid == 0) {
         s_W = 0;
         s_err = ~0ull;
@@ -1193,6 +1194,7 @@ __global__ __launch_bounds__(kAnchorThreads) void k_anchor(SstSet P) {
     __shared__ uint64_t s_stat[5][kAnchorThreads / 64];
     const uint32_t K = a.nchunks, G = a.group, ngroups = (K + G - 1) / G;
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    if (blockIdx.y == 0) PHASE_MARK_AT(1023, 5);
     if (tid == 0) {
         s_W = 0;
         s_err = ~0ull;
@@ -1303,28 +1305,45 @@ __global__ __launch_bounds__(kAnchorThreads) void k_anchor(SstSet P) {
                 tab_hbm(k, o, x, c, b);
             }
         };
-        if (in_lds) {  // stage the tables: eight entries per thread in flight
+        if (in_lds) {
+            // stage the tables: eight entries per thread in flight, every load unconditional (chunk clamped);
+            // entry i's (chunk, candidate) advanced by nt incrementally -- a 64-bit i / W and i % W per entry
+            // was half of this kernel's time on one SST
             constexpr uint32_t kU = 8;
-            for (uint64_t base = 0; base < ntab; base += kU * nt) {
-                uint32_t x[kU], c[kU];
-                uint64_t b[kU];
+            const uint32_t ntab32 = (uint32_t)ntab, qn = nt / W, rn = nt % W;
+            uint32_t kk = tid / W, oo = tid % W;
+            for (uint32_t base = 0; base < ntab32; base += kU * nt) {
+                uint32_t te[kU], tc[kU], ku[kU], ou[kU];
+                uint64_t tb[kU];
 #pragma unroll
                 for (uint32_t u = 0; u < kU; u++) {
-                    const uint64_t i = base + u * nt + tid;
-                    x[u] = c[u] = 0;
-                    b[u] = 0;
-                    if (i < ntab) tab_hbm((uint32_t)(i / W), (uint32_t)(i % W), x[u], c[u], b[u]);
+                    ku[u] = kk;
+                    ou[u] = oo;
+                    oo += rn;
+                    kk += qn;
+                    if (oo >= W) {
+                        oo -= W;
+                        kk++;
+                    }
+                    const uint64_t t = (uint64_t)(ku[u] < K ? ku[u] : K - 1) * a.seg_look + ou[u];
+                    te[u] = a.tab_exit[t];
+                    tc[u] = a.tab_cnt[t];
+                    tb[u] = a.tab_bytes[t];
                 }
 #pragma unroll
                 for (uint32_t u = 0; u < kU; u++) {
-                    const uint64_t i = base + u * nt + tid;
-                    if (i >= ntab) continue;
-                    t_ex[i] = (uint16_t)x[u];
-                    t_cn[i] = (uint16_t)c[u];  // a block count inside one chunk: <= kChunk
-                    t_by[i] = b[u];
+                    const uint32_t i = base + u * nt + tid;
+                    if (i >= ntab32) continue;
+                    const uint64_t cs = (uint64_t)ku[u] * kChunk, ce = cs + kChunk < a.n ? cs + kChunk : a.n;
+                    const bool in = cs + ou[u] < ce;  // as tab_hbm
+                    const uint64_t tx = te[u];
+                    t_ex[i] = (uint16_t)(in ? (tx >= ce && tx - ce < W ? (uint32_t)(tx - ce) : W - 1) : 0u);
+                    t_cn[i] = (uint16_t)(in ? tc[u] : 0u);  // a block count inside one chunk: <= kChunk
+                    t_by[i] = in ? tb[u] : 0ull;
                 }
             }
             __syncthreads();
+            if (blockIdx.y == 0) PHASE_MARK_AT(1023, 1);
         }
         // tables over the LDS (long SSTs: a 256 MiB compaction output has ~565 chunks): the group tables in
         // LDS, and each group's chunk tables staged into one of kSW per-wave buffers when a wave composes
@@ -1364,25 +1383,34 @@ __global__ __launch_bounds__(kAnchorThreads) void k_anchor(SstSet P) {
             auto stage_group = [&](uint32_t q) {
                 const uint32_t k0 = q * Gs, k1 = (q + 1) * Gs < K ? (q + 1) * Gs : K, ne = (k1 - k0) * W;
                 constexpr uint32_t kU = 8;
+                const uint32_t q64 = 64 / W, r64 = 64 % W;
+                uint32_t kq = ln / W, oq = ln % W;  // (chunk, candidate) of entry i, advanced by 64 (no division)
                 for (uint32_t i0 = 0; i0 < ne; i0 += 64 * kU) {
-                    uint32_t te[kU], tc[kU];
+                    uint32_t te[kU], tc[kU], ks[kU], os[kU];
                     uint64_t tbv[kU];
 #pragma unroll
                     for (uint32_t u = 0; u < kU; u++) {
-                        const uint32_t i = i0 + 64 * u + ln, ic = i < ne ? i : ne - 1;
-                        const uint32_t kq = ic / W, o = ic - kq * W;
-                        const uint64_t t = (uint64_t)(k0 + kq) * a.seg_look + o;
+                        const uint32_t i = i0 + 64 * u + ln;
+                        ks[u] = kq;
+                        os[u] = oq;
+                        const bool v = i < ne;
+                        const uint64_t t = (uint64_t)(k0 + (v ? kq : k1 - k0 - 1)) * a.seg_look + (v ? oq : W - 1);
                         te[u] = a.tab_exit[t];
                         tc[u] = a.tab_cnt[t];
                         tbv[u] = a.tab_bytes[t];
+                        oq += r64;
+                        kq += q64;
+                        if (oq >= W) {
+                            oq -= W;
+                            kq++;
+                        }
                     }
 #pragma unroll
                     for (uint32_t u = 0; u < kU; u++) {
                         const uint32_t i = i0 + 64 * u + ln;
                         if (i >= ne) continue;
-                        const uint32_t kq = i / W, o = i - kq * W;
-                        const uint64_t cs = (uint64_t)(k0 + kq) * kChunk, ce = cs + kChunk < a.n ? cs + kChunk : a.n;
-                        const bool in = cs + o < ce;  // as tab_hbm
+                        const uint64_t cs = (uint64_t)(k0 + ks[u]) * kChunk, ce = cs + kChunk < a.n ? cs + kChunk : a.n;
+                        const bool in = cs + os[u] < ce;  // as tab_hbm
                         bx[i] = (uint16_t)(in ? (te[u] >= ce && te[u] - ce < W ? (uint32_t)(te[u] - ce) : W - 1) : 0u);
                         bc[i] = (uint16_t)(in ? tc[u] : 0u);
                         bb[i] = in ? tbv[u] : 0ull;
@@ -1447,8 +1475,8 @@ __global__ __launch_bounds__(kAnchorThreads) void k_anchor(SstSet P) {
         }
         // group tables: lane per (group, candidate)
         for (uint64_t i = tid; i < ng && in_lds; i += nt) {
-            const uint32_t q = (uint32_t)(i / W), k1 = (q + 1) * G < K ? (q + 1) * G : K;
-            uint32_t e = (uint32_t)(i % W), c = 0;
+            const uint32_t q = (uint32_t)i / W, k1 = (q + 1) * G < K ? (q + 1) * G : K;  // (ng < 2^32 in LDS)
+            uint32_t e = (uint32_t)i - q * W, c = 0;
             uint64_t b = 0;
             for (uint32_t k = q * G; k < k1; k++) {
                 uint32_t x, cc;
@@ -1463,6 +1491,7 @@ __global__ __launch_bounds__(kAnchorThreads) void k_anchor(SstSet P) {
             g_by[i] = b;
         }
         __syncthreads();
+        if (blockIdx.y == 0 && in_lds) PHASE_MARK_AT(1023, 2);
         if (tid == 0 && !streamed) {  // the groups from entry 0
             uint32_t e = 0;
             for (uint32_t q = 0; q < ngroups; q++) {
@@ -1491,6 +1520,7 @@ __global__ __launch_bounds__(kAnchorThreads) void k_anchor(SstSet P) {
             }
         }
         __syncthreads();
+        if (blockIdx.y == 0 && in_lds) PHASE_MARK_AT(1023, 4);
         for (uint32_t q = tid; q < ngroups && in_lds; q += nt) {  // each group's chunks from its entry
             uint32_t e = g_ent[2 * q];
             uint64_t blk = g_ent[2 * q + 1], by = g_b64[q];
