@@ -573,13 +573,73 @@ SDB_DEV void seg_chunk(const EncodeArgs &a, uint8_t *smem, uint32_t k) {
     }
     __syncthreads();
     const uint32_t Wc = s_wc;
+    // four-block jumps along the chain (two doubling rounds over the chunk, in the P / R words, which are done
+    // with): each candidate's walk below takes a quarter of the dependent LDS steps (~58 -> ~15 per D1 chunk)
+    uint32_t *j_nx = s_P;                  // kChunk: exit after up to four blocks (rel, 0xFFFF far) | blocks << 16
+    uint64_t *j_bb = (uint64_t *)(s_P + kChunk);  // kChunk: their bytes (8-byte aligned: kChunk is even)
+    static_assert(3 * kChunk <= 2 * kSegSpan + 4, "jump tables alias s_P / s_R");
+    constexpr uint32_t kJU = kChunk / kSegThreads;
+    {
+        uint32_t jn[kJU];
+        uint64_t jb[kJU];
+#pragma unroll
+        for (uint32_t u = 0; u < kJU; u++) {  // two blocks
+            const uint32_t x = tid + u * nt;
+            jn[u] = 0;
+            jb[u] = 0;
+            if (x < cn) {
+                const uint32_t n1 = s_nx[x];
+                uint64_t b = s_bb[x];
+                uint32_t n = n1, c = 1;
+                if (n1 < cn) {
+                    b += s_bb[n1];
+                    n = s_nx[n1];
+                    c = 2;
+                }
+                jn[u] = n | c << 16;
+                jb[u] = b;
+            }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kJU; u++) {
+            const uint32_t x = tid + u * nt;
+            if (x < cn) {
+                j_nx[x] = jn[u];
+                j_bb[x] = jb[u];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < kJU; u++) {  // four blocks
+            const uint32_t x = tid + u * nt;
+            if (x < cn) {
+                const uint32_t n = jn[u] & 0xFFFF;
+                if (n < cn) {
+                    const uint32_t w = j_nx[n];
+                    jb[u] += j_bb[n];
+                    jn[u] = (w & 0xFFFF) | ((jn[u] >> 16) + (w >> 16)) << 16;
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < kJU; u++) {
+            const uint32_t x = tid + u * nt;
+            if (x < cn) {
+                j_nx[x] = jn[u];
+                j_bb[x] = jb[u];
+            }
+        }
+        __syncthreads();
+    }
     for (uint32_t c = tid; c < Wc; c += nt) {
         uint32_t e = c, cnt = 0;
         uint64_t by = 0;
         while (e < cn) {
-            by += s_bb[e];
-            cnt++;
-            e = s_nx[e];
+            const uint32_t v = j_nx[e];
+            by += j_bb[e];
+            cnt += v >> 16;
+            e = v & 0xFFFF;
         }
         const uint64_t t = (uint64_t)k * a.seg_look + c;
         // 0xFFFFFFFF: the exit is beyond the u16 range (resolve then walks next[])
