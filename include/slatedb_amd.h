@@ -666,7 +666,7 @@ sdb_status sdb_decoder_decode_host(sdb_decoder *dec, const uint8_t *blocks,
  * Diagnostics (bench / profiling only)
  * ------------------------------------------------------------------------------------------- */
 /* Stage timing of sdb_encode_sst: when enabled, hipEvents are recorded around each kernel stage
- * (bloom, k_facts, k_seg, k_anchor, k_blocks, k_emit, emit_slow, bloom_fill).  sdb_diag_stage_times synchronises the
+ * (bloom, k_facts, k_seg, k_anchor, k_blocks, k_emit, k_emit_big, bloom_fill).  sdb_diag_stage_times synchronises the
  * recorded events, writes the summed milliseconds per stage into ms[0..max_stages), the number of
  * encodes measured into *launches, clears the record, and returns the number of stages. */
 void sdb_diag_enable_stage_timing(int on);

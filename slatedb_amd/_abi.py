@@ -294,7 +294,7 @@ SIGNATURES = {
 }
 
 
-STAGES = ["bloom", "facts", "seg", "anchor", "blocks", "emit", "emit_slow", "bloom_fill"]  # k_anchor, k_blocks (round 5 on)
+STAGES = ["bloom", "facts", "seg", "anchor", "blocks", "emit", "emit_big", "bloom_fill"]  # k_anchor, k_blocks (round 5 on); emit = k_emit alone
 
 
 def bind(lib, partial=False):

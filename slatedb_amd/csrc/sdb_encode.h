@@ -359,7 +359,7 @@ hipError_t launch_encode_empty(EncodeArgs a, hipStream_t st);
 hipError_t launch_encode_prep(const SstSet &P, hipStream_t st);  // k_facts, k_seg, k_group only
 
 // stage timing (diagnostics)
-enum Stage { kStBloom = 0, kStFacts, kStSeg, kStAnchor, kStBlocks, kStEmit, kStEmitSlow, kStBloomFill, kNumStages };
+enum Stage { kStBloom = 0, kStFacts, kStSeg, kStAnchor, kStBlocks, kStEmit, kStEmitBig, kStBloomFill, kNumStages };
 void stage_mark(hipStream_t st, int stage, bool begin);
 bool stage_timing_on();
 
