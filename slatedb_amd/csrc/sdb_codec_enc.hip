@@ -15,7 +15,7 @@
 // One wave per block (four zlib / zstd or five lz4 / snappy waves per CU); a block is processed in windows of
 // <= 4 KiB staged in the wave's LDS (one window for the default SstBlockSize):
 //   a. matches: every position's longest match among the earlier positions with the same 4-byte hash
-//      (hash heads and chains built 64 positions at a time with LDS exchanges; zlib / zstd walk a 16-deep chain of
+//      (hash heads and chains built 64 positions at a time with LDS exchanges; zlib / zstd walk an 8-deep chain of
 //      earlier positions, lz4 / snappy take the latest one like lz4_flex / snap), extended 4 bytes a step;
 //   b. the parse: one wave-uniform walk over the match bitmap (lane w holds positions [64 w, 64 w + 64):
 //      the next match is one ballot away), lazy by one position, the sequences (literal run, length,
@@ -91,10 +91,13 @@ template <uint32_t C>
 struct CzCfg {
     static constexpr bool kDeep = C == SDB_CODEC_ZLIB || C == SDB_CODEC_ZSTD;
     static constexpr uint32_t kWaves = kDeep ? 4 : 5;
-#ifdef SDB_CZ_DEPTH  // diagnostic: chain depth of zlib / zstd
+    // chain depth of zlib / zstd: 8 (r6, scripts/gpu_r6_czdepth.sh, 4 D1 SSTs): zlib 30.4 -> 22.3 ms at ratio
+    // 1.0980 -> 1.0971 (zlib level 6: 1.0974), zstd 24.7 -> 15.9 ms at 1.1248 -> 1.1226 (level 3: 1.1309); JSON
+    // values zlib 3.73 -> 3.67 (3.75), zstd 3.68 -> 3.63 (3.54).  Depth 4 lost 2-4 % of the ratio on D1.
+#ifdef SDB_CZ_DEPTH  // diagnostic knob
     static constexpr uint32_t kDepth = kDeep ? SDB_CZ_DEPTH : 1;
 #else
-    static constexpr uint32_t kDepth = kDeep ? 16 : 1;
+    static constexpr uint32_t kDepth = kDeep ? 8 : 1;
 #endif
     static constexpr uint32_t kWaveLds = kCzIn + kCzHead + (kDeep ? kCzPrev : 0) + kCzMm;
     static constexpr uint32_t kLds = kCzCrcLds + kWaves * kWaveLds;
