@@ -79,8 +79,14 @@ constexpr uint32_t kCzAuxOff = 8192;                // aux at mm + 8 KiB: litera
 constexpr uint32_t kCzOutCap = kCzAuxOff - kCzOutOff;
 constexpr uint32_t kCzMaxSeq = kCzHead / 8;         // a match is >= 4 bytes: a window has <= 1024 sequences
 constexpr uint32_t kCzMaxMatch = 258;
-constexpr uint32_t kCzNice = 128;                   // a chain walk stops at a match this long (zlib level 6)
-constexpr uint32_t kCzGood = 16;                    // ... and takes half of its remaining steps past this one
+#ifndef SDB_CZ_NICE
+#define SDB_CZ_NICE 128
+#endif
+#ifndef SDB_CZ_GOOD
+#define SDB_CZ_GOOD 16
+#endif
+constexpr uint32_t kCzNice = SDB_CZ_NICE;           // a chain walk stops at a match this long (zlib level 6)
+constexpr uint32_t kCzGood = SDB_CZ_GOOD;           // ... and takes half of its remaining steps past this one
 
 // CRC tables: slicing-by-8 and x^256 only (12 KiB at LDS 0); the six tree-combine steps multiply by their
 // constant in registers (gf_mul) instead of reading 24 KiB of tables, which buys a wave per CU (one CRC per
